@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: WN18-shaped TransE-L1 d=200 PairwiseStochasticTrainer
++ AdaGrad on MI355X (BASELINE.json configs[1]).
+
+One STEP = one training epoch over the synthetic WN18-shaped KG
+(|E|=40943, |R|=18, T=141,442 unique uniform triples, RandomState(0)) at the
+reference's geometry nb=100 (100 batches of 1,414 positives + one of 42),
+each positive with its two RandomModeSampler negatives (mode 0 corrupts s,
+mode 1 corrupts o), margin 2.0, lr 0.1 -- run by the native hipGraph epoch
+runner (device permutation, device sampler, fused score+scatter, fused
+mean+AdaGrad+normalize).  value = positive triples fully processed per second.
+
+Multi-GPU: one process per GPU (torchrun); the WN18 tables do not need
+sharding, so every rank trains an independent replica on its own KG
+(DESIGN.md "replicas only"); value = all ranks' triples / max-over-ranks time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--nb 100]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "scikit-kge_amd"))
+sys.path.insert(0, ROOT)
+
+N_ENT, N_REL, N_TRIPLES = 40943, 18, 141442
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def make_wn18_kg(n_ent=N_ENT, n_rel=N_REL, n_triples=N_TRIPLES, seed=0):
+    """Unique uniform (s, o, p) triples, RandomState(seed)."""
+    rs = np.random.RandomState(seed)
+    out = np.empty((0, 3), dtype=np.int64)
+    while len(out) < n_triples:
+        m = (n_triples - len(out)) * 2 + 1024
+        cand = np.stack([rs.randint(n_ent, size=m), rs.randint(n_ent, size=m),
+                         rs.randint(n_rel, size=m)], axis=1)
+        allt = np.concatenate([out, cand])
+        key = (allt[:, 0] * n_ent + allt[:, 1]) * n_rel + allt[:, 2]
+        _, first = np.unique(key, return_index=True)
+        out = allt[np.sort(first)][:n_triples]
+    return out.astype(np.int32)
+
+
+def algorithmic_bytes(d, B, P, U_E, U_R, opt_k=12):
+    """BYTES(batch) = 4d(3B + P) + k d (U_E + U_R) + 20B."""
+    return 4 * d * (3 * B + P) + opt_k * d * (U_E + U_R) + 20 * B
+
+
+def cpu_baseline(trip, d, nb, seconds=12.0):
+    """The oracle (fp64 NumPy restatement, oracle/skge_oracle.py) on a bounded
+    sample of the same workload: consecutive nb=100 batches of epoch 1,
+    negatives from the reference-semantics host sampler (not timed)."""
+    from oracle import skge_oracle as O
+    rs = np.random.RandomState(42)
+    np.random.seed(42)
+    bnd = np.sqrt(6) / np.sqrt(N_ENT + d)
+    E = O.normalize(rs.uniform(-bnd, bnd, size=(N_ENT, d)), None)
+    R = rs.uniform(-np.sqrt(6) / np.sqrt(N_REL + d), np.sqrt(6) / np.sqrt(N_REL + d), size=(N_REL, d))
+    params = {"E": E, "R": R}
+    state = {k: np.zeros_like(v) for k, v in params.items()}
+    tset = set(map(tuple, trip.tolist()))
+    idx = np.arange(len(trip))
+    np.random.shuffle(idx)
+    bounds = O.batch_bounds(len(trip), nb)
+    t_step = 0.0
+    t_all = 0.0
+    npos = 0
+    nb_done = 0
+    for (a, b) in bounds:
+        t0 = time.perf_counter()
+        pairs = O.random_mode_sample(trip[idx[a:b]], tset, (N_ENT, N_ENT, N_REL))
+        pos = np.array([p for p, _ in pairs])
+        neg = np.array([n for _, n in pairs])
+        t1 = time.perf_counter()
+        O.pairwise_step("transe", params, state, pos, neg, 0.1, 2.0, "adagrad", l1=True)
+        t2 = time.perf_counter()
+        t_step += t2 - t1
+        t_all += t2 - t0
+        npos += b - a
+        nb_done += 1
+        if t_all > seconds:
+            break
+    return {"value": npos / t_step, "unit": "triples/s", "cores": 1, "kind": "port",
+            "sample": "%d nb=100 batches (%d positives) of epoch 1, WN18-shaped KG, TransE-L1 "
+                      "d=%d AdaGrad margin 2.0; oracle/skge_oracle.py fp64 NumPy, 1 thread; "
+                      "score+grad+update only (host sampler untimed)" % (nb_done, npos, d),
+            "e2e_value": npos / t_all}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20, help="timed epochs")
+    ap.add_argument("--warmup", type=int, default=3, help="untimed epochs")
+    ap.add_argument("--nb", type=int, default=100, help="nbatches (reference geometry)")
+    ap.add_argument("--d", type=int, default=200)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import skge_amd as S
+    from skge_amd import _lib as L
+    from skge_amd.device import DeviceKG, EpochRunner
+
+    d, nb = args.d, args.nb
+    trip = make_wn18_kg(seed=rank)        # replica r trains on its own KG
+    np.random.seed(42 + rank)
+    model = S.TransE((N_ENT, N_ENT, N_REL), d, l1=True)
+    model.add_hyperparam("margin", 2.0)
+    upd = {pid: S.AdaGrad(p, 0.1) for pid, p in model.params.items()}
+    kg = DeviceKG(trip, dev)
+    runner = EpochRunner(model, upd, kg, nbatches=nb, seed=1234 + rank)
+    st = runner.stream
+    init = {pid: p.data.clone() for pid, p in model.params.items()}
+
+    # warmup (graph replays), then restore the initial parameters so the timed
+    # epochs are epochs 1..K of a fresh training run (the busiest: most violations)
+    runner.run(args.warmup)
+    runner.synchronize()
+    for pid, p in model.params.items():
+        p.data.copy_(init[pid])
+        upd[pid].reset()
+    runner.nviol_total.zero_()
+    torch.cuda.synchronize()
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(st)
+    runner.run(args.steps)
+    ev1.record(st)
+    runner.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    nviol = int(runner.nviol_total.item())
+    positives = N_TRIPLES * args.steps
+    value = world * positives / elapsed
+
+    # ---- per-kernel timing (HIP events on the runner stream, eager launches of
+    # one more epoch, outside the timed region) for the roofline ----
+    prof = kernel_profile(model, upd, kg, nb, d, st, runner)
+
+    if rank == 0:
+        cpu = None if args.no_cpu else cpu_baseline(trip, d, nb, args.cpu_seconds)
+        k = prof["dominant"]
+        line = {
+            "metric": "triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "triples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442 uniform, RandomState(rank)); "
+                    "random-init params (nunif, seed 42)",
+            "config": {"workload": "TransE-L1 d=%d PairwiseStochasticTrainer+AdaGrad, WN18 shape, "
+                                   "nb=%d (B=%d), margin 2.0, lr 0.1, device RandomModeSampler(1,[0,1]); "
+                                   "step = 1 epoch" % (d, nb, N_TRIPLES // nb),
+                       "global_batch": N_TRIPLES // nb, "parallelism": "replicas%d" % world},
+            "roofline": {"bound": "hbm", "kernel": k["name"],
+                         "achieved": round(k["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                         "traffic": None,
+                         "bytes_per_launch": round(k["bytes_per_launch"]),
+                         "avg_launch_us": round(k["avg_us"], 3)},
+            "cpu_baseline": cpu,
+            "detail": {
+                "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
+                "violations_per_pair": round(nviol / (2.0 * positives), 4),
+                "kernels": {n: {"avg_us": round(v["avg_us"], 3), "launches": v["launches"],
+                                "GB_s": round(v["achieved_gbs"], 1)}
+                            for n, v in prof["kernels"].items()},
+                "step_algorithmic_GB_s": round(prof["epoch_bytes"] / (elapsed / args.steps) / 1e9, 1),
+                "launches_per_step": runner.nlaunches,
+            },
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def kernel_profile(model, upd, kg, nb, d, st, runner):
+    """Launch one epoch eagerly with HIP events around every kernel (on the
+    stream the kernels run on) and count the algorithmic bytes of each launch
+    from the touched-row counts."""
+    import torch
+    from skge_amd import _lib as L
+    lib = L.lib()
+    dev = model.device
+    te = upd["E"].table(model.accumulator("E"))
+    tr = upd["R"].table(model.accumulator("R"))
+    tabs = (L.SkgeTable * 2)(te, tr)
+    nviol = torch.zeros(1, dtype=torch.int32, device=dev)
+    T = kg.T
+    bs = T // nb
+    sp = L.stream_ptr(st)
+    times = {"transe_sample_grad": [], "accum_apply": []}
+    bytes_ = {"transe_sample_grad": 0.0, "accum_apply": 0.0}
+    total = 0.0
+    accE, accR = model.accumulator("E"), model.accumulator("R")
+    with torch.cuda.stream(st):
+        for start in range(0, T, bs):
+            cnt = min(bs, T - start)
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            nviol.zero_()
+            e[0].record(st)
+            L.check(lib.skge_transe_sample_grad(sp, 1, te, tr, d, L.ptr(kg.trip), T, L.ptr(kg.slots),
+                                                kg.capacity, start, cnt, 777, L.ptr(runner.epoch_key),
+                                                2.0, 100, L.ptr(nviol), None, None))
+            e[1].record(st)
+            st.synchronize()
+            UE, UR, V = int(accE.ntouched.item()), int(accR.ntouched.item()), int(nviol.item())
+            e[2].record(st)
+            L.check(lib.skge_accum_apply(sp, tabs, 2, 4 * cnt))
+            e[3].record(st)
+            st.synchronize()
+            times["transe_sample_grad"].append(e[0].elapsed_time(e[1]) * 1e3)
+            times["accum_apply"].append(e[2].elapsed_time(e[3]) * 1e3)
+            P = 2 * cnt
+            # gathers of s, o, p + 2 corrupted rows, index/hash traffic, and the
+            # atomic row adds of the violating positives (<= 5 rows each)
+            b_sg = 4 * d * (3 * cnt + P) + 20 * cnt + 4 * d * min(5 * cnt, 2 * V + 3 * cnt)
+            b_ap = 24 * d * (UE + UR)     # read sum, param, state; write param, state, zero sum
+            bytes_["transe_sample_grad"] += b_sg
+            bytes_["accum_apply"] += b_ap
+            total += algorithmic_bytes(d, cnt, P, UE, UR)
+    kern = {}
+    for n in times:
+        t = np.array(times[n])
+        avg = float(t.mean())
+        bpl = bytes_[n] / len(t)
+        kern[n] = {"name": n, "avg_us": avg, "launches": len(t), "bytes_per_launch": bpl,
+                   "achieved_gbs": bpl / (avg * 1e-6) / 1e9}
+    dom = max(kern.values(), key=lambda v: v["avg_us"])
+    return {"kernels": kern, "dominant": dom, "epoch_bytes": total}
+
+
+if __name__ == "__main__":
+    main()

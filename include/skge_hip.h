@@ -1,0 +1,207 @@
+/*
+ * skge_hip.h -- C ABI of libskgehip.so, the MI355X (gfx950) HIP implementation
+ * of scikit-kge's mini-batch training hot path (score + gradient + update).
+ *
+ * The reference is pure Python/NumPy; its "FFI" for this path is the duck-typed
+ * model / updater / trainer protocol of skge.  Each
+ * entry point below replaces one piece of that protocol; the Python facade
+ * (scikit-kge_amd/skge_amd) binds them with ctypes and keeps the reference's
+ * class names, kwargs and return shapes.
+ *
+ * Conventions
+ *  - Ownership: the caller allocates every buffer (device memory, e.g. torch
+ *    tensors).  The library never frees caller memory.
+ *  - Async: every call is stream-ordered on the caller's hipStream_t (passed as
+ *    void*; NULL = the legacy default stream).  No call synchronises, allocates
+ *    or copies to the host, so sequences of calls can be captured in a hipGraph.
+ *  - Errors: int return, 0 = OK, <0 = error (SKGE_E*); the message of the
+ *    last failure on the calling thread is returned by skge_last_error().
+ *  - Triples are (s, o, p) int32 triplets, row-major [n][3]
+ *    (skge/base.py:511, skge/util.py:104-110).
+ *  - Parameters are fp32 row-major tables [rows][width]; width = d for E / R,
+ *    d*d for RESCAL's W.
+ *  - Accumulator invariant: between batches acc_sum == 0, acc_cnt == 0 and
+ *    *acc_ntouched == 0 for every table (zero them once at allocation).
+ */
+#ifndef SKGE_HIP_H
+#define SKGE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SKGE_ABI_VERSION 1
+
+enum {
+  SKGE_OK = 0,
+  SKGE_EINVAL = -1,   /* bad argument (shape, enum, null pointer) */
+  SKGE_EHIP = -2,     /* a HIP runtime call failed */
+  SKGE_ENOTSUP = -3   /* unsupported configuration (e.g. d > 1024) */
+};
+
+/* models (skge/transe.py, skge/hole.py, skge/rescal.py) */
+enum { SKGE_TRANSE_L1 = 0, SKGE_TRANSE_L2 = 1, SKGE_HOLE = 2, SKGE_RESCAL = 3 };
+/* activation functions (skge/actfun.py:13-57) */
+enum { SKGE_AF_LINEAR = 0, SKGE_AF_SIGMOID = 1, SKGE_AF_TANH = 2, SKGE_AF_RELU = 3 };
+/* updaters (skge/param.py:124-155) */
+enum { SKGE_SGD = 0, SKGE_ADAGRAD = 1 };
+/* post-update projections (skge/param.py:161-174) */
+enum { SKGE_POST_NONE = 0, SKGE_POST_NORMALIZE = 1, SKGE_POST_NORMLESS1 = 2 };
+
+/*
+ * One parameter table with its updater state and its segment-sum accumulator.
+ * The gradient of a touched row r is
+ *     g = (acc_sum[r] + rin * param[r]) / div + rout * param[r],
+ *     div = fixed_div > 0 ? fixed_div : acc_cnt[r]
+ * which covers every variant of the reference:
+ *   mean                 Sm.dot(G) / n                     (transe.py:136)
+ *   mean + rparam*P      hole.py:33,40,83  rescal.py:70,239
+ *   (sum + rparam*P)/n   rescal.py:299-302 (rparam inside)
+ *   (sum + rparam*W)/2   rescal.py:287-290 (divisor quirk)
+ */
+typedef struct skge_table {
+  float *param;        /* [rows][width] */
+  float *state;        /* AdaGrad accumulator p2 [rows][width]; NULL for SGD */
+  float *acc_sum;      /* [rows][width] */
+  int *acc_cnt;        /* [rows] */
+  int *acc_touched;    /* [rows] rows touched in the current batch */
+  int *acc_ntouched;   /* [1] */
+  int *sync;           /* [1] zeroed scratch word used by skge_accum_apply */
+  int rows;
+  int width;
+  int opt;             /* SKGE_SGD | SKGE_ADAGRAD */
+  int post;            /* SKGE_POST_* */
+  float lr;
+  float rin, rout, fixed_div;
+  const int *gate;     /* optional: if non-NULL and *gate == 0, the update is
+                          skipped (the model returned None: no violations) */
+} skge_table_t;
+
+int skge_abi_version(void);
+const char *skge_last_error(void);
+
+/*
+ * Pairwise scoring + contribution scatter for P explicit (positive, negative)
+ * pairs.  Replaces the numeric part of Model._pairwise_gradients:
+ *   TransE  skge/transe.py:48-165   (ent = E, rel = R)
+ *   HolE    skge/hole.py:44-100     (ent = E, rel = R; af applied to scores)
+ *   RESCAL  skge/rescal.py:78-139   (ent = E, rel = W; the dW part is
+ *                                    skge_rescal_wgrad, fed by `coef`)
+ * Writes the raw scores (pscore/nscore may be NULL), atomically adds the
+ * violation count to *nviol, and accumulates every violating pair's
+ * contribution rows into ent->acc_* / rel->acc_* (segment sum + counts).
+ * coef (RESCAL only, [2P]): gp for every pair, then gn for every pair.
+ */
+int skge_pair_grad(void *stream, int model, int af, const skge_table_t *ent,
+                   const skge_table_t *rel, int d, const int *pos, const int *neg, int P,
+                   float margin, float *pscore, float *nscore, float *coef, int *nviol);
+
+/*
+ * Logistic-loss scoring + contribution scatter for T labelled triples.
+ * Replaces HolE._gradients (skge/hole.py:22-42) and RESCAL._gradients
+ * (skge/rescal.py:37-76).  score may be NULL; *loss += sum logaddexp(0,-y*f);
+ * coef [T] receives fs = -y*sigmoid(-y*f) (used by skge_rescal_wgrad).
+ */
+int skge_triple_grad(void *stream, int model, const skge_table_t *ent, const skge_table_t *rel,
+                     int d, const int *trip, const float *ys, int T, float *score, float *coef,
+                     float *loss);
+
+/*
+ * RESCAL relation-matrix gradient: for every relation p appearing in lists
+ * a and b, acc_sum[p] = sum_i coef_i * outer(E[s_i], E[o_i]) and acc_cnt[p] =
+ * number of occurrences (skge/rescal.py:61-70 and 113-125).
+ */
+int skge_rescal_wgrad(void *stream, const skge_table_t *ent, const skge_table_t *rel, int d,
+                      const int *trip_a, const float *coef_a, int n_a, const int *trip_b,
+                      const float *coef_b, int n_b);
+
+/*
+ * Materialise the segment mean held in a table's accumulator as the
+ * reference's (grad_rows, sorted unique idx) pair (skge/util.py:53-101):
+ * idx_out [rows], g_out [rows][width], *U_out = number of touched rows.
+ * Resets the accumulator.  workspace: skge_collect_workspace_bytes(rows).
+ */
+size_t skge_collect_workspace_bytes(int rows);
+int skge_accum_collect(void *stream, const skge_table_t *t, int *idx_out, float *g_out,
+                       int *U_out, void *workspace, size_t ws_bytes);
+
+/* Reset a table's accumulator without producing gradients. */
+int skge_accum_reset(void *stream, const skge_table_t *t, int max_touched);
+
+/*
+ * Updater call: param[idx] -= ... for U explicit (row, gradient) pairs, then
+ * the projection.  Replaces ParameterUpdate.__call__ (skge/param.py:115-118)
+ * with SGD._update (param.py:129-130) or AdaGrad._update (param.py:140-155),
+ * then normalize / normless1 (param.py:161-174).  idx must be unique.
+ */
+int skge_update_rows(void *stream, const skge_table_t *t, const float *g, const int *idx, int U);
+
+/*
+ * Fused: segment mean + updater + projection straight from the accumulators
+ * of up to 4 tables (trainer._batch_step, skge/base.py:1306-1316), then reset
+ * of the accumulators.  max_touched bounds the touched rows of any table.
+ */
+int skge_accum_apply(void *stream, const skge_table_t *tables, int ntables, int max_touched);
+
+/* Explicit-pair training step: skge_pair_grad + (RESCAL wgrad) + apply. */
+int skge_pair_step(void *stream, int model, int af, const skge_table_t *ent,
+                   const skge_table_t *rel, int d, const int *pos, const int *neg, int P,
+                   float margin, float *coef_ws, int *nviol);
+
+/* ---------------- device-resident batch loop (throughput path) ---------------- */
+
+/*
+ * Build the open-addressing set of training triples used by the negative
+ * sampler's rejection test (skge/sample.py:41-44).  slots: capacity int4
+ * entries (power of two >= 2*T), zeroed by this call.
+ */
+int skge_triple_set_build(void *stream, const int *trip, int64_t T, void *slots,
+                          int64_t capacity);
+
+/*
+ * One PairwiseStochasticTrainer mini-batch of TransE, fully on device
+ * (skge/base.py:1268-1284 + 1394-1427 with RandomModeSampler(1, [0, 1])):
+ * positive j of the batch is triple perm_epoch(start + j) (a keyed bijection
+ * of [0, T), keyed by *epoch_key so that a captured graph reshuffles per
+ * epoch); for each positive, mode 0 corrupts s and mode 1 corrupts o with up
+ * to ntries rejection draws against the triple set; both pairs are scored,
+ * margin-tested and their contributions accumulated.  nviol_total (optional)
+ * accumulates over batches; neg_out (optional, [count][2]) records the sampled
+ * corrupted entity per mode (-1 = skipped).
+ */
+int skge_transe_sample_grad(void *stream, int l1, const skge_table_t *ent,
+                            const skge_table_t *rel, int d, const int *trip, int64_t T,
+                            const void *set_slots, int64_t set_capacity, int64_t start, int count,
+                            uint64_t seed, const uint64_t *epoch_key, float margin, int ntries,
+                            int *nviol, int *nviol_total, int *neg_out);
+
+/* perm_out[j] = perm_epoch(j) for j < n (tests / host-side replay). */
+int skge_epoch_permutation(void *stream, int64_t T, uint64_t seed, const uint64_t *epoch_key,
+                           int64_t *perm_out, int64_t n);
+
+/* *epoch_key += 1 (one-thread kernel, so a captured epoch graph advances it). */
+int skge_epoch_advance(void *stream, uint64_t *epoch_key);
+
+/*
+ * Native epoch runner: captures one epoch of the device batch loop
+ * (nbatches sample_grad + apply launches + epoch_advance; the reference's
+ * np.split geometry, skge/base.py:1246-1268) into a hipGraph once, then
+ * replays it.  Returns an opaque handle (NULL on error).
+ */
+typedef struct skge_runner skge_runner_t;
+skge_runner_t *skge_runner_create(void *stream, int l1, const skge_table_t *ent,
+                                  const skge_table_t *rel, int d, const int *trip, int64_t T,
+                                  const void *set_slots, int64_t set_capacity, int nbatches,
+                                  uint64_t seed, uint64_t *epoch_key, float margin, int ntries,
+                                  int *nviol, int *nviol_total);
+int skge_runner_run(skge_runner_t *r, void *stream, int nepochs);
+int skge_runner_nlaunches(const skge_runner_t *r);
+void skge_runner_destroy(skge_runner_t *r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SKGE_HIP_H */

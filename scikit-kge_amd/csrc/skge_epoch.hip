@@ -1,0 +1,417 @@
+// Device-resident mini-batch loop for TransE (the throughput path):
+//   PairwiseStochasticTrainer._optim / _process_batch (skge/base.py:1242-1291,
+//   1394-1427) with RandomModeSampler(1, [0, 1]) (skge/sample.py:28-46).
+//
+// Differences from the host loop are statistical only: the epoch shuffle is
+// a keyed pseudo-random bijection of [0, T) instead of numpy's MT19937
+// shuffle, and the sampler draws come from a counter-based generator.  The
+// arithmetic per pair is the same as skge_pair_grad's (parity-tested by
+// replaying the recorded negatives through the oracle).
+#include <vector>
+
+#include "skge_host.h"
+
+namespace skge {
+
+// ---- keyed permutation of [0, T): 4-round Feistel + cycle walking ----
+struct Perm {
+  uint64_t T;
+  int half;
+  uint64_t key;
+};
+
+__device__ __host__ __forceinline__ uint64_t feistel(uint64_t x, int half, uint64_t key) {
+  const uint64_t mask = (1ull << half) - 1;
+  uint64_t L = x >> half, R = x & mask;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint64_t F = mix64(R ^ (key + 0x632BE59BD9B4E019ull * (uint64_t)(r + 1))) & mask;
+    const uint64_t nL = R;
+    R = L ^ F;
+    L = nL;
+  }
+  return (L << half) | R;
+}
+
+__device__ __host__ __forceinline__ uint64_t perm_index(uint64_t j, const Perm& pm) {
+  uint64_t x = j;
+  do {
+    x = feistel(x, pm.half, pm.key);
+  } while (x >= pm.T);
+  return x;
+}
+
+static int perm_half(int64_t T) {
+  int bits = 1;
+  while ((1ll << bits) < T) ++bits;
+  return (bits + 1) / 2;
+}
+
+__device__ __forceinline__ uint64_t epoch_perm_key(uint64_t seed, uint64_t ek) {
+  return mix64(seed ^ mix64(ek * 0xD6E8FEB86659FD93ull + 1));
+}
+
+__device__ __forceinline__ uint64_t epoch_sample_key(uint64_t seed, uint64_t ek) {
+  return mix64(mix64(seed + 0xA0761D6478BD642Full) ^ (ek * 0xE7037ED1A0B428DBull));
+}
+
+// ---- triple set build: claim a slot by CAS on the tag, then fill it ----
+__global__ void k_set_build(const int* __restrict__ trip, long long T, int4* slots,
+                            unsigned long long mask) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < T;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int s = trip[3 * i], o = trip[3 * i + 1], p = trip[3 * i + 2];
+    uint64_t h = triple_hash(s, o, p) & mask;
+    for (uint64_t probe = 0; probe <= mask; ++probe) {
+      if (atomicCAS(&slots[h].w, 0, 1) == 0) {
+        slots[h].x = s;
+        slots[h].y = o;
+        slots[h].z = p;
+        break;
+      }
+      h = (h + 1) & mask;
+    }
+  }
+}
+
+struct SampleArgs {
+  const float* E;
+  const float* R;
+  Accum accE, accR;
+  const int* trip;
+  long long T;
+  TripleSet set;
+  long long start;
+  int count, d, n_ent, ntries, half;
+  uint64_t seed;
+  const uint64_t* epoch_key;
+  float margin;
+  int* nviol;
+  int* nviol_total;
+  int* neg_out;
+};
+
+// RandomModeSampler._sample for both modes at once: lanes 0-3 draw tries of
+// mode 0 (corrupt s), lanes 4-7 tries of mode 1 (corrupt o); the first
+// accepted try of each mode wins, as in the sequential loop (sample.py:41-46).
+__device__ __forceinline__ void sample_negatives(const SampleArgs& a, uint64_t skey, long long j,
+                                                 int s, int o, int p, int& neg0, int& neg1) {
+  const int l = lane_id();
+  neg0 = -1;
+  neg1 = -1;
+  const uint64_t base = mix64(skey ^ ((uint64_t)j * 0x9E3779B97F4A7C15ull));
+  for (int round = 0; round * 4 < a.ntries; ++round) {
+    const int mode = (l >> 2) & 1;
+    const int tr = round * 4 + (l & 3);
+    const bool want = mode == 0 ? neg0 < 0 : neg1 < 0;
+    const bool active = l < 8 && tr < a.ntries && want;
+    int c = 0;
+    bool ok = false;
+    if (active) {
+      c = rand_below(mix64(base + (uint64_t)(mode * 4096 + tr)), a.n_ent);
+      ok = mode == 0 ? !set_contains(a.set, c, o, p) : !set_contains(a.set, s, c, p);
+    }
+    const uint64_t m0 = __ballot(active && ok && mode == 0);
+    const uint64_t m1 = __ballot(active && ok && mode == 1);
+    if (m0) neg0 = __shfl(c, __ffsll((unsigned long long)m0) - 1, 64);
+    if (m1) neg1 = __shfl(c, __ffsll((unsigned long long)m1) - 1, 64);
+    if (neg0 >= 0 && neg1 >= 0) break;
+  }
+}
+
+template <int KM, bool L1>
+__global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
+  const int wpb = blockDim.x >> 6;
+  const int l = lane_id();
+  const int d = a.d;
+  const uint64_t ek = *a.epoch_key;
+  const Perm pm = {(uint64_t)a.T, a.half, epoch_perm_key(a.seed, ek)};
+  const uint64_t skey = epoch_sample_key(a.seed, ek);
+  int nv = 0;
+  for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < a.count; w += gridDim.x * wpb) {
+    const long long j = a.start + w;
+    const long long t = (long long)perm_index((uint64_t)j, pm);
+    const int s = __builtin_amdgcn_readfirstlane(a.trip[3 * t]);
+    const int o = __builtin_amdgcn_readfirstlane(a.trip[3 * t + 1]);
+    const int p = __builtin_amdgcn_readfirstlane(a.trip[3 * t + 2]);
+    float es[KM], eo[KM], rp[KM];
+    load_row<KM>(a.E, s, d, es);
+    load_row<KM>(a.E, o, d, eo);
+    load_row<KM>(a.R, p, d, rp);
+    int neg0, neg1;
+    sample_negatives(a, skey, j, s, o, p, neg0, neg1);
+    neg0 = __builtin_amdgcn_readfirstlane(neg0);
+    neg1 = __builtin_amdgcn_readfirstlane(neg1);
+    float fs[KM], fo[KM];
+    load_row<KM>(a.E, neg0 >= 0 ? neg0 : s, d, fs);
+    load_row<KM>(a.E, neg1 >= 0 ? neg1 : o, d, fo);
+    float ps = 0.0f, n0 = 0.0f, n1 = 0.0f, gp[KM], g0[KM], g1[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const float vp = (es[k] + rp[k]) - eo[k];
+      const float v0 = (fs[k] + rp[k]) - eo[k];  // pair 0: (s', o, p)
+      const float v1 = (es[k] + rp[k]) - fo[k];  // pair 1: (s, o', p)
+      ps += L1 ? fabsf(vp) : vp * vp;
+      n0 += L1 ? fabsf(v0) : v0 * v0;
+      n1 += L1 ? fabsf(v1) : v1 * v1;
+      const float tp = (eo[k] - rp[k]) - es[k];  // transe.py:103
+      const float t0 = (eo[k] - rp[k]) - fs[k];  // transe.py:104 for pair 0
+      const float t1 = (fo[k] - rp[k]) - es[k];  // ... for pair 1
+      gp[k] = L1 ? signf_np(-tp) : -tp;
+      g0[k] = L1 ? signf_np(t0) : t0;
+      g1[k] = L1 ? signf_np(t1) : t1;
+    }
+    const float pscore = -wave_sum(ps);
+    const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
+    const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;
+    const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
+    if (a.neg_out && l == 0) {
+      a.neg_out[2 * (long long)w] = neg0;
+      a.neg_out[2 * (long long)w + 1] = neg1;
+    }
+    if (v0 + v1 == 0) continue;
+    nv += v0 + v1;
+    const float fv0 = (float)v0, fv1 = (float)v1;
+    float cs[KM], co[KM], c0[KM], c1[KM], cr[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      // pair 0 rows (sp,op,sn,on) = (s,o,s',o): (+gp,-gp,+g0,-g0)
+      // pair 1 rows (sp,op,sn,on) = (s,o,s,o'): (+gp,-gp,+g1,-g1)
+      cs[k] = fv0 * gp[k] + fv1 * (gp[k] + g1[k]);
+      co[k] = -(fv0 * (gp[k] + g0[k]) + fv1 * gp[k]);
+      c0[k] = g0[k];
+      c1[k] = -g1[k];
+      cr[k] = fv0 * (gp[k] + g0[k]) + fv1 * (gp[k] + g1[k]);
+    }
+    acc_row<KM>(a.accE, s, cs, d);
+    acc_row<KM>(a.accE, o, co, d);
+    if (v0) acc_row<KM>(a.accE, neg0, c0, d);
+    if (v1) acc_row<KM>(a.accE, neg1, c1, d);
+    acc_row<KM>(a.accR, p, cr, d);
+    if (l == 0) {
+      acc_count(a.accE, s, v0 + 2 * v1);
+      acc_count(a.accE, o, 2 * v0 + v1);
+      if (v0) acc_count(a.accE, neg0, 1);
+      if (v1) acc_count(a.accE, neg1, 1);
+      acc_count(a.accR, p, 2 * (v0 + v1));
+    }
+  }
+  if (l == 0 && nv) {
+    if (a.nviol) atomicAdd(a.nviol, nv);
+    if (a.nviol_total) atomicAdd(a.nviol_total, nv);
+  }
+}
+
+__global__ void k_perm(long long T, int half, uint64_t seed, const uint64_t* ekp, long long* out,
+                       long long n) {
+  const Perm pm = {(uint64_t)T, half, epoch_perm_key(seed, *ekp)};
+  for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += (long long)gridDim.x * blockDim.x)
+    out[j] = (long long)perm_index((uint64_t)j, pm);
+}
+
+__global__ void k_advance(uint64_t* ek) { *ek += 1; }
+
+static int launch_sample(const SampleArgs& a, bool l1, hipStream_t st) {
+  const int km = km_for(a.d);
+  int blocks = (a.count + 3) / 4;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 16384) blocks = 16384;
+#define SKGE_SG(K)                                                                               \
+  case K:                                                                                        \
+    if (l1)                                                                                      \
+      hipLaunchKernelGGL((k_transe_sample_grad<K, true>), dim3(blocks), dim3(256), 0, st, a);   \
+    else                                                                                         \
+      hipLaunchKernelGGL((k_transe_sample_grad<K, false>), dim3(blocks), dim3(256), 0, st, a);  \
+    break;
+  switch (km) {
+    SKGE_SG(1)
+    SKGE_SG(2)
+    SKGE_SG(3)
+    SKGE_SG(4)
+    SKGE_SG(8)
+    SKGE_SG(16)
+    default:
+      set_error("d=%d unsupported", a.d);
+      return SKGE_ENOTSUP;
+  }
+#undef SKGE_SG
+  SKGE_CHECK_LAUNCH("transe sample grad");
+  return SKGE_OK;
+}
+
+}  // namespace skge
+
+using namespace skge;
+
+extern "C" int skge_triple_set_build(void* stream, const int* trip, int64_t T, void* slots,
+                                     int64_t capacity) {
+  SKGE_CHECK_ARG(trip && slots, "NULL argument");
+  SKGE_CHECK_ARG(capacity > 0 && (capacity & (capacity - 1)) == 0, "capacity must be a power of 2");
+  SKGE_CHECK_ARG(capacity >= 2 * T, "capacity must be >= 2*T");
+  hipStream_t st = as_stream(stream);
+  SKGE_CHECK_HIP(hipMemsetAsync(slots, 0, (size_t)capacity * sizeof(int4), st));
+  if (T == 0) return SKGE_OK;
+  long long blocks = (T + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_set_build, dim3((unsigned)blocks), dim3(256), 0, st, trip, (long long)T,
+                     (int4*)slots, (unsigned long long)(capacity - 1));
+  SKGE_CHECK_LAUNCH("triple set build");
+  return SKGE_OK;
+}
+
+static int fill_sample_args(SampleArgs& a, int l1, const skge_table_t* ent, const skge_table_t* rel,
+                            int d, const int* trip, int64_t T, const void* set_slots,
+                            int64_t set_capacity, uint64_t seed, const uint64_t* epoch_key,
+                            float margin, int ntries, int* nviol, int* nviol_total) {
+  int rc;
+  if ((rc = check_table(ent, "ent", true))) return rc;
+  if ((rc = check_table(rel, "rel", true))) return rc;
+  SKGE_CHECK_ARG(ent->width == d && rel->width == d, "table widths must equal d");
+  SKGE_CHECK_ARG(km_for(d) != 0, "d=%d unsupported", d);
+  SKGE_CHECK_ARG(trip && set_slots && epoch_key, "NULL argument");
+  SKGE_CHECK_ARG(T > 0, "T must be > 0");
+  SKGE_CHECK_ARG(set_capacity > 0 && (set_capacity & (set_capacity - 1)) == 0, "bad set capacity");
+  SKGE_CHECK_ARG(ntries >= 1, "ntries >= 1");
+  a = SampleArgs{};
+  a.E = ent->param;
+  a.R = rel->param;
+  a.accE = accum_of(ent);
+  a.accR = accum_of(rel);
+  a.trip = trip;
+  a.T = T;
+  a.set.slots = (int4*)set_slots;
+  a.set.mask = (uint64_t)(set_capacity - 1);
+  a.d = d;
+  a.n_ent = ent->rows;
+  a.ntries = ntries;
+  a.half = perm_half(T);
+  a.seed = seed;
+  a.epoch_key = epoch_key;
+  a.margin = margin;
+  a.nviol = nviol;
+  a.nviol_total = nviol_total;
+  (void)l1;
+  return SKGE_OK;
+}
+
+extern "C" int skge_transe_sample_grad(void* stream, int l1, const skge_table_t* ent,
+                                       const skge_table_t* rel, int d, const int* trip, int64_t T,
+                                       const void* set_slots, int64_t set_capacity, int64_t start,
+                                       int count, uint64_t seed, const uint64_t* epoch_key,
+                                       float margin, int ntries, int* nviol, int* nviol_total,
+                                       int* neg_out) {
+  SampleArgs a;
+  int rc = fill_sample_args(a, l1, ent, rel, d, trip, T, set_slots, set_capacity, seed, epoch_key,
+                            margin, ntries, nviol, nviol_total);
+  if (rc) return rc;
+  SKGE_CHECK_ARG(start >= 0 && count >= 0 && start + count <= T, "batch out of range");
+  if (count == 0) return SKGE_OK;
+  a.start = start;
+  a.count = count;
+  a.neg_out = neg_out;
+  return launch_sample(a, l1 != 0, as_stream(stream));
+}
+
+extern "C" int skge_epoch_permutation(void* stream, int64_t T, uint64_t seed,
+                                      const uint64_t* epoch_key, int64_t* perm_out, int64_t n) {
+  SKGE_CHECK_ARG(T > 0 && n >= 0 && n <= T && perm_out && epoch_key, "bad arguments");
+  if (n == 0) return SKGE_OK;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_perm, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), (long long)T,
+                     perm_half(T), seed, epoch_key, (long long*)perm_out, (long long)n);
+  SKGE_CHECK_LAUNCH("epoch permutation");
+  return SKGE_OK;
+}
+
+extern "C" int skge_epoch_advance(void* stream, uint64_t* epoch_key) {
+  SKGE_CHECK_ARG(epoch_key, "NULL epoch key");
+  hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, as_stream(stream), epoch_key);
+  SKGE_CHECK_LAUNCH("epoch advance");
+  return SKGE_OK;
+}
+
+// ---- native epoch runner: one hipGraph per epoch ----
+struct skge_runner {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  int nlaunch = 0;
+};
+
+extern "C" skge_runner_t* skge_runner_create(void* stream, int l1, const skge_table_t* ent,
+                                             const skge_table_t* rel, int d, const int* trip,
+                                             int64_t T, const void* set_slots,
+                                             int64_t set_capacity, int nbatches, uint64_t seed,
+                                             uint64_t* epoch_key, float margin, int ntries,
+                                             int* nviol, int* nviol_total) {
+  SampleArgs a;
+  if (fill_sample_args(a, l1, ent, rel, d, trip, T, set_slots, set_capacity, seed, epoch_key,
+                       margin, ntries, nviol, nviol_total))
+    return nullptr;
+  if (nbatches < 1 || nbatches > T) {
+    set_error("nbatches must be in [1, T]");
+    return nullptr;
+  }
+  if (stream == nullptr) {
+    set_error("runner needs a non-default stream (graph capture)");
+    return nullptr;
+  }
+  hipStream_t st = as_stream(stream);
+  // batch geometry of StochasticTrainer._optim (skge/base.py:1246-1268)
+  const int64_t bs = T / nbatches;
+  std::vector<std::pair<int64_t, int64_t>> batches;
+  for (int64_t s0 = 0; s0 < T; s0 += bs) batches.push_back({s0, (s0 + bs <= T) ? bs : T - s0});
+  skge_runner_t* r = new skge_runner_t();
+  skge_table_t tabs[2] = {*ent, *rel};
+  if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    set_error("hipStreamBeginCapture failed");
+    delete r;
+    return nullptr;
+  }
+  int rc = SKGE_OK;
+  for (auto& b : batches) {
+    a.start = b.first;
+    a.count = (int)b.second;
+    a.neg_out = nullptr;
+    if ((rc = launch_sample(a, l1 != 0, st))) break;
+    if ((rc = skge_accum_apply(stream, tabs, 2, (int)(4 * b.second)))) break;
+    r->nlaunch += 2;
+  }
+  if (!rc) {
+    hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, st, epoch_key);
+    r->nlaunch += 1;
+  }
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(st, &g);
+  if (rc || e != hipSuccess) {
+    if (!rc) set_error("hipStreamEndCapture: %s", hipGetErrorString(e));
+    if (g) (void)hipGraphDestroy(g);
+    delete r;
+    return nullptr;
+  }
+  r->graph = g;
+  e = hipGraphInstantiate(&r->exec, g, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    set_error("hipGraphInstantiate: %s", hipGetErrorString(e));
+    (void)hipGraphDestroy(g);
+    delete r;
+    return nullptr;
+  }
+  return r;
+}
+
+extern "C" int skge_runner_run(skge_runner_t* r, void* stream, int nepochs) {
+  SKGE_CHECK_ARG(r && r->exec, "bad runner");
+  for (int i = 0; i < nepochs; ++i) SKGE_CHECK_HIP(hipGraphLaunch(r->exec, as_stream(stream)));
+  return SKGE_OK;
+}
+
+extern "C" int skge_runner_nlaunches(const skge_runner_t* r) { return r ? r->nlaunch : -1; }
+
+extern "C" void skge_runner_destroy(skge_runner_t* r) {
+  if (!r) return;
+  if (r->exec) (void)hipGraphExecDestroy(r->exec);
+  if (r->graph) (void)hipGraphDestroy(r->graph);
+  delete r;
+}

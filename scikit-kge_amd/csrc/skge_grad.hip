@@ -1,0 +1,657 @@
+// Scoring + contribution-scatter kernels for explicit pairs / labelled triples.
+//
+// One wavefront per pair (or triple).  A row of width d lives lane-strided in
+// KM = ceil(d/64) registers per lane (skge_device.h), so every gather and
+// every float atomic of a row is a sequence of 256-byte contiguous
+// wave-instructions.  Contributions are summed into the per-table segment
+// accumulator (Accum): the device form of grad_sum_matrix + Sm.dot(G)
+// (skge/util.py:53-101).  The division by the occurrence count (the mean)
+// happens later, in skge_accum_apply / skge_accum_collect.
+#include <stdarg.h>
+
+#include "skge_host.h"
+
+namespace skge {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+struct PairArgs {
+  const float* E;
+  const float* R;  // relation table [M][d] (TransE, HolE) or W [M][d][d] (RESCAL)
+  Accum accE, accR;
+  const int* pos;
+  const int* neg;
+  const float* ys;  // logistic only
+  int P, d, af;
+  float margin;
+  float* pscore;
+  float* nscore;
+  float* coef;
+  int* nviol;
+  float* loss;
+};
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <int KM>
+__device__ __forceinline__ void to_lds(float* s, const float (&v)[KM], int d) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k;
+    if (e < d) s[e] = v[k];
+  }
+}
+
+// c_k = sum_j a_j b_{(j+k) mod d}      (ccorr, skge/util.py:30-50)
+template <int KM>
+__device__ void ccorr_lds(const float* sa, const float* sb, int d, float (&out)[KM]) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) out[k] = 0.0f;
+  for (int j = 0; j < d; ++j) {
+    const float aj = sa[j];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int kk = l + 64 * k;
+      int ix = j + kk;
+      ix = ix >= d ? ix - d : ix;
+      ix = kk < d ? ix : 0;
+      out[k] = fmaf(aj, sb[ix], out[k]);
+    }
+  }
+}
+
+// c_k = sum_j a_j b_{(k-j) mod d}      (cconv, skge/util.py:8-27)
+template <int KM>
+__device__ void cconv_lds(const float* sa, const float* sb, int d, float (&out)[KM]) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) out[k] = 0.0f;
+  for (int j = 0; j < d; ++j) {
+    const float aj = sa[j];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int kk = l + 64 * k;
+      int ix = kk - j;
+      ix = ix < 0 ? ix + d : ix;
+      ix = kk < d ? ix : 0;
+      out[k] = fmaf(aj, sb[ix], out[k]);
+    }
+  }
+}
+
+// out_i = sum_j W[i][j] x_j   (W[p] . E[o], skge/rescal.py:212)
+template <int KM>
+__device__ void gemv_rows(const float* __restrict__ Wp, const float* sx, int d, float (&out)[KM]) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int i = l + 64 * k;
+    float acc = 0.0f;
+    if (i < d) {
+      const float* row = Wp + (size_t)i * d;
+      for (int j = 0; j < d; ++j) acc = fmaf(row[j], sx[j], acc);
+    }
+    out[k] = acc;
+  }
+}
+
+// out_j = sum_i x_i W[i][j]   (E[s] . W[p], skge/rescal.py:209)
+template <int KM>
+__device__ void gemv_cols(const float* __restrict__ Wp, const float* sx, int d, float (&out)[KM]) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) out[k] = 0.0f;
+  for (int i = 0; i < d; ++i) {
+    const float xi = sx[i];
+    const float* row = Wp + (size_t)i * d;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int j = l + 64 * k;
+      if (j < d) out[k] = fmaf(xi, row[j], out[k]);
+    }
+  }
+}
+
+template <int KM>
+__device__ __forceinline__ void scale(float (&o)[KM], const float (&v)[KM], float c) {
+#pragma unroll
+  for (int k = 0; k < KM; ++k) o[k] = c * v[k];
+}
+
+// add rows x (coefficient already applied) at a and y at b, merging when a == b
+template <int KM>
+__device__ __forceinline__ void acc_two(const Accum& acc, int a, const float (&x)[KM], int b,
+                                        const float (&y)[KM], int d) {
+  if (a == b) {
+    float t[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) t[k] = x[k] + y[k];
+    acc_row<KM>(acc, a, t, d);
+    if (lane_id() == 0) acc_count(acc, a, 2);
+  } else {
+    acc_row<KM>(acc, a, x, d);
+    acc_row<KM>(acc, b, y, d);
+    if (lane_id() == 0) {
+      acc_count(acc, a, 1);
+      acc_count(acc, b, 1);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// TransE pair: skge/transe.py:48-165
+// ---------------------------------------------------------------------------
+template <int KM, bool L1>
+__device__ bool transe_pair(const PairArgs& a, int i) {
+  const int d = a.d;
+  const int sp = uni(a.pos[3 * i]), op = uni(a.pos[3 * i + 1]), pp = uni(a.pos[3 * i + 2]);
+  const int sn = uni(a.neg[3 * i]), on = uni(a.neg[3 * i + 1]), pn = uni(a.neg[3 * i + 2]);
+  float es[KM], eo[KM], rp[KM], fs[KM], fo[KM], rn[KM];
+  load_row<KM>(a.E, sp, d, es);
+  load_row<KM>(a.R, pp, d, rp);
+  load_row<KM>(a.E, op, d, eo);
+  load_row<KM>(a.E, sn, d, fs);
+  load_row<KM>(a.R, pn, d, rn);
+  load_row<KM>(a.E, on, d, fo);
+  float ps = 0.0f, ns = 0.0f, gp[KM], gn[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const float vp = (es[k] + rp[k]) - eo[k];  // score: E[s] + R[p] - E[o]  (transe.py:32)
+    const float vn = (fs[k] + rn[k]) - fo[k];
+    ps += L1 ? fabsf(vp) : vp * vp;
+    ns += L1 ? fabsf(vn) : vn * vn;
+    const float tp = (eo[k] - rp[k]) - es[k];  // pg = E[op] - R[pp] - E[sp]  (transe.py:103)
+    const float tn = (fo[k] - rn[k]) - fs[k];  // ng = E[on] - R[pn] - E[sn]
+    gp[k] = L1 ? signf_np(-tp) : -tp;          // transe.py:115 / 120
+    gn[k] = L1 ? signf_np(tn) : tn;            // transe.py:117 / 121
+  }
+  const float pscore = -wave_sum(ps);
+  const float nscore = -wave_sum(ns);
+  if (lane_id() == 0) {
+    if (a.pscore) a.pscore[i] = pscore;
+    if (a.nscore) a.nscore[i] = nscore;
+  }
+  const bool viol = nscore + a.margin > pscore;  // strict >  (transe.py:73)
+  if (!viol) return false;
+  float ngp[KM], ngn[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    ngp[k] = -gp[k];
+    ngn[k] = -gn[k];
+  }
+  // entity rows (sp, op, sn, on) -> (+gp, -gp, +gn, -gn)   (transe.py:128-136)
+  acc_two<KM>(a.accE, sp, gp, sn, gn, d);
+  acc_two<KM>(a.accE, op, ngp, on, ngn, d);
+  // relation rows (pp, pn) -> (gp, gn)                      (transe.py:158-160)
+  acc_two<KM>(a.accR, pp, gp, pn, gn, d);
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// HolE pair: skge/hole.py:44-100
+// ---------------------------------------------------------------------------
+template <int KM>
+__device__ bool hole_pair(const PairArgs& a, int i, float* sw) {
+  const int d = a.d;
+  const int sp = uni(a.pos[3 * i]), op = uni(a.pos[3 * i + 1]), pp = uni(a.pos[3 * i + 2]);
+  const int sn = uni(a.neg[3 * i]), on = uni(a.neg[3 * i + 1]), pn = uni(a.neg[3 * i + 2]);
+  const int stride = 64 * KM;
+  float* sEs = sw;
+  float* sEo = sw + stride;
+  float* sRp = sw + 2 * stride;
+  float* sFs = sw + 3 * stride;
+  float* sFo = sw + 4 * stride;
+  float* sRn = sw + 5 * stride;
+  float v[KM], rp[KM], rn[KM];
+  load_row<KM>(a.E, sp, d, v);
+  to_lds<KM>(sEs, v, d);
+  load_row<KM>(a.E, op, d, v);
+  to_lds<KM>(sEo, v, d);
+  load_row<KM>(a.R, pp, d, rp);
+  to_lds<KM>(sRp, rp, d);
+  load_row<KM>(a.E, sn, d, v);
+  to_lds<KM>(sFs, v, d);
+  load_row<KM>(a.E, on, d, v);
+  to_lds<KM>(sFo, v, d);
+  load_row<KM>(a.R, pn, d, rn);
+  to_lds<KM>(sRn, rn, d);
+  __builtin_amdgcn_wave_barrier();
+  float cp[KM], cn[KM];
+  ccorr_lds<KM>(sEs, sEo, d, cp);  // ccorr(E[s], E[o])   (hole.py:20)
+  ccorr_lds<KM>(sFs, sFo, d, cn);
+  float ps = 0.0f, ns = 0.0f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    ps += rp[k] * cp[k];
+    ns += rn[k] * cn[k];
+  }
+  const float praw = wave_sum(ps), nraw = wave_sum(ns);
+  if (lane_id() == 0) {
+    if (a.pscore) a.pscore[i] = praw;
+    if (a.nscore) a.nscore[i] = nraw;
+  }
+  const float pf = af_f(a.af, praw), nf = af_f(a.af, nraw);
+  const bool viol = nf + a.margin > pf;  // hole.py:56
+  if (!viol) {
+    __builtin_amdgcn_wave_barrier();
+    return false;
+  }
+  const float gp = -af_g_given_f(a.af, pf);  // hole.py:66
+  const float gn = af_g_given_f(a.af, nf);   // hole.py:67
+  float x[KM], y[KM], t[KM];
+  // relation rows (pp, pn): (gp ccorr(E[sp],E[op]), gn ccorr(E[sn],E[on]))  hole.py:76-82
+  scale<KM>(x, cp, gp);
+  scale<KM>(y, cn, gn);
+  acc_two<KM>(a.accR, pp, x, pn, y, d);
+  // entity rows (sp, sn): gp ccorr(R[pp],E[op]), gn ccorr(R[pn],E[on])   hole.py:93-94
+  ccorr_lds<KM>(sRp, sEo, d, t);
+  scale<KM>(x, t, gp);
+  ccorr_lds<KM>(sRn, sFo, d, t);
+  scale<KM>(y, t, gn);
+  acc_two<KM>(a.accE, sp, x, sn, y, d);
+  // entity rows (op, on): gp cconv(E[sp],R[pp]), gn cconv(E[sn],R[pn])    hole.py:95-96
+  cconv_lds<KM>(sEs, sRp, d, t);
+  scale<KM>(x, t, gp);
+  cconv_lds<KM>(sFs, sRn, d, t);
+  scale<KM>(y, t, gn);
+  acc_two<KM>(a.accE, op, x, on, y, d);
+  __builtin_amdgcn_wave_barrier();
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// RESCAL pair: skge/rescal.py:78-139 (entity part; dW in k_rescal_wgrad)
+// ---------------------------------------------------------------------------
+template <int KM>
+__device__ bool rescal_pair(const PairArgs& a, int i, float* sw) {
+  const int d = a.d;
+  const int sp = uni(a.pos[3 * i]), op = uni(a.pos[3 * i + 1]), pp = uni(a.pos[3 * i + 2]);
+  const int sn = uni(a.neg[3 * i]), on = uni(a.neg[3 * i + 1]), pn = uni(a.neg[3 * i + 2]);
+  const int stride = 64 * KM;
+  float* sEs = sw;
+  float* sEo = sw + stride;
+  float* sFs = sw + 2 * stride;
+  float* sFo = sw + 3 * stride;
+  float es[KM], fs[KM], v[KM];
+  load_row<KM>(a.E, sp, d, es);
+  to_lds<KM>(sEs, es, d);
+  load_row<KM>(a.E, op, d, v);
+  to_lds<KM>(sEo, v, d);
+  load_row<KM>(a.E, sn, d, fs);
+  to_lds<KM>(sFs, fs, d);
+  load_row<KM>(a.E, on, d, v);
+  to_lds<KM>(sFo, v, d);
+  __builtin_amdgcn_wave_barrier();
+  const size_t dd = (size_t)d * d;
+  float wep[KM], wen[KM];
+  gemv_rows<KM>(a.R + pp * dd, sEo, d, wep);  // WEp = W[pp] E[op]   (rescal.py:261)
+  gemv_rows<KM>(a.R + pn * dd, sFo, d, wen);
+  float ps = 0.0f, ns = 0.0f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    ps += es[k] * wep[k];
+    ns += fs[k] * wen[k];
+  }
+  const float praw = wave_sum(ps), nraw = wave_sum(ns);
+  const float pf = af_f(a.af, praw), nf = af_f(a.af, nraw);
+  const float gp = -af_g_given_f(a.af, pf);  // rescal.py:275 (all pairs)
+  const float gn = af_g_given_f(a.af, nf);
+  if (lane_id() == 0) {
+    if (a.pscore) a.pscore[i] = praw;
+    if (a.nscore) a.nscore[i] = nraw;
+    if (a.coef) {
+      a.coef[i] = gp;
+      a.coef[a.P + i] = gn;
+    }
+  }
+  const bool viol = nf + a.margin > pf;  // rescal.py:269
+  if (!viol) {
+    __builtin_amdgcn_wave_barrier();
+    return false;
+  }
+  float x[KM], y[KM], t[KM];
+  // (sp, sn) <- (gp WEp, gn WEn)                    rescal.py:299-300
+  scale<KM>(x, wep, gp);
+  scale<KM>(y, wen, gn);
+  acc_two<KM>(a.accE, sp, x, sn, y, d);
+  // (op, on) <- (gp EWp, gn EWn), EW = E[s] W[p]     rescal.py:296-301
+  gemv_cols<KM>(a.R + pp * dd, sEs, d, t);
+  scale<KM>(x, t, gp);
+  gemv_cols<KM>(a.R + pn * dd, sFs, d, t);
+  scale<KM>(y, t, gn);
+  acc_two<KM>(a.accE, op, x, on, y, d);
+  __builtin_amdgcn_wave_barrier();
+  return true;
+}
+
+template <int MODEL, int KM>
+__global__ __launch_bounds__(256) void k_pair_grad(PairArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wave = threadIdx.x >> 6;
+  const int wpb = blockDim.x >> 6;
+  float* sw = smem + wave * 6 * 64 * KM;
+  int nv = 0;
+  for (int i = blockIdx.x * wpb + wave; i < a.P; i += gridDim.x * wpb) {
+    bool v;
+    if (MODEL == TRANSE_L1)
+      v = transe_pair<KM, true>(a, i);
+    else if (MODEL == TRANSE_L2)
+      v = transe_pair<KM, false>(a, i);
+    else if (MODEL == HOLE)
+      v = hole_pair<KM>(a, i, sw);
+    else
+      v = rescal_pair<KM>(a, i, sw);
+    nv += v ? 1 : 0;
+  }
+  if (lane_id() == 0 && nv && a.nviol) atomicAdd(a.nviol, nv);
+}
+
+// ---------------------------------------------------------------------------
+// logistic loss: HolE skge/hole.py:22-42, RESCAL skge/rescal.py:37-76
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void logistic(float y, float score, float* loss_i, float* fs) {
+  const float ysc = y * score;
+  *loss_i = fmaxf(-ysc, 0.0f) + log1pf(expf(-fabsf(ysc)));  // logaddexp(0, -ys)
+  *fs = -(y * (1.0f / (1.0f + expf(ysc))));                   // -(y * sigmoid(-ys))
+}
+
+template <int MODEL, int KM>
+__global__ __launch_bounds__(256) void k_triple_grad(PairArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wave = threadIdx.x >> 6;
+  const int wpb = blockDim.x >> 6;
+  const int d = a.d;
+  const int stride = 64 * KM;
+  float* sEs = smem + wave * 3 * stride;
+  float* sEo = sEs + stride;
+  float* sRp = sEs + 2 * stride;
+  float lsum = 0.0f;
+  for (int i = blockIdx.x * wpb + wave; i < a.P; i += gridDim.x * wpb) {
+    const int s = uni(a.pos[3 * i]), o = uni(a.pos[3 * i + 1]), p = uni(a.pos[3 * i + 2]);
+    const float y = a.ys[i];
+    float es[KM], eo[KM], x[KM], t[KM];
+    load_row<KM>(a.E, s, d, es);
+    to_lds<KM>(sEs, es, d);
+    load_row<KM>(a.E, o, d, eo);
+    to_lds<KM>(sEo, eo, d);
+    float score, li, fs;
+    if (MODEL == HOLE) {
+      float rp[KM], c[KM];
+      load_row<KM>(a.R, p, d, rp);
+      to_lds<KM>(sRp, rp, d);
+      __builtin_amdgcn_wave_barrier();
+      ccorr_lds<KM>(sEs, sEo, d, c);
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < KM; ++k) acc += rp[k] * c[k];
+      score = wave_sum(acc);
+      logistic(y, score, &li, &fs);
+      scale<KM>(x, c, fs);  // R: fs ccorr(E[s],E[o])   hole.py:32
+      acc_row<KM>(a.accR, p, x, d);
+      if (lane_id() == 0) acc_count(a.accR, p, 1);
+      ccorr_lds<KM>(sRp, sEo, d, t);  // E[s]: fs ccorr(R[p],E[o])   hole.py:37
+      scale<KM>(x, t, fs);
+      cconv_lds<KM>(sEs, sRp, d, t);  // E[o]: fs cconv(E[s],R[p])   hole.py:38
+      float yv[KM];
+      scale<KM>(yv, t, fs);
+      acc_two<KM>(a.accE, s, x, o, yv, d);
+    } else {
+      __builtin_amdgcn_wave_barrier();
+      const size_t dd = (size_t)d * d;
+      float we[KM], ew[KM];
+      gemv_rows<KM>(a.R + p * dd, sEo, d, we);  // WE = W[p] E[o]
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < KM; ++k) acc += es[k] * we[k];
+      score = wave_sum(acc);
+      logistic(y, score, &li, &fs);
+      gemv_cols<KM>(a.R + p * dd, sEs, d, ew);  // EW = E[s] W[p]
+      float yv[KM];
+      scale<KM>(x, we, fs);  // rescal.py:238: (fs WE over ss, fs EW over os)
+      scale<KM>(yv, ew, fs);
+      acc_two<KM>(a.accE, s, x, o, yv, d);
+      if (lane_id() == 0 && a.coef) a.coef[i] = fs;
+    }
+    if (lane_id() == 0 && a.pscore) a.pscore[i] = score;
+    lsum += li;
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane_id() == 0 && a.loss && lsum != 0.0f) atomicAdd(a.loss, lsum);
+}
+
+// ---------------------------------------------------------------------------
+// RESCAL dW: acc[p] = sum_i coef_i outer(E[s_i], E[o_i]) over the items with
+// relation p (skge/rescal.py:61-70, 113-125).  One 256-thread workgroup owns
+// one 64x64 tile of one relation's d x d gradient, so the tile is written
+// with plain stores (no atomics).  Items are compacted per 256-item chunk.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_rescal_wgrad(const float* __restrict__ E, Accum accW,
+                                                      int d, const int* ta, const float* ca,
+                                                      int na, const int* tb, const float* cb,
+                                                      int nb) {
+  const int nt = (d + 63) / 64;
+  const int tiles = nt * nt;
+  const int p = blockIdx.x / tiles;
+  const int tt = blockIdx.x - p * tiles;
+  const int ti = tt / nt, tj = tt - (tt / nt) * nt;
+  __shared__ int s_items[256];
+  __shared__ float s_coef[256];
+  __shared__ int s_n;
+  __shared__ float s_es[16][64];
+  __shared__ float s_eo[16][64];
+  const int t = threadIdx.x;
+  const int r0 = (t >> 4) * 4, c0 = (t & 15) * 4;
+  float acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = 0.0f;
+  int total = 0;
+  for (int list = 0; list < 2; ++list) {
+    const int* tr = list ? tb : ta;
+    const float* cf = list ? cb : ca;
+    const int n = list ? nb : na;
+    if (tr == nullptr) continue;
+    for (int base = 0; base < n; base += 256) {
+      if (t == 0) s_n = 0;
+      __syncthreads();
+      const int it = base + t;
+      if (it < n && tr[3 * it + 2] == p) {
+        const int slot = atomicAdd(&s_n, 1);
+        s_items[slot] = it;
+        s_coef[slot] = cf[it];
+      }
+      __syncthreads();
+      const int m = s_n;
+      total += m;
+      for (int m0 = 0; m0 < m; m0 += 16) {
+        for (int q = t; q < 16 * 64; q += 256) {
+          const int mi = q >> 6, c = q & 63;
+          float vs = 0.0f, vo = 0.0f;
+          if (m0 + mi < m) {
+            const int it2 = s_items[m0 + mi];
+            const int s = tr[3 * it2], o = tr[3 * it2 + 1];
+            const int rr = ti * 64 + c, cc = tj * 64 + c;
+            if (rr < d) vs = E[(size_t)s * d + rr] * s_coef[m0 + mi];
+            if (cc < d) vo = E[(size_t)o * d + cc];
+          }
+          s_es[mi][c] = vs;
+          s_eo[mi][c] = vo;
+        }
+        __syncthreads();
+        const int mm = min(16, m - m0);
+        for (int mi = 0; mi < mm; ++mi) {
+          float a4[4], b4[4];
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            a4[x] = s_es[mi][r0 + x];
+            b4[x] = s_eo[mi][c0 + x];
+          }
+#pragma unroll
+          for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) acc[x][y] = fmaf(a4[x], b4[y], acc[x][y]);
+        }
+        __syncthreads();
+      }
+    }
+  }
+  if (total == 0) return;
+  float* out = accW.sum + (size_t)p * d * d;
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int r = ti * 64 + r0 + x, c = tj * 64 + c0 + y;
+      if (r < d && c < d) out[(size_t)r * d + c] = acc[x][y];
+    }
+  if (tt == 0 && t == 0) {
+    accW.cnt[p] = total;
+    const int slot = atomicAdd(accW.ntouched, 1);
+    accW.touched[slot] = p;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------
+template <int MODEL>
+static int launch_pair(const PairArgs& a, int km, hipStream_t st, bool logistic_mode) {
+  const int threads = 256;
+  int blocks = (a.P + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  const size_t lds = (MODEL == TRANSE_L1 || MODEL == TRANSE_L2) ? 0 : (size_t)4 * 6 * 64 * km * 4;
+#define SKGE_LP(K)                                                                             \
+  case K:                                                                                      \
+    if (logistic_mode)                                                                         \
+      hipLaunchKernelGGL((k_triple_grad<MODEL, K>), dim3(blocks), dim3(threads), lds, st, a); \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_pair_grad<MODEL, K>), dim3(blocks), dim3(threads), lds, st, a);   \
+    break;
+  switch (km) {
+    SKGE_LP(1)
+    SKGE_LP(2)
+    SKGE_LP(3)
+    SKGE_LP(4)
+    SKGE_LP(8)
+    SKGE_LP(16)
+    default:
+      set_error("unsupported d");
+      return SKGE_ENOTSUP;
+  }
+#undef SKGE_LP
+  SKGE_CHECK_LAUNCH("pair/triple grad launch");
+  return SKGE_OK;
+}
+
+}  // namespace skge
+
+using namespace skge;
+
+extern "C" int skge_abi_version(void) { return SKGE_ABI_VERSION; }
+extern "C" const char* skge_last_error(void) { return skge::g_err; }
+
+static int check_model_tables(int model, const skge_table_t* ent, const skge_table_t* rel, int d) {
+  int rc;
+  if ((rc = check_table(ent, "ent", true)) != SKGE_OK) return rc;
+  if ((rc = check_table(rel, "rel", model != SKGE_RESCAL)) != SKGE_OK) return rc;
+  SKGE_CHECK_ARG(model >= 0 && model <= 3, "unknown model %d", model);
+  SKGE_CHECK_ARG(d > 0 && ent->width == d, "entity width %d != d %d", ent->width, d);
+  if (model == SKGE_RESCAL)
+    SKGE_CHECK_ARG(rel->width == d * d, "W width %d != d*d", rel->width);
+  else
+    SKGE_CHECK_ARG(rel->width == d, "relation width %d != d %d", rel->width, d);
+  SKGE_CHECK_ARG(km_for(d) != 0, "d=%d > 1024 unsupported", d);
+  return SKGE_OK;
+}
+
+extern "C" int skge_pair_grad(void* stream, int model, int af, const skge_table_t* ent,
+                              const skge_table_t* rel, int d, const int* pos, const int* neg,
+                              int P, float margin, float* pscore, float* nscore, float* coef,
+                              int* nviol) {
+  int rc = check_model_tables(model, ent, rel, d);
+  if (rc) return rc;
+  SKGE_CHECK_ARG(P >= 0, "P < 0");
+  SKGE_CHECK_ARG(af >= 0 && af <= 3, "unknown activation %d", af);
+  if (P == 0) return SKGE_OK;
+  SKGE_CHECK_ARG(pos && neg, "pos/neg NULL");
+  PairArgs a = {};
+  a.E = ent->param;
+  a.R = rel->param;
+  a.accE = accum_of(ent);
+  if (model != SKGE_RESCAL) a.accR = accum_of(rel);
+  a.pos = pos;
+  a.neg = neg;
+  a.P = P;
+  a.d = d;
+  a.af = af;
+  a.margin = margin;
+  a.pscore = pscore;
+  a.nscore = nscore;
+  a.coef = coef;
+  a.nviol = nviol;
+  const int km = km_for(d);
+  hipStream_t st = as_stream(stream);
+  switch (model) {
+    case SKGE_TRANSE_L1: return launch_pair<TRANSE_L1>(a, km, st, false);
+    case SKGE_TRANSE_L2: return launch_pair<TRANSE_L2>(a, km, st, false);
+    case SKGE_HOLE: return launch_pair<HOLE>(a, km, st, false);
+    default: return launch_pair<RESCAL>(a, km, st, false);
+  }
+}
+
+extern "C" int skge_triple_grad(void* stream, int model, const skge_table_t* ent,
+                                const skge_table_t* rel, int d, const int* trip, const float* ys,
+                                int T, float* score, float* coef, float* loss) {
+  int rc = check_model_tables(model, ent, rel, d);
+  if (rc) return rc;
+  SKGE_CHECK_ARG(model == SKGE_HOLE || model == SKGE_RESCAL,
+                 "logistic loss is defined for HolE and RESCAL only");
+  SKGE_CHECK_ARG(T >= 0, "T < 0");
+  if (T == 0) return SKGE_OK;
+  SKGE_CHECK_ARG(trip && ys, "trip/ys NULL");
+  PairArgs a = {};
+  a.E = ent->param;
+  a.R = rel->param;
+  a.accE = accum_of(ent);
+  if (model != SKGE_RESCAL) a.accR = accum_of(rel);
+  a.pos = trip;
+  a.ys = ys;
+  a.P = T;
+  a.d = d;
+  a.pscore = score;
+  a.coef = coef;
+  a.loss = loss;
+  const int km = km_for(d);
+  hipStream_t st = as_stream(stream);
+  if (model == SKGE_HOLE) return launch_pair<HOLE>(a, km, st, true);
+  return launch_pair<RESCAL>(a, km, st, true);
+}
+
+extern "C" int skge_rescal_wgrad(void* stream, const skge_table_t* ent, const skge_table_t* rel,
+                                 int d, const int* trip_a, const float* coef_a, int n_a,
+                                 const int* trip_b, const float* coef_b, int n_b) {
+  int rc = check_model_tables(SKGE_RESCAL, ent, rel, d);
+  if (rc) return rc;
+  SKGE_CHECK_ARG(rel->acc_sum && rel->acc_cnt && rel->acc_touched && rel->acc_ntouched,
+                 "W accumulator missing");
+  SKGE_CHECK_ARG(n_a >= 0 && n_b >= 0, "negative item count");
+  if (n_a + n_b == 0) return SKGE_OK;
+  const int nt = (d + 63) / 64;
+  const long long blocks = (long long)rel->rows * nt * nt;
+  SKGE_CHECK_ARG(blocks < (1ll << 31), "too many relation tiles");
+  hipLaunchKernelGGL(k_rescal_wgrad, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
+                     ent->param, accum_of(rel), d, trip_a, coef_a, n_a, trip_b, coef_b, n_b);
+  SKGE_CHECK_LAUNCH("rescal wgrad launch");
+  return SKGE_OK;
+}

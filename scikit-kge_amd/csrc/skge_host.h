@@ -1,0 +1,74 @@
+// Host-side helpers for the C ABI: error reporting and argument checks.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#include "../../include/skge_hip.h"
+#include "skge_device.h"
+
+namespace skge {
+
+void set_error(const char* fmt, ...);
+
+#define SKGE_CHECK_ARG(cond, ...)            \
+  do {                                       \
+    if (!(cond)) {                           \
+      ::skge::set_error(__VA_ARGS__);        \
+      return SKGE_EINVAL;                    \
+    }                                        \
+  } while (0)
+
+#define SKGE_CHECK_LAUNCH(what)                                                   \
+  do {                                                                            \
+    hipError_t _e = hipGetLastError();                                            \
+    if (_e != hipSuccess) {                                                       \
+      ::skge::set_error("%s: %s", what, hipGetErrorString(_e));                   \
+      return SKGE_EHIP;                                                           \
+    }                                                                             \
+  } while (0)
+
+#define SKGE_CHECK_HIP(call)                                                      \
+  do {                                                                            \
+    hipError_t _e = (call);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      ::skge::set_error("%s: %s", #call, hipGetErrorString(_e));                  \
+      return SKGE_EHIP;                                                           \
+    }                                                                             \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// registers per lane needed to hold a row of width d in the lane-strided
+// layout (see skge_device.h); 0 = unsupported
+inline int km_for(int d) {
+  if (d <= 64) return 1;
+  if (d <= 128) return 2;
+  if (d <= 192) return 3;
+  if (d <= 256) return 4;
+  if (d <= 512) return 8;
+  if (d <= 1024) return 16;
+  return 0;
+}
+
+inline Accum accum_of(const skge_table_t* t) {
+  Accum a;
+  a.sum = t->acc_sum;
+  a.cnt = t->acc_cnt;
+  a.touched = t->acc_touched;
+  a.ntouched = t->acc_ntouched;
+  a.width = t->width;
+  return a;
+}
+
+inline int check_table(const skge_table_t* t, const char* name, bool need_acc) {
+  SKGE_CHECK_ARG(t != nullptr, "%s: table is NULL", name);
+  SKGE_CHECK_ARG(t->param != nullptr, "%s: param is NULL", name);
+  SKGE_CHECK_ARG(t->rows > 0 && t->width > 0, "%s: bad shape %d x %d", name, t->rows, t->width);
+  if (need_acc) {
+    SKGE_CHECK_ARG(t->acc_sum && t->acc_cnt && t->acc_touched && t->acc_ntouched,
+                   "%s: accumulator buffers missing", name);
+  }
+  return SKGE_OK;
+}
+
+}  // namespace skge

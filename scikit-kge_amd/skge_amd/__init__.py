@@ -1,0 +1,12 @@
+"""skge_amd -- MI355X-native (HIP/gfx950) scikit-kge training hot path.
+
+Drop-in for skge's model / updater / trainer protocol: TransE, HolE, RESCAL,
+StochasticTrainer, PairwiseStochasticTrainer, SGD, AdaGrad,
+RandomModeSampler.  Every numeric step runs in libskgehip.so."""
+from .version import __version__
+from .base import Model, StochasticTrainer, PairwiseStochasticTrainer
+from .transe import TransE
+from .hole import HolE
+from .rescal import RESCAL
+from .param import Parameter, SGD, AdaGrad, normalize, normless1
+from .sample import RandomModeSampler

@@ -1,0 +1,115 @@
+"""ctypes binding of libskgehip.so (declared in include/skge_hip.h).
+
+torch is imported first on purpose: libskgehip.so needs libamdhip64.so.7 and
+torch has already loaded its own copy under that SONAME, so the library binds
+to torch's HIP runtime and device pointers / streams are shared.  There is no
+CPU fallback: if the library or a GPU is missing, calls raise.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libskgehip.so")
+
+SKGE_TRANSE_L1, SKGE_TRANSE_L2, SKGE_HOLE, SKGE_RESCAL = 0, 1, 2, 3
+SKGE_AF_LINEAR, SKGE_AF_SIGMOID, SKGE_AF_TANH, SKGE_AF_RELU = 0, 1, 2, 3
+SKGE_SGD, SKGE_ADAGRAD = 0, 1
+SKGE_POST_NONE, SKGE_POST_NORMALIZE, SKGE_POST_NORMLESS1 = 0, 1, 2
+
+c_p = ctypes.c_void_p
+c_i = ctypes.c_int
+c_f = ctypes.c_float
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+c_sz = ctypes.c_size_t
+
+
+class SkgeTable(ctypes.Structure):
+    """Mirror of skge_table_t."""
+    _fields_ = [("param", c_p), ("state", c_p), ("acc_sum", c_p), ("acc_cnt", c_p),
+                ("acc_touched", c_p), ("acc_ntouched", c_p), ("sync", c_p),
+                ("rows", c_i), ("width", c_i), ("opt", c_i), ("post", c_i),
+                ("lr", c_f), ("rin", c_f), ("rout", c_f), ("fixed_div", c_f),
+                ("gate", c_p)]
+
+
+T_P = ctypes.POINTER(SkgeTable)
+
+# name -> (restype, argtypes); the exact set declared in include/skge_hip.h
+SIGNATURES = {
+    "skge_abi_version": (c_i, []),
+    "skge_last_error": (ctypes.c_char_p, []),
+    "skge_pair_grad": (c_i, [c_p, c_i, c_i, T_P, T_P, c_i, c_p, c_p, c_i, c_f, c_p, c_p, c_p, c_p]),
+    "skge_triple_grad": (c_i, [c_p, c_i, T_P, T_P, c_i, c_p, c_p, c_i, c_p, c_p, c_p]),
+    "skge_rescal_wgrad": (c_i, [c_p, T_P, T_P, c_i, c_p, c_p, c_i, c_p, c_p, c_i]),
+    "skge_collect_workspace_bytes": (c_sz, [c_i]),
+    "skge_accum_collect": (c_i, [c_p, T_P, c_p, c_p, c_p, c_p, c_sz]),
+    "skge_accum_reset": (c_i, [c_p, T_P, c_i]),
+    "skge_update_rows": (c_i, [c_p, T_P, c_p, c_p, c_i]),
+    "skge_accum_apply": (c_i, [c_p, T_P, c_i, c_i]),
+    "skge_pair_step": (c_i, [c_p, c_i, c_i, T_P, T_P, c_i, c_p, c_p, c_i, c_f, c_p, c_p]),
+    "skge_triple_set_build": (c_i, [c_p, c_p, c_i64, c_p, c_i64]),
+    "skge_transe_sample_grad": (c_i, [c_p, c_i, T_P, T_P, c_i, c_p, c_i64, c_p, c_i64, c_i64, c_i,
+                                      c_u64, c_p, c_f, c_i, c_p, c_p, c_p]),
+    "skge_epoch_permutation": (c_i, [c_p, c_i64, c_u64, c_p, c_p, c_i64]),
+    "skge_epoch_advance": (c_i, [c_p, c_p]),
+    "skge_runner_create": (c_p, [c_p, c_i, T_P, T_P, c_i, c_p, c_i64, c_p, c_i64, c_i, c_u64, c_p,
+                                 c_f, c_i, c_p, c_p]),
+    "skge_runner_run": (c_i, [c_p, c_p, c_i]),
+    "skge_runner_nlaunches": (c_i, [c_p]),
+    "skge_runner_destroy": (None, [c_p]),
+}
+
+_lib = None
+
+
+class SkgeError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load and type the library (no GPU needed to load)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SkgeError("libskgehip.so not built (%s): run `make -C scikit-kge_amd` "
+                        "or __graft_entry__.build()" % path)
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.skge_abi_version() != 1:
+        raise SkgeError("ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def lib():
+    return load()
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().skge_last_error()
+        raise SkgeError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise SkgeError("skge_amd needs a ROCm GPU (MI355X); no CPU fallback exists")
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return c_p(s.cuda_stream)
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return c_p(t.data_ptr())

@@ -1,0 +1,102 @@
+"""Device-resident training data and the native epoch runner.
+
+DeviceKG holds the training triples on the GPU ([T, 3] int32, (s, o, p)) and
+the open-addressing triple set the device sampler rejects against.
+EpochRunner wraps skge_runner_* (csrc/skge_epoch.hip): one epoch of
+PairwiseStochasticTrainer batches (nbatches full batches + the remainder,
+skge/base.py:1246-1268), captured once into a hipGraph and replayed."""
+import timeit
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .util import to_device_triples
+
+
+def _next_pow2(n):
+    c = 1
+    while c < n:
+        c <<= 1
+    return c
+
+
+class DeviceKG(object):
+    def __init__(self, xs, device=None, stream=None):
+        L.require_gpu()
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.trip = to_device_triples(xs, dev)
+        self.T = int(self.trip.shape[0])
+        self.capacity = _next_pow2(max(2 * self.T, 2))
+        self.slots = torch.empty(self.capacity * 4, dtype=torch.int32, device=dev)
+        L.check(L.lib().skge_triple_set_build(L.stream_ptr(stream), L.ptr(self.trip), self.T,
+                                              L.ptr(self.slots), self.capacity), "triple set build")
+
+
+class EpochRunner(object):
+    """Native hipGraph epoch of the TransE device batch loop."""
+
+    def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, stream=None,
+                 nviol_total=None):
+        from .transe import TransE
+        if not isinstance(model, TransE):
+            raise NotImplementedError("device_loop supports TransE (the north-star path) only")
+        dev = model.device
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=dev)
+        self.kg = kg
+        self.model = model
+        self.epoch_key = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.nviol_total = nviol_total if nviol_total is not None else \
+            torch.zeros(1, dtype=torch.int32, device=dev)
+        self.te = updaters["E"].table(model.accumulator("E"))
+        self.tr = updaters["R"].table(model.accumulator("R"))
+        self.nbatches = nbatches
+        torch.cuda.current_stream().synchronize()
+        lib = L.lib()
+        h = lib.skge_runner_create(L.stream_ptr(self.stream), int(bool(model.l1)),
+                                   self.te, self.tr,
+                                   model.d, L.ptr(kg.trip), kg.T, L.ptr(kg.slots), kg.capacity,
+                                   int(nbatches), int(seed) & (2 ** 64 - 1), L.ptr(self.epoch_key),
+                                   float(model.margin), int(ntries), None, L.ptr(self.nviol_total))
+        if not h:
+            raise L.SkgeError("skge_runner_create: %s" % lib.skge_last_error().decode())
+        self.handle = h
+        self.nlaunches = lib.skge_runner_nlaunches(h)
+
+    def run(self, nepochs=1):
+        L.check(L.lib().skge_runner_run(self.handle, L.stream_ptr(self.stream), int(nepochs)),
+                "runner run")
+
+    def synchronize(self):
+        self.stream.synchronize()
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                self.stream.synchronize()
+                L.lib().skge_runner_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+def device_optim(trainer, xs):
+    """PairwiseStochasticTrainer.fit with device_loop=True."""
+    model = trainer.model
+    dev = model.device
+    if trainer._nviol_dev is None:
+        trainer._nviol_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+    kg = DeviceKG(xs, dev)
+    runner = EpochRunner(model, trainer._updaters, kg, trainer.nbatches, seed=trainer.seed,
+                         ntries=trainer.ntries, nviol_total=trainer._nviol_dev)
+    trainer._runner = runner
+    with torch.cuda.stream(runner.stream):
+        for trainer.epoch in range(1, trainer.max_epochs + 1):
+            trainer._pre_epoch()
+            trainer.epoch_start = timeit.default_timer()
+            runner.run(1)
+            for f in trainer.post_epoch:
+                if not f(trainer):
+                    break
+    runner.synchronize()

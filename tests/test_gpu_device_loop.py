@@ -1,0 +1,186 @@
+"""Device batch loop (throughput path): permutation, device sampler, fused
+sample+score+scatter kernel, native hipGraph epoch runner (GPU).
+
+Parity: the negatives drawn on the device are recorded (neg_out) and the
+exact pairs are replayed through the CPU oracle; parameters after the update
+must agree within the fp32 tolerance of test_gpu_parity.  Full-size
+(WN18-shaped) runs are checked through size-independent properties.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import skge_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def make_kg(n_ent, n_rel, n_triples, seed=0):
+    rs = np.random.RandomState(seed)
+    trip = set()
+    out = np.empty((n_triples, 3), dtype=np.int32)
+    k = 0
+    while k < n_triples:
+        m = (n_triples - k) * 2
+        s = rs.randint(n_ent, size=m)
+        o = rs.randint(n_ent, size=m)
+        p = rs.randint(n_rel, size=m)
+        for a, b, c in zip(s, o, p):
+            t = (int(a), int(b), int(c))
+            if t not in trip:
+                trip.add(t)
+                out[k] = t
+                k += 1
+                if k == n_triples:
+                    break
+    return out, trip
+
+
+def _setup(n_ent, n_rel, T, d, lr=0.1, margin=2.0, seed=3):
+    import skge_amd as S
+    from skge_amd.device import DeviceKG
+    np.random.seed(seed)
+    m = S.TransE((n_ent, n_ent, n_rel), d)
+    m.add_hyperparam("margin", margin)
+    upd = {pid: S.AdaGrad(p, lr) for pid, p in m.params.items()}
+    trip, tset = make_kg(n_ent, n_rel, T)
+    kg = DeviceKG(trip, m.device)
+    return S, m, upd, trip, tset, kg
+
+
+def test_epoch_permutation_is_a_bijection():
+    from skge_amd import _lib as L
+    for T in (1, 7, 1000, 141442):
+        key = torch.tensor([5], dtype=torch.int64, device="cuda")
+        out = torch.empty(T, dtype=torch.int64, device="cuda")
+        L.check(L.lib().skge_epoch_permutation(L.stream_ptr(), T, 123, L.ptr(key), L.ptr(out), T))
+        p = out.cpu().numpy()
+        assert np.array_equal(np.sort(p), np.arange(T))
+        if T > 100:
+            assert not np.array_equal(p, np.arange(T))
+
+
+def test_sampler_kernel_parity_with_oracle_replay():
+    from skge_amd import _lib as L
+    S, m, upd, trip, tset, kg = _setup(300, 5, 2000, 50)
+    E0 = np.asarray(m.E, dtype=np.float64)
+    R0 = np.asarray(m.R, dtype=np.float64)
+    dev = m.device
+    key = torch.tensor([0], dtype=torch.int64, device=dev)
+    count, start = 256, 512
+    negs = torch.full((count, 2), -7, dtype=torch.int32, device=dev)
+    perm = torch.empty(kg.T, dtype=torch.int64, device=dev)
+    nviol = torch.zeros(1, dtype=torch.int32, device=dev)
+    te = upd["E"].table(m.accumulator("E"))
+    tr = upd["R"].table(m.accumulator("R"))
+    lib = L.lib()
+    st = L.stream_ptr()
+    L.check(lib.skge_epoch_permutation(st, kg.T, 99, L.ptr(key), L.ptr(perm), kg.T))
+    L.check(lib.skge_transe_sample_grad(st, 1, te, tr, m.d, L.ptr(kg.trip), kg.T, L.ptr(kg.slots),
+                                        kg.capacity, start, count, 99, L.ptr(key), float(m.margin),
+                                        100, L.ptr(nviol), None, L.ptr(negs)))
+    arr = (L.SkgeTable * 2)(te, tr)
+    L.check(lib.skge_accum_apply(st, arr, 2, 4 * count))
+    negs = negs.cpu().numpy()
+    pidx = perm.cpu().numpy()[start:start + count]
+    pos_list, neg_list = [], []
+    for j in range(count):
+        s, o, p = trip[pidx[j]]
+        for mode in (0, 1):
+            c = negs[j, mode]
+            assert c >= 0, "a WN18-sparse KG never exhausts 100 tries"
+            nt = (int(c), int(o), int(p)) if mode == 0 else (int(s), int(c), int(p))
+            assert nt not in tset                     # rejection against the training set
+            assert nt != (s, o, p)
+            pos_list.append((s, o, p))
+            neg_list.append(nt)
+    pos = np.array(pos_list)
+    neg = np.array(neg_list)
+    params = {"E": E0.copy(), "R": R0.copy()}
+    state = {"E": np.zeros_like(E0), "R": np.zeros_like(R0)}
+    _, _, nv, g = O.pairwise_step("transe", params, state, pos, neg, 0.1, float(m.margin),
+                                  "adagrad", l1=True)
+    assert int(nviol.item()) == nv
+    np.testing.assert_allclose(np.asarray(m.E), params["E"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(np.asarray(m.R), params["R"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(upd["E"].p2.cpu().numpy(), state["E"], rtol=1e-5, atol=1e-5)
+
+
+def test_sampler_mode_balance():
+    """Mode 0 corrupts s, mode 1 corrupts o, drawn uniformly over entities."""
+    from skge_amd import _lib as L
+    S, m, upd, trip, tset, kg = _setup(64, 3, 500, 8, margin=-1e9)  # no violations: pure sampling
+    dev = m.device
+    key = torch.tensor([1], dtype=torch.int64, device=dev)
+    negs = torch.empty((kg.T, 2), dtype=torch.int32, device=dev)
+    te = upd["E"].table(m.accumulator("E"))
+    tr = upd["R"].table(m.accumulator("R"))
+    L.check(L.lib().skge_transe_sample_grad(L.stream_ptr(), 1, te, tr, m.d, L.ptr(kg.trip), kg.T,
+                                            L.ptr(kg.slots), kg.capacity, 0, kg.T, 7, L.ptr(key),
+                                            -1e9, 100, None, None, L.ptr(negs)))
+    n = negs.cpu().numpy()
+    assert (n >= 0).all()
+    hist = np.bincount(n.ravel(), minlength=64)
+    # 1000 uniform draws over 64 entities: every entity drawn, none wildly over-represented
+    assert hist.min() > 0 and hist.max() < 60
+
+
+def test_runner_small_two_epochs_invariants():
+    S, m, upd, trip, tset, kg = _setup(500, 7, 3000, 50)
+    from skge_amd.device import EpochRunner
+    tr = EpochRunner(m, upd, kg, nbatches=10, seed=1)
+    assert tr.nlaunches == 2 * 10 + 1   # 3000 = 10 x 300: no remainder batch
+    tr.run(2)
+    tr.synchronize()
+    E = np.asarray(m.E, dtype=np.float64)
+    assert np.isfinite(E).all()
+    np.testing.assert_allclose(np.linalg.norm(E, axis=1), 1.0, atol=1e-5)
+    nv = int(tr.nviol_total.item())
+    assert 0 < nv <= 2 * 2 * kg.T
+    for acc in m._acc.values():
+        assert int(acc.ntouched.item()) == 0
+        assert int(acc.cnt.abs().sum().item()) == 0
+        assert float(acc.sum.abs().sum().item()) == 0.0
+    assert int(tr.epoch_key.item()) == 2
+
+
+@pytest.mark.parametrize("l1", [True, False])
+def test_runner_wn18_full_size_properties(l1):
+    """WN18 geometry (|E|=40943, |R|=18, T=141442, d=200, nb=100): one epoch."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, EpochRunner
+    np.random.seed(42)
+    m = S.TransE((40943, 40943, 18), 200, l1=l1)
+    m.add_hyperparam("margin", 2.0)
+    upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
+    trip, _ = make_kg(40943, 18, 141442)
+    kg = DeviceKG(trip, m.device)
+    R0 = np.asarray(m.R).copy()
+    runner = EpochRunner(m, upd, kg, nbatches=100, seed=0)
+    assert runner.nlaunches == 2 * 101 + 1
+    runner.run(1)
+    runner.synchronize()
+    E = np.asarray(m.E, dtype=np.float64)
+    assert np.isfinite(E).all()
+    np.testing.assert_allclose(np.linalg.norm(E, axis=1), 1.0, atol=1e-5)
+    nv = int(runner.nviol_total.item())
+    assert 0 < nv <= 2 * kg.T
+    assert not np.allclose(np.asarray(m.R), R0)
+    for acc in m._acc.values():
+        assert int(acc.ntouched.item()) == 0
+        assert int(acc.cnt.abs().sum().item()) == 0
+
+
+def test_trainer_device_loop_fit():
+    import skge_amd as S
+    np.random.seed(42)
+    m = S.TransE((400, 400, 6), 32)
+    trip, _ = make_kg(400, 6, 3000)
+    seen = []
+    tr = S.PairwiseStochasticTrainer(m, nbatches=10, max_epochs=3, learning_rate=0.1, margin=2.0,
+                                     device_loop=True, file_grad=None, file_embed=None,
+                                     post_epoch=[lambda t: seen.append((t.epoch, t.nviolations))
+                                                 or True])
+    tr.fit([tuple(x) for x in trip.tolist()], [1] * len(trip))
+    assert [e for e, _ in seen] == [1, 2, 3]
+    assert all(v > 0 for _, v in seen)
