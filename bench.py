@@ -218,12 +218,12 @@ def kernel_profile(model, upd, kg, nb, d, st, runner):
     from skge_amd import _lib as L
     lib = L.lib()
     dev = model.device
-    te = upd["E"].table(model.accumulator("E"))
-    tr = upd["R"].table(model.accumulator("R"))
+    bs = kg.T // nb
+    te = upd["E"].table(model.accumulator("E").ensure_slots(4 * bs))
+    tr = upd["R"].table(model.accumulator("R").ensure_slots(bs))
     tabs = (L.SkgeTable * 2)(te, tr)
     nviol = torch.zeros(1, dtype=torch.int32, device=dev)
     T = kg.T
-    bs = T // nb
     sp = L.stream_ptr(st)
     times = {"transe_sample_grad": [], "accum_apply": []}
     bytes_ = {"transe_sample_grad": 0.0, "accum_apply": 0.0}
@@ -240,9 +240,11 @@ def kernel_profile(model, upd, kg, nb, d, st, runner):
                                                 2.0, 100, L.ptr(nviol), None, None))
             e[1].record(st)
             st.synchronize()
-            UE, UR, V = int(accE.ntouched.item()), int(accR.ntouched.item()), int(nviol.item())
+            UE = int((accE.touched[:4 * cnt] >= 0).sum().item())
+            UR = int((accR.touched[:cnt] >= 0).sum().item())
+            V = int(nviol.item())
             e[2].record(st)
-            L.check(lib.skge_accum_apply(sp, tabs, 2, 4 * cnt))
+            L.check(lib.skge_accum_apply(sp, tabs, 2, L.int_array(4 * cnt, cnt)))
             e[3].record(st)
             st.synchronize()
             times["transe_sample_grad"].append(e[0].elapsed_time(e[1]) * 1e3)

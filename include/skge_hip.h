@@ -20,8 +20,8 @@
  *    (skge/base.py:511, skge/util.py:104-110).
  *  - Parameters are fp32 row-major tables [rows][width]; width = d for E / R,
  *    d*d for RESCAL's W.
- *  - Accumulator invariant: between batches acc_sum == 0, acc_cnt == 0 and
- *    *acc_ntouched == 0 for every table (zero them once at allocation).
+ *  - Accumulator invariant: between batches acc_sum == 0 and acc_cnt == 0
+ *    for every table (zero them once at allocation).
  */
 #ifndef SKGE_HIP_H
 #define SKGE_HIP_H
@@ -61,17 +61,26 @@ enum { SKGE_POST_NONE = 0, SKGE_POST_NORMALIZE = 1, SKGE_POST_NORMLESS1 = 2 };
  *   mean + rparam*P      hole.py:33,40,83  rescal.py:70,239
  *   (sum + rparam*P)/n   rescal.py:299-302 (rparam inside)
  *   (sum + rparam*W)/2   rescal.py:287-290 (divisor quirk)
+ *
+ * Touched rows are recorded in FIXED SLOTS (no shared counter): every
+ * contribution site of a launch owns one slot of acc_touched and writes the
+ * row id there if it was the first to count the row (atomicAdd on acc_cnt
+ * returned 0), else -1.  Slot maps:
+ *   skge_pair_grad          ent: 4i+{0:sp,1:op,2:sn,3:on}   rel: 2i+{0:pp,1:pn}
+ *   skge_triple_grad        ent: 2i+{0:s,1:o}               rel (HolE): i
+ *   skge_rescal_wgrad       W:   slot p (all M slots)
+ *   skge_transe_sample_grad ent: 4j+{0:s,1:o,2:s',3:o'}     rel: j
+ * Consumers (apply / reset) take the slot count of the producing launch.
  */
 typedef struct skge_table {
   float *param;        /* [rows][width] */
   float *state;        /* AdaGrad accumulator p2 [rows][width]; NULL for SGD */
   float *acc_sum;      /* [rows][width] */
   int *acc_cnt;        /* [rows] */
-  int *acc_touched;    /* [rows] rows touched in the current batch */
-  int *acc_ntouched;   /* [1] */
-  int *sync;           /* [1] zeroed scratch word used by skge_accum_apply */
+  int *acc_touched;    /* [touched_cap] slot -> row or -1 */
   int rows;
   int width;
+  int touched_cap;     /* capacity of acc_touched (slots) */
   int opt;             /* SKGE_SGD | SKGE_ADAGRAD */
   int post;            /* SKGE_POST_* */
   float lr;
@@ -94,6 +103,7 @@ const char *skge_last_error(void);
  * violation count to *nviol, and accumulates every violating pair's
  * contribution rows into ent->acc_* / rel->acc_* (segment sum + counts).
  * coef (RESCAL only, [2P]): gp for every pair, then gn for every pair.
+ * margin == -INFINITY: score only (nothing accumulated, no slots written).
  */
 int skge_pair_grad(void *stream, int model, int af, const skge_table_t *ent,
                    const skge_table_t *rel, int d, const int *pos, const int *neg, int P,
@@ -128,8 +138,9 @@ size_t skge_collect_workspace_bytes(int rows);
 int skge_accum_collect(void *stream, const skge_table_t *t, int *idx_out, float *g_out,
                        int *U_out, void *workspace, size_t ws_bytes);
 
-/* Reset a table's accumulator without producing gradients. */
-int skge_accum_reset(void *stream, const skge_table_t *t, int max_touched);
+/* Reset a table's accumulator (the rows in the first nslots slots) without
+ * producing gradients. */
+int skge_accum_reset(void *stream, const skge_table_t *t, int nslots);
 
 /*
  * Updater call: param[idx] -= ... for U explicit (row, gradient) pairs, then
@@ -141,10 +152,11 @@ int skge_update_rows(void *stream, const skge_table_t *t, const float *g, const 
 
 /*
  * Fused: segment mean + updater + projection straight from the accumulators
- * of up to 4 tables (trainer._batch_step, skge/base.py:1306-1316), then reset
- * of the accumulators.  max_touched bounds the touched rows of any table.
+ * of up to 4 tables (trainer._batch_step, skge/base.py:1306-1316), resetting
+ * the accumulator rows it reads.  nslots[i]: slot count of table i (the
+ * producing launch's slot map, see skge_table_t).
  */
-int skge_accum_apply(void *stream, const skge_table_t *tables, int ntables, int max_touched);
+int skge_accum_apply(void *stream, const skge_table_t *tables, int ntables, const int *nslots);
 
 /* Explicit-pair training step: skge_pair_grad + (RESCAL wgrad) + apply. */
 int skge_pair_step(void *stream, int model, int af, const skge_table_t *ent,
@@ -154,11 +166,14 @@ int skge_pair_step(void *stream, int model, int af, const skge_table_t *ent,
 /* ---------------- device-resident batch loop (throughput path) ---------------- */
 
 /*
- * Build the open-addressing set of training triples used by the negative
- * sampler's rejection test (skge/sample.py:41-44).  slots: capacity int4
- * entries (power of two >= 2*T), zeroed by this call.
+ * Build the set of training triples used by the negative sampler's rejection
+ * test (skge/sample.py:41-44): an open-addressing table of `capacity` 16-byte
+ * slots (power of two >= 2*T) followed by a one-hash filter of 8*capacity
+ * bits that answers most "not a training triple" queries with one load.
+ * `set` must hold skge_triple_set_bytes(capacity) bytes; zeroed by this call.
  */
-int skge_triple_set_build(void *stream, const int *trip, int64_t T, void *slots,
+size_t skge_triple_set_bytes(int64_t capacity);
+int skge_triple_set_build(void *stream, const int *trip, int64_t T, void *set,
                           int64_t capacity);
 
 /*
@@ -174,7 +189,7 @@ int skge_triple_set_build(void *stream, const int *trip, int64_t T, void *slots,
  */
 int skge_transe_sample_grad(void *stream, int l1, const skge_table_t *ent,
                             const skge_table_t *rel, int d, const int *trip, int64_t T,
-                            const void *set_slots, int64_t set_capacity, int64_t start, int count,
+                            const void *set, int64_t set_capacity, int64_t start, int count,
                             uint64_t seed, const uint64_t *epoch_key, float margin, int ntries,
                             int *nviol, int *nviol_total, int *neg_out);
 
@@ -194,7 +209,7 @@ int skge_epoch_advance(void *stream, uint64_t *epoch_key);
 typedef struct skge_runner skge_runner_t;
 skge_runner_t *skge_runner_create(void *stream, int l1, const skge_table_t *ent,
                                   const skge_table_t *rel, int d, const int *trip, int64_t T,
-                                  const void *set_slots, int64_t set_capacity, int nbatches,
+                                  const void *set, int64_t set_capacity, int nbatches,
                                   uint64_t seed, uint64_t *epoch_key, float margin, int ntries,
                                   int *nviol, int *nviol_total);
 int skge_runner_run(skge_runner_t *r, void *stream, int nepochs);

@@ -54,23 +54,31 @@ __device__ __forceinline__ float signf_np(float x) {  // numpy.sign
 
 // Segment-sum accumulator for one parameter table (the device form of
 // grad_sum_matrix + Sm.dot(G), skge/util.py:53-101): a dense fp32 sum
-// [rows][width], an occurrence count per row and the list of rows touched
-// in this batch.  Invariant between batches: sum == 0, cnt == 0, *ntouched == 0.
+// [rows][width], an occurrence count per row, and fixed-slot touched records
+// (see skge_table_t in include/skge_hip.h).  Invariant between batches:
+// sum == 0 and cnt == 0.
 struct Accum {
   float* sum;
   int* cnt;
   int* touched;
-  int* ntouched;
   int width;
 };
 
-// add `c` occurrences of `row` (lane-uniform call; one lane issues it)
-__device__ __forceinline__ void acc_count(const Accum& a, int row, int c) {
-  const int old = atomicAdd(a.cnt + row, c);
-  if (old == 0) {
-    const int slot = atomicAdd(a.ntouched, 1);
-    a.touched[slot] = row;
+// Count `c` occurrences of `row` and record it in `slot` if this was the
+// first count of the row in the batch (else -1).  Called by one lane per
+// (row, slot); different lanes' calls are independent, so a wave issues all
+// its returning atomics at once (one round trip, not one per row).
+__device__ __forceinline__ void commit_slot(const Accum& a, int row, int c, int slot) {
+  if (c > 0) {
+    const int old = atomicAdd(a.cnt + row, c);
+    a.touched[slot] = old == 0 ? row : -1;
+  } else {
+    a.touched[slot] = -1;
   }
+}
+
+__device__ __forceinline__ int sel4(int l, int a, int b, int c, int d) {
+  return l == 0 ? a : (l == 1 ? b : (l == 2 ? c : d));
 }
 
 template <int KM>
@@ -109,12 +117,16 @@ __device__ __forceinline__ int rand_below(uint64_t r, int n) {
   return (int)(((r >> 32) * (uint64_t)(uint32_t)n) >> 32);
 }
 
-// Open-addressing set of training triples (s, o, p): 16-byte slots
-// {s, o, p, tag}; tag 0 = empty.  Used for the RandomModeSampler rejection
-// test `tuple(nex) not in self.xs` (skge/sample.py:44).
+// Set of training triples (s, o, p) for the RandomModeSampler rejection test
+// `tuple(nex) not in self.xs` (skge/sample.py:44): open addressing over
+// 16-byte slots {s, o, p, tag} (tag 0 = empty), preceded by a one-hash bit
+// filter of 8 bits per slot, so a query for a non-member (the common case)
+// usually costs one 4-byte load.
 struct TripleSet {
-  int4* slots;
-  uint64_t mask;  // capacity - 1 (power of two)
+  const int4* slots;
+  const uint32_t* filter;
+  uint64_t mask;   // capacity - 1 (power of two)
+  uint64_t fmask;  // filter bits - 1
 };
 
 __device__ __host__ __forceinline__ uint64_t triple_hash(int s, int o, int p) {
@@ -122,7 +134,10 @@ __device__ __host__ __forceinline__ uint64_t triple_hash(int s, int o, int p) {
 }
 
 __device__ __forceinline__ bool set_contains(const TripleSet& ts, int s, int o, int p) {
-  uint64_t h = triple_hash(s, o, p) & ts.mask;
+  const uint64_t hv = triple_hash(s, o, p);
+  const uint64_t bit = (hv >> 29) & ts.fmask;
+  if (((ts.filter[bit >> 5] >> (bit & 31)) & 1u) == 0) return false;
+  uint64_t h = hv & ts.mask;
   for (uint64_t probe = 0; probe <= ts.mask; ++probe) {
     const int4 v = ts.slots[h];
     if (v.w == 0) return false;

@@ -57,11 +57,14 @@ __device__ __forceinline__ uint64_t epoch_sample_key(uint64_t seed, uint64_t ek)
 
 // ---- triple set build: claim a slot by CAS on the tag, then fill it ----
 __global__ void k_set_build(const int* __restrict__ trip, long long T, int4* slots,
-                            unsigned long long mask) {
+                            unsigned long long mask, uint32_t* filter, unsigned long long fmask) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < T;
        i += (long long)gridDim.x * blockDim.x) {
     const int s = trip[3 * i], o = trip[3 * i + 1], p = trip[3 * i + 2];
-    uint64_t h = triple_hash(s, o, p) & mask;
+    const uint64_t hv = triple_hash(s, o, p);
+    const uint64_t bit = (hv >> 29) & fmask;
+    atomicOr(&filter[bit >> 5], 1u << (bit & 31));
+    uint64_t h = hv & mask;
     for (uint64_t probe = 0; probe <= mask; ++probe) {
       if (atomicCAS(&slots[h].w, 0, 1) == 0) {
         slots[h].x = s;
@@ -169,6 +172,14 @@ __global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
       a.neg_out[2 * (long long)w] = neg0;
       a.neg_out[2 * (long long)w + 1] = neg1;
     }
+    {
+      // occurrence counts + touched slots (entity slots 4w+{s,o,s',o'}, relation slot w):
+      // pair 0 lists (sp,op,sn,on) = (s,o,s',o), pair 1 = (s,o,s,o')
+      const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
+      const int rE = sel4(l, s, o, neg0, neg1);
+      if (l < 4) commit_slot(a.accE, rE, cE, 4 * w + l);
+      else if (l == 4) commit_slot(a.accR, p, 2 * (v0 + v1), w);
+    }
     if (v0 + v1 == 0) continue;
     nv += v0 + v1;
     const float fv0 = (float)v0, fv1 = (float)v1;
@@ -188,13 +199,6 @@ __global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
     if (v0) acc_row<KM>(a.accE, neg0, c0, d);
     if (v1) acc_row<KM>(a.accE, neg1, c1, d);
     acc_row<KM>(a.accR, p, cr, d);
-    if (l == 0) {
-      acc_count(a.accE, s, v0 + 2 * v1);
-      acc_count(a.accE, o, 2 * v0 + v1);
-      if (v0) acc_count(a.accE, neg0, 1);
-      if (v1) acc_count(a.accE, neg1, 1);
-      acc_count(a.accR, p, 2 * (v0 + v1));
-    }
   }
   if (l == 0 && nv) {
     if (a.nviol) atomicAdd(a.nviol, nv);
@@ -244,18 +248,35 @@ static int launch_sample(const SampleArgs& a, bool l1, hipStream_t st) {
 
 using namespace skge;
 
-extern "C" int skge_triple_set_build(void* stream, const int* trip, int64_t T, void* slots,
+extern "C" size_t skge_triple_set_bytes(int64_t capacity) {
+  return (size_t)capacity * sizeof(int4) + (size_t)capacity;   // slots + 8 filter bits per slot
+}
+
+static TripleSet triple_set_of(const void* set, int64_t capacity) {
+  TripleSet ts;
+  ts.slots = (const int4*)set;
+  ts.filter = (const uint32_t*)((const int4*)set + capacity);
+  ts.mask = (uint64_t)(capacity - 1);
+  ts.fmask = (uint64_t)(8 * capacity - 1);
+  return ts;
+}
+
+extern "C" int skge_triple_set_build(void* stream, const int* trip, int64_t T, void* set,
                                      int64_t capacity) {
-  SKGE_CHECK_ARG(trip && slots, "NULL argument");
-  SKGE_CHECK_ARG(capacity > 0 && (capacity & (capacity - 1)) == 0, "capacity must be a power of 2");
+  SKGE_CHECK_ARG(trip && set, "NULL argument");
+  SKGE_CHECK_ARG(capacity >= 4 && (capacity & (capacity - 1)) == 0,
+                 "capacity must be a power of 2 >= 4");
   SKGE_CHECK_ARG(capacity >= 2 * T, "capacity must be >= 2*T");
+  SKGE_CHECK_ARG(capacity <= (1ll << 32), "capacity too large");
   hipStream_t st = as_stream(stream);
-  SKGE_CHECK_HIP(hipMemsetAsync(slots, 0, (size_t)capacity * sizeof(int4), st));
+  SKGE_CHECK_HIP(hipMemsetAsync(set, 0, skge_triple_set_bytes(capacity), st));
   if (T == 0) return SKGE_OK;
   long long blocks = (T + 255) / 256;
   if (blocks > 8192) blocks = 8192;
+  TripleSet ts = triple_set_of(set, capacity);
   hipLaunchKernelGGL(k_set_build, dim3((unsigned)blocks), dim3(256), 0, st, trip, (long long)T,
-                     (int4*)slots, (unsigned long long)(capacity - 1));
+                     (int4*)ts.slots, (unsigned long long)ts.mask, (uint32_t*)ts.filter,
+                     (unsigned long long)ts.fmask);
   SKGE_CHECK_LAUNCH("triple set build");
   return SKGE_OK;
 }
@@ -280,8 +301,7 @@ static int fill_sample_args(SampleArgs& a, int l1, const skge_table_t* ent, cons
   a.accR = accum_of(rel);
   a.trip = trip;
   a.T = T;
-  a.set.slots = (int4*)set_slots;
-  a.set.mask = (uint64_t)(set_capacity - 1);
+  a.set = triple_set_of(set_slots, set_capacity);
   a.d = d;
   a.n_ent = ent->rows;
   a.ntries = ntries;
@@ -307,6 +327,8 @@ extern "C" int skge_transe_sample_grad(void* stream, int l1, const skge_table_t*
   if (rc) return rc;
   SKGE_CHECK_ARG(start >= 0 && count >= 0 && start + count <= T, "batch out of range");
   if (count == 0) return SKGE_OK;
+  if ((rc = check_slots(ent, 4ll * count, "ent")) || (rc = check_slots(rel, count, "rel")))
+    return rc;
   a.start = start;
   a.count = count;
   a.neg_out = neg_out;
@@ -374,8 +396,10 @@ extern "C" skge_runner_t* skge_runner_create(void* stream, int l1, const skge_ta
     a.start = b.first;
     a.count = (int)b.second;
     a.neg_out = nullptr;
+    const int ns[2] = {(int)(4 * b.second), (int)b.second};
+    if ((rc = check_slots(ent, ns[0], "ent")) || (rc = check_slots(rel, ns[1], "rel"))) break;
     if ((rc = launch_sample(a, l1 != 0, st))) break;
-    if ((rc = skge_accum_apply(stream, tabs, 2, (int)(4 * b.second)))) break;
+    if ((rc = skge_accum_apply(stream, tabs, 2, ns))) break;
     r->nlaunch += 2;
   }
   if (!rc) {

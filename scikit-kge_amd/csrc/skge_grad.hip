@@ -36,6 +36,7 @@ struct PairArgs {
   float* coef;
   int* nviol;
   float* loss;
+  int record;  // 0: score only (no contribution scatter, no slot writes)
 };
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -128,6 +129,7 @@ __device__ __forceinline__ void scale(float (&o)[KM], const float (&v)[KM], floa
 }
 
 // add rows x (coefficient already applied) at a and y at b, merging when a == b
+// (the matching counts are committed by commit_pair / commit_triple)
 template <int KM>
 __device__ __forceinline__ void acc_two(const Accum& acc, int a, const float (&x)[KM], int b,
                                         const float (&y)[KM], int d) {
@@ -136,14 +138,39 @@ __device__ __forceinline__ void acc_two(const Accum& acc, int a, const float (&x
 #pragma unroll
     for (int k = 0; k < KM; ++k) t[k] = x[k] + y[k];
     acc_row<KM>(acc, a, t, d);
-    if (lane_id() == 0) acc_count(acc, a, 2);
   } else {
     acc_row<KM>(acc, a, x, d);
     acc_row<KM>(acc, b, y, d);
-    if (lane_id() == 0) {
-      acc_count(acc, a, 1);
-      acc_count(acc, b, 1);
+  }
+}
+
+// Occurrence counts + touched slots of one pair (slot maps: skge_hip.h).
+// Entity list (sp, op, sn, on), relation list (pp, pn), each occurrence
+// counted once per violating pair, as grad_sum_matrix counts duplicates.
+// Lanes 0-3 / 4-5 issue their returning atomics concurrently.
+__device__ __forceinline__ void commit_pair(const Accum& aE, const Accum* aR, bool viol,
+                                            const int (&ix)[6], int i) {
+  const int l = lane_id();
+  const int v = viol ? 1 : 0;
+  const int sp = ix[0], op = ix[1], pp = ix[2], sn = ix[3], on = ix[4], pn = ix[5];
+  int c0 = v, c1 = v, c2 = v, c3 = v;
+  if (sp == sn) {
+    c0 += c2;
+    c2 = 0;
+  }
+  if (op == on) {
+    c1 += c3;
+    c3 = 0;
+  }
+  if (l < 4) {
+    commit_slot(aE, sel4(l, sp, op, sn, on), sel4(l, c0, c1, c2, c3), 4 * i + l);
+  } else if (aR != nullptr && l < 6) {
+    int r0 = v, r1 = v;
+    if (pp == pn) {
+      r0 += r1;
+      r1 = 0;
     }
+    commit_slot(*aR, l == 4 ? pp : pn, l == 4 ? r0 : r1, 2 * i + (l - 4));
   }
 }
 
@@ -151,10 +178,9 @@ __device__ __forceinline__ void acc_two(const Accum& acc, int a, const float (&x
 // TransE pair: skge/transe.py:48-165
 // ---------------------------------------------------------------------------
 template <int KM, bool L1>
-__device__ bool transe_pair(const PairArgs& a, int i) {
+__device__ bool transe_pair(const PairArgs& a, int i, const int (&ix)[6]) {
   const int d = a.d;
-  const int sp = uni(a.pos[3 * i]), op = uni(a.pos[3 * i + 1]), pp = uni(a.pos[3 * i + 2]);
-  const int sn = uni(a.neg[3 * i]), on = uni(a.neg[3 * i + 1]), pn = uni(a.neg[3 * i + 2]);
+  const int sp = ix[0], op = ix[1], pp = ix[2], sn = ix[3], on = ix[4], pn = ix[5];
   float es[KM], eo[KM], rp[KM], fs[KM], fo[KM], rn[KM];
   load_row<KM>(a.E, sp, d, es);
   load_row<KM>(a.R, pp, d, rp);
@@ -200,10 +226,9 @@ __device__ bool transe_pair(const PairArgs& a, int i) {
 // HolE pair: skge/hole.py:44-100
 // ---------------------------------------------------------------------------
 template <int KM>
-__device__ bool hole_pair(const PairArgs& a, int i, float* sw) {
+__device__ bool hole_pair(const PairArgs& a, int i, float* sw, const int (&ix)[6]) {
   const int d = a.d;
-  const int sp = uni(a.pos[3 * i]), op = uni(a.pos[3 * i + 1]), pp = uni(a.pos[3 * i + 2]);
-  const int sn = uni(a.neg[3 * i]), on = uni(a.neg[3 * i + 1]), pn = uni(a.neg[3 * i + 2]);
+  const int sp = ix[0], op = ix[1], pp = ix[2], sn = ix[3], on = ix[4], pn = ix[5];
   const int stride = 64 * KM;
   float* sEs = sw;
   float* sEo = sw + stride;
@@ -272,10 +297,9 @@ __device__ bool hole_pair(const PairArgs& a, int i, float* sw) {
 // RESCAL pair: skge/rescal.py:78-139 (entity part; dW in k_rescal_wgrad)
 // ---------------------------------------------------------------------------
 template <int KM>
-__device__ bool rescal_pair(const PairArgs& a, int i, float* sw) {
+__device__ bool rescal_pair(const PairArgs& a, int i, float* sw, const int (&ix)[6]) {
   const int d = a.d;
-  const int sp = uni(a.pos[3 * i]), op = uni(a.pos[3 * i + 1]), pp = uni(a.pos[3 * i + 2]);
-  const int sn = uni(a.neg[3 * i]), on = uni(a.neg[3 * i + 1]), pn = uni(a.neg[3 * i + 2]);
+  const int sp = ix[0], op = ix[1], pp = ix[2], sn = ix[3], on = ix[4], pn = ix[5];
   const int stride = 64 * KM;
   float* sEs = sw;
   float* sEo = sw + stride;
@@ -341,15 +365,18 @@ __global__ __launch_bounds__(256) void k_pair_grad(PairArgs a) {
   float* sw = smem + wave * 6 * 64 * KM;
   int nv = 0;
   for (int i = blockIdx.x * wpb + wave; i < a.P; i += gridDim.x * wpb) {
+    const int ix[6] = {uni(a.pos[3 * i]), uni(a.pos[3 * i + 1]), uni(a.pos[3 * i + 2]),
+                       uni(a.neg[3 * i]), uni(a.neg[3 * i + 1]), uni(a.neg[3 * i + 2])};
     bool v;
     if (MODEL == TRANSE_L1)
-      v = transe_pair<KM, true>(a, i);
+      v = transe_pair<KM, true>(a, i, ix);
     else if (MODEL == TRANSE_L2)
-      v = transe_pair<KM, false>(a, i);
+      v = transe_pair<KM, false>(a, i, ix);
     else if (MODEL == HOLE)
-      v = hole_pair<KM>(a, i, sw);
+      v = hole_pair<KM>(a, i, sw, ix);
     else
-      v = rescal_pair<KM>(a, i, sw);
+      v = rescal_pair<KM>(a, i, sw, ix);
+    if (a.record) commit_pair(a.accE, MODEL == RESCAL ? nullptr : &a.accR, v, ix, i);
     nv += v ? 1 : 0;
   }
   if (lane_id() == 0 && nv && a.nviol) atomicAdd(a.nviol, nv);
@@ -397,7 +424,7 @@ __global__ __launch_bounds__(256) void k_triple_grad(PairArgs a) {
       logistic(y, score, &li, &fs);
       scale<KM>(x, c, fs);  // R: fs ccorr(E[s],E[o])   hole.py:32
       acc_row<KM>(a.accR, p, x, d);
-      if (lane_id() == 0) acc_count(a.accR, p, 1);
+      if (lane_id() == 2) commit_slot(a.accR, p, 1, i);
       ccorr_lds<KM>(sRp, sEo, d, t);  // E[s]: fs ccorr(R[p],E[o])   hole.py:37
       scale<KM>(x, t, fs);
       cconv_lds<KM>(sEs, sRp, d, t);  // E[o]: fs cconv(E[s],R[p])   hole.py:38
@@ -420,6 +447,10 @@ __global__ __launch_bounds__(256) void k_triple_grad(PairArgs a) {
       scale<KM>(yv, ew, fs);
       acc_two<KM>(a.accE, s, x, o, yv, d);
       if (lane_id() == 0 && a.coef) a.coef[i] = fs;
+    }
+    {
+      const int l = lane_id();  // entity occurrences (s, o): slots 2i, 2i+1
+      if (l < 2) commit_slot(a.accE, l == 0 ? s : o, s == o ? (l == 0 ? 2 : 0) : 1, 2 * i + l);
     }
     if (lane_id() == 0 && a.pscore) a.pscore[i] = score;
     lsum += li;
@@ -505,6 +536,7 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad(const float* __restrict__ 
       }
     }
   }
+  if (tt == 0 && t == 0) accW.touched[p] = total > 0 ? p : -1;   // slot p
   if (total == 0) return;
   float* out = accW.sum + (size_t)p * d * d;
 #pragma unroll
@@ -514,11 +546,7 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad(const float* __restrict__ 
       const int r = ti * 64 + r0 + x, c = tj * 64 + c0 + y;
       if (r < d && c < d) out[(size_t)r * d + c] = acc[x][y];
     }
-  if (tt == 0 && t == 0) {
-    accW.cnt[p] = total;
-    const int slot = atomicAdd(accW.ntouched, 1);
-    accW.touched[slot] = p;
-  }
+  if (tt == 0 && t == 0) accW.cnt[p] = total;
 }
 
 // ---------------------------------------------------------------------------
@@ -600,6 +628,11 @@ extern "C" int skge_pair_grad(void* stream, int model, int af, const skge_table_
   a.nscore = nscore;
   a.coef = coef;
   a.nviol = nviol;
+  a.record = margin == -INFINITY ? 0 : 1;   // -inf margin: score only
+  if (a.record) {
+    if ((rc = check_slots(ent, 4ll * P, "ent"))) return rc;
+    if (model != SKGE_RESCAL && (rc = check_slots(rel, 2ll * P, "rel"))) return rc;
+  }
   const int km = km_for(d);
   hipStream_t st = as_stream(stream);
   switch (model) {
@@ -632,6 +665,9 @@ extern "C" int skge_triple_grad(void* stream, int model, const skge_table_t* ent
   a.pscore = score;
   a.coef = coef;
   a.loss = loss;
+  a.record = 1;
+  if ((rc = check_slots(ent, 2ll * T, "ent"))) return rc;
+  if (model == SKGE_HOLE && (rc = check_slots(rel, T, "rel"))) return rc;
   const int km = km_for(d);
   hipStream_t st = as_stream(stream);
   if (model == SKGE_HOLE) return launch_pair<HOLE>(a, km, st, true);
@@ -643,8 +679,8 @@ extern "C" int skge_rescal_wgrad(void* stream, const skge_table_t* ent, const sk
                                  const int* trip_b, const float* coef_b, int n_b) {
   int rc = check_model_tables(SKGE_RESCAL, ent, rel, d);
   if (rc) return rc;
-  SKGE_CHECK_ARG(rel->acc_sum && rel->acc_cnt && rel->acc_touched && rel->acc_ntouched,
-                 "W accumulator missing");
+  SKGE_CHECK_ARG(rel->acc_sum && rel->acc_cnt && rel->acc_touched, "W accumulator missing");
+  if ((rc = check_slots(rel, rel->rows, "W"))) return rc;
   SKGE_CHECK_ARG(n_a >= 0 && n_b >= 0, "negative item count");
   if (n_a + n_b == 0) return SKGE_OK;
   const int nt = (d + 63) / 64;

@@ -55,7 +55,6 @@ inline Accum accum_of(const skge_table_t* t) {
   a.sum = t->acc_sum;
   a.cnt = t->acc_cnt;
   a.touched = t->acc_touched;
-  a.ntouched = t->acc_ntouched;
   a.width = t->width;
   return a;
 }
@@ -65,9 +64,15 @@ inline int check_table(const skge_table_t* t, const char* name, bool need_acc) {
   SKGE_CHECK_ARG(t->param != nullptr, "%s: param is NULL", name);
   SKGE_CHECK_ARG(t->rows > 0 && t->width > 0, "%s: bad shape %d x %d", name, t->rows, t->width);
   if (need_acc) {
-    SKGE_CHECK_ARG(t->acc_sum && t->acc_cnt && t->acc_touched && t->acc_ntouched,
+    SKGE_CHECK_ARG(t->acc_sum && t->acc_cnt && t->acc_touched,
                    "%s: accumulator buffers missing", name);
   }
+  return SKGE_OK;
+}
+
+inline int check_slots(const skge_table_t* t, long long nslots, const char* name) {
+  SKGE_CHECK_ARG(nslots >= 0 && nslots <= t->touched_cap,
+                 "%s: %lld touched slots needed, capacity %d", name, nslots, t->touched_cap);
   return SKGE_OK;
 }
 

@@ -13,7 +13,6 @@ struct TableDev {
   float* P;
   float* A;
   Accum acc;
-  int* sync;
   int rows, width, opt, post;
   float lr, rin, rout, fdiv;
   const int* gate;
@@ -24,7 +23,6 @@ static TableDev table_dev(const skge_table_t* t) {
   d.P = t->param;
   d.A = t->state;
   d.acc = accum_of(t);
-  d.sync = t->sync;
   d.rows = t->rows;
   d.width = t->width;
   d.opt = t->opt;
@@ -39,6 +37,7 @@ static TableDev table_dev(const skge_table_t* t) {
 
 struct Tables4 {
   TableDev t[4];
+  int nslots[4];
   int n;
 };
 
@@ -90,12 +89,11 @@ __device__ __forceinline__ void update_row(const TableDev& t, int row, const flo
 
 // g = (sum + rin*P) / div + rout*P; then reset the accumulator row
 template <int KM>
-__device__ __forceinline__ void mean_row(const TableDev& t, int row, float (&g)[KM]) {
+__device__ __forceinline__ void mean_row(const TableDev& t, int row, int c, float (&g)[KM]) {
   const int l = lane_id();
   const int w = t.width;
   float* srow = t.acc.sum + (size_t)row * w;
   const float* prow = t.P + (size_t)row * w;
-  const int c = __builtin_amdgcn_readfirstlane(t.acc.cnt[row]);
   const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
   const bool reg = t.rin != 0.0f || t.rout != 0.0f;
 #pragma unroll
@@ -117,61 +115,47 @@ __device__ __forceinline__ void mean_row(const TableDev& t, int row, float (&g)[
   if (l == 0) t.acc.cnt[row] = 0;
 }
 
-__device__ __forceinline__ void last_block_reset(const Tables4& ts) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const int old = atomicAdd(ts.t[0].sync, 1);
-    if (old == (int)gridDim.x - 1) {
-      for (int i = 0; i < ts.n; ++i) *ts.t[i].acc.ntouched = 0;
-      *ts.t[0].sync = 0;
-      __threadfence();
-    }
-  }
-}
-
-// fused apply: one wavefront per touched row of any of the tables
+// fused apply: one wavefront per touched slot of any of the tables
 template <int KM>
 __global__ __launch_bounds__(256) void k_apply(Tables4 ts) {
   const int wpb = blockDim.x >> 6;
   const int w0 = blockIdx.x * wpb + (threadIdx.x >> 6);
   const int nw = gridDim.x * wpb;
-  int n[4], gate[4];
   int total = 0;
-  for (int i = 0; i < 4; ++i) {
-    n[i] = i < ts.n ? *ts.t[i].acc.ntouched : 0;
-    gate[i] = (i < ts.n && ts.t[i].gate) ? *ts.t[i].gate : 1;
-    total += n[i];
-  }
+  for (int i = 0; i < ts.n; ++i) total += ts.nslots[i];
   for (int w = w0; w < total; w += nw) {
     int ti = 0, r = w;
-    while (r >= n[ti]) {
-      r -= n[ti];
+    while (r >= ts.nslots[ti]) {
+      r -= ts.nslots[ti];
       ++ti;
     }
     const TableDev& t = ts.t[ti];
     const int row = __builtin_amdgcn_readfirstlane(t.acc.touched[r]);
+    if (row < 0) continue;
+    const int c = __builtin_amdgcn_readfirstlane(t.acc.cnt[row]);
+    if (c == 0) continue;   // stale slot (accumulator already consumed)
     float g[KM];
-    mean_row<KM>(t, row, g);
-    if (gate[ti]) update_row<KM>(t, row, g);
+    mean_row<KM>(t, row, c, g);
+    if (t.gate == nullptr || *t.gate != 0) update_row<KM>(t, row, g);
   }
-  last_block_reset(ts);
 }
 
-// wide rows (RESCAL W): elementwise mean + update, no projection
-__global__ __launch_bounds__(256) void k_apply_wide(Tables4 ts) {
-  const TableDev& t = ts.t[0];
-  const long long n = *t.acc.ntouched;
+// wide rows (RESCAL W): elementwise mean + update, no projection; the counts
+// are cleared afterwards by k_zero_counts_slots
+__global__ __launch_bounds__(256) void k_apply_wide(TableDev t, int nslots) {
   const int gate = t.gate ? *t.gate : 1;
   const long long w = t.width;
-  const long long total = n * w;
+  const long long total = (long long)nslots * w;
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
     const long long ti = idx / w;
     const long long e = idx - ti * w;
     const int row = t.acc.touched[ti];
+    if (row < 0) continue;
+    const int c = t.acc.cnt[row];
+    if (c == 0) continue;
     const size_t off = (size_t)row * w + e;
-    const float div = t.fdiv > 0.0f ? t.fdiv : (float)t.acc.cnt[row];
+    const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
     const float pv = t.P[off];
     const float g = (t.acc.sum[off] + t.rin * pv) / div + t.rout * pv;
     t.acc.sum[off] = 0.0f;
@@ -185,17 +169,13 @@ __global__ __launch_bounds__(256) void k_apply_wide(Tables4 ts) {
       }
     }
   }
-  // counts are read by every element of a row: clear them once all blocks are done
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const int old = atomicAdd(t.sync, 1);
-    if (old == (int)gridDim.x - 1) {
-      for (long long i = 0; i < n; ++i) t.acc.cnt[t.acc.touched[i]] = 0;
-      *t.acc.ntouched = 0;
-      *t.sync = 0;
-      __threadfence();
-    }
+}
+
+__global__ void k_zero_counts_slots(int* __restrict__ cnt, const int* __restrict__ touched,
+                                    int nslots) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += gridDim.x * blockDim.x) {
+    const int row = touched[i];
+    if (row >= 0) cnt[row] = 0;
   }
 }
 
@@ -313,8 +293,9 @@ __global__ __launch_bounds__(256) void k_gather_mean(TableDev t, const int* __re
   const int l = lane_id();
   for (int i = blockIdx.x * wpb + (threadIdx.x >> 6); i < U; i += gridDim.x * wpb) {
     const int row = __builtin_amdgcn_readfirstlane(idx[i]);
+    const int c = __builtin_amdgcn_readfirstlane(t.acc.cnt[row]);
     float g[KM];
-    mean_row<KM>(t, row, g);
+    mean_row<KM>(t, row, c, g);
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
       const int e = l + 64 * k;
@@ -341,34 +322,22 @@ __global__ __launch_bounds__(256) void k_gather_mean_wide(TableDev t, const int*
   }
 }
 
-// zero the counts of the listed rows (and the touched counter)
+// zero the counts of the listed rows
 __global__ void k_zero_counts(int* __restrict__ cnt, const int* __restrict__ idx,
-                              const int* __restrict__ Up, int* __restrict__ ntouched) {
+                              const int* __restrict__ Up) {
   const int U = *Up;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < U; i += gridDim.x * blockDim.x)
     cnt[idx[i]] = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *ntouched = 0;
 }
 
-// reset: zero every touched row's sum and count (model returned None)
-__global__ __launch_bounds__(256) void k_reset(TableDev t) {
-  const long long n = *t.acc.ntouched;
+// reset: zero every touched row's sum (counts by k_zero_counts_slots)
+__global__ __launch_bounds__(256) void k_reset(TableDev t, int nslots) {
   const long long w = t.width;
-  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n * w;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < (long long)nslots * w;
        q += (long long)gridDim.x * blockDim.x) {
     const long long i = q / w;
-    t.acc.sum[(size_t)t.acc.touched[i] * w + (q - i * w)] = 0.0f;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const int old = atomicAdd(t.sync, 1);
-    if (old == (int)gridDim.x - 1) {
-      for (long long i = 0; i < n; ++i) t.acc.cnt[t.acc.touched[i]] = 0;
-      *t.acc.ntouched = 0;
-      *t.sync = 0;
-      __threadfence();
-    }
+    const int row = t.acc.touched[i];
+    if (row >= 0) t.acc.sum[(size_t)row * w + (q - i * w)] = 0.0f;
   }
 }
 
@@ -425,21 +394,23 @@ extern "C" int skge_accum_collect(void* stream, const skge_table_t* t, int* idx_
       hipLaunchKernelGGL(k_gather_mean_wide, dim3(grid_for_elems((long long)t->rows * t->width)),
                          dim3(256), 0, st, td, idx_out, U_out, g_out);
       hipLaunchKernelGGL(k_zero_counts, dim3(grid_for_elems(t->rows)), dim3(256), 0, st,
-                         t->acc_cnt, idx_out, U_out, t->acc_ntouched);
+                         t->acc_cnt, idx_out, U_out);
   }
 #undef SKGE_GM
-  if (km != 0) SKGE_CHECK_HIP(hipMemsetAsync(t->acc_ntouched, 0, sizeof(int), st));
   SKGE_CHECK_LAUNCH("collect");
   return SKGE_OK;
 }
 
-extern "C" int skge_accum_reset(void* stream, const skge_table_t* t, int max_touched) {
+extern "C" int skge_accum_reset(void* stream, const skge_table_t* t, int nslots) {
   int rc = check_table(t, "table", true);
   if (rc) return rc;
-  SKGE_CHECK_ARG(t->sync, "sync word missing");
-  const long long bound = max_touched > 0 ? max_touched : t->rows;
-  hipLaunchKernelGGL(k_reset, dim3(grid_for_elems(bound * t->width)), dim3(256), 0,
-                     as_stream(stream), table_dev(t));
+  if ((rc = check_slots(t, nslots, "table"))) return rc;
+  if (nslots == 0) return SKGE_OK;
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(k_reset, dim3(grid_for_elems((long long)nslots * t->width)), dim3(256), 0, st,
+                     table_dev(t), nslots);
+  hipLaunchKernelGGL(k_zero_counts_slots, dim3(grid_for_elems(nslots)), dim3(256), 0, st,
+                     t->acc_cnt, t->acc_touched, nslots);
   SKGE_CHECK_LAUNCH("reset");
   return SKGE_OK;
 }
@@ -477,35 +448,37 @@ extern "C" int skge_update_rows(void* stream, const skge_table_t* t, const float
 }
 
 extern "C" int skge_accum_apply(void* stream, const skge_table_t* tables, int ntables,
-                                int max_touched) {
-  SKGE_CHECK_ARG(tables && ntables >= 1 && ntables <= 4, "1..4 tables");
+                                const int* nslots) {
+  SKGE_CHECK_ARG(tables && nslots && ntables >= 1 && ntables <= 4, "1..4 tables");
   hipStream_t st = as_stream(stream);
   // narrow tables share one launch; each wide table gets its own
   Tables4 narrow = {};
   int km = 0;
-  long long bound = 0;
+  long long waves = 0;
   for (int i = 0; i < ntables; ++i) {
     const skge_table_t* t = tables + i;
     int rc = check_table(t, "table", true);
     if (rc) return rc;
-    SKGE_CHECK_ARG(t->sync, "sync word missing");
+    if ((rc = check_slots(t, nslots[i], "table"))) return rc;
     SKGE_CHECK_ARG(t->opt == SKGE_SGD || t->state, "AdaGrad needs state");
+    SKGE_CHECK_ARG(t->post >= 0 && t->post <= 2, "unknown post %d", t->post);
+    if (nslots[i] == 0) continue;
     const int k = km_for(t->width);
-    const long long b = max_touched > 0 ? (max_touched < t->rows ? max_touched : t->rows) : t->rows;
     if (k == 0) {
       SKGE_CHECK_ARG(t->post == SKGE_POST_NONE, "projection needs width <= 1024");
-      Tables4 one = {};
-      one.t[0] = table_dev(t);
-      one.n = 1;
-      hipLaunchKernelGGL(k_apply_wide, dim3(grid_for_elems(b * t->width)), dim3(256), 0, st, one);
+      hipLaunchKernelGGL(k_apply_wide, dim3(grid_for_elems((long long)nslots[i] * t->width)),
+                         dim3(256), 0, st, table_dev(t), nslots[i]);
+      hipLaunchKernelGGL(k_zero_counts_slots, dim3(grid_for_elems(nslots[i])), dim3(256), 0, st,
+                         t->acc_cnt, t->acc_touched, nslots[i]);
     } else {
-      narrow.t[narrow.n++] = table_dev(t);
+      narrow.t[narrow.n] = table_dev(t);
+      narrow.nslots[narrow.n++] = nslots[i];
       if (k > km) km = k;
-      bound += b;
+      waves += nslots[i];
     }
   }
   if (narrow.n) {
-    const int gw = grid_for_waves(bound);
+    const int gw = grid_for_waves(waves);
 #define SKGE_AP(K) \
   case K: hipLaunchKernelGGL((k_apply<K>), dim3(gw), dim3(256), 0, st, narrow); break;
     switch (km) {
@@ -537,10 +510,6 @@ extern "C" int skge_pair_step(void* stream, int model, int af, const skge_table_
   skge_table_t t[2] = {*ent, *rel};
   t[0].gate = nviol;
   t[1].gate = nviol;
-  if (model == SKGE_RESCAL) {
-    rc = skge_accum_apply(stream, &t[0], 1, 4 * P);
-    if (rc) return rc;
-    return skge_accum_apply(stream, &t[1], 1, 2 * P);
-  }
-  return skge_accum_apply(stream, t, 2, 4 * P);
+  const int ns[2] = {4 * P, model == SKGE_RESCAL ? rel->rows : 2 * P};
+  return skge_accum_apply(stream, t, 2, ns);
 }

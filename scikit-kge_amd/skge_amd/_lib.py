@@ -29,10 +29,9 @@ c_sz = ctypes.c_size_t
 class SkgeTable(ctypes.Structure):
     """Mirror of skge_table_t."""
     _fields_ = [("param", c_p), ("state", c_p), ("acc_sum", c_p), ("acc_cnt", c_p),
-                ("acc_touched", c_p), ("acc_ntouched", c_p), ("sync", c_p),
-                ("rows", c_i), ("width", c_i), ("opt", c_i), ("post", c_i),
-                ("lr", c_f), ("rin", c_f), ("rout", c_f), ("fixed_div", c_f),
-                ("gate", c_p)]
+                ("acc_touched", c_p), ("rows", c_i), ("width", c_i), ("touched_cap", c_i),
+                ("opt", c_i), ("post", c_i), ("lr", c_f), ("rin", c_f), ("rout", c_f),
+                ("fixed_div", c_f), ("gate", c_p)]
 
 
 T_P = ctypes.POINTER(SkgeTable)
@@ -47,8 +46,9 @@ SIGNATURES = {
     "skge_collect_workspace_bytes": (c_sz, [c_i]),
     "skge_accum_collect": (c_i, [c_p, T_P, c_p, c_p, c_p, c_p, c_sz]),
     "skge_accum_reset": (c_i, [c_p, T_P, c_i]),
+    "skge_triple_set_bytes": (c_sz, [c_i64]),
     "skge_update_rows": (c_i, [c_p, T_P, c_p, c_p, c_i]),
-    "skge_accum_apply": (c_i, [c_p, T_P, c_i, c_i]),
+    "skge_accum_apply": (c_i, [c_p, T_P, c_i, ctypes.POINTER(c_i)]),
     "skge_pair_step": (c_i, [c_p, c_i, c_i, T_P, T_P, c_i, c_p, c_p, c_i, c_f, c_p, c_p]),
     "skge_triple_set_build": (c_i, [c_p, c_p, c_i64, c_p, c_i64]),
     "skge_transe_sample_grad": (c_i, [c_p, c_i, T_P, T_P, c_i, c_p, c_i64, c_p, c_i64, c_i64, c_i,
@@ -106,6 +106,10 @@ def require_gpu():
 def stream_ptr(stream=None):
     s = stream if stream is not None else torch.cuda.current_stream()
     return c_p(s.cuda_stream)
+
+
+def int_array(*vals):
+    return (c_i * len(vals))(*vals)
 
 
 def ptr(t):

@@ -114,14 +114,14 @@ class Model(object):
     def _reg(self, mode):
         return {"E": (0.0, 0.0, 0.0), self.rel_id: (0.0, 0.0, 0.0)}
 
-    def _tables(self, mode, updaters=None, gate=None):
-        """skge_table_t for E and R/W, with the accumulator and (optionally)
-        the updater fields filled."""
+    def _tables(self, mode, updaters=None, gate=None, slots=(0, 0)):
+        """skge_table_t for E and R/W, with the accumulator (grown to hold
+        `slots` touched slots) and, optionally, the updater fields."""
         out = []
         reg = self._reg(mode)
-        for pid in ("E", self.rel_id):
+        for pid, ns in zip(("E", self.rel_id), slots):
             rin, rout, fdiv = reg[pid]
-            acc = self.accumulator(pid)
+            acc = self.accumulator(pid).ensure_slots(ns)
             if updaters is not None:
                 t = updaters[pid].table(acc, rin=rin, rout=rout, fixed_div=fdiv, gate=gate)
             else:
@@ -162,6 +162,13 @@ class Model(object):
     def _kernel_model(self):
         return self.model_code
 
+    def _pair_slots(self, P):
+        """touched slots per table written by skge_pair_grad (+ wgrad)"""
+        return (4 * P, self.params[self.rel_id].rows if self.rel_id == "W" else 2 * P)
+
+    def _triple_slots(self, T):
+        return (2 * T, self.params[self.rel_id].rows if self.rel_id == "W" else T)
+
     def _pairwise_gradients(self, pxs, nxs):
         """Pairwise margin gradients (see the subclass docstring for the
         reference lines).  Returns None when no pair violates the margin,
@@ -174,7 +181,7 @@ class Model(object):
         self._pscore = torch.empty(P, dtype=torch.float32, device=dev)
         self._nscore = torch.empty(P, dtype=torch.float32, device=dev)
         coef = torch.empty(2 * P, dtype=torch.float32, device=dev) if self.rel_id == "W" else None
-        te, tr = self._tables("pairwise")
+        te, tr = self._tables("pairwise", slots=self._pair_slots(P))
         L.check(L.lib().skge_pair_grad(L.stream_ptr(), self._kernel_model(), self._af_code(), te,
                                        tr, self.d, L.ptr(pos), L.ptr(neg), P, float(self.margin),
                                        L.ptr(self._pscore), L.ptr(self._nscore), L.ptr(coef),
@@ -197,7 +204,7 @@ class Model(object):
         loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self._score = torch.empty(T, dtype=torch.float32, device=dev)
         coef = torch.empty(T, dtype=torch.float32, device=dev)
-        te, tr = self._tables("logistic")
+        te, tr = self._tables("logistic", slots=self._triple_slots(T))
         L.check(L.lib().skge_triple_grad(L.stream_ptr(), self._kernel_model(), te, tr, self.d,
                                          L.ptr(trip), L.ptr(ys), T, L.ptr(self._score),
                                          L.ptr(coef), L.ptr(loss)), "triple_grad")
@@ -216,7 +223,7 @@ class Model(object):
         coef = None
         if self.rel_id == "W":
             coef = torch.empty(2 * P, dtype=torch.float32, device=dev)
-        te, tr = self._tables("pairwise", updaters, gate=nviol)
+        te, tr = self._tables("pairwise", updaters, gate=nviol, slots=self._pair_slots(P))
         L.check(L.lib().skge_pair_step(L.stream_ptr(), self._kernel_model(), self._af_code(), te,
                                        tr, self.d, L.ptr(pos), L.ptr(neg), P, float(self.margin),
                                        L.ptr(coef), L.ptr(nviol)), "pair_step")
@@ -225,7 +232,8 @@ class Model(object):
         dev = self.device
         T = trip.shape[0]
         coef = torch.empty(T, dtype=torch.float32, device=dev)
-        te, tr = self._tables("logistic", updaters)
+        slots = self._triple_slots(T)
+        te, tr = self._tables("logistic", updaters, slots=slots)
         lib = L.lib()
         st = L.stream_ptr()
         L.check(lib.skge_triple_grad(st, self._kernel_model(), te, tr, self.d, L.ptr(trip),
@@ -233,11 +241,8 @@ class Model(object):
         if self.rel_id == "W":
             L.check(lib.skge_rescal_wgrad(st, te, tr, self.d, L.ptr(trip), L.ptr(coef), T, None,
                                           None, 0), "rescal_wgrad")
-            L.check(lib.skge_accum_apply(st, te, 1, 2 * T), "apply E")
-            L.check(lib.skge_accum_apply(st, tr, 1, T), "apply W")
-        else:
-            arr = (L.SkgeTable * 2)(te, tr)
-            L.check(lib.skge_accum_apply(st, arr, 2, 2 * T), "apply")
+        arr = (L.SkgeTable * 2)(te, tr)
+        L.check(lib.skge_accum_apply(st, arr, 2, L.int_array(*slots)), "apply")
 
 
 class StochasticTrainer(object):
@@ -410,7 +415,7 @@ class PairwiseStochasticTrainer(StochasticTrainer):
 
     def _pre_epoch(self):
         self.nviolations = 0
-        if self.samplef is None:
+        if self.samplef is None and not self.device_loop:
             shuffle(self.pxs)
             shuffle(self.nxs)
 

@@ -27,8 +27,9 @@ class DeviceKG(object):
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.trip = to_device_triples(xs, dev)
         self.T = int(self.trip.shape[0])
-        self.capacity = _next_pow2(max(2 * self.T, 2))
-        self.slots = torch.empty(self.capacity * 4, dtype=torch.int32, device=dev)
+        self.capacity = _next_pow2(max(2 * self.T, 4))
+        nbytes = int(L.lib().skge_triple_set_bytes(self.capacity))
+        self.slots = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         L.check(L.lib().skge_triple_set_build(L.stream_ptr(stream), L.ptr(self.trip), self.T,
                                               L.ptr(self.slots), self.capacity), "triple set build")
 
@@ -48,8 +49,9 @@ class EpochRunner(object):
         self.epoch_key = torch.zeros(1, dtype=torch.int64, device=dev)
         self.nviol_total = nviol_total if nviol_total is not None else \
             torch.zeros(1, dtype=torch.int32, device=dev)
-        self.te = updaters["E"].table(model.accumulator("E"))
-        self.tr = updaters["R"].table(model.accumulator("R"))
+        bs = kg.T // nbatches
+        self.te = updaters["E"].table(model.accumulator("E").ensure_slots(4 * bs))
+        self.tr = updaters["R"].table(model.accumulator("R").ensure_slots(bs))
         self.nbatches = nbatches
         torch.cuda.current_stream().synchronize()
         lib = L.lib()

@@ -181,8 +181,8 @@ def table_struct(param, state=None, acc=None, opt=L.SKGE_SGD, post=L.SKGE_POST_N
     t.state = L.ptr(state)
     if acc is not None:
         t.acc_sum, t.acc_cnt = L.ptr(acc.sum), L.ptr(acc.cnt)
-        t.acc_touched, t.acc_ntouched = L.ptr(acc.touched), L.ptr(acc.ntouched)
-        t.sync = L.ptr(acc.sync)
+        t.acc_touched = L.ptr(acc.touched)
+        t.touched_cap = acc.touched.numel()
     t.rows = param.rows
     t.width = param.width
     t.opt, t.post, t.lr = opt, post, lr
@@ -204,15 +204,21 @@ def _project_device(M, idx, code):
 
 
 class Accumulator(object):
-    """Device segment-sum accumulator of one table (see skge_table_t)."""
+    """Device segment-sum accumulator of one table (see skge_table_t): dense
+    fp32 sums, occurrence counts and the fixed-slot touched records."""
 
-    def __init__(self, rows, width, device):
+    def __init__(self, rows, width, device, slots=1024):
         self.rows, self.width = rows, width
         self.sum = torch.zeros(rows * width, dtype=torch.float32, device=device)
         self.cnt = torch.zeros(rows, dtype=torch.int32, device=device)
-        self.touched = torch.zeros(rows, dtype=torch.int32, device=device)
-        self.ntouched = torch.zeros(1, dtype=torch.int32, device=device)
-        self.sync = torch.zeros(1, dtype=torch.int32, device=device)
+        self.touched = torch.full((max(slots, 1),), -1, dtype=torch.int32, device=device)
+
+    def ensure_slots(self, n):
+        """Grow the touched-slot array to hold n slots (before building tables)."""
+        if n > self.touched.numel():
+            self.touched = torch.full((max(n, 2 * self.touched.numel()),), -1, dtype=torch.int32,
+                                      device=self.sum.device)
+        return self
 
 
 # --------------------------------------------------------------------------

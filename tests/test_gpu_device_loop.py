@@ -71,8 +71,8 @@ def test_sampler_kernel_parity_with_oracle_replay():
     negs = torch.full((count, 2), -7, dtype=torch.int32, device=dev)
     perm = torch.empty(kg.T, dtype=torch.int64, device=dev)
     nviol = torch.zeros(1, dtype=torch.int32, device=dev)
-    te = upd["E"].table(m.accumulator("E"))
-    tr = upd["R"].table(m.accumulator("R"))
+    te = upd["E"].table(m.accumulator("E").ensure_slots(4 * count))
+    tr = upd["R"].table(m.accumulator("R").ensure_slots(count))
     lib = L.lib()
     st = L.stream_ptr()
     L.check(lib.skge_epoch_permutation(st, kg.T, 99, L.ptr(key), L.ptr(perm), kg.T))
@@ -80,7 +80,7 @@ def test_sampler_kernel_parity_with_oracle_replay():
                                         kg.capacity, start, count, 99, L.ptr(key), float(m.margin),
                                         100, L.ptr(nviol), None, L.ptr(negs)))
     arr = (L.SkgeTable * 2)(te, tr)
-    L.check(lib.skge_accum_apply(st, arr, 2, 4 * count))
+    L.check(lib.skge_accum_apply(st, arr, 2, L.int_array(4 * count, count)))
     negs = negs.cpu().numpy()
     pidx = perm.cpu().numpy()[start:start + count]
     pos_list, neg_list = [], []
@@ -113,8 +113,8 @@ def test_sampler_mode_balance():
     dev = m.device
     key = torch.tensor([1], dtype=torch.int64, device=dev)
     negs = torch.empty((kg.T, 2), dtype=torch.int32, device=dev)
-    te = upd["E"].table(m.accumulator("E"))
-    tr = upd["R"].table(m.accumulator("R"))
+    te = upd["E"].table(m.accumulator("E").ensure_slots(4 * kg.T))
+    tr = upd["R"].table(m.accumulator("R").ensure_slots(kg.T))
     L.check(L.lib().skge_transe_sample_grad(L.stream_ptr(), 1, te, tr, m.d, L.ptr(kg.trip), kg.T,
                                             L.ptr(kg.slots), kg.capacity, 0, kg.T, 7, L.ptr(key),
                                             -1e9, 100, None, None, L.ptr(negs)))
@@ -138,7 +138,6 @@ def test_runner_small_two_epochs_invariants():
     nv = int(tr.nviol_total.item())
     assert 0 < nv <= 2 * 2 * kg.T
     for acc in m._acc.values():
-        assert int(acc.ntouched.item()) == 0
         assert int(acc.cnt.abs().sum().item()) == 0
         assert float(acc.sum.abs().sum().item()) == 0.0
     assert int(tr.epoch_key.item()) == 2
@@ -167,8 +166,8 @@ def test_runner_wn18_full_size_properties(l1):
     assert 0 < nv <= 2 * kg.T
     assert not np.allclose(np.asarray(m.R), R0)
     for acc in m._acc.values():
-        assert int(acc.ntouched.item()) == 0
         assert int(acc.cnt.abs().sum().item()) == 0
+        assert float(acc.sum.abs().sum().item()) == 0.0
 
 
 def test_trainer_device_loop_fit():
