@@ -102,6 +102,8 @@ def main():
     ap.add_argument("--d", type=int, default=200)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--acc", choices=["auto", "f32"], default="auto",
+                    help="accumulator encoding (auto: exact packed int16x2 for TransE-L1)")
     args = ap.parse_args()
 
     import torch
@@ -125,7 +127,8 @@ def main():
     model.add_hyperparam("margin", 2.0)
     upd = {pid: S.AdaGrad(p, 0.1) for pid, p in model.params.items()}
     kg = DeviceKG(trip, dev)
-    runner = EpochRunner(model, upd, kg, nbatches=nb, seed=1234 + rank)
+    runner = EpochRunner(model, upd, kg, nbatches=nb, seed=1234 + rank,
+                         force_f32=args.acc == "f32")
     st = runner.stream
     init = {pid: p.data.clone() for pid, p in model.params.items()}
 
@@ -203,6 +206,7 @@ def main():
                             for n, v in prof["kernels"].items()},
                 "step_algorithmic_GB_s": round(prof["epoch_bytes"] / (elapsed / args.steps) / 1e9, 1),
                 "launches_per_step": runner.nlaunches,
+                "accumulator": "int16x2 exact" if runner.packed else "fp32",
             },
         }
         print(json.dumps(line))
@@ -218,17 +222,16 @@ def kernel_profile(model, upd, kg, nb, d, st, runner):
     from skge_amd import _lib as L
     lib = L.lib()
     dev = model.device
-    bs = kg.T // nb
-    te = upd["E"].table(model.accumulator("E").ensure_slots(4 * bs))
-    tr = upd["R"].table(model.accumulator("R").ensure_slots(bs))
+    te, tr = runner.te, runner.tr
     tabs = (L.SkgeTable * 2)(te, tr)
     nviol = torch.zeros(1, dtype=torch.int32, device=dev)
     T = kg.T
+    bs = T // nb
     sp = L.stream_ptr(st)
     times = {"transe_sample_grad": [], "accum_apply": []}
     bytes_ = {"transe_sample_grad": 0.0, "accum_apply": 0.0}
     total = 0.0
-    accE, accR = model.accumulator("E"), model.accumulator("R")
+    accE, accR = runner.accE, runner.accR
     with torch.cuda.stream(st):
         for start in range(0, T, bs):
             cnt = min(bs, T - start)
@@ -240,8 +243,8 @@ def kernel_profile(model, upd, kg, nb, d, st, runner):
                                                 2.0, 100, L.ptr(nviol), None, None))
             e[1].record(st)
             st.synchronize()
-            UE = int((accE.touched[:4 * cnt] >= 0).sum().item())
-            UR = int((accR.touched[:cnt] >= 0).sum().item())
+            UE = int((accE.cnt != 0).sum().item())
+            UR = int((accR.cnt != 0).sum().item())
             V = int(nviol.item())
             e[2].record(st)
             L.check(lib.skge_accum_apply(sp, tabs, 2, L.int_array(4 * cnt, cnt)))

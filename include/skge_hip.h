@@ -50,6 +50,15 @@ enum { SKGE_AF_LINEAR = 0, SKGE_AF_SIGMOID = 1, SKGE_AF_TANH = 2, SKGE_AF_RELU =
 enum { SKGE_SGD = 0, SKGE_ADAGRAD = 1 };
 /* post-update projections (skge/param.py:161-174) */
 enum { SKGE_POST_NONE = 0, SKGE_POST_NORMALIZE = 1, SKGE_POST_NORMLESS1 = 2 };
+/* accumulator encodings */
+enum {
+  SKGE_ACC_F32 = 0,    /* acc_sum: fp32 [rows][width] */
+  SKGE_ACC_I16X2 = 1   /* acc_sum: exact integer sums of TransE-L1 sign contributions,
+                          two elements per int32 (elements 2q, 2q+1 in dword q; a
+                          packed add whose halves stay within +-32767) -- used only by
+                          skge_transe_sample_grad with l1 != 0, even width, and
+                          4 * count <= 32767 */
+};
 
 /*
  * One parameter table with its updater state and its segment-sum accumulator.
@@ -71,16 +80,20 @@ enum { SKGE_POST_NONE = 0, SKGE_POST_NORMALIZE = 1, SKGE_POST_NORMLESS1 = 2 };
  *   skge_rescal_wgrad       W:   slot p (all M slots)
  *   skge_transe_sample_grad ent: 4j+{0:s,1:o,2:s',3:o'}     rel: j
  * Consumers (apply / reset) take the slot count of the producing launch.
+ * A narrow table with acc_touched == NULL is applied DENSELY: every row whose
+ * count is non-zero (meant for small tables such as TransE's R; producers
+ * then record nothing for it).
  */
 typedef struct skge_table {
   float *param;        /* [rows][width] */
   float *state;        /* AdaGrad accumulator p2 [rows][width]; NULL for SGD */
   float *acc_sum;      /* [rows][width] */
   int *acc_cnt;        /* [rows] */
-  int *acc_touched;    /* [touched_cap] slot -> row or -1 */
+  int *acc_touched;    /* [touched_cap] slot -> row or -1; NULL: dense apply */
   int rows;
   int width;
   int touched_cap;     /* capacity of acc_touched (slots) */
+  int acc_mode;        /* SKGE_ACC_F32 | SKGE_ACC_I16X2 */
   int opt;             /* SKGE_SGD | SKGE_ADAGRAD */
   int post;            /* SKGE_POST_* */
   float lr;

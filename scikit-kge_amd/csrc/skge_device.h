@@ -58,23 +58,36 @@ __device__ __forceinline__ float signf_np(float x) {  // numpy.sign
 // (see skge_table_t in include/skge_hip.h).  Invariant between batches:
 // sum == 0 and cnt == 0.
 struct Accum {
-  float* sum;
+  float* sum;      // fp32 [rows][width], or int32 [rows][width/2] in ACC_I16X2 mode
   int* cnt;
-  int* touched;
+  int* touched;    // nullptr: dense table (no slot records)
   int width;
+  int mode;
 };
 
-// Count `c` occurrences of `row` and record it in `slot` if this was the
-// first count of the row in the batch (else -1).  Called by one lane per
-// (row, slot); different lanes' calls are independent, so a wave issues all
-// its returning atomics at once (one round trip, not one per row).
+enum AccMode : int { ACC_F32 = 0, ACC_I16X2 = 1 };
+
+// Count `c` occurrences of `row` (no-return atomic) and record the row in
+// `slot` (or -1 when c == 0).  Several slots may name the same row; the
+// consumer claims each row once with an atomicExch on its count (k_apply).
+// Called by one lane per (row, slot): a wave's count atomics all issue at
+// once and nothing waits for them.
+__device__ __forceinline__ void commit_slot(int* cnt, int* touched, int row, int c, int slot) {
+  if (c > 0) atomicAdd(cnt + row, c);
+  if (touched) touched[slot] = c > 0 ? row : -1;
+}
 __device__ __forceinline__ void commit_slot(const Accum& a, int row, int c, int slot) {
-  if (c > 0) {
-    const int old = atomicAdd(a.cnt + row, c);
-    a.touched[slot] = old == 0 ? row : -1;
-  } else {
-    a.touched[slot] = -1;
-  }
+  commit_slot(a.cnt, a.touched, row, c, slot);
+}
+
+// 32-bit finaliser (murmur3 fmix32): cheap counter-based hashing
+__device__ __host__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
 }
 
 __device__ __forceinline__ int sel4(int l, int a, int b, int c, int d) {
@@ -92,6 +105,9 @@ __device__ __forceinline__ void acc_row(const Accum& a, int row, const float (&v
   }
 }
 
+// Row gather.  Lanes past the row end load the row's last element (a valid
+// address) and zero it with a select: a conditional load would make hipcc
+// branch around each load and wait for it (serialising the gathers).
 template <int KM>
 __device__ __forceinline__ void load_row(const float* __restrict__ T, int row, int d, float (&v)[KM]) {
   const float* base = T + (size_t)row * d;
@@ -99,7 +115,46 @@ __device__ __forceinline__ void load_row(const float* __restrict__ T, int row, i
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     const int e = l + 64 * k;
-    v[k] = e < d ? base[e] : 0.0f;
+    const float x = base[e < d ? e : d - 1];
+    v[k] = e < d ? x : 0.0f;
+  }
+}
+
+// ---- "pair" row layout: lane l holds elements 128m + 2l + {0, 1} as a float2,
+// m < KP = ceil(d / 128) (d even).  8-byte loads, and an element pair per lane
+// is what one packed int16x2 accumulator dword holds. ----
+template <int KP>
+__device__ __forceinline__ void load_row2(const float* __restrict__ T, int row, int d,
+                                          float2 (&v)[KP]) {
+  const float2* base = reinterpret_cast<const float2*>(T + (size_t)row * d);
+  const int l = lane_id(), h = d >> 1;
+#pragma unroll
+  for (int m = 0; m < KP; ++m) {
+    const int q = 64 * m + l;
+    const float2 x = base[q < h ? q : h - 1];
+    v[m] = q < h ? x : make_float2(0.0f, 0.0f);
+  }
+}
+
+// packed exact add of integer pairs (lo = element 2q, hi = element 2q+1)
+__device__ __forceinline__ int pack_i16x2(float lo, float hi) {
+  return (int)hi * 65536 + (int)lo;
+}
+__device__ __forceinline__ void unpack_i16x2(int x, float& lo, float& hi) {
+  const int l = (int)(short)(x & 0xFFFF);
+  lo = (float)l;
+  hi = (float)((x - l) >> 16);
+}
+
+template <int KP>
+__device__ __forceinline__ void acc_row2_i16(const Accum& a, int row, const float2 (&c)[KP],
+                                             int d) {
+  int* base = reinterpret_cast<int*>(a.sum) + (size_t)row * (d >> 1);
+  const int l = lane_id(), h = d >> 1;
+#pragma unroll
+  for (int m = 0; m < KP; ++m) {
+    const int q = 64 * m + l;
+    if (q < h) atomicAdd(base + q, pack_i16x2(c[m].x, c[m].y));
   }
 }
 

@@ -20,12 +20,14 @@ struct Perm {
   uint64_t key;
 };
 
+// half <= 32, so each half fits 32 bits and the round function is fmix32
 __device__ __host__ __forceinline__ uint64_t feistel(uint64_t x, int half, uint64_t key) {
   const uint64_t mask = (1ull << half) - 1;
   uint64_t L = x >> half, R = x & mask;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const uint64_t F = mix64(R ^ (key + 0x632BE59BD9B4E019ull * (uint64_t)(r + 1))) & mask;
+    const uint32_t kr = (uint32_t)(key >> (16 * r)) ^ (0x9E3779B9u * (uint32_t)(r + 1));
+    const uint64_t F = (uint64_t)fmix32((uint32_t)R ^ kr) & mask;
     const uint64_t nL = R;
     R = L ^ F;
     L = nL;
@@ -94,24 +96,31 @@ struct SampleArgs {
   int* neg_out;
 };
 
-// RandomModeSampler._sample for both modes at once: lanes 0-3 draw tries of
-// mode 0 (corrupt s), lanes 4-7 tries of mode 1 (corrupt o); the first
-// accepted try of each mode wins, as in the sequential loop (sample.py:41-46).
-__device__ __forceinline__ void sample_negatives(const SampleArgs& a, uint64_t skey, long long j,
-                                                 int s, int o, int p, int& neg0, int& neg1) {
+// Counter-based draw `randint(n_ent)` for try `tr` of mode `mode` of global
+// positive j in the epoch keyed by skey.
+__device__ __forceinline__ int draw(uint64_t skey, long long j, int mode, int tr, int n) {
+  uint32_t h = fmix32((uint32_t)j * 0x9E3779B1u ^ (uint32_t)skey);
+  h = fmix32(h ^ (uint32_t)(skey >> 32) ^ ((uint32_t)((unsigned long long)j >> 32) * 0x85EBCA77u) ^
+             ((uint32_t)mode * 0x27D4EB2Fu + (uint32_t)tr * 0x165667B1u));
+  return (int)(((uint64_t)h * (uint32_t)n) >> 32);
+}
+
+// RandomModeSampler._sample (skge/sample.py:41-46), tries first_try.. for the
+// modes still unresolved: lanes 0-3 try mode 0 (corrupt s), lanes 4-7 mode 1
+// (corrupt o), four tries per mode per round; the lowest accepted try wins,
+// as in the sequential loop.
+__device__ __forceinline__ void sample_rest(const SampleArgs& a, uint64_t skey, long long j, int s,
+                                        int o, int p, int first_try, int& neg0, int& neg1) {
   const int l = lane_id();
-  neg0 = -1;
-  neg1 = -1;
-  const uint64_t base = mix64(skey ^ ((uint64_t)j * 0x9E3779B97F4A7C15ull));
-  for (int round = 0; round * 4 < a.ntries; ++round) {
+  for (int round = 0; first_try + round * 4 < a.ntries; ++round) {
     const int mode = (l >> 2) & 1;
-    const int tr = round * 4 + (l & 3);
+    const int tr = first_try + round * 4 + (l & 3);
     const bool want = mode == 0 ? neg0 < 0 : neg1 < 0;
     const bool active = l < 8 && tr < a.ntries && want;
     int c = 0;
     bool ok = false;
     if (active) {
-      c = rand_below(mix64(base + (uint64_t)(mode * 4096 + tr)), a.n_ent);
+      c = draw(skey, j, mode, tr, a.n_ent);
       ok = mode == 0 ? !set_contains(a.set, c, o, p) : !set_contains(a.set, s, c, p);
     }
     const uint64_t m0 = __ballot(active && ok && mode == 0);
@@ -134,6 +143,12 @@ __global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
   for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < a.count; w += gridDim.x * wpb) {
     const long long j = a.start + w;
     const long long t = (long long)perm_index((uint64_t)j, pm);
+    // first tries of both modes do not depend on the positive: load their rows
+    // speculatively, in the same memory round trip as the triple itself
+    const int cand0 = draw(skey, j, 0, 0, a.n_ent), cand1 = draw(skey, j, 1, 0, a.n_ent);
+    float fs[KM], fo[KM];
+    load_row<KM>(a.E, cand0, d, fs);
+    load_row<KM>(a.E, cand1, d, fo);
     const int s = __builtin_amdgcn_readfirstlane(a.trip[3 * t]);
     const int o = __builtin_amdgcn_readfirstlane(a.trip[3 * t + 1]);
     const int p = __builtin_amdgcn_readfirstlane(a.trip[3 * t + 2]);
@@ -141,13 +156,19 @@ __global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
     load_row<KM>(a.E, s, d, es);
     load_row<KM>(a.E, o, d, eo);
     load_row<KM>(a.R, p, d, rp);
-    int neg0, neg1;
-    sample_negatives(a, skey, j, s, o, p, neg0, neg1);
-    neg0 = __builtin_amdgcn_readfirstlane(neg0);
-    neg1 = __builtin_amdgcn_readfirstlane(neg1);
-    float fs[KM], fo[KM];
-    load_row<KM>(a.E, neg0 >= 0 ? neg0 : s, d, fs);
-    load_row<KM>(a.E, neg1 >= 0 ? neg1 : o, d, fo);
+    // rejection test of the first tries (lane 0: (cand0, o, p), lane 1: (s, cand1, p))
+    bool ok = true;
+    if (l < 2) ok = l == 0 ? !set_contains(a.set, cand0, o, p) : !set_contains(a.set, s, cand1, p);
+    const uint64_t okm = __ballot(ok);
+    int neg0 = (okm & 1ull) ? cand0 : -1;
+    int neg1 = (okm & 2ull) ? cand1 : -1;
+    if (neg0 < 0 || neg1 < 0) {   // rare: a first draw hit a training triple
+      sample_rest(a, skey, j, s, o, p, 1, neg0, neg1);
+      neg0 = __builtin_amdgcn_readfirstlane(neg0);
+      neg1 = __builtin_amdgcn_readfirstlane(neg1);
+      if (neg0 >= 0 && neg0 != cand0) load_row<KM>(a.E, neg0, d, fs);
+      if (neg1 >= 0 && neg1 != cand1) load_row<KM>(a.E, neg1, d, fo);
+    }
     float ps = 0.0f, n0 = 0.0f, n1 = 0.0f, gp[KM], g0[KM], g1[KM];
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
@@ -177,8 +198,11 @@ __global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
       // pair 0 lists (sp,op,sn,on) = (s,o,s',o), pair 1 = (s,o,s,o')
       const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
       const int rE = sel4(l, s, o, neg0, neg1);
-      if (l < 4) commit_slot(a.accE, rE, cE, 4 * w + l);
-      else if (l == 4) commit_slot(a.accR, p, 2 * (v0 + v1), w);
+      if (l < 5) {
+        const bool ent = l < 4;
+        commit_slot(ent ? a.accE.cnt : a.accR.cnt, ent ? a.accE.touched : a.accR.touched,
+                    ent ? rE : p, ent ? cE : 2 * (v0 + v1), ent ? 4 * w + l : w);
+      }
     }
     if (v0 + v1 == 0) continue;
     nv += v0 + v1;
@@ -194,11 +218,118 @@ __global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
       c1[k] = -g1[k];
       cr[k] = fv0 * (gp[k] + g0[k]) + fv1 * (gp[k] + g1[k]);
     }
+#ifndef SKGE_ABL_NO_EATOM   // timing-only ablation builds (tools/ablate.sh)
     acc_row<KM>(a.accE, s, cs, d);
     acc_row<KM>(a.accE, o, co, d);
     if (v0) acc_row<KM>(a.accE, neg0, c0, d);
     if (v1) acc_row<KM>(a.accE, neg1, c1, d);
+#endif
+#ifndef SKGE_ABL_NO_RATOM
     acc_row<KM>(a.accR, p, cr, d);
+#endif
+  }
+  if (l == 0 && nv) {
+    if (a.nviol) atomicAdd(a.nviol, nv);
+    if (a.nviol_total) atomicAdd(a.nviol_total, nv);
+  }
+}
+
+// TransE-L1 variant with exact packed int16x2 accumulation (ACC_I16X2) and the
+// pair row layout: the sign contributions are small integers, so two elements
+// share one 32-bit integer atomic -- half the atomic bytes of the fp32 form.
+template <int KP>
+__global__ __launch_bounds__(256) void k_transe_l1_sample_grad_i16(SampleArgs a) {
+  const int wpb = blockDim.x >> 6;
+  const int l = lane_id();
+  const int d = a.d;
+  const uint64_t ek = *a.epoch_key;
+  const Perm pm = {(uint64_t)a.T, a.half, epoch_perm_key(a.seed, ek)};
+  const uint64_t skey = epoch_sample_key(a.seed, ek);
+  int nv = 0;
+  for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < a.count; w += gridDim.x * wpb) {
+    const long long j = a.start + w;
+    const long long t = (long long)perm_index((uint64_t)j, pm);
+    const int cand0 = draw(skey, j, 0, 0, a.n_ent), cand1 = draw(skey, j, 1, 0, a.n_ent);
+    float2 fs[KP], fo[KP];
+    load_row2<KP>(a.E, cand0, d, fs);
+    load_row2<KP>(a.E, cand1, d, fo);
+    const int s = __builtin_amdgcn_readfirstlane(a.trip[3 * t]);
+    const int o = __builtin_amdgcn_readfirstlane(a.trip[3 * t + 1]);
+    const int p = __builtin_amdgcn_readfirstlane(a.trip[3 * t + 2]);
+    float2 es[KP], eo[KP], rp[KP];
+    load_row2<KP>(a.E, s, d, es);
+    load_row2<KP>(a.E, o, d, eo);
+    load_row2<KP>(a.R, p, d, rp);
+    bool ok = true;
+    if (l < 2) ok = l == 0 ? !set_contains(a.set, cand0, o, p) : !set_contains(a.set, s, cand1, p);
+    const uint64_t okm = __ballot(ok);
+    int neg0 = (okm & 1ull) ? cand0 : -1;
+    int neg1 = (okm & 2ull) ? cand1 : -1;
+    if (neg0 < 0 || neg1 < 0) {
+      sample_rest(a, skey, j, s, o, p, 1, neg0, neg1);
+      neg0 = __builtin_amdgcn_readfirstlane(neg0);
+      neg1 = __builtin_amdgcn_readfirstlane(neg1);
+      if (neg0 >= 0 && neg0 != cand0) load_row2<KP>(a.E, neg0, d, fs);
+      if (neg1 >= 0 && neg1 != cand1) load_row2<KP>(a.E, neg1, d, fo);
+    }
+    float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
+    float2 gp[KP], g0[KP], g1[KP];
+#pragma unroll
+    for (int m = 0; m < KP; ++m) {
+#define SKGE_EL(X)                                                                    \
+  {                                                                                   \
+    const float vp = (es[m].X + rp[m].X) - eo[m].X;                                   \
+    const float v0 = (fs[m].X + rp[m].X) - eo[m].X;                                   \
+    const float v1 = (es[m].X + rp[m].X) - fo[m].X;                                   \
+    ps += fabsf(vp);                                                                  \
+    n0 += fabsf(v0);                                                                  \
+    n1 += fabsf(v1);                                                                  \
+    gp[m].X = signf_np(-((eo[m].X - rp[m].X) - es[m].X)); /* transe.py:103,115 */     \
+    g0[m].X = signf_np((eo[m].X - rp[m].X) - fs[m].X);    /* transe.py:104,117 */     \
+    g1[m].X = signf_np((fo[m].X - rp[m].X) - es[m].X);                                \
+  }
+      SKGE_EL(x)
+      SKGE_EL(y)
+#undef SKGE_EL
+    }
+    const float pscore = -wave_sum(ps);
+    const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
+    const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;
+    const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
+    if (a.neg_out && l == 0) {
+      a.neg_out[2 * (long long)w] = neg0;
+      a.neg_out[2 * (long long)w + 1] = neg1;
+    }
+    {
+      const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
+      const int rE = sel4(l, s, o, neg0, neg1);
+      if (l < 5) {
+        const bool ent = l < 4;
+        commit_slot(ent ? a.accE.cnt : a.accR.cnt, ent ? a.accE.touched : a.accR.touched,
+                    ent ? rE : p, ent ? cE : 2 * (v0 + v1), ent ? 4 * w + l : w);
+      }
+    }
+    if (v0 + v1 == 0) continue;
+    nv += v0 + v1;
+    const float fv0 = (float)v0, fv1 = (float)v1;
+    float2 cs[KP], co[KP], c0[KP], c1[KP], cr[KP];
+#pragma unroll
+    for (int m = 0; m < KP; ++m) {
+#define SKGE_CO(X)                                                   \
+  cs[m].X = fv0 * gp[m].X + fv1 * (gp[m].X + g1[m].X);               \
+  co[m].X = -(fv0 * (gp[m].X + g0[m].X) + fv1 * gp[m].X);            \
+  c0[m].X = g0[m].X;                                                 \
+  c1[m].X = -g1[m].X;                                                \
+  cr[m].X = fv0 * (gp[m].X + g0[m].X) + fv1 * (gp[m].X + g1[m].X);
+      SKGE_CO(x)
+      SKGE_CO(y)
+#undef SKGE_CO
+    }
+    acc_row2_i16<KP>(a.accE, s, cs, d);
+    acc_row2_i16<KP>(a.accE, o, co, d);
+    if (v0) acc_row2_i16<KP>(a.accE, neg0, c0, d);
+    if (v1) acc_row2_i16<KP>(a.accE, neg1, c1, d);
+    acc_row2_i16<KP>(a.accR, p, cr, d);
   }
   if (l == 0 && nv) {
     if (a.nviol) atomicAdd(a.nviol, nv);
@@ -221,6 +352,33 @@ static int launch_sample(const SampleArgs& a, bool l1, hipStream_t st) {
   int blocks = (a.count + 3) / 4;
   if (blocks < 1) blocks = 1;
   if (blocks > 16384) blocks = 16384;
+  if (a.accE.mode == ACC_I16X2) {
+    if (!l1 || a.accR.mode != ACC_I16X2 || (a.d & 1) || 4ll * a.count > 32767) {
+      set_error("packed accumulators need TransE-L1, both tables packed, even d, 4*count <= 32767");
+      return SKGE_EINVAL;
+    }
+    const int kp = (a.d + 127) / 128;
+#define SKGE_SP(K) \
+  case K: hipLaunchKernelGGL((k_transe_l1_sample_grad_i16<K>), dim3(blocks), dim3(256), 0, st, a); break;
+    switch (kp) {
+      SKGE_SP(1)
+      SKGE_SP(2)
+      SKGE_SP(4)
+      SKGE_SP(8)
+      default:
+        switch (kp) {
+          case 3: hipLaunchKernelGGL((k_transe_l1_sample_grad_i16<4>), dim3(blocks), dim3(256), 0, st, a); break;
+          default: hipLaunchKernelGGL((k_transe_l1_sample_grad_i16<8>), dim3(blocks), dim3(256), 0, st, a);
+        }
+    }
+#undef SKGE_SP
+    SKGE_CHECK_LAUNCH("transe l1 packed sample grad");
+    return SKGE_OK;
+  }
+  if (a.accR.mode != ACC_F32) {
+    set_error("mixed accumulator modes");
+    return SKGE_EINVAL;
+  }
 #define SKGE_SG(K)                                                                               \
   case K:                                                                                        \
     if (l1)                                                                                      \

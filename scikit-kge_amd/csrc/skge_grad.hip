@@ -53,7 +53,7 @@ __device__ __forceinline__ void to_lds(float* s, const float (&v)[KM], int d) {
 
 // c_k = sum_j a_j b_{(j+k) mod d}      (ccorr, skge/util.py:30-50)
 template <int KM>
-__device__ void ccorr_lds(const float* sa, const float* sb, int d, float (&out)[KM]) {
+__device__ __forceinline__ void ccorr_lds(const float* sa, const float* sb, int d, float (&out)[KM]) {
   const int l = lane_id();
 #pragma unroll
   for (int k = 0; k < KM; ++k) out[k] = 0.0f;
@@ -72,7 +72,7 @@ __device__ void ccorr_lds(const float* sa, const float* sb, int d, float (&out)[
 
 // c_k = sum_j a_j b_{(k-j) mod d}      (cconv, skge/util.py:8-27)
 template <int KM>
-__device__ void cconv_lds(const float* sa, const float* sb, int d, float (&out)[KM]) {
+__device__ __forceinline__ void cconv_lds(const float* sa, const float* sb, int d, float (&out)[KM]) {
   const int l = lane_id();
 #pragma unroll
   for (int k = 0; k < KM; ++k) out[k] = 0.0f;
@@ -91,7 +91,7 @@ __device__ void cconv_lds(const float* sa, const float* sb, int d, float (&out)[
 
 // out_i = sum_j W[i][j] x_j   (W[p] . E[o], skge/rescal.py:212)
 template <int KM>
-__device__ void gemv_rows(const float* __restrict__ Wp, const float* sx, int d, float (&out)[KM]) {
+__device__ __forceinline__ void gemv_rows(const float* __restrict__ Wp, const float* sx, int d, float (&out)[KM]) {
   const int l = lane_id();
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
@@ -107,7 +107,7 @@ __device__ void gemv_rows(const float* __restrict__ Wp, const float* sx, int d, 
 
 // out_j = sum_i x_i W[i][j]   (E[s] . W[p], skge/rescal.py:209)
 template <int KM>
-__device__ void gemv_cols(const float* __restrict__ Wp, const float* sx, int d, float (&out)[KM]) {
+__device__ __forceinline__ void gemv_cols(const float* __restrict__ Wp, const float* sx, int d, float (&out)[KM]) {
   const int l = lane_id();
 #pragma unroll
   for (int k = 0; k < KM; ++k) out[k] = 0.0f;
@@ -178,7 +178,7 @@ __device__ __forceinline__ void commit_pair(const Accum& aE, const Accum* aR, bo
 // TransE pair: skge/transe.py:48-165
 // ---------------------------------------------------------------------------
 template <int KM, bool L1>
-__device__ bool transe_pair(const PairArgs& a, int i, const int (&ix)[6]) {
+__device__ __forceinline__ bool transe_pair(const PairArgs& a, int i, const int (&ix)[6]) {
   const int d = a.d;
   const int sp = ix[0], op = ix[1], pp = ix[2], sn = ix[3], on = ix[4], pn = ix[5];
   float es[KM], eo[KM], rp[KM], fs[KM], fo[KM], rn[KM];
@@ -226,7 +226,7 @@ __device__ bool transe_pair(const PairArgs& a, int i, const int (&ix)[6]) {
 // HolE pair: skge/hole.py:44-100
 // ---------------------------------------------------------------------------
 template <int KM>
-__device__ bool hole_pair(const PairArgs& a, int i, float* sw, const int (&ix)[6]) {
+__device__ __forceinline__ bool hole_pair(const PairArgs& a, int i, float* sw, const int (&ix)[6]) {
   const int d = a.d;
   const int sp = ix[0], op = ix[1], pp = ix[2], sn = ix[3], on = ix[4], pn = ix[5];
   const int stride = 64 * KM;
@@ -297,7 +297,7 @@ __device__ bool hole_pair(const PairArgs& a, int i, float* sw, const int (&ix)[6
 // RESCAL pair: skge/rescal.py:78-139 (entity part; dW in k_rescal_wgrad)
 // ---------------------------------------------------------------------------
 template <int KM>
-__device__ bool rescal_pair(const PairArgs& a, int i, float* sw, const int (&ix)[6]) {
+__device__ __forceinline__ bool rescal_pair(const PairArgs& a, int i, float* sw, const int (&ix)[6]) {
   const int d = a.d;
   const int sp = ix[0], op = ix[1], pp = ix[2], sn = ix[3], on = ix[4], pn = ix[5];
   const int stride = 64 * KM;
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad(const float* __restrict__ 
       }
     }
   }
-  if (tt == 0 && t == 0) accW.touched[p] = total > 0 ? p : -1;   // slot p
+  if (tt == 0 && t == 0 && accW.touched) accW.touched[p] = total > 0 ? p : -1;   // slot p
   if (total == 0) return;
   float* out = accW.sum + (size_t)p * d * d;
 #pragma unroll
@@ -593,6 +593,7 @@ static int check_model_tables(int model, const skge_table_t* ent, const skge_tab
   int rc;
   if ((rc = check_table(ent, "ent", true)) != SKGE_OK) return rc;
   if ((rc = check_table(rel, "rel", model != SKGE_RESCAL)) != SKGE_OK) return rc;
+  if ((rc = check_f32(ent, "ent")) || (rc = check_f32(rel, "rel"))) return rc;
   SKGE_CHECK_ARG(model >= 0 && model <= 3, "unknown model %d", model);
   SKGE_CHECK_ARG(d > 0 && ent->width == d, "entity width %d != d %d", ent->width, d);
   if (model == SKGE_RESCAL)
@@ -679,7 +680,7 @@ extern "C" int skge_rescal_wgrad(void* stream, const skge_table_t* ent, const sk
                                  const int* trip_b, const float* coef_b, int n_b) {
   int rc = check_model_tables(SKGE_RESCAL, ent, rel, d);
   if (rc) return rc;
-  SKGE_CHECK_ARG(rel->acc_sum && rel->acc_cnt && rel->acc_touched, "W accumulator missing");
+  SKGE_CHECK_ARG(rel->acc_sum && rel->acc_cnt, "W accumulator missing");
   if ((rc = check_slots(rel, rel->rows, "W"))) return rc;
   SKGE_CHECK_ARG(n_a >= 0 && n_b >= 0, "negative item count");
   if (n_a + n_b == 0) return SKGE_OK;

@@ -56,6 +56,7 @@ inline Accum accum_of(const skge_table_t* t) {
   a.cnt = t->acc_cnt;
   a.touched = t->acc_touched;
   a.width = t->width;
+  a.mode = t->acc_mode;
   return a;
 }
 
@@ -63,14 +64,25 @@ inline int check_table(const skge_table_t* t, const char* name, bool need_acc) {
   SKGE_CHECK_ARG(t != nullptr, "%s: table is NULL", name);
   SKGE_CHECK_ARG(t->param != nullptr, "%s: param is NULL", name);
   SKGE_CHECK_ARG(t->rows > 0 && t->width > 0, "%s: bad shape %d x %d", name, t->rows, t->width);
+  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 || t->acc_mode == SKGE_ACC_I16X2,
+                 "%s: unknown accumulator mode %d", name, t->acc_mode);
+  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 || (t->width % 2 == 0 && t->width <= 1024),
+                 "%s: packed accumulator needs an even width <= 1024", name);
   if (need_acc) {
-    SKGE_CHECK_ARG(t->acc_sum && t->acc_cnt && t->acc_touched,
-                   "%s: accumulator buffers missing", name);
+    SKGE_CHECK_ARG(t->acc_sum && t->acc_cnt, "%s: accumulator buffers missing", name);
   }
   return SKGE_OK;
 }
 
+// producers that only write fp32 accumulators
+inline int check_f32(const skge_table_t* t, const char* name) {
+  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32, "%s: this producer needs an fp32 accumulator", name);
+  return SKGE_OK;
+}
+
+// slot records: a table without acc_touched is dense (nothing recorded)
 inline int check_slots(const skge_table_t* t, long long nslots, const char* name) {
+  if (t->acc_touched == nullptr) return SKGE_OK;
   SKGE_CHECK_ARG(nslots >= 0 && nslots <= t->touched_cap,
                  "%s: %lld touched slots needed, capacity %d", name, nslots, t->touched_cap);
   return SKGE_OK;

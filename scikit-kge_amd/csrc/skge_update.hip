@@ -5,6 +5,8 @@
 // the row in registers, so the projection's row norm is a wave reduction and
 // the row is read and written exactly once.  Wide rows (RESCAL's W, width
 // d*d, no projection) are updated elementwise.
+#include <algorithm>
+
 #include "skge_host.h"
 
 namespace skge {
@@ -35,11 +37,6 @@ static TableDev table_dev(const skge_table_t* t) {
   return d;
 }
 
-struct Tables4 {
-  TableDev t[4];
-  int nslots[4];
-  int n;
-};
 
 // SGD._update / AdaGrad._update + post projection for one register-resident row
 template <int KM>
@@ -48,42 +45,44 @@ __device__ __forceinline__ void update_row(const TableDev& t, int row, const flo
   const int w = t.width;
   float* prow = t.P + (size_t)row * w;
   float* arow = t.A ? t.A + (size_t)row * w : nullptr;
-  float p[KM];
+  const bool ada = t.opt == OPT_ADAGRAD;
+  float p[KM], a[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {   // unconditional loads (see load_row)
+    const int e = l + 64 * k;
+    const int ec = e < w ? e : w - 1;
+    p[k] = prow[ec];
+    a[k] = ada ? arow[ec] : 0.0f;
+  }
   float ss = 0.0f;
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     const int e = l + 64 * k;
-    float pv = 0.0f;
-    if (e < w) {
-      pv = prow[e];
-      if (t.opt == OPT_ADAGRAD) {
-        const float av = arow[e] + g[k] * g[k];         // p2[idx] += g*g        param.py:147
-        arow[e] = av;
-        const float h = fmaxf(sqrtf(av), 1e-7f);         // H = max(sqrt(p2),1e-7) param.py:152
-        pv = pv - (t.lr * g[k]) / h;                     // P -= lr*g/H           param.py:155
-      } else {
-        pv = pv - t.lr * g[k];                           // P -= lr*g             param.py:130
-      }
+    float pv = p[k];
+    if (ada) {
+      a[k] = a[k] + g[k] * g[k];                       // p2[idx] += g*g        param.py:147
+      const float h = fmaxf(sqrtf(a[k]), 1e-7f);       // H = max(sqrt(p2),1e-7) param.py:152
+      pv = pv - (t.lr * g[k]) / h;                     // P -= lr*g/H           param.py:155
+    } else {
+      pv = pv - t.lr * g[k];                           // P -= lr*g             param.py:130
     }
-    p[k] = pv;
-    ss += pv * pv;
+    p[k] = e < w ? pv : 0.0f;
+    ss += p[k] * p[k];
   }
   if (t.post != POST_NONE) {
     ss = wave_sum(ss);
-    if (t.post == POST_NORMALIZE) {
-      const float nrm = sqrtf(ss);                       // param.py:165-166
+    const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss)              // param.py:165-166
+                                               : (ss < 1.0f ? 1.0f : ss); // param.py:171-173
 #pragma unroll
-      for (int k = 0; k < KM; ++k) p[k] = p[k] / nrm;
-    } else {
-      const float nrm = ss < 1.0f ? 1.0f : ss;           // param.py:171-173
-#pragma unroll
-      for (int k = 0; k < KM; ++k) p[k] = p[k] / nrm;
-    }
+    for (int k = 0; k < KM; ++k) p[k] = p[k] / nrm;
   }
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     const int e = l + 64 * k;
-    if (e < w) prow[e] = p[k];
+    if (e < w) {
+      prow[e] = p[k];
+      if (ada) arow[e] = a[k];
+    }
   }
 }
 
@@ -95,48 +94,177 @@ __device__ __forceinline__ void mean_row(const TableDev& t, int row, int c, floa
   float* srow = t.acc.sum + (size_t)row * w;
   const float* prow = t.P + (size_t)row * w;
   const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
-  const bool reg = t.rin != 0.0f || t.rout != 0.0f;
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     const int e = l + 64 * k;
-    float gv = 0.0f;
-    if (e < w) {
-      const float s = srow[e];
-      if (reg) {
-        const float pv = prow[e];
-        gv = (s + t.rin * pv) / div + t.rout * pv;
-      } else {
-        gv = s / div;
-      }
-      srow[e] = 0.0f;
-    }
-    g[k] = gv;
+    const int ec = e < w ? e : w - 1;
+    const float sv = srow[ec], pv = prow[ec];
+    g[k] = e < w ? (sv + t.rin * pv) / div + t.rout * pv : 0.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k;
+    if (e < w) srow[e] = 0.0f;
   }
   if (l == 0) t.acc.cnt[row] = 0;
 }
 
-// fused apply: one wavefront per touched slot of any of the tables
+// Segment mean + updater + projection of one row, with every load of the row
+// (sum, param, state) issued together right after the row id is known: one
+// memory round trip instead of a chain (the sum is zeroed afterwards).
 template <int KM>
-__global__ __launch_bounds__(256) void k_apply(Tables4 ts) {
-  const int wpb = blockDim.x >> 6;
-  const int w0 = blockIdx.x * wpb + (threadIdx.x >> 6);
-  const int nw = gridDim.x * wpb;
-  int total = 0;
-  for (int i = 0; i < ts.n; ++i) total += ts.nslots[i];
-  for (int w = w0; w < total; w += nw) {
-    int ti = 0, r = w;
-    while (r >= ts.nslots[ti]) {
-      r -= ts.nslots[ti];
-      ++ti;
+__device__ __forceinline__ void apply_row(const TableDev& t, int row, bool upd) {
+  const int l = lane_id();
+  // claim the row: the first wave to swap its count out owns it (touched
+  // slots may repeat a row); issued together with the row loads below
+  int c = 0;
+  if (l == 0) c = atomicExch(t.acc.cnt + row, 0);
+  const int w = t.width;
+  float* __restrict__ srow = t.acc.sum + (size_t)row * w;
+  float* __restrict__ prow = t.P + (size_t)row * w;
+  float* __restrict__ arow = t.A ? t.A + (size_t)row * w : nullptr;
+  const bool ada = t.opt == OPT_ADAGRAD;
+  float s[KM], p[KM], a[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k;
+    const bool in = e < w;
+    const int ec = in ? e : w - 1;   // unconditional loads (see load_row)
+    const float sv = srow[ec], pv = prow[ec];
+    const float av = ada ? arow[ec] : 0.0f;
+    s[k] = in ? sv : 0.0f;
+    p[k] = in ? pv : 0.0f;
+    a[k] = in ? av : 0.0f;
+  }
+  c = __builtin_amdgcn_readfirstlane(c);
+  if (c == 0) return;   // another wave owns the row, or a stale slot
+  const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
+  float ss = 0.0f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const float g = (s[k] + t.rin * p[k]) / div + t.rout * p[k];   // segment mean (+ rparam)
+    float pv = p[k];
+    if (ada) {
+      const float av = a[k] + g * g;                 // p2[idx] += g*g           param.py:147
+      a[k] = av;
+      pv = pv - (t.lr * g) / fmaxf(sqrtf(av), 1e-7f); // P -= lr*g/max(sqrt,1e-7) param.py:152-155
+    } else {
+      pv = pv - t.lr * g;                            // P -= lr*g                param.py:130
     }
-    const TableDev& t = ts.t[ti];
-    const int row = __builtin_amdgcn_readfirstlane(t.acc.touched[r]);
-    if (row < 0) continue;
-    const int c = __builtin_amdgcn_readfirstlane(t.acc.cnt[row]);
-    if (c == 0) continue;   // stale slot (accumulator already consumed)
-    float g[KM];
-    mean_row<KM>(t, row, c, g);
-    if (t.gate == nullptr || *t.gate != 0) update_row<KM>(t, row, g);
+    p[k] = pv;
+    ss += pv * pv;
+  }
+  if (t.post != POST_NONE && upd) {
+    ss = wave_sum(ss);
+    const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss) : (ss < 1.0f ? 1.0f : ss);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) p[k] = p[k] / nrm;   // param.py:165-166 / 171-173
+  }
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k;
+    if (e < w) {
+      srow[e] = 0.0f;
+      if (upd) {
+        prow[e] = p[k];
+        if (ada) arow[e] = a[k];
+      }
+    }
+  }
+}
+
+// ACC_I16X2 form of apply_row: the accumulator holds exact integer pair sums;
+// rows in the pair layout (float2 per lane, see load_row2)
+template <int KP>
+__device__ __forceinline__ void apply_row_i16(const TableDev& t, int row, bool upd) {
+  const int l = lane_id();
+  const int w = t.width, h = w >> 1;
+  int c = 0;
+  if (l == 0) c = atomicExch(t.acc.cnt + row, 0);
+  int* __restrict__ srow = reinterpret_cast<int*>(t.acc.sum) + (size_t)row * h;
+  float2* __restrict__ prow = reinterpret_cast<float2*>(t.P + (size_t)row * w);
+  float2* __restrict__ arow = t.A ? reinterpret_cast<float2*>(t.A + (size_t)row * w) : nullptr;
+  const bool ada = t.opt == OPT_ADAGRAD;
+  int sv[KP];
+  float2 p[KP], a[KP];
+#pragma unroll
+  for (int m = 0; m < KP; ++m) {
+    const int q = 64 * m + l, qc = q < h ? q : h - 1;
+    sv[m] = srow[qc];
+    p[m] = prow[qc];
+    a[m] = ada ? arow[qc] : make_float2(0.0f, 0.0f);
+  }
+  c = __builtin_amdgcn_readfirstlane(c);
+  if (c == 0) return;
+  const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
+  float ss = 0.0f;
+#pragma unroll
+  for (int m = 0; m < KP; ++m) {
+    const bool in = 64 * m + l < h;
+    float s0, s1;
+    unpack_i16x2(in ? sv[m] : 0, s0, s1);
+#define SKGE_UP(X, S)                                                   \
+  {                                                                     \
+    const float g = (S + t.rin * p[m].X) / div + t.rout * p[m].X;       \
+    float pv = p[m].X;                                                  \
+    if (ada) {                                                          \
+      a[m].X = a[m].X + g * g;                                          \
+      pv = pv - (t.lr * g) / fmaxf(sqrtf(a[m].X), 1e-7f);               \
+    } else {                                                            \
+      pv = pv - t.lr * g;                                               \
+    }                                                                   \
+    p[m].X = in ? pv : 0.0f;                                            \
+    ss += p[m].X * p[m].X;                                              \
+  }
+    SKGE_UP(x, s0)
+    SKGE_UP(y, s1)
+#undef SKGE_UP
+  }
+  if (t.post != POST_NONE && upd) {
+    ss = wave_sum(ss);
+    const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss) : (ss < 1.0f ? 1.0f : ss);
+#pragma unroll
+    for (int m = 0; m < KP; ++m) {
+      p[m].x = p[m].x / nrm;
+      p[m].y = p[m].y / nrm;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < KP; ++m) {
+    const int q = 64 * m + l;
+    if (q < h) {
+      srow[q] = 0;
+      if (upd) {
+        prow[q] = p[m];
+        if (ada) arow[q] = a[m];
+      }
+    }
+  }
+}
+
+template <int K, int MODE>
+__device__ __forceinline__ void apply_slot(const TableDev& t, int slot) {
+  const int row = t.acc.touched ? __builtin_amdgcn_readfirstlane(t.acc.touched[slot]) : slot;
+  if (row < 0) return;
+  const bool upd = t.gate == nullptr || *t.gate != 0;
+  if (MODE == ACC_I16X2)
+    apply_row_i16<K>(t, row, upd);
+  else
+    apply_row<K>(t, row, upd);
+}
+
+// fused apply: one wavefront per slot of table 0 (slots [0, n0)) or table 1
+// (slots [n0, n0 + n1)); a dense table (no slot records) has one slot per
+// row.  Two explicit table arguments keep every table field in scalar registers.
+template <int K, int MODE>
+__global__ __launch_bounds__(256) void k_apply(TableDev t0, int n0, TableDev t1, int n1) {
+  const int wpb = blockDim.x >> 6;
+  const int nw = gridDim.x * wpb;
+  for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < n0 + n1; w += nw) {
+    if (w < n0)
+      apply_slot<K, MODE>(t0, w);
+    else
+      apply_slot<K, MODE>(t1, w - n0);
   }
 }
 
@@ -191,7 +319,8 @@ __global__ __launch_bounds__(256) void k_update_rows(TableDev t, const float* __
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
       const int e = l + 64 * k;
-      gv[k] = e < t.width ? g[(size_t)i * t.width + e] : 0.0f;
+      const float x = g[(size_t)i * t.width + (e < t.width ? e : t.width - 1)];
+      gv[k] = e < t.width ? x : 0.0f;
     }
     update_row<KM>(t, row, gv);
   }
@@ -369,6 +498,7 @@ extern "C" int skge_accum_collect(void* stream, const skge_table_t* t, int* idx_
   int rc = check_table(t, "table", true);
   if (rc) return rc;
   SKGE_CHECK_ARG(idx_out && g_out && U_out, "outputs NULL");
+  if ((rc = check_f32(t, "table"))) return rc;
   SKGE_CHECK_ARG(workspace && ws_bytes >= skge_collect_workspace_bytes(t->rows),
                  "workspace too small");
   hipStream_t st = as_stream(stream);
@@ -405,10 +535,18 @@ extern "C" int skge_accum_reset(void* stream, const skge_table_t* t, int nslots)
   int rc = check_table(t, "table", true);
   if (rc) return rc;
   if ((rc = check_slots(t, nslots, "table"))) return rc;
-  if (nslots == 0) return SKGE_OK;
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(k_reset, dim3(grid_for_elems((long long)nslots * t->width)), dim3(256), 0, st,
-                     table_dev(t), nslots);
+  const size_t row_bytes = (size_t)t->width * 4 / (t->acc_mode == SKGE_ACC_I16X2 ? 2 : 1);
+  if (t->acc_touched == nullptr) {   // dense table: clear everything
+    SKGE_CHECK_HIP(hipMemsetAsync(t->acc_sum, 0, row_bytes * t->rows, st));
+    SKGE_CHECK_HIP(hipMemsetAsync(t->acc_cnt, 0, sizeof(int) * t->rows, st));
+    return SKGE_OK;
+  }
+  if (nslots == 0) return SKGE_OK;
+  TableDev td = table_dev(t);
+  td.width = (int)(row_bytes / 4);   // zero dwords, whatever their encoding
+  hipLaunchKernelGGL(k_reset, dim3(grid_for_elems((long long)nslots * td.width)), dim3(256), 0, st,
+                     td, nslots);
   hipLaunchKernelGGL(k_zero_counts_slots, dim3(grid_for_elems(nslots)), dim3(256), 0, st,
                      t->acc_cnt, t->acc_touched, nslots);
   SKGE_CHECK_LAUNCH("reset");
@@ -451,10 +589,45 @@ extern "C" int skge_accum_apply(void* stream, const skge_table_t* tables, int nt
                                 const int* nslots) {
   SKGE_CHECK_ARG(tables && nslots && ntables >= 1 && ntables <= 4, "1..4 tables");
   hipStream_t st = as_stream(stream);
-  // narrow tables share one launch; each wide table gets its own
-  Tables4 narrow = {};
-  int km = 0;
-  long long waves = 0;
+  // narrow tables are applied two per launch (same accumulator mode); each
+  // wide table gets its own launch
+  auto kdim = [&](int i) {
+    return tables[i].acc_mode == SKGE_ACC_I16X2 ? (tables[i].width / 2 + 63) / 64
+                                                : km_for(tables[i].width);
+  };
+  auto slots_of = [&](int i) {
+    return tables[i].acc_touched ? nslots[i] : tables[i].rows;   // dense: one slot per row
+  };
+  auto launch_pair = [&](int i, int j) -> int {
+    int k = kdim(i);
+    if (j >= 0) k = std::max(k, kdim(j));
+    const int mode = tables[i].acc_mode;
+    const long long waves = (long long)slots_of(i) + (j >= 0 ? slots_of(j) : 0);
+    const int gw = grid_for_waves(waves);
+    TableDev a = table_dev(tables + i);
+    TableDev b = j >= 0 ? table_dev(tables + j) : a;
+    const int na = slots_of(i), nb = j >= 0 ? slots_of(j) : 0;
+#define SKGE_AP(K, M) \
+  hipLaunchKernelGGL((k_apply<K, M>), dim3(gw), dim3(256), 0, st, a, na, b, nb)
+    if (mode == SKGE_ACC_I16X2) {
+      if (k <= 1) SKGE_AP(1, ACC_I16X2);
+      else if (k <= 2) SKGE_AP(2, ACC_I16X2);
+      else if (k <= 4) SKGE_AP(4, ACC_I16X2);
+      else SKGE_AP(8, ACC_I16X2);
+    } else {
+      switch (k) {
+        case 1: SKGE_AP(1, ACC_F32); break;
+        case 2: SKGE_AP(2, ACC_F32); break;
+        case 3: SKGE_AP(3, ACC_F32); break;
+        case 4: SKGE_AP(4, ACC_F32); break;
+        case 8: SKGE_AP(8, ACC_F32); break;
+        default: SKGE_AP(16, ACC_F32); break;
+      }
+    }
+#undef SKGE_AP
+    return SKGE_OK;
+  };
+  int pend = -1;   // narrow table waiting for a partner
   for (int i = 0; i < ntables; ++i) {
     const skge_table_t* t = tables + i;
     int rc = check_table(t, "table", true);
@@ -462,35 +635,25 @@ extern "C" int skge_accum_apply(void* stream, const skge_table_t* tables, int nt
     if ((rc = check_slots(t, nslots[i], "table"))) return rc;
     SKGE_CHECK_ARG(t->opt == SKGE_SGD || t->state, "AdaGrad needs state");
     SKGE_CHECK_ARG(t->post >= 0 && t->post <= 2, "unknown post %d", t->post);
-    if (nslots[i] == 0) continue;
-    const int k = km_for(t->width);
-    if (k == 0) {
+    if (slots_of(i) == 0) continue;
+    if (km_for(t->width) == 0) {
       SKGE_CHECK_ARG(t->post == SKGE_POST_NONE, "projection needs width <= 1024");
+      SKGE_CHECK_ARG(t->acc_touched != nullptr, "wide tables need slot records");
       hipLaunchKernelGGL(k_apply_wide, dim3(grid_for_elems((long long)nslots[i] * t->width)),
                          dim3(256), 0, st, table_dev(t), nslots[i]);
       hipLaunchKernelGGL(k_zero_counts_slots, dim3(grid_for_elems(nslots[i])), dim3(256), 0, st,
                          t->acc_cnt, t->acc_touched, nslots[i]);
+    } else if (pend < 0) {
+      pend = i;
+    } else if (tables[pend].acc_mode == t->acc_mode) {
+      launch_pair(pend, i);
+      pend = -1;
     } else {
-      narrow.t[narrow.n] = table_dev(t);
-      narrow.nslots[narrow.n++] = nslots[i];
-      if (k > km) km = k;
-      waves += nslots[i];
+      launch_pair(pend, -1);
+      pend = i;
     }
   }
-  if (narrow.n) {
-    const int gw = grid_for_waves(waves);
-#define SKGE_AP(K) \
-  case K: hipLaunchKernelGGL((k_apply<K>), dim3(gw), dim3(256), 0, st, narrow); break;
-    switch (km) {
-      SKGE_AP(1)
-      SKGE_AP(2)
-      SKGE_AP(3)
-      SKGE_AP(4)
-      SKGE_AP(8)
-      SKGE_AP(16)
-    }
-#undef SKGE_AP
-  }
+  if (pend >= 0) launch_pair(pend, -1);
   SKGE_CHECK_LAUNCH("apply");
   return SKGE_OK;
 }

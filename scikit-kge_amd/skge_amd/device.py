@@ -38,7 +38,7 @@ class EpochRunner(object):
     """Native hipGraph epoch of the TransE device batch loop."""
 
     def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, stream=None,
-                 nviol_total=None):
+                 nviol_total=None, force_f32=False):
         from .transe import TransE
         if not isinstance(model, TransE):
             raise NotImplementedError("device_loop supports TransE (the north-star path) only")
@@ -50,8 +50,17 @@ class EpochRunner(object):
         self.nviol_total = nviol_total if nviol_total is not None else \
             torch.zeros(1, dtype=torch.int32, device=dev)
         bs = kg.T // nbatches
-        self.te = updaters["E"].table(model.accumulator("E").ensure_slots(4 * bs))
-        self.tr = updaters["R"].table(model.accumulator("R").ensure_slots(bs))
+        # TransE-L1 sign contributions are small integers: exact packed int16x2
+        # accumulation when every per-batch sum fits (4 * batch <= 32767)
+        packed = bool(model.l1) and model.d % 2 == 0 and 4 * bs <= 32767 and not force_f32
+        mode = L.SKGE_ACC_I16X2 if packed else L.SKGE_ACC_F32
+        from .param import Accumulator
+        E, R = model.params["E"], model.params["R"]
+        self.accE = Accumulator(E.rows, E.width, dev, slots=4 * bs, mode=mode)
+        self.accR = Accumulator(R.rows, R.width, dev, mode=mode, dense=True)
+        self.packed = packed
+        self.te = updaters["E"].table(self.accE)
+        self.tr = updaters["R"].table(self.accR)
         self.nbatches = nbatches
         torch.cuda.current_stream().synchronize()
         lib = L.lib()

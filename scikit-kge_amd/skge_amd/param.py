@@ -181,8 +181,9 @@ def table_struct(param, state=None, acc=None, opt=L.SKGE_SGD, post=L.SKGE_POST_N
     t.state = L.ptr(state)
     if acc is not None:
         t.acc_sum, t.acc_cnt = L.ptr(acc.sum), L.ptr(acc.cnt)
-        t.acc_touched = L.ptr(acc.touched)
-        t.touched_cap = acc.touched.numel()
+        t.acc_touched = L.ptr(acc.touched)          # None -> dense table
+        t.touched_cap = acc.touched.numel() if acc.touched is not None else 0
+        t.acc_mode = acc.mode
     t.rows = param.rows
     t.width = param.width
     t.opt, t.post, t.lr = opt, post, lr
@@ -207,15 +208,16 @@ class Accumulator(object):
     """Device segment-sum accumulator of one table (see skge_table_t): dense
     fp32 sums, occurrence counts and the fixed-slot touched records."""
 
-    def __init__(self, rows, width, device, slots=1024):
-        self.rows, self.width = rows, width
+    def __init__(self, rows, width, device, slots=1024, mode=L.SKGE_ACC_F32, dense=False):
+        self.rows, self.width, self.mode = rows, width, mode
         self.sum = torch.zeros(rows * width, dtype=torch.float32, device=device)
         self.cnt = torch.zeros(rows, dtype=torch.int32, device=device)
-        self.touched = torch.full((max(slots, 1),), -1, dtype=torch.int32, device=device)
+        self.touched = None if dense else \
+            torch.full((max(slots, 1),), -1, dtype=torch.int32, device=device)
 
     def ensure_slots(self, n):
         """Grow the touched-slot array to hold n slots (before building tables)."""
-        if n > self.touched.numel():
+        if self.touched is not None and n > self.touched.numel():
             self.touched = torch.full((max(n, 2 * self.touched.numel()),), -1, dtype=torch.int32,
                                       device=self.sum.device)
         return self

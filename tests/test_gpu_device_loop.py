@@ -60,8 +60,13 @@ def test_epoch_permutation_is_a_bijection():
             assert not np.array_equal(p, np.arange(T))
 
 
-def test_sampler_kernel_parity_with_oracle_replay():
+@pytest.mark.parametrize("packed,dense_r", [(False, False), (True, True), (False, True)])
+def test_sampler_kernel_parity_with_oracle_replay(packed, dense_r):
+    """Device sampler + fused score/scatter + apply, in every accumulator form
+    (fp32 / exact packed int16x2; relation table with slots / dense), against
+    the oracle replaying the recorded pairs."""
     from skge_amd import _lib as L
+    from skge_amd.param import Accumulator
     S, m, upd, trip, tset, kg = _setup(300, 5, 2000, 50)
     E0 = np.asarray(m.E, dtype=np.float64)
     R0 = np.asarray(m.R, dtype=np.float64)
@@ -71,8 +76,11 @@ def test_sampler_kernel_parity_with_oracle_replay():
     negs = torch.full((count, 2), -7, dtype=torch.int32, device=dev)
     perm = torch.empty(kg.T, dtype=torch.int64, device=dev)
     nviol = torch.zeros(1, dtype=torch.int32, device=dev)
-    te = upd["E"].table(m.accumulator("E").ensure_slots(4 * count))
-    tr = upd["R"].table(m.accumulator("R").ensure_slots(count))
+    mode = L.SKGE_ACC_I16X2 if packed else L.SKGE_ACC_F32
+    accE = Accumulator(m.E.rows, m.E.width, dev, slots=4 * count, mode=mode)
+    accR = Accumulator(m.R.rows, m.R.width, dev, slots=count, mode=mode, dense=dense_r)
+    te = upd["E"].table(accE)
+    tr = upd["R"].table(accR)
     lib = L.lib()
     st = L.stream_ptr()
     L.check(lib.skge_epoch_permutation(st, kg.T, 99, L.ptr(key), L.ptr(perm), kg.T))
@@ -104,6 +112,10 @@ def test_sampler_kernel_parity_with_oracle_replay():
     np.testing.assert_allclose(np.asarray(m.E), params["E"], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(np.asarray(m.R), params["R"], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(upd["E"].p2.cpu().numpy(), state["E"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(upd["R"].p2.cpu().numpy(), state["R"], rtol=1e-5, atol=1e-5)
+    for acc in (accE, accR):   # accumulators are clean again
+        assert int(acc.cnt.abs().sum().item()) == 0
+        assert float(acc.sum.abs().sum().item()) == 0.0
 
 
 def test_sampler_mode_balance():
@@ -137,7 +149,8 @@ def test_runner_small_two_epochs_invariants():
     np.testing.assert_allclose(np.linalg.norm(E, axis=1), 1.0, atol=1e-5)
     nv = int(tr.nviol_total.item())
     assert 0 < nv <= 2 * 2 * kg.T
-    for acc in m._acc.values():
+    assert tr.packed
+    for acc in (tr.accE, tr.accR):
         assert int(acc.cnt.abs().sum().item()) == 0
         assert float(acc.sum.abs().sum().item()) == 0.0
     assert int(tr.epoch_key.item()) == 2
@@ -165,7 +178,8 @@ def test_runner_wn18_full_size_properties(l1):
     nv = int(runner.nviol_total.item())
     assert 0 < nv <= 2 * kg.T
     assert not np.allclose(np.asarray(m.R), R0)
-    for acc in m._acc.values():
+    assert runner.packed == l1
+    for acc in (runner.accE, runner.accR):
         assert int(acc.cnt.abs().sum().item()) == 0
         assert float(acc.sum.abs().sum().item()) == 0.0
 
