@@ -103,7 +103,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--acc", choices=["auto", "f32"], default="auto",
-                    help="accumulator encoding (auto: exact packed int16x2 for TransE-L1)")
+                    help="accumulator encoding (auto: exact packed int16x4 for TransE-L1)")
+    ap.add_argument("--reps", type=int, default=1, help="relation accumulator copies")
     args = ap.parse_args()
 
     import torch
@@ -128,7 +129,7 @@ def main():
     upd = {pid: S.AdaGrad(p, 0.1) for pid, p in model.params.items()}
     kg = DeviceKG(trip, dev)
     runner = EpochRunner(model, upd, kg, nbatches=nb, seed=1234 + rank,
-                         force_f32=args.acc == "f32")
+                         force_f32=args.acc == "f32", replicas=args.reps)
     st = runner.stream
     init = {pid: p.data.clone() for pid, p in model.params.items()}
 
@@ -206,7 +207,7 @@ def main():
                             for n, v in prof["kernels"].items()},
                 "step_algorithmic_GB_s": round(prof["epoch_bytes"] / (elapsed / args.steps) / 1e9, 1),
                 "launches_per_step": runner.nlaunches,
-                "accumulator": "int16x2 exact" if runner.packed else "fp32",
+                "accumulator": "int16x4 exact" if runner.packed else "fp32",
             },
         }
         print(json.dumps(line))

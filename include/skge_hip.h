@@ -53,10 +53,11 @@ enum { SKGE_POST_NONE = 0, SKGE_POST_NORMALIZE = 1, SKGE_POST_NORMLESS1 = 2 };
 /* accumulator encodings */
 enum {
   SKGE_ACC_F32 = 0,    /* acc_sum: fp32 [rows][width] */
-  SKGE_ACC_I16X2 = 1   /* acc_sum: exact integer sums of TransE-L1 sign contributions,
-                          two elements per int32 (elements 2q, 2q+1 in dword q; a
-                          packed add whose halves stay within +-32767) -- used only by
-                          skge_transe_sample_grad with l1 != 0, even width, and
+  SKGE_ACC_I16X4 = 1   /* acc_sum: exact integer sums of TransE-L1 sign contributions,
+                          four elements per int64 (elements 4q..4q+3 in qword q, added
+                          with one 64-bit integer atomic; each 16-bit field's total
+                          stays within +-32767) -- produced only by
+                          skge_transe_sample_grad with l1 != 0, width % 4 == 0 and
                           4 * count <= 32767 */
 };
 
@@ -82,7 +83,8 @@ enum {
  * Consumers (apply / reset) take the slot count of the producing launch.
  * A narrow table with acc_touched == NULL is applied DENSELY: every row whose
  * count is non-zero (meant for small tables such as TransE's R; producers
- * then record nothing for it).
+ * then record nothing for it).  Replicated accumulators (acc_replicas > 1)
+ * are produced by skge_transe_sample_grad only.
  */
 typedef struct skge_table {
   float *param;        /* [rows][width] */
@@ -93,7 +95,13 @@ typedef struct skge_table {
   int rows;
   int width;
   int touched_cap;     /* capacity of acc_touched (slots) */
-  int acc_mode;        /* SKGE_ACC_F32 | SKGE_ACC_I16X2 */
+  int acc_mode;        /* SKGE_ACC_F32 | SKGE_ACC_I16X4 */
+  int acc_replicas;    /* dense tables only: acc_sum / acc_cnt hold this many
+                          copies ([replicas][rows][...]); producers spread their
+                          adds over the copies (fewer same-address atomics on
+                          hot rows such as TransE's 18 relations) and the apply
+                          sums them.  0 or 1 = a single copy; else 2, 4, 8, 16
+                          or 32. */
   int opt;             /* SKGE_SGD | SKGE_ADAGRAD */
   int post;            /* SKGE_POST_* */
   float lr;

@@ -30,6 +30,12 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+__device__ __forceinline__ int wave_sum_int(int v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
 // activation functions, skge/actfun.py:13-57
 __device__ __forceinline__ float af_f(int af, float x) {
   switch (af) {
@@ -58,14 +64,34 @@ __device__ __forceinline__ float signf_np(float x) {  // numpy.sign
 // (see skge_table_t in include/skge_hip.h).  Invariant between batches:
 // sum == 0 and cnt == 0.
 struct Accum {
-  float* sum;      // fp32 [rows][width], or int32 [rows][width/2] in ACC_I16X2 mode
+  float* sum;      // fp32 [rows][width], or int64 [rows][width/4] in ACC_I16X4 mode
   int* cnt;
   int* touched;    // nullptr: dense table (no slot records)
   int width;
   int mode;
+  int replicas;    // >= 1; copies of sum/cnt, [replicas][rows][...]
+  int rows;
 };
 
-enum AccMode : int { ACC_F32 = 0, ACC_I16X2 = 1 };
+enum AccMode : int { ACC_F32 = 0, ACC_I16X4 = 1 };
+
+// accumulator dwords per row
+__device__ __host__ __forceinline__ int acc_row_dwords(int mode, int width) {
+  return mode == ACC_I16X4 ? (width >> 1) : width;
+}
+
+// the copy a producer item adds into (dense replicated tables)
+__device__ __forceinline__ Accum replica(const Accum& a, long long item) {
+  if (a.replicas <= 1) return a;
+  Accum r = a;
+  const int k = (int)(item % a.replicas);
+  const size_t row_dw = (size_t)acc_row_dwords(a.mode, a.width);
+  r.sum = a.sum + (size_t)k * a.rows * row_dw;
+  r.cnt = a.cnt + (size_t)k * a.rows;
+  return r;
+}
+
+
 
 // Count `c` occurrences of `row` (no-return atomic) and record the row in
 // `slot` (or -1 when c == 0).  Several slots may name the same row; the
@@ -120,41 +146,52 @@ __device__ __forceinline__ void load_row(const float* __restrict__ T, int row, i
   }
 }
 
-// ---- "pair" row layout: lane l holds elements 128m + 2l + {0, 1} as a float2,
-// m < KP = ceil(d / 128) (d even).  8-byte loads, and an element pair per lane
-// is what one packed int16x2 accumulator dword holds. ----
-template <int KP>
-__device__ __forceinline__ void load_row2(const float* __restrict__ T, int row, int d,
-                                          float2 (&v)[KP]) {
-  const float2* base = reinterpret_cast<const float2*>(T + (size_t)row * d);
-  const int l = lane_id(), h = d >> 1;
+// ---- "quad" row layout (TransE-L1 packed path): lane l holds elements
+// 4q .. 4q+3, q = 64m + l, as a float4, m < KQ = ceil(d / 256) (d % 4 == 0):
+// a 1 KB row slice is ONE 16-byte-per-lane wave-instruction, and a lane's four
+// elements are what one exact int16x4 accumulator qword holds. ----
+template <int KQ>
+__device__ __forceinline__ void load_row4(const float* __restrict__ T, int row, int d,
+                                          float4 (&v)[KQ]) {
+  const float4* base = reinterpret_cast<const float4*>(T + (size_t)row * d);
+  const int l = lane_id(), nq = d >> 2;
 #pragma unroll
-  for (int m = 0; m < KP; ++m) {
+  for (int m = 0; m < KQ; ++m) {
     const int q = 64 * m + l;
-    const float2 x = base[q < h ? q : h - 1];
-    v[m] = q < h ? x : make_float2(0.0f, 0.0f);
+    const float4 x = base[q < nq ? q : nq - 1];
+    v[m] = q < nq ? x : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
 }
 
-// packed exact add of integer pairs (lo = element 2q, hi = element 2q+1)
-__device__ __forceinline__ int pack_i16x2(float lo, float hi) {
-  return (int)hi * 65536 + (int)lo;
+// four small integers (exactly representable floats) as one int64 whose
+// 16-bit fields are added independently by a 64-bit integer add: the fields
+// borrow/carry into each other, which the signed decode below undoes exactly
+// as long as every field's running total stays within +-32767
+__device__ __forceinline__ unsigned long long pack_i16x4(const float4& c) {
+  const long long v = (((long long)c.w * 65536 + (long long)c.z) * 65536 + (long long)c.y) * 65536 +
+                      (long long)c.x;
+  return (unsigned long long)v;
 }
-__device__ __forceinline__ void unpack_i16x2(int x, float& lo, float& hi) {
-  const int l = (int)(short)(x & 0xFFFF);
-  lo = (float)l;
-  hi = (float)((x - l) >> 16);
+__device__ __forceinline__ float4 unpack_i16x4(unsigned long long u) {
+  long long x = (long long)u;
+  const long long f0 = (short)(x & 0xFFFF);
+  x = (x - f0) >> 16;
+  const long long f1 = (short)(x & 0xFFFF);
+  x = (x - f1) >> 16;
+  const long long f2 = (short)(x & 0xFFFF);
+  x = (x - f2) >> 16;
+  return make_float4((float)f0, (float)f1, (float)f2, (float)x);
 }
 
-template <int KP>
-__device__ __forceinline__ void acc_row2_i16(const Accum& a, int row, const float2 (&c)[KP],
+template <int KQ>
+__device__ __forceinline__ void acc_row4_i16(const Accum& a, int row, const float4 (&c)[KQ],
                                              int d) {
-  int* base = reinterpret_cast<int*>(a.sum) + (size_t)row * (d >> 1);
-  const int l = lane_id(), h = d >> 1;
+  unsigned long long* base = reinterpret_cast<unsigned long long*>(a.sum) + (size_t)row * (d >> 2);
+  const int l = lane_id(), nq = d >> 2;
 #pragma unroll
-  for (int m = 0; m < KP; ++m) {
+  for (int m = 0; m < KQ; ++m) {
     const int q = 64 * m + l;
-    if (q < h) atomicAdd(base + q, pack_i16x2(c[m].x, c[m].y));
+    if (q < nq) atomicAdd(base + q, pack_i16x4(c[m]));
   }
 }
 

@@ -198,9 +198,10 @@ __global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
       // pair 0 lists (sp,op,sn,on) = (s,o,s',o), pair 1 = (s,o,s,o')
       const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
       const int rE = sel4(l, s, o, neg0, neg1);
+      const Accum aR = replica(a.accR, j);
       if (l < 5) {
         const bool ent = l < 4;
-        commit_slot(ent ? a.accE.cnt : a.accR.cnt, ent ? a.accE.touched : a.accR.touched,
+        commit_slot(ent ? a.accE.cnt : aR.cnt, ent ? a.accE.touched : aR.touched,
                     ent ? rE : p, ent ? cE : 2 * (v0 + v1), ent ? 4 * w + l : w);
       }
     }
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
     if (v1) acc_row<KM>(a.accE, neg1, c1, d);
 #endif
 #ifndef SKGE_ABL_NO_RATOM
-    acc_row<KM>(a.accR, p, cr, d);
+    acc_row<KM>(replica(a.accR, j), p, cr, d);
 #endif
   }
   if (l == 0 && nv) {
@@ -234,10 +235,11 @@ __global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
   }
 }
 
-// TransE-L1 variant with exact packed int16x2 accumulation (ACC_I16X2) and the
-// pair row layout: the sign contributions are small integers, so two elements
-// share one 32-bit integer atomic -- half the atomic bytes of the fp32 form.
-template <int KP>
+// TransE-L1 variant with exact packed int16x4 accumulation (ACC_I16X4) and the
+// quad row layout: the sign contributions are small integers, so four
+// elements share one 64-bit integer atomic, and every row gather / row atomic
+// is a single 16-byte-per-lane wave-instruction (d <= 256).
+template <int KQ>
 __global__ __launch_bounds__(256) void k_transe_l1_sample_grad_i16(SampleArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
@@ -248,37 +250,45 @@ __global__ __launch_bounds__(256) void k_transe_l1_sample_grad_i16(SampleArgs a)
   int nv = 0;
   for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < a.count; w += gridDim.x * wpb) {
     const long long j = a.start + w;
+#ifndef SKGE_ABL_NO_PERM
     const long long t = (long long)perm_index((uint64_t)j, pm);
+#else
+    const long long t = j;
+#endif
+    // first tries of both modes do not depend on the positive: their rows load
+    // in the same memory round trip as the triple
     const int cand0 = draw(skey, j, 0, 0, a.n_ent), cand1 = draw(skey, j, 1, 0, a.n_ent);
-    float2 fs[KP], fo[KP];
-    load_row2<KP>(a.E, cand0, d, fs);
-    load_row2<KP>(a.E, cand1, d, fo);
+    float4 fs[KQ], fo[KQ];
+    load_row4<KQ>(a.E, cand0, d, fs);
+    load_row4<KQ>(a.E, cand1, d, fo);
     const int s = __builtin_amdgcn_readfirstlane(a.trip[3 * t]);
     const int o = __builtin_amdgcn_readfirstlane(a.trip[3 * t + 1]);
     const int p = __builtin_amdgcn_readfirstlane(a.trip[3 * t + 2]);
-    float2 es[KP], eo[KP], rp[KP];
-    load_row2<KP>(a.E, s, d, es);
-    load_row2<KP>(a.E, o, d, eo);
-    load_row2<KP>(a.R, p, d, rp);
+    float4 es[KQ], eo[KQ], rp[KQ];
+    load_row4<KQ>(a.E, s, d, es);
+    load_row4<KQ>(a.E, o, d, eo);
+    load_row4<KQ>(a.R, p, d, rp);
     bool ok = true;
+#ifndef SKGE_ABL_NO_FILTER
     if (l < 2) ok = l == 0 ? !set_contains(a.set, cand0, o, p) : !set_contains(a.set, s, cand1, p);
+#endif
     const uint64_t okm = __ballot(ok);
     int neg0 = (okm & 1ull) ? cand0 : -1;
     int neg1 = (okm & 2ull) ? cand1 : -1;
-    if (neg0 < 0 || neg1 < 0) {
+    if (neg0 < 0 || neg1 < 0) {   // rare: a first draw hit a training triple
       sample_rest(a, skey, j, s, o, p, 1, neg0, neg1);
       neg0 = __builtin_amdgcn_readfirstlane(neg0);
       neg1 = __builtin_amdgcn_readfirstlane(neg1);
-      if (neg0 >= 0 && neg0 != cand0) load_row2<KP>(a.E, neg0, d, fs);
-      if (neg1 >= 0 && neg1 != cand1) load_row2<KP>(a.E, neg1, d, fo);
+      if (neg0 >= 0 && neg0 != cand0) load_row4<KQ>(a.E, neg0, d, fs);
+      if (neg1 >= 0 && neg1 != cand1) load_row4<KQ>(a.E, neg1, d, fo);
     }
     float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
-    float2 gp[KP], g0[KP], g1[KP];
+    float4 gp[KQ], g0[KQ], g1[KQ];
 #pragma unroll
-    for (int m = 0; m < KP; ++m) {
+    for (int m = 0; m < KQ; ++m) {
 #define SKGE_EL(X)                                                                    \
   {                                                                                   \
-    const float vp = (es[m].X + rp[m].X) - eo[m].X;                                   \
+    const float vp = (es[m].X + rp[m].X) - eo[m].X;   /* transe.py:32 */              \
     const float v0 = (fs[m].X + rp[m].X) - eo[m].X;                                   \
     const float v1 = (es[m].X + rp[m].X) - fo[m].X;                                   \
     ps += fabsf(vp);                                                                  \
@@ -290,31 +300,36 @@ __global__ __launch_bounds__(256) void k_transe_l1_sample_grad_i16(SampleArgs a)
   }
       SKGE_EL(x)
       SKGE_EL(y)
+      SKGE_EL(z)
+      SKGE_EL(w)
 #undef SKGE_EL
     }
     const float pscore = -wave_sum(ps);
     const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
-    const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;
+    const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // strict >, transe.py:73
     const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
     if (a.neg_out && l == 0) {
       a.neg_out[2 * (long long)w] = neg0;
       a.neg_out[2 * (long long)w + 1] = neg1;
     }
     {
+      // occurrence counts + touched slots (entity slots 4w+{s,o,s',o'}):
+      // pair 0 lists (sp,op,sn,on) = (s,o,s',o), pair 1 = (s,o,s,o')
       const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
       const int rE = sel4(l, s, o, neg0, neg1);
+      const Accum aR = replica(a.accR, j);
       if (l < 5) {
         const bool ent = l < 4;
-        commit_slot(ent ? a.accE.cnt : a.accR.cnt, ent ? a.accE.touched : a.accR.touched,
+        commit_slot(ent ? a.accE.cnt : aR.cnt, ent ? a.accE.touched : aR.touched,
                     ent ? rE : p, ent ? cE : 2 * (v0 + v1), ent ? 4 * w + l : w);
       }
     }
     if (v0 + v1 == 0) continue;
     nv += v0 + v1;
     const float fv0 = (float)v0, fv1 = (float)v1;
-    float2 cs[KP], co[KP], c0[KP], c1[KP], cr[KP];
+    float4 cs[KQ], co[KQ], c0[KQ], c1[KQ], cr[KQ];
 #pragma unroll
-    for (int m = 0; m < KP; ++m) {
+    for (int m = 0; m < KQ; ++m) {
 #define SKGE_CO(X)                                                   \
   cs[m].X = fv0 * gp[m].X + fv1 * (gp[m].X + g1[m].X);               \
   co[m].X = -(fv0 * (gp[m].X + g0[m].X) + fv1 * gp[m].X);            \
@@ -323,13 +338,17 @@ __global__ __launch_bounds__(256) void k_transe_l1_sample_grad_i16(SampleArgs a)
   cr[m].X = fv0 * (gp[m].X + g0[m].X) + fv1 * (gp[m].X + g1[m].X);
       SKGE_CO(x)
       SKGE_CO(y)
+      SKGE_CO(z)
+      SKGE_CO(w)
 #undef SKGE_CO
     }
-    acc_row2_i16<KP>(a.accE, s, cs, d);
-    acc_row2_i16<KP>(a.accE, o, co, d);
-    if (v0) acc_row2_i16<KP>(a.accE, neg0, c0, d);
-    if (v1) acc_row2_i16<KP>(a.accE, neg1, c1, d);
-    acc_row2_i16<KP>(a.accR, p, cr, d);
+#ifndef SKGE_ABL_NO_ATOM   // timing-only ablation builds (tools/ablate.sh)
+    acc_row4_i16<KQ>(a.accE, s, cs, d);
+    acc_row4_i16<KQ>(a.accE, o, co, d);
+    if (v0) acc_row4_i16<KQ>(a.accE, neg0, c0, d);
+    if (v1) acc_row4_i16<KQ>(a.accE, neg1, c1, d);
+    acc_row4_i16<KQ>(replica(a.accR, j), p, cr, d);
+#endif
   }
   if (l == 0 && nv) {
     if (a.nviol) atomicAdd(a.nviol, nv);
@@ -352,25 +371,18 @@ static int launch_sample(const SampleArgs& a, bool l1, hipStream_t st) {
   int blocks = (a.count + 3) / 4;
   if (blocks < 1) blocks = 1;
   if (blocks > 16384) blocks = 16384;
-  if (a.accE.mode == ACC_I16X2) {
-    if (!l1 || a.accR.mode != ACC_I16X2 || (a.d & 1) || 4ll * a.count > 32767) {
-      set_error("packed accumulators need TransE-L1, both tables packed, even d, 4*count <= 32767");
+  if (a.accE.mode == ACC_I16X4) {
+    if (!l1 || a.accR.mode != ACC_I16X4 || (a.d & 3) || a.d > 1024 || 4ll * a.count > 32767) {
+      set_error("packed accumulators need TransE-L1, both tables packed, d %% 4 == 0, "
+                "d <= 1024, 4*count <= 32767");
       return SKGE_EINVAL;
     }
-    const int kp = (a.d + 127) / 128;
+    const int kq = (a.d / 4 + 63) / 64;
 #define SKGE_SP(K) \
-  case K: hipLaunchKernelGGL((k_transe_l1_sample_grad_i16<K>), dim3(blocks), dim3(256), 0, st, a); break;
-    switch (kp) {
-      SKGE_SP(1)
-      SKGE_SP(2)
-      SKGE_SP(4)
-      SKGE_SP(8)
-      default:
-        switch (kp) {
-          case 3: hipLaunchKernelGGL((k_transe_l1_sample_grad_i16<4>), dim3(blocks), dim3(256), 0, st, a); break;
-          default: hipLaunchKernelGGL((k_transe_l1_sample_grad_i16<8>), dim3(blocks), dim3(256), 0, st, a);
-        }
-    }
+  hipLaunchKernelGGL((k_transe_l1_sample_grad_i16<K>), dim3(blocks), dim3(256), 0, st, a)
+    if (kq <= 1) SKGE_SP(1);
+    else if (kq <= 2) SKGE_SP(2);
+    else SKGE_SP(4);
 #undef SKGE_SP
     SKGE_CHECK_LAUNCH("transe l1 packed sample grad");
     return SKGE_OK;
@@ -446,6 +458,7 @@ static int fill_sample_args(SampleArgs& a, int l1, const skge_table_t* ent, cons
   int rc;
   if ((rc = check_table(ent, "ent", true))) return rc;
   if ((rc = check_table(rel, "rel", true))) return rc;
+  if ((rc = check_single(ent, "ent"))) return rc;
   SKGE_CHECK_ARG(ent->width == d && rel->width == d, "table widths must equal d");
   SKGE_CHECK_ARG(km_for(d) != 0, "d=%d unsupported", d);
   SKGE_CHECK_ARG(trip && set_slots && epoch_key, "NULL argument");

@@ -594,6 +594,7 @@ static int check_model_tables(int model, const skge_table_t* ent, const skge_tab
   if ((rc = check_table(ent, "ent", true)) != SKGE_OK) return rc;
   if ((rc = check_table(rel, "rel", model != SKGE_RESCAL)) != SKGE_OK) return rc;
   if ((rc = check_f32(ent, "ent")) || (rc = check_f32(rel, "rel"))) return rc;
+  if ((rc = check_single(ent, "ent")) || (rc = check_single(rel, "rel"))) return rc;
   SKGE_CHECK_ARG(model >= 0 && model <= 3, "unknown model %d", model);
   SKGE_CHECK_ARG(d > 0 && ent->width == d, "entity width %d != d %d", ent->width, d);
   if (model == SKGE_RESCAL)

@@ -57,6 +57,8 @@ inline Accum accum_of(const skge_table_t* t) {
   a.touched = t->acc_touched;
   a.width = t->width;
   a.mode = t->acc_mode;
+  a.replicas = t->acc_replicas > 1 ? t->acc_replicas : 1;
+  a.rows = t->rows;
   return a;
 }
 
@@ -64,13 +66,24 @@ inline int check_table(const skge_table_t* t, const char* name, bool need_acc) {
   SKGE_CHECK_ARG(t != nullptr, "%s: table is NULL", name);
   SKGE_CHECK_ARG(t->param != nullptr, "%s: param is NULL", name);
   SKGE_CHECK_ARG(t->rows > 0 && t->width > 0, "%s: bad shape %d x %d", name, t->rows, t->width);
-  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 || t->acc_mode == SKGE_ACC_I16X2,
+  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 || t->acc_mode == SKGE_ACC_I16X4,
                  "%s: unknown accumulator mode %d", name, t->acc_mode);
-  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 || (t->width % 2 == 0 && t->width <= 1024),
-                 "%s: packed accumulator needs an even width <= 1024", name);
+  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 || (t->width % 4 == 0 && t->width <= 1024),
+                 "%s: packed accumulator needs width %% 4 == 0 and <= 1024", name);
   if (need_acc) {
     SKGE_CHECK_ARG(t->acc_sum && t->acc_cnt, "%s: accumulator buffers missing", name);
   }
+  SKGE_CHECK_ARG(t->acc_replicas <= 1 || t->acc_touched == nullptr,
+                 "%s: replicated accumulators must be dense (acc_touched NULL)", name);
+  SKGE_CHECK_ARG(t->acc_replicas <= 1 || t->acc_replicas == 2 || t->acc_replicas == 4 ||
+                     t->acc_replicas == 8 || t->acc_replicas == 16 || t->acc_replicas == 32,
+                 "%s: acc_replicas must be 1, 2, 4, 8, 16 or 32", name);
+  return SKGE_OK;
+}
+
+// producers that do not spread over replicas
+inline int check_single(const skge_table_t* t, const char* name) {
+  SKGE_CHECK_ARG(t->acc_replicas <= 1, "%s: this producer needs a single accumulator copy", name);
   return SKGE_OK;
 }
 

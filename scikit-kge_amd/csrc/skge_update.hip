@@ -173,67 +173,72 @@ __device__ __forceinline__ void apply_row(const TableDev& t, int row, bool upd) 
   }
 }
 
-// ACC_I16X2 form of apply_row: the accumulator holds exact integer pair sums;
-// rows in the pair layout (float2 per lane, see load_row2)
-template <int KP>
+// ACC_I16X4 form of apply_row: the accumulator holds exact integer sums,
+// four per qword; rows in the quad layout (see load_row4): one 16-byte load /
+// store per lane per 1 KB of row
+template <int KQ>
 __device__ __forceinline__ void apply_row_i16(const TableDev& t, int row, bool upd) {
   const int l = lane_id();
-  const int w = t.width, h = w >> 1;
+  const int w = t.width, nq = w >> 2;
   int c = 0;
   if (l == 0) c = atomicExch(t.acc.cnt + row, 0);
-  int* __restrict__ srow = reinterpret_cast<int*>(t.acc.sum) + (size_t)row * h;
-  float2* __restrict__ prow = reinterpret_cast<float2*>(t.P + (size_t)row * w);
-  float2* __restrict__ arow = t.A ? reinterpret_cast<float2*>(t.A + (size_t)row * w) : nullptr;
+  unsigned long long* __restrict__ srow =
+      reinterpret_cast<unsigned long long*>(t.acc.sum) + (size_t)row * nq;
+  float4* __restrict__ prow = reinterpret_cast<float4*>(t.P + (size_t)row * w);
+  float4* __restrict__ arow = t.A ? reinterpret_cast<float4*>(t.A + (size_t)row * w) : nullptr;
   const bool ada = t.opt == OPT_ADAGRAD;
-  int sv[KP];
-  float2 p[KP], a[KP];
+  unsigned long long sv[KQ];
+  float4 p[KQ], a[KQ];
 #pragma unroll
-  for (int m = 0; m < KP; ++m) {
-    const int q = 64 * m + l, qc = q < h ? q : h - 1;
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
     sv[m] = srow[qc];
     p[m] = prow[qc];
-    a[m] = ada ? arow[qc] : make_float2(0.0f, 0.0f);
+    a[m] = ada ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
   c = __builtin_amdgcn_readfirstlane(c);
-  if (c == 0) return;
+  if (c == 0) return;   // another wave owns the row, or a stale slot
   const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
   float ss = 0.0f;
 #pragma unroll
-  for (int m = 0; m < KP; ++m) {
-    const bool in = 64 * m + l < h;
-    float s0, s1;
-    unpack_i16x2(in ? sv[m] : 0, s0, s1);
-#define SKGE_UP(X, S)                                                   \
+  for (int m = 0; m < KQ; ++m) {
+    const bool in = 64 * m + l < nq;
+    const float4 sm = unpack_i16x4(in ? sv[m] : 0ull);
+#define SKGE_UP(X)                                                      \
   {                                                                     \
-    const float g = (S + t.rin * p[m].X) / div + t.rout * p[m].X;       \
+    const float g = (sm.X + t.rin * p[m].X) / div + t.rout * p[m].X;    \
     float pv = p[m].X;                                                  \
     if (ada) {                                                          \
-      a[m].X = a[m].X + g * g;                                          \
-      pv = pv - (t.lr * g) / fmaxf(sqrtf(a[m].X), 1e-7f);               \
+      a[m].X = a[m].X + g * g;                        /* param.py:147 */\
+      pv = pv - (t.lr * g) / fmaxf(sqrtf(a[m].X), 1e-7f); /* 152-155 */ \
     } else {                                                            \
-      pv = pv - t.lr * g;                                               \
+      pv = pv - t.lr * g;                             /* param.py:130 */\
     }                                                                   \
     p[m].X = in ? pv : 0.0f;                                            \
     ss += p[m].X * p[m].X;                                              \
   }
-    SKGE_UP(x, s0)
-    SKGE_UP(y, s1)
+    SKGE_UP(x)
+    SKGE_UP(y)
+    SKGE_UP(z)
+    SKGE_UP(w)
 #undef SKGE_UP
   }
   if (t.post != POST_NONE && upd) {
     ss = wave_sum(ss);
     const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss) : (ss < 1.0f ? 1.0f : ss);
 #pragma unroll
-    for (int m = 0; m < KP; ++m) {
+    for (int m = 0; m < KQ; ++m) {
       p[m].x = p[m].x / nrm;
       p[m].y = p[m].y / nrm;
+      p[m].z = p[m].z / nrm;
+      p[m].w = p[m].w / nrm;
     }
   }
 #pragma unroll
-  for (int m = 0; m < KP; ++m) {
+  for (int m = 0; m < KQ; ++m) {
     const int q = 64 * m + l;
-    if (q < h) {
-      srow[q] = 0;
+    if (q < nq) {
+      srow[q] = 0ull;
       if (upd) {
         prow[q] = p[m];
         if (ada) arow[q] = a[m];
@@ -242,12 +247,120 @@ __device__ __forceinline__ void apply_row_i16(const TableDev& t, int row, bool u
   }
 }
 
+// Dense table with replicated accumulators: one WORKGROUP per row.  Its 256
+// threads spread over (copy, dword) pairs, fold the copies into LDS with
+// integer adds (packed sums are linear) or float adds, and clear them; wave 0
+// then updates the row.  Few registers, so the entity waves sharing the launch
+// keep their occupancy.
+template <int MODE, int KR>
+__device__ __forceinline__ void apply_row_rep_block(const TableDev& t, int row, bool upd,
+                                                    int* lds) {
+  const int tid = threadIdx.x, R = t.acc.replicas, rows = t.rows, w = t.width;
+  const int dw = acc_row_dwords(MODE, w);             // accumulator dwords per row
+  for (int i = tid; i <= dw; i += blockDim.x) lds[i] = 0;   // lds[dw]: the count
+  __syncthreads();
+  for (int k = tid; k < R; k += blockDim.x) {
+    int* cp = t.acc.cnt + (size_t)k * rows + row;
+    const int c = *cp;
+    if (c) {
+      atomicAdd(lds + dw, c);
+      *cp = 0;
+    }
+  }
+  if (MODE == ACC_I16X4) {   // fold qwords: packed sums are linear under integer adds
+    const int nq = w >> 2, total = R * nq;
+    unsigned long long* l64 = reinterpret_cast<unsigned long long*>(lds);
+#pragma unroll 4
+    for (int f = tid; f < total; f += blockDim.x) {
+      const int k = f / nq, q = f - k * nq;
+      unsigned long long* sp =
+          reinterpret_cast<unsigned long long*>(t.acc.sum) + ((size_t)k * rows + row) * nq + q;
+      const unsigned long long v = *sp;
+      if (v) {
+        atomicAdd(l64 + q, v);
+        *sp = 0ull;
+      }
+    }
+  } else {
+    const int total = R * dw;
+#pragma unroll 4
+    for (int f = tid; f < total; f += blockDim.x) {
+      const int k = f / dw, q = f - k * dw;
+      float* sp = t.acc.sum + ((size_t)k * rows + row) * dw + q;
+      const float v = *sp;
+      if (v != 0.0f) {
+        atomicAdd(reinterpret_cast<float*>(lds) + q, v);
+        *sp = 0.0f;
+      }
+    }
+  }
+  __syncthreads();
+  const int c = lds[dw];
+  if (tid < 64 && c != 0) {
+    const int l = tid;
+    const bool ada = t.opt == OPT_ADAGRAD;
+    const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
+    float ss = 0.0f;
+    // element e = l + 64k, KR = ceil(width / 64) per lane
+    float p[KR], a[KR];
+    float* prow = t.P + (size_t)row * w;
+    float* arow = t.A ? t.A + (size_t)row * w : nullptr;
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int e = l + 64 * k;
+      p[k] = 0.0f;
+      a[k] = 0.0f;
+      {
+        const int ec = e < w ? e : w - 1;
+        float sv;
+        if (MODE == ACC_I16X4) {
+          const float4 q4 = unpack_i16x4(reinterpret_cast<unsigned long long*>(lds)[ec >> 2]);
+          const int r4 = ec & 3;
+          sv = r4 == 0 ? q4.x : (r4 == 1 ? q4.y : (r4 == 2 ? q4.z : q4.w));
+        } else {
+          sv = __int_as_float(lds[ec]);
+        }
+        const float pv = prow[ec];
+        const float av = ada ? arow[ec] : 0.0f;
+        const float g = (sv + t.rin * pv) / div + t.rout * pv;
+        float np = pv, na = av;
+        if (ada) {
+          na = av + g * g;
+          np = pv - (t.lr * g) / fmaxf(sqrtf(na), 1e-7f);
+        } else {
+          np = pv - t.lr * g;
+        }
+        p[k] = e < w ? np : 0.0f;
+        a[k] = na;
+        ss += p[k] * p[k];
+      }
+    }
+    if (t.post != POST_NONE && upd) {
+      ss = wave_sum(ss);
+      const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss) : (ss < 1.0f ? 1.0f : ss);
+#pragma unroll
+      for (int k = 0; k < KR; ++k) p[k] = p[k] / nrm;
+    }
+    if (upd) {
+#pragma unroll
+      for (int k = 0; k < KR; ++k) {
+        const int e = l + 64 * k;
+        if (e < w) {
+          prow[e] = p[k];
+          if (ada) arow[e] = a[k];
+        }
+      }
+    }
+  }
+  __syncthreads();   // lds is reused by the next row
+}
+
 template <int K, int MODE>
 __device__ __forceinline__ void apply_slot(const TableDev& t, int slot) {
   const int row = t.acc.touched ? __builtin_amdgcn_readfirstlane(t.acc.touched[slot]) : slot;
   if (row < 0) return;
   const bool upd = t.gate == nullptr || *t.gate != 0;
-  if (MODE == ACC_I16X2)
+  if (MODE == ACC_I16X4)
     apply_row_i16<K>(t, row, upd);
   else
     apply_row<K>(t, row, upd);
@@ -255,11 +368,23 @@ __device__ __forceinline__ void apply_slot(const TableDev& t, int slot) {
 
 // fused apply: one wavefront per slot of table 0 (slots [0, n0)) or table 1
 // (slots [n0, n0 + n1)); a dense table (no slot records) has one slot per
-// row.  Two explicit table arguments keep every table field in scalar registers.
-template <int K, int MODE>
-__global__ __launch_bounds__(256) void k_apply(TableDev t0, int n0, TableDev t1, int n1) {
+// row.  If table 1 is dense with replicated accumulators, its rows are handled
+// by the workgroups past nblk0 instead (one workgroup per row).  Two explicit
+// table arguments keep every table field in scalar registers.
+template <int K, int MODE, int KR>
+__global__ __launch_bounds__(256) void k_apply(TableDev t0, int n0, TableDev t1, int n1,
+                                               int nblk0) {
+  __shared__ int lds[1025];
+  if (t1.acc.replicas > 1) {
+    if ((int)blockIdx.x >= nblk0) {
+      for (int r = blockIdx.x - nblk0; r < n1; r += gridDim.x - nblk0)
+        apply_row_rep_block<MODE, KR>(t1, r, t1.gate == nullptr || *t1.gate != 0, lds);
+      return;
+    }
+    n1 = 0;   // table 1 is not a wave-per-slot table
+  }
   const int wpb = blockDim.x >> 6;
-  const int nw = gridDim.x * wpb;
+  const int nw = (t1.acc.replicas > 1 ? nblk0 : gridDim.x) * wpb;
   for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < n0 + n1; w += nw) {
     if (w < n0)
       apply_slot<K, MODE>(t0, w);
@@ -536,10 +661,11 @@ extern "C" int skge_accum_reset(void* stream, const skge_table_t* t, int nslots)
   if (rc) return rc;
   if ((rc = check_slots(t, nslots, "table"))) return rc;
   hipStream_t st = as_stream(stream);
-  const size_t row_bytes = (size_t)t->width * 4 / (t->acc_mode == SKGE_ACC_I16X2 ? 2 : 1);
-  if (t->acc_touched == nullptr) {   // dense table: clear everything
-    SKGE_CHECK_HIP(hipMemsetAsync(t->acc_sum, 0, row_bytes * t->rows, st));
-    SKGE_CHECK_HIP(hipMemsetAsync(t->acc_cnt, 0, sizeof(int) * t->rows, st));
+  const size_t row_bytes = (size_t)acc_row_dwords(t->acc_mode, t->width) * 4;
+  if (t->acc_touched == nullptr) {   // dense table: clear everything (every copy)
+    const size_t reps = t->acc_replicas > 1 ? (size_t)t->acc_replicas : 1;
+    SKGE_CHECK_HIP(hipMemsetAsync(t->acc_sum, 0, reps * row_bytes * t->rows, st));
+    SKGE_CHECK_HIP(hipMemsetAsync(t->acc_cnt, 0, reps * sizeof(int) * t->rows, st));
     return SKGE_OK;
   }
   if (nslots == 0) return SKGE_OK;
@@ -592,28 +718,50 @@ extern "C" int skge_accum_apply(void* stream, const skge_table_t* tables, int nt
   // narrow tables are applied two per launch (same accumulator mode); each
   // wide table gets its own launch
   auto kdim = [&](int i) {
-    return tables[i].acc_mode == SKGE_ACC_I16X2 ? (tables[i].width / 2 + 63) / 64
+    return tables[i].acc_mode == SKGE_ACC_I16X4 ? (tables[i].width / 4 + 63) / 64
                                                 : km_for(tables[i].width);
   };
   auto slots_of = [&](int i) {
     return tables[i].acc_touched ? nslots[i] : tables[i].rows;   // dense: one slot per row
   };
+  auto reps = [&](int i) { return tables[i].acc_replicas > 1 ? tables[i].acc_replicas : 1; };
   auto launch_pair = [&](int i, int j) -> int {
-    int k = kdim(i);
-    if (j >= 0) k = std::max(k, kdim(j));
-    const int mode = tables[i].acc_mode;
-    const long long waves = (long long)slots_of(i) + (j >= 0 ? slots_of(j) : 0);
-    const int gw = grid_for_waves(waves);
-    TableDev a = table_dev(tables + i);
-    TableDev b = j >= 0 ? table_dev(tables + j) : a;
-    const int na = slots_of(i), nb = j >= 0 ? slots_of(j) : 0;
-#define SKGE_AP(K, M) \
-  hipLaunchKernelGGL((k_apply<K, M>), dim3(gw), dim3(256), 0, st, a, na, b, nb)
-    if (mode == SKGE_ACC_I16X2) {
-      if (k <= 1) SKGE_AP(1, ACC_I16X2);
-      else if (k <= 2) SKGE_AP(2, ACC_I16X2);
-      else if (k <= 4) SKGE_AP(4, ACC_I16X2);
-      else SKGE_AP(8, ACC_I16X2);
+    if (j >= 0 && reps(i) > 1) std::swap(i, j);   // a replicated table goes second
+    if (j < 0 && reps(i) > 1) {                   // a replicated table alone
+      j = i;
+      i = -1;
+    }
+    int k = i >= 0 ? kdim(i) : 1;
+    if (j >= 0 && reps(j) == 1) k = std::max(k, kdim(j));
+    const int mode = tables[i >= 0 ? i : j].acc_mode;
+    const int na = i >= 0 ? slots_of(i) : 0;
+    const int nb = j >= 0 ? slots_of(j) : 0;
+    int nblk0, grid;
+    if (j >= 0 && reps(j) > 1) {
+      nblk0 = std::max(1, std::min((na + 3) / 4, 16384));
+      grid = nblk0 + std::min(nb, 4096);
+    } else {
+      nblk0 = grid = grid_for_waves((long long)na + nb);
+    }
+    TableDev b = j >= 0 ? table_dev(tables + j) : table_dev(tables + i);
+    TableDev a = i >= 0 ? table_dev(tables + i) : b;
+    if (i < 0) a.acc.replicas = 1;   // placeholder table 0 with no slots
+    if (j < 0) b.acc.replicas = 1;
+    const int kr = (j >= 0 && reps(j) > 1) ? km_for(tables[j].width) : 1;
+#define SKGE_AP3(K, M, KR) \
+  hipLaunchKernelGGL((k_apply<K, M, KR>), dim3(grid), dim3(256), 0, st, a, na, b, nb, nblk0)
+#define SKGE_AP(K, M)                             \
+  do {                                            \
+    if (kr <= 1) SKGE_AP3(K, M, 1);               \
+    else if (kr <= 2) SKGE_AP3(K, M, 2);          \
+    else if (kr <= 4) SKGE_AP3(K, M, 4);          \
+    else if (kr <= 8) SKGE_AP3(K, M, 8);          \
+    else SKGE_AP3(K, M, 16);                      \
+  } while (0)
+    if (mode == SKGE_ACC_I16X4) {
+      if (k <= 1) SKGE_AP(1, ACC_I16X4);
+      else if (k <= 2) SKGE_AP(2, ACC_I16X4);
+      else SKGE_AP(4, ACC_I16X4);
     } else {
       switch (k) {
         case 1: SKGE_AP(1, ACC_F32); break;
@@ -624,6 +772,7 @@ extern "C" int skge_accum_apply(void* stream, const skge_table_t* tables, int nt
         default: SKGE_AP(16, ACC_F32); break;
       }
     }
+#undef SKGE_AP3
 #undef SKGE_AP
     return SKGE_OK;
   };

@@ -18,7 +18,7 @@ SKGE_TRANSE_L1, SKGE_TRANSE_L2, SKGE_HOLE, SKGE_RESCAL = 0, 1, 2, 3
 SKGE_AF_LINEAR, SKGE_AF_SIGMOID, SKGE_AF_TANH, SKGE_AF_RELU = 0, 1, 2, 3
 SKGE_SGD, SKGE_ADAGRAD = 0, 1
 SKGE_POST_NONE, SKGE_POST_NORMALIZE, SKGE_POST_NORMLESS1 = 0, 1, 2
-SKGE_ACC_F32, SKGE_ACC_I16X2 = 0, 1
+SKGE_ACC_F32, SKGE_ACC_I16X4 = 0, 1
 
 c_p = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -32,7 +32,7 @@ class SkgeTable(ctypes.Structure):
     """Mirror of skge_table_t."""
     _fields_ = [("param", c_p), ("state", c_p), ("acc_sum", c_p), ("acc_cnt", c_p),
                 ("acc_touched", c_p), ("rows", c_i), ("width", c_i), ("touched_cap", c_i),
-                ("acc_mode", c_i), ("opt", c_i), ("post", c_i), ("lr", c_f), ("rin", c_f), ("rout", c_f),
+                ("acc_mode", c_i), ("acc_replicas", c_i), ("opt", c_i), ("post", c_i), ("lr", c_f), ("rin", c_f), ("rout", c_f),
                 ("fixed_div", c_f), ("gate", c_p)]
 
 

@@ -38,7 +38,7 @@ class EpochRunner(object):
     """Native hipGraph epoch of the TransE device batch loop."""
 
     def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, stream=None,
-                 nviol_total=None, force_f32=False):
+                 nviol_total=None, force_f32=False, replicas=1):
         from .transe import TransE
         if not isinstance(model, TransE):
             raise NotImplementedError("device_loop supports TransE (the north-star path) only")
@@ -52,12 +52,15 @@ class EpochRunner(object):
         bs = kg.T // nbatches
         # TransE-L1 sign contributions are small integers: exact packed int16x2
         # accumulation when every per-batch sum fits (4 * batch <= 32767)
-        packed = bool(model.l1) and model.d % 2 == 0 and 4 * bs <= 32767 and not force_f32
-        mode = L.SKGE_ACC_I16X2 if packed else L.SKGE_ACC_F32
+        packed = bool(model.l1) and model.d % 4 == 0 and 4 * bs <= 32767 and not force_f32
+        mode = L.SKGE_ACC_I16X4 if packed else L.SKGE_ACC_F32
         from .param import Accumulator
         E, R = model.params["E"], model.params["R"]
         self.accE = Accumulator(E.rows, E.width, dev, slots=4 * bs, mode=mode)
-        self.accR = Accumulator(R.rows, R.width, dev, mode=mode, dense=True)
+        # relation rows are hot (every positive adds to one of |R| rows):
+        # `replicas` > 1 spreads the adds over accumulator copies (dense apply sums them)
+        self.accR = Accumulator(R.rows, R.width, dev, mode=mode, dense=True,
+                                replicas=replicas)
         self.packed = packed
         self.te = updaters["E"].table(self.accE)
         self.tr = updaters["R"].table(self.accR)

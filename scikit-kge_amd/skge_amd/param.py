@@ -184,6 +184,7 @@ def table_struct(param, state=None, acc=None, opt=L.SKGE_SGD, post=L.SKGE_POST_N
         t.acc_touched = L.ptr(acc.touched)          # None -> dense table
         t.touched_cap = acc.touched.numel() if acc.touched is not None else 0
         t.acc_mode = acc.mode
+        t.acc_replicas = acc.replicas
     t.rows = param.rows
     t.width = param.width
     t.opt, t.post, t.lr = opt, post, lr
@@ -208,10 +209,12 @@ class Accumulator(object):
     """Device segment-sum accumulator of one table (see skge_table_t): dense
     fp32 sums, occurrence counts and the fixed-slot touched records."""
 
-    def __init__(self, rows, width, device, slots=1024, mode=L.SKGE_ACC_F32, dense=False):
+    def __init__(self, rows, width, device, slots=1024, mode=L.SKGE_ACC_F32, dense=False,
+                 replicas=1):
         self.rows, self.width, self.mode = rows, width, mode
-        self.sum = torch.zeros(rows * width, dtype=torch.float32, device=device)
-        self.cnt = torch.zeros(rows, dtype=torch.int32, device=device)
+        self.replicas = replicas if dense else 1
+        self.sum = torch.zeros(self.replicas * rows * width, dtype=torch.float32, device=device)
+        self.cnt = torch.zeros(self.replicas * rows, dtype=torch.int32, device=device)
         self.touched = None if dense else \
             torch.full((max(slots, 1),), -1, dtype=torch.int32, device=device)
 

@@ -60,14 +60,16 @@ def test_epoch_permutation_is_a_bijection():
             assert not np.array_equal(p, np.arange(T))
 
 
-@pytest.mark.parametrize("packed,dense_r", [(False, False), (True, True), (False, True)])
-def test_sampler_kernel_parity_with_oracle_replay(packed, dense_r):
+@pytest.mark.parametrize("packed,dense_r,reps", [(False, False, 1), (True, True, 1),
+                                                 (False, True, 1), (True, True, 32),
+                                                 (False, True, 8)])
+def test_sampler_kernel_parity_with_oracle_replay(packed, dense_r, reps):
     """Device sampler + fused score/scatter + apply, in every accumulator form
     (fp32 / exact packed int16x2; relation table with slots / dense), against
     the oracle replaying the recorded pairs."""
     from skge_amd import _lib as L
     from skge_amd.param import Accumulator
-    S, m, upd, trip, tset, kg = _setup(300, 5, 2000, 50)
+    S, m, upd, trip, tset, kg = _setup(300, 5, 2000, 200)
     E0 = np.asarray(m.E, dtype=np.float64)
     R0 = np.asarray(m.R, dtype=np.float64)
     dev = m.device
@@ -76,9 +78,10 @@ def test_sampler_kernel_parity_with_oracle_replay(packed, dense_r):
     negs = torch.full((count, 2), -7, dtype=torch.int32, device=dev)
     perm = torch.empty(kg.T, dtype=torch.int64, device=dev)
     nviol = torch.zeros(1, dtype=torch.int32, device=dev)
-    mode = L.SKGE_ACC_I16X2 if packed else L.SKGE_ACC_F32
+    mode = L.SKGE_ACC_I16X4 if packed else L.SKGE_ACC_F32
     accE = Accumulator(m.E.rows, m.E.width, dev, slots=4 * count, mode=mode)
-    accR = Accumulator(m.R.rows, m.R.width, dev, slots=count, mode=mode, dense=dense_r)
+    accR = Accumulator(m.R.rows, m.R.width, dev, slots=count, mode=mode, dense=dense_r,
+                       replicas=reps)
     te = upd["E"].table(accE)
     tr = upd["R"].table(accR)
     lib = L.lib()

@@ -37,9 +37,9 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 def test_table_struct_layout():
     from skge_amd import _lib as L
-    # 5 pointers, 5 ints, 4 floats, pad, 1 pointer (natural alignment) = 88 bytes
-    assert ctypes.sizeof(L.SkgeTable) == 88
-    assert L.SkgeTable.gate.offset == 80
+    # 5 pointers, 7 ints, 4 floats, pad, 1 pointer (natural alignment) = 96 bytes
+    assert ctypes.sizeof(L.SkgeTable) == 96
+    assert L.SkgeTable.gate.offset == 88
 
 
 def test_errors_are_reported_without_a_gpu():
