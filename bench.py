@@ -47,6 +47,21 @@ def make_wn18_kg(n_ent=N_ENT, n_rel=N_REL, n_triples=N_TRIPLES, seed=0):
     return out.astype(np.int32)
 
 
+def pmc_traffic(kernel_substr):
+    """Per-launch HBM-side traffic of a kernel from the newest committed rocprofv3
+    PMC summary (profiles/*/pmc.json, made by tools/gpu_profile.sh): 2*FETCH_SIZE
+    + WRITE_SIZE per the gfx950 correction in MI355X_MICROARCH.md "HBM"."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc.json")))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    for name, e in data.items():
+        if kernel_substr in name and "traffic_bytes_per_launch" in e:
+            return e["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def algorithmic_bytes(d, B, P, U_E, U_R, opt_k=12):
     """BYTES(batch) = 4d(3B + P) + k d (U_E + U_R) + 20B."""
     return 4 * d * (3 * B + P) + opt_k * d * (U_E + U_R) + 20 * B
@@ -169,11 +184,15 @@ def main():
 
     # ---- per-kernel timing (HIP events on the runner stream, eager launches of
     # one more epoch, outside the timed region) for the roofline ----
-    prof = kernel_profile(model, upd, kg, nb, d, st, runner)
+    prof = pipe_profile(runner, kg, nb, d) if runner.pipelined else \
+        kernel_profile(model, upd, kg, nb, d, st, runner)
 
     if rank == 0:
         cpu = None if args.no_cpu else cpu_baseline(trip, d, nb, args.cpu_seconds)
         k = prof["dominant"]
+        kname = {"transe_sample_grad": "sample_grad", "accum_apply": "k_apply",
+                 "pipe_batch": "k_pipe_batch"}[k["name"]]
+        traffic, traffic_src = pmc_traffic(kname)
         line = {
             "metric": "triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X",
             "value": round(value, 1),
@@ -195,7 +214,8 @@ def main():
             "roofline": {"bound": "hbm", "kernel": k["name"],
                          "achieved": round(k["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 4),
-                         "traffic": None,
+                         "traffic": None if traffic is None else round(traffic),
+                         "traffic_source": traffic_src,
                          "bytes_per_launch": round(k["bytes_per_launch"]),
                          "avg_launch_us": round(k["avg_us"], 3)},
             "cpu_baseline": cpu,
@@ -207,12 +227,51 @@ def main():
                             for n, v in prof["kernels"].items()},
                 "step_algorithmic_GB_s": round(prof["epoch_bytes"] / (elapsed / args.steps) / 1e9, 1),
                 "launches_per_step": runner.nlaunches,
+                "runner": "pipelined (1 launch/batch)" if runner.pipelined else "two-launch",
                 "accumulator": "int16x4 exact" if runner.packed else "fp32",
             },
         }
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def _score_bytes(d, cnt, V):
+    """Scoring part of a batch: gathers of s, o, p + 2
+    corrupted rows, 20 B of index/hash traffic per positive, and the atomic row
+    adds of the violating positives (<= 5 rows each)."""
+    return 4 * d * (3 * cnt + 2 * cnt) + 20 * cnt + 4 * d * min(5 * cnt, 2 * V + 3 * cnt)
+
+
+def pipe_profile(runner, kg, nb, d):
+    """Pipelined runner: one eager epoch with HIP events around every launch
+    (skge_pipe_runner_profile, on the runner's stream).  Launch i >= 1 scores
+    batch i-1 and applies batch i-2: its algorithmic bytes are the scoring
+    bytes of its batch plus 24 B/element for each row it applied (read sum,
+    param, state; write param, state, zero sum), with the applied-row and
+    violation counts the kernel itself recorded."""
+    us, stats = runner.profile()
+    T = kg.T
+    bs = T // nb
+    counts = [min(bs, T - s) for s in range(0, T, bs)] + [0]   # + the flush launch
+    b_pipe, t_pipe, total = 0.0, 0.0, 0.0
+    for i, cnt in enumerate(counts, start=1):
+        UE, UR, V = (int(x) for x in stats[i])
+        b = _score_bytes(d, cnt, V) + 24 * d * (UE + UR)
+        b_pipe += b
+        t_pipe += float(us[i])
+        if cnt:
+            total += algorithmic_bytes(d, cnt, 2 * cnt, 0, 0)
+        total += 12 * d * (UE + UR)
+    n = len(counts)
+    kern = {"pipe_batch": {"name": "pipe_batch", "avg_us": t_pipe / n, "launches": n,
+                           "bytes_per_launch": b_pipe / n,
+                           "achieved_gbs": b_pipe / (t_pipe * 1e-6) / 1e9},
+            # per positive: triple 12 B, two filter words 8 B, record 20 B
+            "epoch_sample": {"name": "epoch_sample", "avg_us": float(us[0]), "launches": 1,
+                             "bytes_per_launch": 40.0 * T,
+                             "achieved_gbs": 40.0 * T / (float(us[0]) * 1e-6) / 1e9}}
+    return {"kernels": kern, "dominant": kern["pipe_batch"], "epoch_bytes": total}
 
 
 def kernel_profile(model, upd, kg, nb, d, st, runner):
@@ -254,9 +313,7 @@ def kernel_profile(model, upd, kg, nb, d, st, runner):
             times["transe_sample_grad"].append(e[0].elapsed_time(e[1]) * 1e3)
             times["accum_apply"].append(e[2].elapsed_time(e[3]) * 1e3)
             P = 2 * cnt
-            # gathers of s, o, p + 2 corrupted rows, index/hash traffic, and the
-            # atomic row adds of the violating positives (<= 5 rows each)
-            b_sg = 4 * d * (3 * cnt + P) + 20 * cnt + 4 * d * min(5 * cnt, 2 * V + 3 * cnt)
+            b_sg = _score_bytes(d, cnt, V)
             b_ap = 24 * d * (UE + UR)     # read sum, param, state; write param, state, zero sum
             bytes_["transe_sample_grad"] += b_sg
             bytes_["accum_apply"] += b_ap

@@ -237,6 +237,45 @@ int skge_runner_run(skge_runner_t *r, void *stream, int nepochs);
 int skge_runner_nlaunches(const skge_runner_t *r);
 void skge_runner_destroy(skge_runner_t *r);
 
+/*
+ * Pipelined epoch runner for TransE-L1 with packed accumulators (the
+ * throughput path).  Same result, bit for bit, as skge_runner_create's loop
+ * with the same tables and arguments: all negatives of an epoch are drawn in
+ * one launch, then each mini-batch is ONE launch that scores batch b while
+ * applying batch b-1's updates (accumulators double-buffered by batch parity;
+ * a scoring wave that reads a row batch b-1 touched applies it first or waits
+ * for its publisher).  Needs ent/rel in SKGE_ACC_I16X4 mode, d % 4 == 0,
+ * 4 * (T / nbatches) <= 32767, an entity table with slot records (capacity
+ * >= 4 * batch), a dense single-copy relation table and no gates.  Allocates
+ * the second accumulator copy and per-row batch marks itself (freed by
+ * destroy).  *epoch_key must only advance (the runner advances it once per
+ * epoch).  Replaces the per-batch loop of skge/base.py:1268-1284.
+ */
+typedef struct skge_pipe_runner skge_pipe_runner_t;
+skge_pipe_runner_t *skge_pipe_runner_create(void *stream, const skge_table_t *ent,
+                                            const skge_table_t *rel, int d, const int *trip,
+                                            int64_t T, const void *set, int64_t set_capacity,
+                                            int nbatches, uint64_t seed, uint64_t *epoch_key,
+                                            float margin, int ntries, int *nviol_total);
+int skge_pipe_runner_run(skge_pipe_runner_t *r, void *stream, int nepochs);
+/* synchronizes the stream; returns 0, or 1 if a bounded cross-workgroup wait
+ * gave up (results then invalid), or a negative SKGE error code */
+int skge_pipe_runner_error(skge_pipe_runner_t *r, void *stream);
+int skge_pipe_runner_nlaunches(const skge_pipe_runner_t *r);
+/* One epoch launched eagerly (trains like run(1)) with HIP events around every
+ * launch: us_out[i] = launch i's duration (i = 0: negative draws, 1..nb1:
+ * batches, nb1+1: flush, nb1+2: key advance); stats_out[3i..3i+2] = entity
+ * rows applied, relation rows applied, violating pairs scored by launch i.
+ * Both arrays need nlaunches entries (x3 for stats).  For the roofline.
+ * Diagnostics: if trace_out is given, batch launch trace_launch (1..nb1+1)
+ * records per-wave s_memrealtime stamps (10 ns): trace_out[0] = scoring
+ * waves B, [1] = apply waves A, then 6 words per scoring wave (start, rows
+ * loaded, pending rows settled, scored, atomics done, pending mask | 256 if
+ * violating) and 2 per apply wave (start, end); trace_len must hold them. */
+int skge_pipe_runner_profile(skge_pipe_runner_t *r, void *stream, float *us_out, int *stats_out,
+                             int n, int trace_launch, uint64_t *trace_out, int64_t trace_len);
+void skge_pipe_runner_destroy(skge_pipe_runner_t *r);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,804 @@
+// Pipelined device batch loop for TransE-L1 (the throughput path, one launch
+// per mini-batch).
+//
+// The reference processes mini-batches strictly in sequence: batch b reads
+// the parameters produced by batch b-1's updates (skge/base.py:1268-1284,
+// 1306-1316).  The two-launch loop (skge_epoch.hip) honours that with a
+// score/scatter kernel and an apply kernel per batch.  Here batch b's scoring
+// and batch b-1's updates share ONE launch:
+//
+//   * all negatives of the epoch are drawn up front (k_epoch_sample: the same
+//     counter-based draws and rejection test as k_transe_sample_grad, so the
+//     epoch's pairs are identical), giving per-positive records (s, o, p, s', o');
+//   * launch g scores batch b ("B" role, workgroups [0, nB)) while workgroups
+//     [nB, grid) apply batch b-1's updates ("A" role);
+//   * entity rows (many, each touched by few positives): accumulators
+//     double-buffered by batch parity.  A B wave about to read a row batch
+//     b-1 touched (pend[row] == g-1, recorded by the previous launch) makes
+//     sure that row's update has landed first: it claims (atomicExch on the
+//     count) and applies it itself, or waits (bounded) on the row's `done`
+//     word.  Appliers publish with write-through (sc1) stores, a vmcnt(0)
+//     drain, then the done word; waiters poll it with sc1 loads and re-read
+//     the row with sc1 loads (MI355X_MICROARCH.md, hand-off forms, row 1).  A
+//     claimer never waits, so dispatch order never matters;
+//   * relation rows (few, each read by most positives of a batch): no waiting
+//     at all.  Parameters and AdaGrad state are double-buffered (R_b lives in
+//     buffer W(b)), accumulators triple-buffered by launch id.  Every B wave
+//     recomputes R_b[p] from R_{b-1}[p] and batch b-1's sum itself (a few
+//     hundred bytes of L2-hot reads); one A wave per row writes R_b[p] for the
+//     next launch and clears the accumulator copy two launches old.
+//
+// Every row update depends only on that row's own (exact integer) sums, count,
+// parameters and AdaGrad state, computed by the same code (row_update), so the
+// result is bitwise identical to the two-launch loop (tested).
+#include <vector>
+
+#include "skge_host.h"
+#include "skge_sampler.h"
+
+namespace skge {
+
+// Counters many waves add to are sharded over NSHARD words on lines of their
+// own: no-return atomics on ONE word serialise at the memory side (~12 ns
+// each, MI355X_MICROARCH.md "fanin"), which for ~1.4k adders per launch would
+// cost more than the launch's real work.
+constexpr int NSHARD = 64, SHARD_STRIDE = 32;   // 32 ints = one 128-B line
+__device__ __forceinline__ int* shard_of(int* base) {
+  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  return base + (wave & (NSHARD - 1)) * SHARD_STRIDE;
+}
+
+struct UpdParams {
+  int opt, post;
+  float lr, rin, rout, fdiv;   // g = (sum + rin*P)/div + rout*P, div = fdiv > 0 ? fdiv : count
+};
+
+struct PipeTab {               // entity table
+  float* P;
+  float* A;                    // AdaGrad state or nullptr (SGD)
+  unsigned long long* sum[2];  // exact int16x4 sums, by batch parity
+  int* cnt[2];
+  int* touched[2];             // slot records of the batch
+  int* pend[2];                // [rows]: id of the launch that last accumulated into the row
+  int* done;                   // [rows]: id of the launch whose update of the row was last applied
+  UpdParams u;
+  int* claims;                 // profile only: rows applied in this launch (sharded)
+};
+
+struct RelTab {                // relation table
+  float* P[2];                 // P[0]: the caller's parameters; P[1]: the other buffer
+  float* A[2];                 // AdaGrad state, likewise (nullptr: SGD)
+  unsigned long long* acc[3];  // [rows][rw]: int16x4 sums in words [0, d/4), count in word d/4
+  int rows, rw;
+  UpdParams u;
+  int* updated;                // profile only: rows with a nonzero count (sharded)
+};
+
+struct PipeArgs {
+  PipeTab E;
+  RelTab R;
+  const int4* rec;             // [T]: (s, o, p, s') of the epoch's positive j
+  const int* rec_n1;           // [T]: o'
+  long long start;             // B role: this batch's positives [start, start + count)
+  int count;
+  int prev_slots;              // A role: entity slots of the previous batch
+  int b, nb1;                  // batch index in the epoch (nb1: the flush), batches per epoch
+  const uint64_t* epoch_key;
+  int d, nA;                   // nA: workgroups of the A role
+  float margin;
+  int* nviol_total;            // the caller's counter: += the epoch's violations, at the flush
+  int* nviol_shards;           // [NSHARD][SHARD_STRIDE]: this epoch's violations so far
+  int* stats_viol;             // profile only: violating pairs of this launch (sharded)
+  unsigned long long* trace;   // diagnostics only: per-wave timestamps of one launch
+  int* err;                    // set when a bounded wait gives up
+};
+
+// Launch id: consecutive within an epoch (batches 0..nb1-1, then the flush)
+// and across epochs (epoch e+1's batch 0 follows epoch e's flush); >= 2, so
+// zero-initialised marks never look pending.
+__device__ __forceinline__ int launch_id(const PipeArgs& a) {
+  return (int)(*a.epoch_key * (uint64_t)(a.nb1 + 1)) + a.b + 2;
+}
+
+// 16-B write-through (sc1) row accesses through a buffer descriptor over one
+// row (MI355X_MICROARCH.md: 4-B sc1 stores are ~6x the 16-B time per byte).
+// Lanes past the row fall outside the descriptor: loads return 0, stores drop.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int AUX_SC1 = 16;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const float* T, int row, int d) {
+  row = __builtin_amdgcn_readfirstlane(row);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(T) + (size_t)row * d, 0, d * 4,
+                                           0x00020000);
+}
+
+template <int KQ>
+__device__ __forceinline__ void load_row4_sc1(const float* T, int row, int d, float4 (&v)[KQ]) {
+  const __amdgpu_buffer_rsrc_t rs = row_rsrc(T, row, d);
+  const int l = lane_id();
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, (64 * m + l) * 16, 0, AUX_SC1);
+    v[m] = *reinterpret_cast<const float4*>(&x);
+  }
+}
+
+template <int KQ>
+__device__ __forceinline__ void store_row4_sc1(float* T, int row, int d, const float4 (&v)[KQ]) {
+  const __amdgpu_buffer_rsrc_t rs = row_rsrc(T, row, d);
+  const int l = lane_id();
+#pragma unroll
+  for (int m = 0; m < KQ; ++m)
+    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&v[m]), rs,
+                                           (64 * m + l) * 16, 0, AUX_SC1);
+}
+
+// load a quad-layout row of P, A (optional) and packed sums (clamped,
+// unconditional loads; lanes past the row read the last quad)
+template <int KQ>
+__device__ __forceinline__ void load_upd_row(const float* P, const float* A,
+                                             const unsigned long long* S, int d, float4 (&p)[KQ],
+                                             float4 (&a)[KQ], unsigned long long (&sv)[KQ]) {
+  const int l = lane_id(), nq = d >> 2;
+  const float4* prow = reinterpret_cast<const float4*>(P);
+  const float4* arow = reinterpret_cast<const float4*>(A);
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
+    sv[m] = S[qc];
+    p[m] = prow[qc];
+    a[m] = A ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+}
+
+// One row's update from its packed sums and occurrence count c > 0: segment
+// mean + AdaGrad / SGD + projection; the same arithmetic as apply_row_i16
+// (skge_update.hip) and the reference (skge/param.py:130, 147-155;
+// skge/transe.py normalize).  Lanes past the row end with zeros.
+template <int KQ>
+__device__ __forceinline__ void row_update(const UpdParams& t, int c, int d,
+                                           const unsigned long long (&sv)[KQ], float4 (&p)[KQ],
+                                           float4 (&a)[KQ]) {
+  const int l = lane_id(), nq = d >> 2;
+  const bool ada = t.opt == OPT_ADAGRAD;
+  const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
+  float ss = 0.0f;
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const bool in = 64 * m + l < nq;
+    const float4 sm = unpack_i16x4(in ? sv[m] : 0ull);
+#define SKGE_UP(X)                                                      \
+  {                                                                     \
+    const float g = (sm.X + t.rin * p[m].X) / div + t.rout * p[m].X;    \
+    float pv = p[m].X;                                                  \
+    if (ada) {                                                          \
+      a[m].X = a[m].X + g * g;                        /* param.py:147 */\
+      pv = pv - (t.lr * g) / fmaxf(sqrtf(a[m].X), 1e-7f); /* 152-155 */ \
+    } else {                                                            \
+      pv = pv - t.lr * g;                             /* param.py:130 */\
+    }                                                                   \
+    p[m].X = in ? pv : 0.0f;                                            \
+    ss += p[m].X * p[m].X;                                              \
+  }
+    SKGE_UP(x)
+    SKGE_UP(y)
+    SKGE_UP(z)
+    SKGE_UP(w)
+#undef SKGE_UP
+  }
+  if (t.post != POST_NONE) {
+    ss = wave_sum(ss);
+    const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss) : (ss < 1.0f ? 1.0f : ss);
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+      p[m].x = p[m].x / nrm;
+      p[m].y = p[m].y / nrm;
+      p[m].z = p[m].z / nrm;
+      p[m].w = p[m].w / nrm;
+    }
+  }
+}
+
+// Claim a pending entity row's update (the first wave to swap its count out
+// applies it) and, if claimed, apply it from accumulator copy `pp` and publish
+// it as launch `gp` (write-through stores, drain, done word).  The row's sums,
+// parameters and state are loaded in the same memory round trip as the claim:
+// nobody writes them before the claim is won, and a loser discards them.
+template <int KQ>
+__device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int row, int d, int gp) {
+  const int l = lane_id(), nq = d >> 2;
+  int c = 0;
+  if (l == 0) c = atomicExch(t.cnt[pp] + row, 0);
+  unsigned long long* srow = t.sum[pp] + (size_t)row * nq;
+  unsigned long long sv[KQ];
+  float4 p[KQ], a[KQ];
+  load_upd_row<KQ>(t.P + (size_t)row * d, t.A ? t.A + (size_t)row * d : nullptr, srow, d, p, a,
+                   sv);
+  c = __builtin_amdgcn_readfirstlane(c);
+  if (c == 0) return;   // another wave owns the row
+  row_update<KQ>(t.u, c, d, sv, p, a);
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l;
+    if (q < nq) srow[q] = 0ull;
+  }
+  store_row4_sc1<KQ>(t.P, row, d, p);
+  if (t.A) store_row4_sc1<KQ>(t.A, row, d, a);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+  if (l == 0) __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
+}
+
+// B role: make sure launch gp's update of entity `row` (pending at launch
+// start) has landed -- apply it if nobody has claimed it yet, else wait for
+// its publisher
+template <int KQ>
+__device__ __forceinline__ void ensure_applied(const PipeTab& t, int pp, int row, int d, int gp,
+                                               int* err) {
+  if (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gp) return;
+  claim_and_apply<KQ>(t, pp, row, d, gp);
+  unsigned spins = 0;
+  while (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gp) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > (1u << 22)) {   // ~0.5 s: never hang the GPU; report instead
+      if (lane_id() == 0) atomicOr(err, 1);
+      break;
+    }
+    if ((spins & 1023u) == 0 &&   // once one wait has given up, the rest stop too
+        __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      break;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the re-read below the poll
+}
+
+// relation row R_b[row] (the value batch b scores with): R_{b-1}[row] from
+// buffer rd updated with batch b-1's sums (accumulator copy ra)
+template <int KQ>
+__device__ __forceinline__ void rel_row(const RelTab& t, int row, int d, int rd, int ra,
+                                        float4 (&p)[KQ], float4 (&a)[KQ], int& c) {
+  unsigned long long sv[KQ];
+  const unsigned long long* acc = t.acc[ra] + (size_t)row * t.rw;
+  load_upd_row<KQ>(t.P[rd] + (size_t)row * d, t.A[rd] ? t.A[rd] + (size_t)row * d : nullptr, acc,
+                   d, p, a, sv);
+  c = __builtin_amdgcn_readfirstlane((int)acc[d >> 2]);
+  if (c) row_update<KQ>(t.u, c, d, sv, p, a);
+}
+
+__device__ __forceinline__ unsigned long long now_10ns() { return __builtin_amdgcn_s_memrealtime(); }
+
+template <int KQ>
+__global__ __launch_bounds__(256) void k_pipe_batch(PipeArgs a) {
+  const int wpb = blockDim.x >> 6;
+  const int l = lane_id();
+  const int d = a.d, nq = d >> 2;
+  const int g = launch_id(a), gp = g - 1;
+  const int cp = a.b & 1, pp = cp ^ 1;   // entity accumulator copies: this / previous batch
+  const int rd = a.b & 1;                // relation buffer holding R_{b-1}
+  const int rw = a.b < a.nb1 ? rd ^ 1 : 0;   // ... receiving R_b (the flush: the caller's)
+  const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
+  // scoring workgroups first: they are the critical path and dispatch in order
+  const int nB = gridDim.x - a.nA;
+  if ((int)blockIdx.x >= nB) {
+    // ---- A role: write R_b, then apply the previous batch's entity rows ----
+    const int nR = a.R.rows;
+    const int total = a.prev_slots + nR;
+    const int wa = (blockIdx.x - nB) * wpb + (threadIdx.x >> 6);
+    const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
+    if (a.b == a.nb1 && wa == 0) {   // the flush: fold the epoch's violation count
+      int v = 0;
+      if (l < NSHARD) {
+        v = a.nviol_shards[l * SHARD_STRIDE];
+        a.nviol_shards[l * SHARD_STRIDE] = 0;
+      }
+      v = wave_sum_int(v);
+      if (l == 0 && a.nviol_total && v) atomicAdd(a.nviol_total, v);
+    }
+    for (int w = wa; w < total; w += a.nA * wpb) {
+      if (w < nR) {
+        float4 p[KQ], av[KQ];
+        int c;
+        rel_row<KQ>(a.R, w, d, rd, ra_prev, p, av, c);
+        float4* prow = reinterpret_cast<float4*>(a.R.P[rw] + (size_t)w * d);
+        float4* arow = a.R.A[rw] ? reinterpret_cast<float4*>(a.R.A[rw] + (size_t)w * d) : nullptr;
+        unsigned long long* old = a.R.acc[ra_old] + (size_t)w * a.R.rw;
+        unsigned long long* prev = a.R.acc[ra_prev] + (size_t)w * a.R.rw;
+        const bool flush = a.b == a.nb1;   // no scoring waves read copy ra_prev any more
+#pragma unroll
+        for (int m = 0; m < KQ; ++m) {
+          const int q = 64 * m + l;
+          if (q < nq) {
+            prow[q] = p[m];
+            if (arow) arow[q] = av[m];
+          }
+        }
+        for (int q = l; q <= nq; q += 64) {
+          old[q] = 0ull;
+          if (flush) prev[q] = 0ull;
+        }
+        if (c && a.R.updated && l == 0) atomicAdd(shard_of(a.R.updated), 1);
+      } else {
+        const int row = __builtin_amdgcn_readfirstlane(a.E.touched[pp][w - nR]);
+#ifndef SKGE_PIPE_ABL_NOAPPLY_E   // timing-only ablation: entity rows never updated
+        if (row >= 0) claim_and_apply<KQ>(a.E, pp, row, d, gp);
+#else
+        if (row >= 0 && l == 0) a.E.cnt[pp][row] = 0;
+#endif
+      }
+    }
+    if (a.trace && l == 0) {
+      unsigned long long* tr = a.trace + 2 + 6 * (size_t)a.count + 2 * (size_t)wa;
+      tr[0] = ta0;
+      tr[1] = now_10ns();
+    }
+    return;
+  }
+  // ---- B role: score batch b, scatter into accumulator copies cp / ra_cur ----
+  int nv = 0;
+  for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
+    const long long j = a.start + w;
+    unsigned long long tt[4];
+    if (a.trace) tt[0] = now_10ns();
+    const int4 r4 = a.rec[j];
+    const int s = __builtin_amdgcn_readfirstlane(r4.x);
+    const int o = __builtin_amdgcn_readfirstlane(r4.y);
+    const int p = __builtin_amdgcn_readfirstlane(r4.z);
+    const int neg0 = __builtin_amdgcn_readfirstlane(r4.w);
+    const int neg1 = __builtin_amdgcn_readfirstlane(a.rec_n1[j]);
+    const int n0r = neg0 >= 0 ? neg0 : s, n1r = neg1 >= 0 ? neg1 : o;
+    // entity rows as of the launch start (plain loads), their pending marks,
+    // and the relation row this batch scores with
+    float4 es[KQ], eo[KQ], rp[KQ], fs[KQ], fo[KQ];
+    load_row4<KQ>(a.E.P, s, d, es);
+    load_row4<KQ>(a.E.P, o, d, eo);
+    load_row4<KQ>(a.E.P, n0r, d, fs);
+    load_row4<KQ>(a.E.P, n1r, d, fo);
+    int mark = 0;
+    if (l < 4) mark = a.E.pend[pp][sel4(l, s, o, n0r, n1r)];
+    {
+      float4 ra[KQ];
+      int c;
+      rel_row<KQ>(a.R, p, d, rd, ra_prev, rp, ra, c);
+    }
+#ifdef SKGE_PIPE_ABL_NOENSURE   // timing-only ablation (tools/ablate.sh): ignore pending rows
+    const uint64_t pend = 0ull * __ballot(mark == gp);
+#else
+    const uint64_t pend = __ballot(mark == gp) & 0xfull;
+#endif
+    if (a.trace) tt[1] = now_10ns();
+    if (pend) {   // some entity rows have an update of batch b-1 outstanding
+      // one (not unrolled) copy of the claim/apply/wait code keeps registers low
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) {
+        if (!((pend >> k) & 1ull)) continue;
+        ensure_applied<KQ>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err);
+      }
+      if (pend & 1ull) load_row4_sc1<KQ>(a.E.P, s, d, es);
+      if (pend & 2ull) load_row4_sc1<KQ>(a.E.P, o, d, eo);
+      if (pend & 4ull) load_row4_sc1<KQ>(a.E.P, n0r, d, fs);
+      if (pend & 8ull) load_row4_sc1<KQ>(a.E.P, n1r, d, fo);
+    }
+    if (a.trace) tt[2] = now_10ns();
+    float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
+    float4 gp4[KQ], g0[KQ], g1[KQ];
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+#define SKGE_EL(X)                                                                    \
+  {                                                                                   \
+    const float vp = (es[m].X + rp[m].X) - eo[m].X;   /* transe.py:32 */              \
+    const float v0 = (fs[m].X + rp[m].X) - eo[m].X;                                   \
+    const float v1 = (es[m].X + rp[m].X) - fo[m].X;                                   \
+    ps += fabsf(vp);                                                                  \
+    n0 += fabsf(v0);                                                                  \
+    n1 += fabsf(v1);                                                                  \
+    gp4[m].X = signf_np(-((eo[m].X - rp[m].X) - es[m].X)); /* transe.py:103,115 */    \
+    g0[m].X = signf_np((eo[m].X - rp[m].X) - fs[m].X);     /* transe.py:104,117 */    \
+    g1[m].X = signf_np((fo[m].X - rp[m].X) - es[m].X);                                \
+  }
+      SKGE_EL(x)
+      SKGE_EL(y)
+      SKGE_EL(z)
+      SKGE_EL(w)
+#undef SKGE_EL
+    }
+    const float pscore = -wave_sum(ps);
+    const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
+    const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // strict >, transe.py:73
+    const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
+    if (a.trace) tt[3] = now_10ns();
+    {
+      // counts, touched slots and pending marks of this batch
+      const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
+      const int rE = sel4(l, s, o, neg0, neg1);
+      if (l < 4) {
+        commit_slot(a.E.cnt[cp], a.E.touched[cp], rE, cE, 4 * w + l);
+        if (cE > 0) a.E.pend[cp][rE] = g;
+      } else if (l == 4 && v0 + v1 > 0) {
+        atomicAdd(a.R.acc[ra_cur] + (size_t)p * a.R.rw + nq, (unsigned long long)(2 * (v0 + v1)));
+      }
+    }
+    if (v0 + v1 > 0) {
+      nv += v0 + v1;
+      const float fv0 = (float)v0, fv1 = (float)v1;
+      float4 cs[KQ], co[KQ], c0[KQ], c1[KQ], cr[KQ];
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) {
+#define SKGE_CO(X)                                                   \
+  cs[m].X = fv0 * gp4[m].X + fv1 * (gp4[m].X + g1[m].X);             \
+  co[m].X = -(fv0 * (gp4[m].X + g0[m].X) + fv1 * gp4[m].X);          \
+  c0[m].X = g0[m].X;                                                 \
+  c1[m].X = -g1[m].X;                                                \
+  cr[m].X = fv0 * (gp4[m].X + g0[m].X) + fv1 * (gp4[m].X + g1[m].X);
+        SKGE_CO(x)
+        SKGE_CO(y)
+        SKGE_CO(z)
+        SKGE_CO(w)
+#undef SKGE_CO
+      }
+      Accum aE, aR;
+      aE.sum = reinterpret_cast<float*>(a.E.sum[cp]);
+      acc_row4_i16<KQ>(aE, s, cs, d);
+      acc_row4_i16<KQ>(aE, o, co, d);
+      if (v0) acc_row4_i16<KQ>(aE, neg0, c0, d);
+      if (v1) acc_row4_i16<KQ>(aE, neg1, c1, d);
+      // relation sums: rows of rw words (acc_row4_i16 indexes rows of d/4 words)
+      aR.sum = reinterpret_cast<float*>(a.R.acc[ra_cur] + (size_t)p * a.R.rw);
+      acc_row4_i16<KQ>(aR, 0, cr, d);
+    }
+    if (a.trace) {   // stamp after issue (no drain: the trace must not slow the launch)
+      if (l == 0) {
+        unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
+        tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
+        tr[5] = pend | ((unsigned long long)(v0 + v1 > 0) << 8);
+      }
+    }
+  }
+  if (l == 0 && nv) {
+    atomicAdd(shard_of(a.nviol_shards), nv);
+    if (a.stats_viol) atomicAdd(shard_of(a.stats_viol), nv);
+  }
+}
+
+__global__ void k_pipe_advance(uint64_t* ek) { *ek += 1; }
+
+// draw every negative of the epoch: one thread per positive, the same draws and
+// first-accepted-try rule as k_transe_sample_grad (skge/sample.py:41-46)
+__global__ void k_epoch_sample(const int* __restrict__ trip, long long T, int half, uint64_t seed,
+                               const uint64_t* ekp, TripleSet set, int n_ent, int ntries,
+                               int4* rec, int* rec_n1) {
+  const uint64_t ek = *ekp;
+  const Perm pm = {(uint64_t)T, half, epoch_perm_key(seed, ek)};
+  const uint64_t skey = epoch_sample_key(seed, ek);
+  for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < T;
+       j += (long long)gridDim.x * blockDim.x) {
+    const long long t = (long long)perm_index((uint64_t)j, pm);
+    const int s = trip[3 * t], o = trip[3 * t + 1], p = trip[3 * t + 2];
+    int neg0 = -1, neg1 = -1;
+    for (int tr = 0; tr < ntries; ++tr) {
+      const int c = draw(skey, j, 0, tr, n_ent);
+      if (!set_contains(set, c, o, p)) {
+        neg0 = c;
+        break;
+      }
+    }
+    for (int tr = 0; tr < ntries; ++tr) {
+      const int c = draw(skey, j, 1, tr, n_ent);
+      if (!set_contains(set, s, c, p)) {
+        neg1 = c;
+        break;
+      }
+    }
+    rec[j] = make_int4(s, o, p, neg0);
+    rec_n1[j] = neg1;
+  }
+}
+
+}  // namespace skge
+
+using namespace skge;
+
+// ---- pipelined runner ----
+struct skge_pipe_runner {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  std::vector<void*> bufs;
+  int* err = nullptr;
+  int* stats = nullptr;            // [nlaunch][3] (profile only)
+  // the epoch's launches
+  const int* trip = nullptr;
+  long long T = 0;
+  int half = 0, n_ent = 0, ntries = 0, kq = 1;
+  uint64_t seed = 0;
+  uint64_t* epoch_key = nullptr;
+  TripleSet set;
+  int4* rec = nullptr;
+  int* rec_n1 = nullptr;
+  std::vector<PipeArgs> batch;     // nb1 batches + the flush
+  std::vector<int> grid;
+  int nlaunch() const { return (int)batch.size() + 2; }
+};
+
+static void* dalloc(skge_pipe_runner* r, size_t bytes) {
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes ? bytes : 4) != hipSuccess) return nullptr;
+  r->bufs.push_back(p);
+  if (hipMemset(p, 0, bytes ? bytes : 4) != hipSuccess) return nullptr;
+  return p;
+}
+
+static void pipe_free(skge_pipe_runner* r) {
+  if (!r) return;
+  if (r->exec) (void)hipGraphExecDestroy(r->exec);
+  if (r->graph) (void)hipGraphDestroy(r->graph);
+  for (void* p : r->bufs) (void)hipFree(p);
+  delete r;
+}
+
+// Enqueue one epoch: draw the negatives, nb1 batch launches, the flush, the
+// key advance.  ev (optional, nlaunch + 1 events) brackets every launch;
+// stats (optional) collects per-launch claim / violation counts.
+static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t* ev, int* stats,
+                          int trace_launch = -1, unsigned long long* trace = nullptr) {
+  int i = 0;
+  if (ev) (void)hipEventRecord(ev[i], st);
+  {
+    long long blocks = (r->T + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_epoch_sample, dim3((unsigned)blocks), dim3(256), 0, st, r->trip, r->T,
+                       r->half, r->seed, (const uint64_t*)r->epoch_key, r->set, r->n_ent,
+                       r->ntries, r->rec, r->rec_n1);
+  }
+  ++i;
+  if (ev) (void)hipEventRecord(ev[i], st);
+  for (size_t k = 0; k < r->batch.size(); ++k, ++i) {
+    PipeArgs a = r->batch[k];
+    if (stats) {
+      const int sh = NSHARD * SHARD_STRIDE;
+      a.E.claims = stats + (3 * i) * sh;
+      a.R.updated = stats + (3 * i + 1) * sh;
+      a.stats_viol = stats + (3 * i + 2) * sh;
+    }
+    if (trace && i == trace_launch) a.trace = trace;
+#define SKGE_PB(K) \
+  hipLaunchKernelGGL((k_pipe_batch<K>), dim3(r->grid[k]), dim3(256), 0, st, a)
+    if (r->kq <= 1) SKGE_PB(1);
+    else if (r->kq <= 2) SKGE_PB(2);
+    else SKGE_PB(4);
+#undef SKGE_PB
+    if (ev) (void)hipEventRecord(ev[i + 1], st);
+  }
+  hipLaunchKernelGGL(k_pipe_advance, dim3(1), dim3(1), 0, st, r->epoch_key);
+  if (ev) (void)hipEventRecord(ev[i + 1], st);
+}
+
+extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_table_t* ent,
+                                                       const skge_table_t* rel, int d,
+                                                       const int* trip, int64_t T, const void* set,
+                                                       int64_t set_capacity, int nbatches,
+                                                       uint64_t seed, uint64_t* epoch_key,
+                                                       float margin, int ntries,
+                                                       int* nviol_total) {
+  // the pipelined loop is the packed TransE-L1 path
+  if (check_table(ent, "ent", true) || check_table(rel, "rel", true)) return nullptr;
+  if (ent->acc_mode != SKGE_ACC_I16X4 || rel->acc_mode != SKGE_ACC_I16X4 || d % 4 || d > 1024 ||
+      ent->width != d || rel->width != d || ent->acc_touched == nullptr ||
+      rel->acc_touched != nullptr || rel->acc_replicas > 1 || ent->acc_replicas > 1 ||
+      ent->gate || rel->gate) {
+    set_error("pipelined runner: needs packed (SKGE_ACC_I16X4) tables, d %% 4 == 0, an entity "
+              "table with slot records and a dense single-copy relation table, no gates");
+    return nullptr;
+  }
+  if (!trip || !set || !epoch_key || T <= 0 || nbatches < 1 || nbatches > T || !stream ||
+      set_capacity < 4 || (set_capacity & (set_capacity - 1)) || ntries < 1) {
+    set_error("pipelined runner: bad arguments");
+    return nullptr;
+  }
+  // batch geometry of StochasticTrainer._optim (skge/base.py:1246-1268)
+  const int64_t bs = T / nbatches;
+  if (4 * bs > 32767 || 4 * bs > ent->touched_cap) {
+    set_error("pipelined runner: batch too large for packed sums or the slot capacity");
+    return nullptr;
+  }
+  std::vector<std::pair<int64_t, int64_t>> batches;
+  for (int64_t s0 = 0; s0 < T; s0 += bs) batches.push_back({s0, (s0 + bs <= T) ? bs : T - s0});
+  const int nb1 = (int)batches.size();
+  skge_pipe_runner* r = new skge_pipe_runner();
+  const int nq = d / 4;
+  PipeArgs a = {};
+  auto upd = [](const skge_table_t* s) {
+    UpdParams u;
+    u.opt = s->opt;
+    u.post = s->post;
+    u.lr = s->lr;
+    u.rin = s->rin;
+    u.rout = s->rout;
+    u.fdiv = s->fixed_div;
+    return u;
+  };
+  {
+    PipeTab& t = a.E;
+    const int N = ent->rows;
+    t.P = ent->param;
+    t.A = ent->opt == SKGE_ADAGRAD ? ent->state : nullptr;
+    t.u = upd(ent);
+    t.claims = nullptr;
+    t.sum[0] = reinterpret_cast<unsigned long long*>(ent->acc_sum);
+    t.cnt[0] = ent->acc_cnt;
+    t.touched[0] = ent->acc_touched;
+    t.sum[1] = (unsigned long long*)dalloc(r, (size_t)N * nq * 8);
+    t.cnt[1] = (int*)dalloc(r, (size_t)N * 4);
+    t.touched[1] = (int*)dalloc(r, (size_t)4 * bs * 4);
+    t.pend[0] = (int*)dalloc(r, (size_t)N * 4);
+    t.pend[1] = (int*)dalloc(r, (size_t)N * 4);
+    t.done = (int*)dalloc(r, (size_t)N * 4);
+    RelTab& q = a.R;
+    const int M = rel->rows;
+    const bool ada = rel->opt == SKGE_ADAGRAD;
+    q.rows = M;
+    q.rw = (nq + 1 + 15) / 16 * 16;   // sums + count, rows on whole 128-B lines
+    q.u = upd(rel);
+    q.updated = nullptr;
+    q.P[0] = rel->param;
+    q.P[1] = (float*)dalloc(r, (size_t)M * d * 4);
+    q.A[0] = ada ? rel->state : nullptr;
+    q.A[1] = ada ? (float*)dalloc(r, (size_t)M * d * 4) : nullptr;
+    for (int k = 0; k < 3; ++k) q.acc[k] = (unsigned long long*)dalloc(r, (size_t)M * q.rw * 8);
+    if (!t.sum[1] || !t.cnt[1] || !t.touched[1] || !t.pend[0] || !t.pend[1] || !t.done ||
+        !q.P[1] || (ada && !q.A[1]) || !q.acc[0] || !q.acc[1] || !q.acc[2]) {
+      set_error("pipelined runner: device allocation failed");
+      pipe_free(r);
+      return nullptr;
+    }
+  }
+  r->rec = (int4*)dalloc(r, (size_t)T * sizeof(int4));
+  r->rec_n1 = (int*)dalloc(r, (size_t)T * 4);
+  r->err = (int*)dalloc(r, 4);
+  r->stats = (int*)dalloc(r, (size_t)(nb1 + 3) * 3 * NSHARD * SHARD_STRIDE * 4);
+  int* vsh = (int*)dalloc(r, (size_t)NSHARD * SHARD_STRIDE * 4);
+  if (!r->rec || !r->rec_n1 || !r->err || !r->stats || !vsh) {
+    set_error("pipelined runner: device allocation failed");
+    pipe_free(r);
+    return nullptr;
+  }
+  r->trip = trip;
+  r->T = T;
+  r->half = perm_half(T);
+  r->n_ent = ent->rows;
+  r->ntries = ntries;
+  r->seed = seed;
+  r->epoch_key = epoch_key;
+  r->set.slots = (const int4*)set;
+  r->set.filter = (const uint32_t*)((const int4*)set + set_capacity);
+  r->set.mask = (uint64_t)(set_capacity - 1);
+  r->set.fmask = (uint64_t)(8 * set_capacity - 1);
+  r->kq = (nq + 63) / 64;
+  a.rec = r->rec;
+  a.rec_n1 = r->rec_n1;
+  a.nb1 = nb1;
+  a.epoch_key = epoch_key;
+  a.d = d;
+  a.margin = margin;
+  a.nviol_total = nviol_total;
+  a.nviol_shards = vsh;
+  a.stats_viol = nullptr;
+  a.trace = nullptr;
+  a.err = r->err;
+  int prev = 0;
+  for (int b = 0; b <= nb1; ++b) {   // b == nb1: flush of the last batch (A role only)
+    a.b = b;
+    a.start = b < nb1 ? batches[b].first : 0;
+    a.count = b < nb1 ? (int)batches[b].second : 0;
+    a.prev_slots = 4 * prev;
+    const int a_items = 4 * prev + rel->rows;   // entity slots + every relation row
+    a.nA = std::max(1, std::min((a_items + 3) / 4, 16384));
+    const int nBb = std::max(1, std::min((a.count + 3) / 4, 16384));
+    r->batch.push_back(a);
+    r->grid.push_back(a.nA + (a.count > 0 ? nBb : 0));
+    prev = a.count;
+  }
+  hipStream_t st = as_stream(stream);
+  if (hipStreamSynchronize(st) != hipSuccess ||
+      hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    set_error("hipStreamBeginCapture failed");
+    pipe_free(r);
+    return nullptr;
+  }
+  enqueue_epoch(r, st, nullptr, nullptr);
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(st, &g);
+  if (e != hipSuccess || hipGetLastError() != hipSuccess) {
+    set_error("pipelined runner capture failed: %s", hipGetErrorString(e));
+    if (g) (void)hipGraphDestroy(g);
+    pipe_free(r);
+    return nullptr;
+  }
+  r->graph = g;
+  if (hipGraphInstantiate(&r->exec, g, nullptr, nullptr, 0) != hipSuccess) {
+    set_error("hipGraphInstantiate failed");
+    pipe_free(r);
+    return nullptr;
+  }
+  return r;
+}
+
+extern "C" int skge_pipe_runner_run(skge_pipe_runner_t* r, void* stream, int nepochs) {
+  SKGE_CHECK_ARG(r && r->exec, "bad runner");
+  for (int i = 0; i < nepochs; ++i) SKGE_CHECK_HIP(hipGraphLaunch(r->exec, as_stream(stream)));
+  return SKGE_OK;
+}
+
+extern "C" int skge_pipe_runner_profile(skge_pipe_runner_t* r, void* stream, float* us_out,
+                                        int* stats_out, int n, int trace_launch,
+                                        uint64_t* trace_out, int64_t trace_len) {
+  SKGE_CHECK_ARG(r && us_out && stats_out, "NULL argument");
+  const int nl = r->nlaunch();
+  SKGE_CHECK_ARG(n >= nl, "output arrays need nlaunches entries");
+  hipStream_t st = as_stream(stream);
+  std::vector<hipEvent_t> ev(nl + 1, nullptr);
+  int rc = SKGE_OK;
+  for (auto& e : ev)
+    if (hipEventCreate(&e) != hipSuccess) rc = SKGE_EHIP;
+  const size_t sh = (size_t)NSHARD * SHARD_STRIDE;
+  if (rc == SKGE_OK && hipMemsetAsync(r->stats, 0, (size_t)nl * 3 * sh * 4, st) != hipSuccess)
+    rc = SKGE_EHIP;
+  unsigned long long* dtrace = nullptr;
+  if (rc == SKGE_OK && trace_out && trace_launch >= 1 && trace_launch <= (int)r->batch.size()) {
+    const PipeArgs& tb = r->batch[trace_launch - 1];
+    const int64_t need = 2 + 6 * (int64_t)tb.count + 2 * 4 * (int64_t)tb.nA;
+    if (trace_len < need) {
+      set_error("trace buffer needs %lld entries", (long long)need);
+      rc = SKGE_EINVAL;
+    } else if (hipMalloc(&dtrace, need * 8) != hipSuccess ||
+               hipMemsetAsync(dtrace, 0, need * 8, st) != hipSuccess) {
+      rc = SKGE_EHIP;
+    } else {
+      const unsigned long long hdr[2] = {(unsigned long long)tb.count, 4ull * tb.nA};
+      if (hipMemcpyAsync(dtrace, hdr, 16, hipMemcpyHostToDevice, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)   // ordered after the memset, on st
+        rc = SKGE_EHIP;
+    }
+  }
+  if (rc == SKGE_OK) {
+    enqueue_epoch(r, st, ev.data(), r->stats, trace_launch, dtrace);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) rc = SKGE_EHIP;
+  }
+  if (rc == SKGE_OK) {
+    for (int i = 0; i < nl; ++i) {
+      float ms = 0.0f;
+      if (hipEventElapsedTime(&ms, ev[i], ev[i + 1]) != hipSuccess) rc = SKGE_EHIP;
+      us_out[i] = 1e3f * ms;
+    }
+    std::vector<int> h((size_t)nl * 3 * sh);
+    if (hipMemcpy(h.data(), r->stats, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = SKGE_EHIP;
+    for (int k = 0; k < 3 * nl; ++k) {
+      int v = 0;
+      for (int q = 0; q < NSHARD; ++q) v += h[(size_t)k * sh + (size_t)q * SHARD_STRIDE];
+      stats_out[k] = v;
+    }
+    if (dtrace) {
+      const PipeArgs& tb = r->batch[trace_launch - 1];
+      const int64_t need = 2 + 6 * (int64_t)tb.count + 2 * 4 * (int64_t)tb.nA;
+      if (hipMemcpy(trace_out, dtrace, need * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = SKGE_EHIP;
+    }
+  }
+  if (dtrace) (void)hipFree(dtrace);
+  for (auto& e : ev)
+    if (e) (void)hipEventDestroy(e);
+  if (rc != SKGE_OK) set_error("pipelined runner profile failed");
+  return rc;
+}
+
+extern "C" int skge_pipe_runner_error(skge_pipe_runner_t* r, void* stream) {
+  SKGE_CHECK_ARG(r, "bad runner");
+  int v = 0;
+  SKGE_CHECK_HIP(hipStreamSynchronize(as_stream(stream)));
+  SKGE_CHECK_HIP(hipMemcpy(&v, r->err, 4, hipMemcpyDeviceToHost));
+  return v;
+}
+
+extern "C" int skge_pipe_runner_nlaunches(const skge_pipe_runner_t* r) {
+  return r ? r->nlaunch() : -1;
+}
+
+extern "C" void skge_pipe_runner_destroy(skge_pipe_runner_t* r) { pipe_free(r); }

@@ -35,10 +35,17 @@ class DeviceKG(object):
 
 
 class EpochRunner(object):
-    """Native hipGraph epoch of the TransE device batch loop."""
+    """Native hipGraph epoch of the TransE device batch loop.
+
+    pipelined: None (auto) uses the one-launch-per-batch pipelined runner
+    (skge_pipe_runner_*) whenever it applies (TransE-L1, packed accumulators,
+    single-copy relation accumulator) and the two-launch runner otherwise;
+    True demands it, False forces the two-launch runner.  Both give identical
+    parameters.
+    """
 
     def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, stream=None,
-                 nviol_total=None, force_f32=False, replicas=1):
+                 nviol_total=None, force_f32=False, replicas=1, pipelined=None):
         from .transe import TransE
         if not isinstance(model, TransE):
             raise NotImplementedError("device_loop supports TransE (the north-star path) only")
@@ -67,6 +74,21 @@ class EpochRunner(object):
         self.nbatches = nbatches
         torch.cuda.current_stream().synchronize()
         lib = L.lib()
+        can_pipe = packed and replicas <= 1
+        if pipelined and not can_pipe:
+            raise ValueError("pipelined runner needs TransE-L1, d % 4 == 0, 4*batch <= 32767, "
+                             "no forced f32 and replicas == 1")
+        self.pipelined = can_pipe if pipelined is None else bool(pipelined)
+        if self.pipelined:
+            h = lib.skge_pipe_runner_create(
+                L.stream_ptr(self.stream), self.te, self.tr, model.d, L.ptr(kg.trip), kg.T,
+                L.ptr(kg.slots), kg.capacity, int(nbatches), int(seed) & (2 ** 64 - 1),
+                L.ptr(self.epoch_key), float(model.margin), int(ntries), L.ptr(self.nviol_total))
+            if not h:
+                raise L.SkgeError("skge_pipe_runner_create: %s" % lib.skge_last_error().decode())
+            self.handle = h
+            self.nlaunches = lib.skge_pipe_runner_nlaunches(h)
+            return
         h = lib.skge_runner_create(L.stream_ptr(self.stream), int(bool(model.l1)),
                                    self.te, self.tr,
                                    model.d, L.ptr(kg.trip), kg.T, L.ptr(kg.slots), kg.capacity,
@@ -78,18 +100,48 @@ class EpochRunner(object):
         self.nlaunches = lib.skge_runner_nlaunches(h)
 
     def run(self, nepochs=1):
-        L.check(L.lib().skge_runner_run(self.handle, L.stream_ptr(self.stream), int(nepochs)),
-                "runner run")
+        lib = L.lib()
+        fn = lib.skge_pipe_runner_run if self.pipelined else lib.skge_runner_run
+        L.check(fn(self.handle, L.stream_ptr(self.stream), int(nepochs)), "runner run")
+
+    def profile(self, trace_launch=None):
+        """Pipelined runner only: one eager epoch with HIP events around every
+        launch (trains like run(1)).  Returns (us, stats): per-launch durations
+        and [entity rows applied, relation rows applied, violating pairs];
+        with trace_launch (1..nb1+1) also the per-wave timestamp trace of that
+        launch (include/skge_hip.h, skge_pipe_runner_profile)."""
+        if not self.pipelined:
+            raise ValueError("profile() needs the pipelined runner")
+        import numpy as np
+        n = self.nlaunches
+        us = np.zeros(n, dtype=np.float32)
+        stats = np.zeros((n, 3), dtype=np.int32)
+        tr = np.zeros(2 + 6 * self.kg.T + 8 * self.kg.T + 64, dtype=np.uint64) \
+            if trace_launch else None
+        L.check(L.lib().skge_pipe_runner_profile(
+            self.handle, L.stream_ptr(self.stream), us.ctypes.data, stats.ctypes.data, n,
+            int(trace_launch or 0), None if tr is None else tr.ctypes.data,
+            0 if tr is None else len(tr)), "runner profile")
+        if trace_launch:
+            return us, stats, tr
+        return us, stats
 
     def synchronize(self):
         self.stream.synchronize()
+        if self.pipelined:
+            rc = L.lib().skge_pipe_runner_error(self.handle, L.stream_ptr(self.stream))
+            if rc != 0:
+                raise L.SkgeError("pipelined runner: %s" % (
+                    "a cross-workgroup wait timed out" if rc > 0 else
+                    L.lib().skge_last_error().decode()))
 
     def __del__(self):
         h = getattr(self, "handle", None)
         if h:
             try:
                 self.stream.synchronize()
-                L.lib().skge_runner_destroy(h)
+                lib = L.lib()
+                (lib.skge_pipe_runner_destroy if self.pipelined else lib.skge_runner_destroy)(h)
             except Exception:
                 pass
             self.handle = None

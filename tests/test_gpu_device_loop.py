@@ -141,10 +141,12 @@ def test_sampler_mode_balance():
 
 
 def test_runner_small_two_epochs_invariants():
-    S, m, upd, trip, tset, kg = _setup(500, 7, 3000, 50)
+    S, m, upd, trip, tset, kg = _setup(500, 7, 3000, 52)
     from skge_amd.device import EpochRunner
     tr = EpochRunner(m, upd, kg, nbatches=10, seed=1)
-    assert tr.nlaunches == 2 * 10 + 1   # 3000 = 10 x 300: no remainder batch
+    assert tr.pipelined
+    # 3000 = 10 x 300, no remainder batch: epoch sample + 10 batches + flush + advance
+    assert tr.nlaunches == 10 + 3
     tr.run(2)
     tr.synchronize()
     E = np.asarray(m.E, dtype=np.float64)
@@ -172,7 +174,8 @@ def test_runner_wn18_full_size_properties(l1):
     kg = DeviceKG(trip, m.device)
     R0 = np.asarray(m.R).copy()
     runner = EpochRunner(m, upd, kg, nbatches=100, seed=0)
-    assert runner.nlaunches == 2 * 101 + 1
+    assert runner.pipelined == l1
+    assert runner.nlaunches == (101 + 3 if l1 else 2 * 101 + 1)
     runner.run(1)
     runner.synchronize()
     E = np.asarray(m.E, dtype=np.float64)
@@ -185,6 +188,49 @@ def test_runner_wn18_full_size_properties(l1):
     for acc in (runner.accE, runner.accR):
         assert int(acc.cnt.abs().sum().item()) == 0
         assert float(acc.sum.abs().sum().item()) == 0.0
+
+
+def _runner_result(n_ent, n_rel, T, d, nb, pipelined, epochs=2, seed=11, trip=None):
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, EpochRunner
+    np.random.seed(seed)
+    m = S.TransE((n_ent, n_ent, n_rel), d)
+    m.add_hyperparam("margin", 2.0)
+    upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
+    if trip is None:
+        trip, _ = make_kg(n_ent, n_rel, T)
+    kg = DeviceKG(trip, m.device)
+    r = EpochRunner(m, upd, kg, nbatches=nb, seed=seed, pipelined=pipelined)
+    assert r.pipelined == pipelined
+    r.run(epochs)
+    r.synchronize()
+    for acc in (r.accE, r.accR):
+        assert int(acc.cnt.abs().sum().item()) == 0
+        assert float(acc.sum.abs().sum().item()) == 0.0
+    out = {"E": m.E.data.cpu().numpy().copy(), "R": m.R.data.cpu().numpy().copy(),
+           "pE": upd["E"].p2.cpu().numpy().copy(), "pR": upd["R"].p2.cpu().numpy().copy(),
+           "nviol": int(r.nviol_total.item()), "key": int(r.epoch_key.item())}
+    del r
+    return out, trip
+
+
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb", [
+    (500, 7, 3000, 52, 10),       # even batches
+    (500, 7, 3001, 200, 7),       # ragged remainder batch (np.split geometry)
+    (40, 3, 1200, 200, 4),        # tiny graph: most rows pending every batch (claim/wait stress)
+    (2000, 11, 8000, 400, 20),    # two quads per lane
+    (1000, 5, 4000, 1024, 8),     # widest packed row
+    (40943, 18, 141442, 200, 100),  # WN18 geometry
+])
+def test_pipelined_runner_bitwise_equals_two_launch(n_ent, n_rel, T, d, nb):
+    """The pipelined runner (one launch per batch, cross-workgroup hand-off of
+    the previous batch's updates) must reproduce the two-launch loop exactly."""
+    a, trip = _runner_result(n_ent, n_rel, T, d, nb, pipelined=False)
+    b, _ = _runner_result(n_ent, n_rel, T, d, nb, pipelined=True, trip=trip)
+    assert a["key"] == b["key"] == 2
+    assert a["nviol"] == b["nviol"] > 0
+    for k in ("E", "R", "pE", "pR"):
+        assert np.array_equal(a[k], b[k]), k
 
 
 def test_trainer_device_loop_fit():
