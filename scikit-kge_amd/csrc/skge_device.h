@@ -93,6 +93,47 @@ __device__ __forceinline__ Accum replica(const Accum& a, long long item) {
 
 
 
+// Counters many waves add to are sharded over NSHARD words on lines of their
+// own: no-return atomics on ONE word serialise at the memory side (~12 ns
+// each, MI355X_MICROARCH.md "fanin"), which for ~1.4k adders per launch costs
+// more than the launch's real work.
+constexpr int NSHARD = 64, SHARD_STRIDE = 32;   // 32 ints = one 128-B line
+__device__ __forceinline__ int* shard_of(int* base) {
+  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  return base + (wave & (NSHARD - 1)) * SHARD_STRIDE;
+}
+
+// float version (a loss): one global atomic per workgroup
+__device__ __forceinline__ void block_sum_add(float* dst, float v, float* lds_word) {
+  if (threadIdx.x == 0) *lds_word = 0.0f;
+  __syncthreads();
+  if (lane_id() == 0 && v != 0.0f) atomicAdd(lds_word, v);
+  __syncthreads();
+  if (threadIdx.x == 0 && dst && *lds_word != 0.0f) atomicAdd(dst, *lds_word);
+}
+
+// one wave (lanes 0..63): add the shards' total to *dst (if any) and clear them
+__device__ __forceinline__ void fold_shards(int* shards, int* dst) {
+  const int l = lane_id();
+  int v = 0;
+  if (l < NSHARD) {
+    v = shards[l * SHARD_STRIDE];
+    shards[l * SHARD_STRIDE] = 0;
+  }
+  v = wave_sum_int(v);
+  if (l == 0 && dst && v) atomicAdd(dst, v);
+}
+
+// workgroup total of a per-wave count, added to *dst with ONE atomic (every
+// wave of the workgroup must call it)
+__device__ __forceinline__ void block_count_add(int* dst, int v, int* lds_word) {
+  if (threadIdx.x == 0) *lds_word = 0;
+  __syncthreads();
+  if (lane_id() == 0 && v) atomicAdd(lds_word, v);
+  __syncthreads();
+  if (threadIdx.x == 0 && dst && *lds_word) atomicAdd(dst, *lds_word);
+}
+
 // Count `c` occurrences of `row` (no-return atomic) and record the row in
 // `slot` (or -1 when c == 0).  Several slots may name the same row; the
 // consumer claims each row once with an atomicExch on its count (k_apply).

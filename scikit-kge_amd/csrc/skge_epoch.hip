@@ -50,8 +50,20 @@ struct SampleArgs {
   float margin;
   int* nviol;
   int* nviol_total;
+  int* vshards;   // runner: violations go to these shards (folded at the epoch end), not nviol_total
   int* neg_out;
 };
+
+// a wave's violation count: sharded (runner) or one atomic per workgroup
+__device__ __forceinline__ void count_violations(const SampleArgs& a, int nv) {
+  __shared__ int lds_nv;
+  if (a.vshards) {
+    if (lane_id() == 0 && nv) atomicAdd(shard_of(a.vshards), nv);
+  } else {
+    block_count_add(a.nviol_total, nv, &lds_nv);
+  }
+  if (a.nviol) block_count_add(a.nviol, nv, &lds_nv);
+}
 
 // RandomModeSampler._sample (skge/sample.py:41-46), tries first_try.. for the
 // modes still unresolved: lanes 0-3 try mode 0 (corrupt s), lanes 4-7 mode 1
@@ -177,10 +189,7 @@ __global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
     acc_row<KM>(replica(a.accR, j), p, cr, d);
 #endif
   }
-  if (l == 0 && nv) {
-    if (a.nviol) atomicAdd(a.nviol, nv);
-    if (a.nviol_total) atomicAdd(a.nviol_total, nv);
-  }
+  count_violations(a, nv);
 }
 
 // TransE-L1 variant with exact packed int16x4 accumulation (ACC_I16X4) and the
@@ -298,10 +307,7 @@ __global__ __launch_bounds__(256) void k_transe_l1_sample_grad_i16(SampleArgs a)
     acc_row4_i16<KQ>(replica(a.accR, j), p, cr, d);
 #endif
   }
-  if (l == 0 && nv) {
-    if (a.nviol) atomicAdd(a.nviol, nv);
-    if (a.nviol_total) atomicAdd(a.nviol_total, nv);
-  }
+  count_violations(a, nv);
 }
 
 __global__ void k_perm(long long T, int half, uint64_t seed, const uint64_t* ekp, long long* out,
@@ -313,6 +319,12 @@ __global__ void k_perm(long long T, int half, uint64_t seed, const uint64_t* ekp
 }
 
 __global__ void k_advance(uint64_t* ek) { *ek += 1; }
+
+// epoch end of the runner: fold the violation shards, advance the key (one wave)
+__global__ void k_epoch_end(uint64_t* ek, int* shards, int* nviol_total) {
+  fold_shards(shards, nviol_total);
+  if (threadIdx.x == 0) *ek += 1;
+}
 
 static int launch_sample(const SampleArgs& a, bool l1, hipStream_t st) {
   const int km = km_for(a.d);
@@ -430,6 +442,7 @@ static int fill_sample_args(SampleArgs& a, int l1, const skge_table_t* ent, cons
   a.margin = margin;
   a.nviol = nviol;
   a.nviol_total = nviol_total;
+  a.vshards = nullptr;
   (void)l1;
   return SKGE_OK;
 }
@@ -478,7 +491,16 @@ struct skge_runner {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   int nlaunch = 0;
+  int* shards = nullptr;
 };
+
+static void runner_free(skge_runner_t* r) {
+  if (!r) return;
+  if (r->exec) (void)hipGraphExecDestroy(r->exec);
+  if (r->graph) (void)hipGraphDestroy(r->graph);
+  if (r->shards) (void)hipFree(r->shards);
+  delete r;
+}
 
 extern "C" skge_runner_t* skge_runner_create(void* stream, int l1, const skge_table_t* ent,
                                              const skge_table_t* rel, int d, const int* trip,
@@ -505,9 +527,17 @@ extern "C" skge_runner_t* skge_runner_create(void* stream, int l1, const skge_ta
   for (int64_t s0 = 0; s0 < T; s0 += bs) batches.push_back({s0, (s0 + bs <= T) ? bs : T - s0});
   skge_runner_t* r = new skge_runner_t();
   skge_table_t tabs[2] = {*ent, *rel};
-  if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+  if (hipMalloc(&r->shards, NSHARD * SHARD_STRIDE * 4) != hipSuccess ||
+      hipMemset(r->shards, 0, NSHARD * SHARD_STRIDE * 4) != hipSuccess) {
+    set_error("runner: device allocation failed");
+    runner_free(r);
+    return nullptr;
+  }
+  a.vshards = r->shards;
+  if (hipStreamSynchronize(st) != hipSuccess ||
+      hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
     set_error("hipStreamBeginCapture failed");
-    delete r;
+    runner_free(r);
     return nullptr;
   }
   int rc = SKGE_OK;
@@ -522,7 +552,7 @@ extern "C" skge_runner_t* skge_runner_create(void* stream, int l1, const skge_ta
     r->nlaunch += 2;
   }
   if (!rc) {
-    hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, st, epoch_key);
+    hipLaunchKernelGGL(k_epoch_end, dim3(1), dim3(64), 0, st, epoch_key, r->shards, nviol_total);
     r->nlaunch += 1;
   }
   hipGraph_t g = nullptr;
@@ -530,15 +560,14 @@ extern "C" skge_runner_t* skge_runner_create(void* stream, int l1, const skge_ta
   if (rc || e != hipSuccess) {
     if (!rc) set_error("hipStreamEndCapture: %s", hipGetErrorString(e));
     if (g) (void)hipGraphDestroy(g);
-    delete r;
+    runner_free(r);
     return nullptr;
   }
   r->graph = g;
   e = hipGraphInstantiate(&r->exec, g, nullptr, nullptr, 0);
   if (e != hipSuccess) {
     set_error("hipGraphInstantiate: %s", hipGetErrorString(e));
-    (void)hipGraphDestroy(g);
-    delete r;
+    runner_free(r);
     return nullptr;
   }
   return r;
@@ -552,9 +581,4 @@ extern "C" int skge_runner_run(skge_runner_t* r, void* stream, int nepochs) {
 
 extern "C" int skge_runner_nlaunches(const skge_runner_t* r) { return r ? r->nlaunch : -1; }
 
-extern "C" void skge_runner_destroy(skge_runner_t* r) {
-  if (!r) return;
-  if (r->exec) (void)hipGraphExecDestroy(r->exec);
-  if (r->graph) (void)hipGraphDestroy(r->graph);
-  delete r;
-}
+extern "C" void skge_runner_destroy(skge_runner_t* r) { runner_free(r); }

@@ -379,7 +379,8 @@ __global__ __launch_bounds__(256) void k_pair_grad(PairArgs a) {
     if (a.record) commit_pair(a.accE, MODEL == RESCAL ? nullptr : &a.accR, v, ix, i);
     nv += v ? 1 : 0;
   }
-  if (lane_id() == 0 && nv && a.nviol) atomicAdd(a.nviol, nv);
+  __shared__ int lds_nv;
+  if (a.nviol) block_count_add(a.nviol, nv, &lds_nv);   // one atomic per workgroup
 }
 
 // ---------------------------------------------------------------------------
@@ -456,7 +457,8 @@ __global__ __launch_bounds__(256) void k_triple_grad(PairArgs a) {
     lsum += li;
     __builtin_amdgcn_wave_barrier();
   }
-  if (lane_id() == 0 && a.loss && lsum != 0.0f) atomicAdd(a.loss, lsum);
+  __shared__ float lds_loss;
+  if (a.loss) block_sum_add(a.loss, lsum, &lds_loss);   // one atomic per workgroup
 }
 
 // ---------------------------------------------------------------------------

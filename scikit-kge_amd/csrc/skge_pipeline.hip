@@ -38,16 +38,6 @@
 
 namespace skge {
 
-// Counters many waves add to are sharded over NSHARD words on lines of their
-// own: no-return atomics on ONE word serialise at the memory side (~12 ns
-// each, MI355X_MICROARCH.md "fanin"), which for ~1.4k adders per launch would
-// cost more than the launch's real work.
-constexpr int NSHARD = 64, SHARD_STRIDE = 32;   // 32 ints = one 128-B line
-__device__ __forceinline__ int* shard_of(int* base) {
-  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  return base + (wave & (NSHARD - 1)) * SHARD_STRIDE;
-}
-
 struct UpdParams {
   int opt, post;
   float lr, rin, rout, fdiv;   // g = (sum + rin*P)/div + rout*P, div = fdiv > 0 ? fdiv : count
@@ -281,18 +271,11 @@ __global__ __launch_bounds__(256) void k_pipe_batch(PipeArgs a) {
   if ((int)blockIdx.x >= nB) {
     // ---- A role: write R_b, then apply the previous batch's entity rows ----
     const int nR = a.R.rows;
-    const int total = a.prev_slots + nR;
+    const int total = nR + a.prev_slots;   // relation rows, then entity slots
     const int wa = (blockIdx.x - nB) * wpb + (threadIdx.x >> 6);
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
-    if (a.b == a.nb1 && wa == 0) {   // the flush: fold the epoch's violation count
-      int v = 0;
-      if (l < NSHARD) {
-        v = a.nviol_shards[l * SHARD_STRIDE];
-        a.nviol_shards[l * SHARD_STRIDE] = 0;
-      }
-      v = wave_sum_int(v);
-      if (l == 0 && a.nviol_total && v) atomicAdd(a.nviol_total, v);
-    }
+    if (a.b == a.nb1 && wa == 0)   // the flush: fold the epoch's violation count
+      fold_shards(a.nviol_shards, a.nviol_total);
     for (int w = wa; w < total; w += a.nA * wpb) {
       if (w < nR) {
         float4 p[KQ], av[KQ];
