@@ -73,9 +73,10 @@ enum {
  *   (sum + rparam*W)/2   rescal.py:287-290 (divisor quirk)
  *
  * Touched rows are recorded in FIXED SLOTS (no shared counter): every
- * contribution site of a launch owns one slot of acc_touched and writes the
- * row id there if it was the first to count the row (atomicAdd on acc_cnt
- * returned 0), else -1.  Slot maps:
+ * contribution site of a launch owns one slot of acc_touched and writes there
+ * the row id it counted (or -1 if it added nothing); several slots may name
+ * the same row, and consumers claim each row once (atomicExch on acc_cnt).
+ * Slot maps:
  *   skge_pair_grad          ent: 4i+{0:sp,1:op,2:sn,3:on}   rel: 2i+{0:pp,1:pn}
  *   skge_triple_grad        ent: 2i+{0:s,1:o}               rel (HolE): i
  *   skge_rescal_wgrad       W:   slot p (all M slots)
