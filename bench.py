@@ -62,6 +62,30 @@ def pmc_traffic(kernel_substr):
     return None, None
 
 
+def dist_env():
+    """(world, rank, local_rank) from the torchrun environment (1, 0, 0 alone)."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def max_over_ranks(x, world, device="cpu"):
+    """The maximum of a per-rank float over all ranks (the timed region's
+    wall clock: the job is done when the slowest replica is)."""
+    if world <= 1:
+        return float(x)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def replica_value(positives_per_rank, world, elapsed_max):
+    """Whole-job throughput of N independent replicas (weak scaling): every
+    rank's positives over the slowest rank's time."""
+    return world * positives_per_rank / elapsed_max
+
+
 def algorithmic_bytes(d, B, P, U_E, U_R, opt_k=12):
     """BYTES(batch) = 4d(3B + P) + k d (U_E + U_R) + 20B."""
     return 4 * d * (3 * B + P) + opt_k * d * (U_E + U_R) + 20 * B
@@ -124,9 +148,7 @@ def main():
 
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = dist_env()
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local)
@@ -174,13 +196,10 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     gpu_ms = ev0.elapsed_time(ev1)
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(elapsed, world, dev)
     nviol = int(runner.nviol_total.item())
     positives = N_TRIPLES * args.steps
-    value = world * positives / elapsed
+    value = replica_value(positives, world, elapsed)
 
     # ---- per-kernel timing (HIP events on the runner stream, eager launches of
     # one more epoch, outside the timed region) for the roofline ----

@@ -1,0 +1,62 @@
+"""bench.py's multi-GPU (replicas) bookkeeping on CPU: a world-size-2 gloo job
+checks the rank environment, the max-over-ranks timing and the whole-job
+value (replicas only, weak scaling)."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import bench
+    dist.init_process_group("gloo", init_method="env://")
+    w, r, lr = bench.dist_env()
+    elapsed = 1.0 + rank   # rank 1 is the slow replica
+    mx = bench.max_over_ranks(elapsed, w, "cpu")
+    val = bench.replica_value(1000, w, mx)
+    dist.barrier()
+    dist.destroy_process_group()
+    out.put((r, w, lr, mx, val))
+
+
+def test_replica_bookkeeping_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [(r, w, lr) for r, w, lr, _, _ in res] == [(0, 2, 0), (1, 2, 1)]
+    for _, _, _, mx, val in res:
+        assert mx == 2.0                      # the slowest replica's time on every rank
+        assert val == pytest.approx(1000.0)   # 2 ranks x 1000 positives / 2 s
+
+
+def test_single_process_defaults(monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    assert bench.dist_env() == (1, 0, 0)
+    assert bench.max_over_ranks(3.5, 1) == 3.5
+    assert bench.replica_value(10, 1, 2.0) == 5.0
