@@ -10,8 +10,8 @@
 //   * all negatives of the epoch are drawn up front (k_epoch_sample: the same
 //     counter-based draws and rejection test as k_transe_sample_grad, so the
 //     epoch's pairs are identical), giving per-positive records (s, o, p, s', o');
-//   * launch g scores batch b ("B" role, workgroups [0, nB)) while workgroups
-//     [nB, grid) apply batch b-1's updates ("A" role);
+//   * launch g scores batch b ("B" role) while the first nA workgroups apply
+//     batch b-1's updates ("A" role);
 //   * entity rows (many, each touched by few positives): accumulators
 //     double-buffered by batch parity.  A B wave about to read a row batch
 //     b-1 touched (pend[row] == g-1, recorded by the previous launch) makes
@@ -256,8 +256,13 @@ __device__ __forceinline__ void rel_row(const RelTab& t, int row, int d, int rd,
 
 __device__ __forceinline__ unsigned long long now_10ns() { return __builtin_amdgcn_s_memrealtime(); }
 
+#ifdef SKGE_PIPE_WAVES_PER_EU
+#define SKGE_PIPE_OCC __attribute__((amdgpu_waves_per_eu(SKGE_PIPE_WAVES_PER_EU, 8)))
+#else
+#define SKGE_PIPE_OCC
+#endif
 template <int KQ>
-__global__ __launch_bounds__(256) void k_pipe_batch(PipeArgs a) {
+__global__ __launch_bounds__(256) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
   const int d = a.d, nq = d >> 2;
@@ -266,13 +271,15 @@ __global__ __launch_bounds__(256) void k_pipe_batch(PipeArgs a) {
   const int rd = a.b & 1;                // relation buffer holding R_{b-1}
   const int rw = a.b < a.nb1 ? rd ^ 1 : 0;   // ... receiving R_b (the flush: the caller's)
   const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
-  // scoring workgroups first: they are the critical path and dispatch in order
   const int nB = gridDim.x - a.nA;
-  if ((int)blockIdx.x >= nB) {
+  // apply workgroups first: they start the hand-offs the scoring waves may wait
+  // on (measured: 6% faster than scoring first, 9% faster than interleaved)
+  const int blk_a = (int)blockIdx.x, blk_b = (int)blockIdx.x - a.nA;
+  if ((int)blockIdx.x < a.nA) {
     // ---- A role: write R_b, then apply the previous batch's entity rows ----
     const int nR = a.R.rows;
     const int total = nR + a.prev_slots;   // relation rows, then entity slots
-    const int wa = (blockIdx.x - nB) * wpb + (threadIdx.x >> 6);
+    const int wa = blk_a * wpb + (threadIdx.x >> 6);
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
     if (a.b == a.nb1 && wa == 0)   // the flush: fold the epoch's violation count
       fold_shards(a.nviol_shards, a.nviol_total);
@@ -317,7 +324,7 @@ __global__ __launch_bounds__(256) void k_pipe_batch(PipeArgs a) {
   }
   // ---- B role: score batch b, scatter into accumulator copies cp / ra_cur ----
   int nv = 0;
-  for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
+  for (int w = blk_b * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
     const long long j = a.start + w;
     unsigned long long tt[4];
     if (a.trace) tt[0] = now_10ns();
