@@ -180,10 +180,18 @@ int skge_update_rows(void *stream, const skge_table_t *t, const float *g, const 
  */
 int skge_accum_apply(void *stream, const skge_table_t *tables, int ntables, const int *nslots);
 
-/* Explicit-pair training step: skge_pair_grad + (RESCAL wgrad) + apply. */
+/*
+ * Explicit-pair training step: skge_pair_grad + (RESCAL dW) + apply
+ * (one _pairwise_gradients + _batch_step, skge/base.py:1417-1427).  RESCAL
+ * needs a workspace of skge_pair_step_workspace_bytes(model, P, rel->rows, d)
+ * bytes (0 for the other models): for d <= 480 the triples are grouped by
+ * relation and W[p] E[o], E[s] W[p] and dW run as fp32 MFMA GEMMs
+ * (skge_rescal.hip), otherwise as per-pair GEMVs.
+ */
+size_t skge_pair_step_workspace_bytes(int model, int P, int M, int d);
 int skge_pair_step(void *stream, int model, int af, const skge_table_t *ent,
                    const skge_table_t *rel, int d, const int *pos, const int *neg, int P,
-                   float margin, float *coef_ws, int *nviol);
+                   float margin, void *workspace, size_t ws_bytes, int *nviol);
 
 /* ---------------- device-resident batch loop (throughput path) ---------------- */
 

@@ -130,49 +130,6 @@ __device__ __forceinline__ void scale(float (&o)[KM], const float (&v)[KM], floa
 
 // add rows x (coefficient already applied) at a and y at b, merging when a == b
 // (the matching counts are committed by commit_pair / commit_triple)
-template <int KM>
-__device__ __forceinline__ void acc_two(const Accum& acc, int a, const float (&x)[KM], int b,
-                                        const float (&y)[KM], int d) {
-  if (a == b) {
-    float t[KM];
-#pragma unroll
-    for (int k = 0; k < KM; ++k) t[k] = x[k] + y[k];
-    acc_row<KM>(acc, a, t, d);
-  } else {
-    acc_row<KM>(acc, a, x, d);
-    acc_row<KM>(acc, b, y, d);
-  }
-}
-
-// Occurrence counts + touched slots of one pair (slot maps: skge_hip.h).
-// Entity list (sp, op, sn, on), relation list (pp, pn), each occurrence
-// counted once per violating pair, as grad_sum_matrix counts duplicates.
-// Lanes 0-3 / 4-5 issue their returning atomics concurrently.
-__device__ __forceinline__ void commit_pair(const Accum& aE, const Accum* aR, bool viol,
-                                            const int (&ix)[6], int i) {
-  const int l = lane_id();
-  const int v = viol ? 1 : 0;
-  const int sp = ix[0], op = ix[1], pp = ix[2], sn = ix[3], on = ix[4], pn = ix[5];
-  int c0 = v, c1 = v, c2 = v, c3 = v;
-  if (sp == sn) {
-    c0 += c2;
-    c2 = 0;
-  }
-  if (op == on) {
-    c1 += c3;
-    c3 = 0;
-  }
-  if (l < 4) {
-    commit_slot(aE, sel4(l, sp, op, sn, on), sel4(l, c0, c1, c2, c3), 4 * i + l);
-  } else if (aR != nullptr && l < 6) {
-    int r0 = v, r1 = v;
-    if (pp == pn) {
-      r0 += r1;
-      r1 = 0;
-    }
-    commit_slot(*aR, l == 4 ? pp : pn, l == 4 ? r0 : r1, 2 * i + (l - 4));
-  }
-}
 
 // ---------------------------------------------------------------------------
 // TransE pair: skge/transe.py:48-165

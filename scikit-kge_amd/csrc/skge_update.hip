@@ -807,18 +807,57 @@ extern "C" int skge_accum_apply(void* stream, const skge_table_t* tables, int nt
   return SKGE_OK;
 }
 
+// RESCAL on the matrix cores (skge_rescal.hip)
+size_t skge_rescal_mfma_ws_bytes(int P, int M, int d);
+bool skge_rescal_mfma_ok(int d, int M);
+int skge_rescal_pair_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
+                               const skge_table_t* rel, int d, const int* pos, const int* neg,
+                               int P, float margin, void* workspace, size_t ws_bytes,
+                               float* pscore, float* nscore, int* nviol);
+
+// SKGE_RESCAL_VALU=1 forces the per-pair GEMV path (A/B comparisons)
+static bool rescal_use_mfma(int d, int M) {
+  static const bool valu = getenv("SKGE_RESCAL_VALU") && atoi(getenv("SKGE_RESCAL_VALU")) != 0;
+  return !valu && skge_rescal_mfma_ok(d, M);
+}
+
+extern "C" size_t skge_pair_step_workspace_bytes(int model, int P, int M, int d) {
+  if (model != SKGE_RESCAL || P <= 0) return 0;
+  const size_t coef = (size_t)2 * P * sizeof(float);   // coef of every pair (VALU path)
+  if (skge_rescal_mfma_ok(d, M)) return std::max(coef, skge_rescal_mfma_ws_bytes(P, M, d));
+  return coef;
+}
+
 extern "C" int skge_pair_step(void* stream, int model, int af, const skge_table_t* ent,
                               const skge_table_t* rel, int d, const int* pos, const int* neg,
-                              int P, float margin, float* coef_ws, int* nviol) {
+                              int P, float margin, void* workspace, size_t ws_bytes, int* nviol) {
   SKGE_CHECK_ARG(nviol, "nviol word required (it gates the update)");
-  int rc = skge_pair_grad(stream, model, af, ent, rel, d, pos, neg, P, margin, nullptr, nullptr,
-                          model == SKGE_RESCAL ? coef_ws : nullptr, nviol);
-  if (rc) return rc;
-  if (model == SKGE_RESCAL) {
-    SKGE_CHECK_ARG(coef_ws, "RESCAL needs a coef workspace of 2P floats");
-    rc = skge_rescal_wgrad(stream, ent, rel, d, pos, coef_ws, P, neg, coef_ws + P, P);
-    if (rc) return rc;
+  int rc;
+  if (model == SKGE_RESCAL && P > 0) {
+    const size_t need = skge_pair_step_workspace_bytes(model, P, rel->rows, d);
+    SKGE_CHECK_ARG(workspace && ws_bytes >= need, "RESCAL needs a %zu-byte workspace", need);
+    if (rescal_use_mfma(d, rel->rows)) {
+      if ((rc = check_table(ent, "ent", true)) || (rc = check_table(rel, "rel", false)) ||
+          (rc = check_f32(ent, "ent")) || (rc = check_f32(rel, "rel")) ||
+          (rc = check_single(ent, "ent")) || (rc = check_single(rel, "rel")))
+        return rc;
+      SKGE_CHECK_ARG(ent->width == d && rel->width == d * d, "RESCAL table widths");
+      SKGE_CHECK_ARG(af >= 0 && af <= 3, "unknown activation %d", af);
+      if ((rc = check_slots(ent, 4ll * P, "ent")) || (rc = check_slots(rel, rel->rows, "W")))
+        return rc;
+      rc = skge_rescal_pair_grad_mfma(as_stream(stream), af, ent, rel, d, pos, neg, P, margin,
+                                      workspace, ws_bytes, nullptr, nullptr, nviol);
+    } else {
+      float* coef = (float*)workspace;
+      rc = skge_pair_grad(stream, model, af, ent, rel, d, pos, neg, P, margin, nullptr, nullptr,
+                          coef, nviol);
+      if (!rc) rc = skge_rescal_wgrad(stream, ent, rel, d, pos, coef, P, neg, coef + P, P);
+    }
+  } else {
+    rc = skge_pair_grad(stream, model, af, ent, rel, d, pos, neg, P, margin, nullptr, nullptr,
+                        nullptr, nviol);
   }
+  if (rc) return rc;
   skge_table_t t[2] = {*ent, *rel};
   t[0].gate = nviol;
   t[1].gate = nviol;

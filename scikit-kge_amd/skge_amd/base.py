@@ -218,15 +218,25 @@ class Model(object):
     def _pairwise_step(self, pos, neg, updaters, nviol):
         """score + grad + update for explicit pairs in one skge_pair_step.
         `nviol` must be zero on entry; it receives the violation count."""
-        dev = self.device
         P = pos.shape[0]
-        coef = None
-        if self.rel_id == "W":
-            coef = torch.empty(2 * P, dtype=torch.float32, device=dev)
+        lib = L.lib()
+        nbytes = lib.skge_pair_step_workspace_bytes(self._kernel_model(), P,
+                                                    self.params[self.rel_id].rows, self.d)
+        ws = self._workspace(nbytes)
         te, tr = self._tables("pairwise", updaters, gate=nviol, slots=self._pair_slots(P))
-        L.check(L.lib().skge_pair_step(L.stream_ptr(), self._kernel_model(), self._af_code(), te,
-                                       tr, self.d, L.ptr(pos), L.ptr(neg), P, float(self.margin),
-                                       L.ptr(coef), L.ptr(nviol)), "pair_step")
+        L.check(lib.skge_pair_step(L.stream_ptr(), self._kernel_model(), self._af_code(), te,
+                                   tr, self.d, L.ptr(pos), L.ptr(neg), P, float(self.margin),
+                                   L.ptr(ws), nbytes, L.ptr(nviol)), "pair_step")
+
+    def _workspace(self, nbytes):
+        """Device scratch of at least nbytes (kept and grown across calls)."""
+        if nbytes == 0:
+            return None
+        ws = getattr(self, "_ws", None)
+        if ws is None or ws.numel() < nbytes:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self._ws = ws
+        return ws
 
     def _logistic_step(self, trip, ys, updaters, loss):
         dev = self.device

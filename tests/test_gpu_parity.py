@@ -53,7 +53,7 @@ def build(c):
 GRAD_ROUNDING = 1e-8   # absolute fp32 rounding bound of a gradient element here
 
 
-def close_adagrad(got, want, p2, lr, what):
+def close_adagrad(got, want, p2, lr, what, grad_rounding=None):
     """Parameters after AdaGrad steps.  The step lr*g/max(sqrt(p2), 1e-7)
     turns an absolute gradient rounding error e into a parameter error
     lr*e/H, up to 1e6 * lr * e where the reference's own gradient element is
@@ -64,7 +64,8 @@ def close_adagrad(got, want, p2, lr, what):
     got = _np(got).astype(np.float64)
     want = np.asarray(want, dtype=np.float64)
     H = np.maximum(np.sqrt(np.asarray(p2, dtype=np.float64)), 1e-7)
-    tol = ATOL + RTOL * np.abs(want) + lr * GRAD_ROUNDING / H
+    e = GRAD_ROUNDING if grad_rounding is None else grad_rounding
+    tol = ATOL + RTOL * np.abs(want) + lr * e / H
     bad = np.abs(got - want) > tol
     assert not bad.any(), "%s: %d elements off, max excess %g" % (
         what, int(bad.sum()), float(np.max(np.abs(got - want) - tol)))
