@@ -89,6 +89,80 @@ __device__ __forceinline__ void cconv_lds(const float* sa, const float* sb, int 
   }
 }
 
+// ---- register-tiled circular correlation (HolE, d % 4 == 0, d <= 256) ----
+// c_k = sum_j a_j b_{(j+k) mod d}: lane l owns outputs 4l..4l+3 and slides an
+// 8-float window of b along j (b stored twice in LDS so j+k needs no mod):
+// per 4 j's one broadcast 16-B read of a, one 16-B read of b, 8 v_pk_fma_f32.
+// cconv(a, b) = ccorr(a', b) with a'_m = a_{(-m) mod d} (stored reversed).
+// The quad result goes through a wave-private LDS row back to the lane-
+// strided layout of the rest of the kernel.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ bool hole_fast(int d) { return (d & 3) == 0 && d >= 4 && d <= 256; }
+// wave-private LDS floats of the fast HolE pair kernel
+__host__ __device__ __forceinline__ int hole_fast_lds_floats(int d) { return 13 * d + 16; }
+
+template <int KM>
+__device__ __forceinline__ void to_lds_dbl(float* s2, const float (&v)[KM], int d) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k;
+    if (e < d) {
+      s2[e] = v[k];
+      s2[e + d] = v[k];
+    }
+  }
+  if (l < 4) s2[2 * d + l] = 0.0f;   // read (unused) by the last window refill
+}
+
+template <int KM>
+__device__ __forceinline__ void to_lds_rev(float* s, const float (&v)[KM], int d) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k;
+    if (e < d) s[e == 0 ? 0 : d - e] = v[k];
+  }
+}
+
+template <int KM>
+__device__ __forceinline__ void corr_fast(const float* sa, const float* sb2, float* sout, int d,
+                                          float (&out)[KM]) {
+  const int l = lane_id(), base = 4 * l;
+  if (base < d) {
+    f2 c01 = {0.0f, 0.0f}, c23 = {0.0f, 0.0f}, e01 = {0.0f, 0.0f}, e23 = {0.0f, 0.0f};
+    float4 lo = *reinterpret_cast<const float4*>(sb2 + base);
+    float4 hi = *reinterpret_cast<const float4*>(sb2 + base + 4);
+    for (int j0 = 0; j0 < d; j0 += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(sa + j0);   // broadcast
+      const f2 w01 = {lo.x, lo.y}, w12 = {lo.y, lo.z}, w23 = {lo.z, lo.w}, w34 = {lo.w, hi.x};
+      const f2 w45 = {hi.x, hi.y}, w56 = {hi.y, hi.z};
+      const f2 ax = {a.x, a.x}, ay = {a.y, a.y}, az = {a.z, a.z}, aw = {a.w, a.w};
+      c01 = __builtin_elementwise_fma(ax, w01, c01);   // c_r += a_{j0+s} b_{j0+s+base+r}
+      c23 = __builtin_elementwise_fma(ax, w23, c23);
+      e01 = __builtin_elementwise_fma(ay, w12, e01);
+      e23 = __builtin_elementwise_fma(ay, w34, e23);
+      c01 = __builtin_elementwise_fma(az, w23, c01);
+      c23 = __builtin_elementwise_fma(az, w45, c23);
+      e01 = __builtin_elementwise_fma(aw, w34, e01);
+      e23 = __builtin_elementwise_fma(aw, w56, e23);
+      lo = hi;
+      hi = *reinterpret_cast<const float4*>(sb2 + j0 + 8 + base);
+    }
+    c01 += e01;
+    c23 += e23;
+    *reinterpret_cast<float4*>(sout + base) = make_float4(c01.x, c01.y, c23.x, c23.y);
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k;
+    out[k] = e < d ? sout[e] : 0.0f;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 // out_i = sum_j W[i][j] x_j   (W[p] . E[o], skge/rescal.py:212)
 template <int KM>
 __device__ __forceinline__ void gemv_rows(const float* __restrict__ Wp, const float* sx, int d, float (&out)[KM]) {
@@ -250,6 +324,81 @@ __device__ __forceinline__ bool hole_pair(const PairArgs& a, int i, float* sw, c
   return true;
 }
 
+// HolE pair with the register-tiled correlations (hole_fast(d)); same
+// arithmetic steps as hole_pair, LDS per wave: hole_fast_lds_floats(d)
+template <int KM>
+__device__ __forceinline__ bool hole_pair_fast(const PairArgs& a, int i, float* sw,
+                                               const int (&ix)[6]) {
+  const int d = a.d;
+  const int sp = ix[0], op = ix[1], pp = ix[2], sn = ix[3], on = ix[4], pn = ix[5];
+  float* sEs = sw;               // a operands: E[sp], E[sn], reversed copies
+  float* sFs = sw + d;
+  float* rEs = sw + 2 * d;
+  float* rFs = sw + 3 * d;
+  float* sRp = sw + 4 * d;       // doubled rows (2d + 4)
+  float* sRn = sRp + 2 * d + 4;
+  float* sEo = sRn + 2 * d + 4;
+  float* sFo = sEo + 2 * d + 4;
+  float* sout = sFo + 2 * d + 4;
+  float es[KM], eo[KM], fs[KM], fo[KM], rp[KM], rn[KM];
+  load_row<KM>(a.E, sp, d, es);
+  load_row<KM>(a.E, op, d, eo);
+  load_row<KM>(a.R, pp, d, rp);
+  load_row<KM>(a.E, sn, d, fs);
+  load_row<KM>(a.E, on, d, fo);
+  load_row<KM>(a.R, pn, d, rn);
+  to_lds<KM>(sEs, es, d);
+  to_lds<KM>(sFs, fs, d);
+  to_lds_rev<KM>(rEs, es, d);
+  to_lds_rev<KM>(rFs, fs, d);
+  to_lds_dbl<KM>(sRp, rp, d);
+  to_lds_dbl<KM>(sRn, rn, d);
+  to_lds_dbl<KM>(sEo, eo, d);
+  to_lds_dbl<KM>(sFo, fo, d);
+  __builtin_amdgcn_wave_barrier();
+  float cp[KM], cn[KM];
+  corr_fast<KM>(sEs, sEo, sout, d, cp);  // ccorr(E[s], E[o])   (hole.py:20)
+  corr_fast<KM>(sFs, sFo, sout, d, cn);
+  float ps = 0.0f, ns = 0.0f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    ps += rp[k] * cp[k];
+    ns += rn[k] * cn[k];
+  }
+  const float praw = wave_sum(ps), nraw = wave_sum(ns);
+  if (lane_id() == 0) {
+    if (a.pscore) a.pscore[i] = praw;
+    if (a.nscore) a.nscore[i] = nraw;
+  }
+  const float pf = af_f(a.af, praw), nf = af_f(a.af, nraw);
+  const bool viol = nf + a.margin > pf;  // hole.py:56
+  if (!viol) {
+    __builtin_amdgcn_wave_barrier();
+    return false;
+  }
+  const float gp = -af_g_given_f(a.af, pf);  // hole.py:66
+  const float gn = af_g_given_f(a.af, nf);   // hole.py:67
+  float x[KM], y[KM], t[KM];
+  // relation rows (pp, pn): (gp ccorr(E[sp],E[op]), gn ccorr(E[sn],E[on]))  hole.py:76-82
+  scale<KM>(x, cp, gp);
+  scale<KM>(y, cn, gn);
+  acc_two<KM>(a.accR, pp, x, pn, y, d);
+  // entity rows (sp, sn): gp ccorr(R[pp],E[op]), gn ccorr(R[pn],E[on])   hole.py:93-94
+  corr_fast<KM>(sRp, sEo, sout, d, t);
+  scale<KM>(x, t, gp);
+  corr_fast<KM>(sRn, sFo, sout, d, t);
+  scale<KM>(y, t, gn);
+  acc_two<KM>(a.accE, sp, x, sn, y, d);
+  // entity rows (op, on): gp cconv(E[sp],R[pp]), gn cconv(E[sn],R[pn])    hole.py:95-96
+  corr_fast<KM>(rEs, sRp, sout, d, t);
+  scale<KM>(x, t, gp);
+  corr_fast<KM>(rFs, sRn, sout, d, t);
+  scale<KM>(y, t, gn);
+  acc_two<KM>(a.accE, op, x, on, y, d);
+  __builtin_amdgcn_wave_barrier();
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // RESCAL pair: skge/rescal.py:78-139 (entity part; dW in k_rescal_wgrad)
 // ---------------------------------------------------------------------------
@@ -340,6 +489,26 @@ __global__ __launch_bounds__(256) void k_pair_grad(PairArgs a) {
   if (a.nviol) block_count_add(a.nviol, nv, &lds_nv);   // one atomic per workgroup
 }
 
+// HolE pairs with the register-tiled correlations (hole_fast(d)): its own
+// kernel, so the generic path's registers do not limit its occupancy
+template <int KM>
+__global__ __launch_bounds__(256) void k_hole_pair_fast(PairArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wave = threadIdx.x >> 6;
+  const int wpb = blockDim.x >> 6;
+  float* sw = smem + wave * hole_fast_lds_floats(a.d);
+  int nv = 0;
+  for (int i = blockIdx.x * wpb + wave; i < a.P; i += gridDim.x * wpb) {
+    const int ix[6] = {uni(a.pos[3 * i]), uni(a.pos[3 * i + 1]), uni(a.pos[3 * i + 2]),
+                       uni(a.neg[3 * i]), uni(a.neg[3 * i + 1]), uni(a.neg[3 * i + 2])};
+    const bool v = hole_pair_fast<KM>(a, i, sw, ix);
+    if (a.record) commit_pair(a.accE, &a.accR, v, ix, i);
+    nv += v ? 1 : 0;
+  }
+  __shared__ int lds_nv;
+  if (a.nviol) block_count_add(a.nviol, nv, &lds_nv);   // one atomic per workgroup
+}
+
 // ---------------------------------------------------------------------------
 // logistic loss: HolE skge/hole.py:22-42, RESCAL skge/rescal.py:37-76
 // ---------------------------------------------------------------------------
@@ -356,20 +525,50 @@ __global__ __launch_bounds__(256) void k_triple_grad(PairArgs a) {
   const int wpb = blockDim.x >> 6;
   const int d = a.d;
   const int stride = 64 * KM;
-  float* sEs = smem + wave * 3 * stride;
+  const bool fast = MODEL == HOLE && KM <= 4 && hole_fast(d);
+  float* sEs = smem + wave * (fast ? hole_fast_lds_floats(d) : 3 * stride);
   float* sEo = sEs + stride;
   float* sRp = sEs + 2 * stride;
+  // fast layout: E[s], E[s] reversed (d each), E[o], R[p] doubled, output row
+  float* fEs = sEs;
+  float* fEsr = sEs + d;
+  float* fEo2 = sEs + 2 * d;
+  float* fRp2 = fEo2 + 2 * d + 4;
+  float* fout = fRp2 + 2 * d + 4;
   float lsum = 0.0f;
   for (int i = blockIdx.x * wpb + wave; i < a.P; i += gridDim.x * wpb) {
     const int s = uni(a.pos[3 * i]), o = uni(a.pos[3 * i + 1]), p = uni(a.pos[3 * i + 2]);
     const float y = a.ys[i];
     float es[KM], eo[KM], x[KM], t[KM];
     load_row<KM>(a.E, s, d, es);
-    to_lds<KM>(sEs, es, d);
     load_row<KM>(a.E, o, d, eo);
-    to_lds<KM>(sEo, eo, d);
     float score, li, fs;
-    if (MODEL == HOLE) {
+    if (MODEL == HOLE && KM <= 4 && fast) {
+      float rp[KM], c[KM];
+      load_row<KM>(a.R, p, d, rp);
+      to_lds<KM>(fEs, es, d);
+      to_lds_rev<KM>(fEsr, es, d);
+      to_lds_dbl<KM>(fEo2, eo, d);
+      to_lds_dbl<KM>(fRp2, rp, d);
+      __builtin_amdgcn_wave_barrier();
+      corr_fast<KM>(fEs, fEo2, fout, d, c);
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < KM; ++k) acc += rp[k] * c[k];
+      score = wave_sum(acc);
+      logistic(y, score, &li, &fs);
+      scale<KM>(x, c, fs);  // R: fs ccorr(E[s],E[o])   hole.py:32
+      acc_row<KM>(a.accR, p, x, d);
+      if (lane_id() == 2) commit_slot(a.accR, p, 1, i);
+      corr_fast<KM>(fRp2, fEo2, fout, d, t);  // E[s]: fs ccorr(R[p],E[o])
+      scale<KM>(x, t, fs);
+      corr_fast<KM>(fEsr, fRp2, fout, d, t);  // E[o]: fs cconv(E[s],R[p])
+      float yv[KM];
+      scale<KM>(yv, t, fs);
+      acc_two<KM>(a.accE, s, x, o, yv, d);
+    } else if (MODEL == HOLE) {
+      to_lds<KM>(sEs, es, d);
+      to_lds<KM>(sEo, eo, d);
       float rp[KM], c[KM];
       load_row<KM>(a.R, p, d, rp);
       to_lds<KM>(sRp, rp, d);
@@ -390,6 +589,8 @@ __global__ __launch_bounds__(256) void k_triple_grad(PairArgs a) {
       scale<KM>(yv, t, fs);
       acc_two<KM>(a.accE, s, x, o, yv, d);
     } else {
+      to_lds<KM>(sEs, es, d);
+      to_lds<KM>(sEo, eo, d);
       __builtin_amdgcn_wave_barrier();
       const size_t dd = (size_t)d * d;
       float we[KM], ew[KM];
@@ -517,7 +718,19 @@ static int launch_pair(const PairArgs& a, int km, hipStream_t st, bool logistic_
   int blocks = (a.P + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
-  const size_t lds = (MODEL == TRANSE_L1 || MODEL == TRANSE_L2) ? 0 : (size_t)4 * 6 * 64 * km * 4;
+  size_t lds = (MODEL == TRANSE_L1 || MODEL == TRANSE_L2) ? 0 : (size_t)4 * 6 * 64 * km * 4;
+  const bool hfast = MODEL == HOLE && km <= 4 && (a.d & 3) == 0 && a.d >= 4 && a.d <= 256;
+  if (hfast) lds = std::max(lds, (size_t)4 * hole_fast_lds_floats(a.d) * 4);
+  if (hfast && !logistic_mode) {
+    switch (km) {
+      case 1: hipLaunchKernelGGL((k_hole_pair_fast<1>), dim3(blocks), dim3(threads), lds, st, a); break;
+      case 2: hipLaunchKernelGGL((k_hole_pair_fast<2>), dim3(blocks), dim3(threads), lds, st, a); break;
+      case 3: hipLaunchKernelGGL((k_hole_pair_fast<3>), dim3(blocks), dim3(threads), lds, st, a); break;
+      default: hipLaunchKernelGGL((k_hole_pair_fast<4>), dim3(blocks), dim3(threads), lds, st, a); break;
+    }
+    SKGE_CHECK_LAUNCH("hole fast pair launch");
+    return SKGE_OK;
+  }
 #define SKGE_LP(K)                                                                             \
   case K:                                                                                      \
     if (logistic_mode)                                                                         \
