@@ -253,9 +253,12 @@ void skge_runner_destroy(skge_runner_t *r);
  * one launch, then each mini-batch is ONE launch that scores batch b while
  * applying batch b-1's updates (accumulators double-buffered by batch parity;
  * a scoring wave that reads a row batch b-1 touched applies it first or waits
- * for its publisher).  Needs ent/rel in SKGE_ACC_I16X4 mode, d % 4 == 0,
- * 4 * (T / nbatches) <= 32767, an entity table with slot records (capacity
- * >= 4 * batch), a dense single-copy relation table and no gates.  Allocates
+ * for its publisher).  Needs ent/rel in SKGE_ACC_I16X4 mode, d % 4 == 0, an
+ * entity table with slot records (capacity >= 4 * batch), a dense
+ * single-copy relation table and no gates.  Any batch size: a row's packed
+ * sums are exact while its per-batch count is <= 32767 (each occurrence adds
+ * a coefficient no larger than the count it adds), and the apply reports a
+ * larger count through skge_pipe_runner_error (bit 2).  Allocates
  * the second accumulator copy and per-row batch marks itself (freed by
  * destroy).  *epoch_key must only advance (the runner advances it once per
  * epoch).  Replaces the per-batch loop of skge/base.py:1268-1284.
@@ -267,8 +270,9 @@ skge_pipe_runner_t *skge_pipe_runner_create(void *stream, const skge_table_t *en
                                             int nbatches, uint64_t seed, uint64_t *epoch_key,
                                             float margin, int ntries, int *nviol_total);
 int skge_pipe_runner_run(skge_pipe_runner_t *r, void *stream, int nepochs);
-/* synchronizes the stream; returns 0, or 1 if a bounded cross-workgroup wait
- * gave up (results then invalid), or a negative SKGE error code */
+/* synchronizes the stream; returns 0, or a bit set (results then invalid):
+ * 1 = a bounded cross-workgroup wait gave up, 2 = a row's per-batch count
+ * exceeded 32767 (packed sums may have wrapped); or a negative error code */
 int skge_pipe_runner_error(skge_pipe_runner_t *r, void *stream);
 int skge_pipe_runner_nlaunches(const skge_pipe_runner_t *r);
 /* One epoch launched eagerly (trains like run(1)) with HIP events around every

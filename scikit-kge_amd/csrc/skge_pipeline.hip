@@ -38,6 +38,14 @@
 
 namespace skge {
 
+// Packed int16x4 sums are exact while every field's total stays within
+// +-32767.  Each occurrence adds a coefficient no larger in magnitude than the
+// count it adds (s: |v0 gp + v1 (gp + g1)| <= v0 + 2 v1, relation:
+// |v0 (gp + g0) + v1 (gp + g1)| <= 2 (v0 + v1), ...), so a row whose count c
+// is <= 32767 cannot have wrapped; the apply flags any larger count.
+constexpr int PACKED_MAX = 32767;
+enum : int { ERR_WAIT = 1, ERR_PACKED = 2 };
+
 struct UpdParams {
   int opt, post;
   float lr, rin, rout, fdiv;   // g = (sum + rin*P)/div + rout*P, div = fdiv > 0 ? fdiv : count
@@ -53,6 +61,7 @@ struct PipeTab {               // entity table
   int* done;                   // [rows]: id of the launch whose update of the row was last applied
   UpdParams u;
   int* claims;                 // profile only: rows applied in this launch (sharded)
+  int* err;                    // ERR_* bits
 };
 
 struct RelTab {                // relation table
@@ -206,6 +215,7 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
                    sv);
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row
+  if (c > PACKED_MAX && l == 0) atomicOr(t.err, ERR_PACKED);   // a 16-bit field may have wrapped
   row_update<KQ>(t.u, c, d, sv, p, a);
 #pragma unroll
   for (int m = 0; m < KQ; ++m) {
@@ -231,7 +241,7 @@ __device__ __forceinline__ void ensure_applied(const PipeTab& t, int pp, int row
   while (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gp) {
     __builtin_amdgcn_s_sleep(2);
     if (++spins > (1u << 22)) {   // ~0.5 s: never hang the GPU; report instead
-      if (lane_id() == 0) atomicOr(err, 1);
+      if (lane_id() == 0) atomicOr(err, ERR_WAIT);
       break;
     }
     if ((spins & 1023u) == 0 &&   // once one wait has given up, the rest stop too
@@ -261,8 +271,11 @@ __device__ __forceinline__ unsigned long long now_10ns() { return __builtin_amdg
 #else
 #define SKGE_PIPE_OCC
 #endif
+#ifndef SKGE_PIPE_WG
+#define SKGE_PIPE_WG 256   // threads per workgroup
+#endif
 template <int KQ>
-__global__ __launch_bounds__(256) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
+__global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
   const int d = a.d, nq = d >> 2;
@@ -306,6 +319,7 @@ __global__ __launch_bounds__(256) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
           if (flush) prev[q] = 0ull;
         }
         if (c && a.R.updated && l == 0) atomicAdd(shard_of(a.R.updated), 1);
+        if (c > PACKED_MAX && l == 0) atomicOr(a.err, ERR_PACKED);
       } else {
         const int row = __builtin_amdgcn_readfirstlane(a.E.touched[pp][w - nR]);
 #ifndef SKGE_PIPE_ABL_NOAPPLY_E   // timing-only ablation: entity rows never updated
@@ -549,7 +563,7 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
     }
     if (trace && i == trace_launch) a.trace = trace;
 #define SKGE_PB(K) \
-  hipLaunchKernelGGL((k_pipe_batch<K>), dim3(r->grid[k]), dim3(256), 0, st, a)
+  hipLaunchKernelGGL((k_pipe_batch<K>), dim3(r->grid[k]), dim3(SKGE_PIPE_WG), 0, st, a)
     if (r->kq <= 1) SKGE_PB(1);
     else if (r->kq <= 2) SKGE_PB(2);
     else SKGE_PB(4);
@@ -584,8 +598,8 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
   }
   // batch geometry of StochasticTrainer._optim (skge/base.py:1246-1268)
   const int64_t bs = T / nbatches;
-  if (4 * bs > 32767 || 4 * bs > ent->touched_cap) {
-    set_error("pipelined runner: batch too large for packed sums or the slot capacity");
+  if (4 * bs > ent->touched_cap || 4 * bs > (1ll << 30)) {
+    set_error("pipelined runner: batch too large for the slot capacity");
     return nullptr;
   }
   std::vector<std::pair<int64_t, int64_t>> batches;
@@ -611,6 +625,7 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
     t.A = ent->opt == SKGE_ADAGRAD ? ent->state : nullptr;
     t.u = upd(ent);
     t.claims = nullptr;
+    t.err = nullptr;   // set below, once r->err exists
     t.sum[0] = reinterpret_cast<unsigned long long*>(ent->acc_sum);
     t.cnt[0] = ent->acc_cnt;
     t.touched[0] = ent->acc_touched;
@@ -672,6 +687,7 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
   a.stats_viol = nullptr;
   a.trace = nullptr;
   a.err = r->err;
+  a.E.err = r->err;
   int prev = 0;
   for (int b = 0; b <= nb1; ++b) {   // b == nb1: flush of the last batch (A role only)
     a.b = b;
@@ -679,8 +695,9 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
     a.count = b < nb1 ? (int)batches[b].second : 0;
     a.prev_slots = 4 * prev;
     const int a_items = 4 * prev + rel->rows;   // entity slots + every relation row
-    a.nA = std::max(1, std::min((a_items + 3) / 4, 16384));
-    const int nBb = std::max(1, std::min((a.count + 3) / 4, 16384));
+    constexpr int WPB = SKGE_PIPE_WG / 64;
+    a.nA = std::max(1, std::min((a_items + WPB - 1) / WPB, 16384));
+    const int nBb = std::max(1, std::min((a.count + WPB - 1) / WPB, 16384));
     r->batch.push_back(a);
     r->grid.push_back(a.nA + (a.count > 0 ? nBb : 0));
     prev = a.count;

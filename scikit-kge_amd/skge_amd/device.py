@@ -57,9 +57,12 @@ class EpochRunner(object):
         self.nviol_total = nviol_total if nviol_total is not None else \
             torch.zeros(1, dtype=torch.int32, device=dev)
         bs = kg.T // nbatches
-        # TransE-L1 sign contributions are small integers: exact packed int16x2
-        # accumulation when every per-batch sum fits (4 * batch <= 32767)
-        packed = bool(model.l1) and model.d % 4 == 0 and 4 * bs <= 32767 and not force_f32
+        # TransE-L1 sign contributions are small integers: exact packed int16x4
+        # sums.  The pipelined runner checks every row's count at run time (any
+        # batch size); the two-launch runner needs the static bound 4*batch <= 32767.
+        can_pack = bool(model.l1) and model.d % 4 == 0 and not force_f32
+        can_pipe = can_pack and replicas <= 1 and pipelined is not False
+        packed = can_pack and (can_pipe or 4 * bs <= 32767)
         mode = L.SKGE_ACC_I16X4 if packed else L.SKGE_ACC_F32
         from .param import Accumulator
         E, R = model.params["E"], model.params["R"]
@@ -74,9 +77,8 @@ class EpochRunner(object):
         self.nbatches = nbatches
         torch.cuda.current_stream().synchronize()
         lib = L.lib()
-        can_pipe = packed and replicas <= 1
         if pipelined and not can_pipe:
-            raise ValueError("pipelined runner needs TransE-L1, d % 4 == 0, 4*batch <= 32767, "
+            raise ValueError("pipelined runner needs TransE-L1, d % 4 == 0, "
                              "no forced f32 and replicas == 1")
         self.pipelined = can_pipe if pipelined is None else bool(pipelined)
         if self.pipelined:
@@ -130,10 +132,13 @@ class EpochRunner(object):
         self.stream.synchronize()
         if self.pipelined:
             rc = L.lib().skge_pipe_runner_error(self.handle, L.stream_ptr(self.stream))
-            if rc != 0:
-                raise L.SkgeError("pipelined runner: %s" % (
-                    "a cross-workgroup wait timed out" if rc > 0 else
-                    L.lib().skge_last_error().decode()))
+            if rc < 0:
+                raise L.SkgeError("pipelined runner: %s" % L.lib().skge_last_error().decode())
+            if rc & 1:
+                raise L.SkgeError("pipelined runner: a cross-workgroup wait timed out")
+            if rc & 2:
+                raise L.SkgeError("pipelined runner: a row's per-batch count exceeded 32767 "
+                                  "(packed sums may have wrapped); use force_f32=True")
 
     def __del__(self):
         h = getattr(self, "handle", None)

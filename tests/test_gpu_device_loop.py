@@ -246,3 +246,57 @@ def test_trainer_device_loop_fit():
     tr.fit([tuple(x) for x in trip.tolist()], [1] * len(trip))
     assert [e for e, _ in seen] == [1, 2, 3]
     assert all(v > 0 for _, v in seen)
+
+
+def test_pipelined_large_batch_matches_fp32_runner():
+    """Batches past the static packed bound (4 * 10000 > 32767): the pipelined
+    runner's exact packed sums, checked per row at run time, against the
+    two-launch runner's fp32 sums of the same integer contributions (exact in
+    fp32 too).  Same negatives; only the projections' summation order differs
+    (quad vs lane-strided layout), so the parameters agree to fp32 rounding."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, EpochRunner
+    trip, _ = make_kg(3000, 11, 20000)
+    out = []
+    for pipelined in (True, False):
+        np.random.seed(7)
+        m = S.TransE((3000, 3000, 11), 64)
+        m.add_hyperparam("margin", 2.0)
+        upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
+        kg = DeviceKG(trip, m.device)
+        r = EpochRunner(m, upd, kg, nbatches=2, seed=3, pipelined=pipelined,
+                        force_f32=not pipelined)
+        assert r.pipelined == pipelined and r.packed == pipelined
+        r.run(1)
+        r.synchronize()   # raises on a packed-sum overflow
+        out.append((m.E.data.cpu().numpy().copy(), m.R.data.cpu().numpy().copy(),
+                    int(r.nviol_total.item())))
+        del r
+    (E1, R1, v1), (E2, R2, v2) = out
+    assert v1 > 0
+    assert abs(v1 - v2) <= 2   # a margin test may flip on a rounding-level score difference
+    np.testing.assert_allclose(E1, E2, atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(R1, R2, atol=1e-5, rtol=1e-5)
+
+
+def test_pipelined_wn18_two_batches_per_epoch():
+    """WN18 geometry at nb=2 (70721 positives per batch) on the pipelined runner."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, EpochRunner
+    np.random.seed(42)
+    m = S.TransE((40943, 40943, 18), 200)
+    m.add_hyperparam("margin", 2.0)
+    upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
+    trip, _ = make_kg(40943, 18, 141442)
+    kg = DeviceKG(trip, m.device)
+    runner = EpochRunner(m, upd, kg, nbatches=2, seed=0)
+    assert runner.pipelined and runner.packed
+    runner.run(2)
+    runner.synchronize()
+    E = np.asarray(m.E, dtype=np.float64)
+    assert np.isfinite(E).all()
+    np.testing.assert_allclose(np.linalg.norm(E, axis=1), 1.0, atol=1e-5)
+    assert 0 < int(runner.nviol_total.item()) <= 2 * 2 * kg.T
+    for acc in (runner.accE, runner.accR):
+        assert int(acc.cnt.abs().sum().item()) == 0
+        assert float(acc.sum.abs().sum().item()) == 0.0
