@@ -184,14 +184,26 @@ int skge_accum_apply(void *stream, const skge_table_t *tables, int ntables, cons
  * Explicit-pair training step: skge_pair_grad + (RESCAL dW) + apply
  * (one _pairwise_gradients + _batch_step, skge/base.py:1417-1427).  RESCAL
  * needs a workspace of skge_pair_step_workspace_bytes(model, P, rel->rows, d)
- * bytes (0 for the other models): for d <= 480 the triples are grouped by
- * relation and W[p] E[o], E[s] W[p] and dW run as fp32 MFMA GEMMs
- * (skge_rescal.hip), otherwise as per-pair GEMVs.
+ * bytes (0 for the other models): for d <= 1024 and <= 8192 relations the
+ * triples are grouped by relation and W[p] E[o], E[s] W[p] and dW run as fp32
+ * MFMA GEMMs (skge_rescal.hip), otherwise as per-pair GEMVs.
  */
 size_t skge_pair_step_workspace_bytes(int model, int P, int M, int d);
 int skge_pair_step(void *stream, int model, int af, const skge_table_t *ent,
                    const skge_table_t *rel, int d, const int *pos, const int *neg, int P,
                    float margin, void *workspace, size_t ws_bytes, int *nviol);
+
+/*
+ * Labelled-triple (logistic) training step: skge_triple_grad + (RESCAL dW) +
+ * apply (one StochasticTrainer._process_batch, skge/base.py:1293-1316).
+ * RESCAL needs skge_triple_step_workspace_bytes(model, T, rel->rows, d)
+ * bytes of workspace (0 for HolE): relation-grouped fp32 MFMA GEMMs for
+ * d <= 1024 and <= 8192 relations, per-triple GEMVs otherwise.
+ */
+size_t skge_triple_step_workspace_bytes(int model, int T, int M, int d);
+int skge_triple_step(void *stream, int model, const skge_table_t *ent, const skge_table_t *rel,
+                     int d, const int *trip, const float *ys, int T, void *workspace,
+                     size_t ws_bytes, float *loss);
 
 /* ---------------- device-resident batch loop (throughput path) ---------------- */
 

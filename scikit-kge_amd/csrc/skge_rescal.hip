@@ -59,8 +59,10 @@ struct RescalWs {
 static int rs_tmax(int n, int M) { return n / RT_ITEMS + M + 1; }
 
 // carve the workspace (base may be null: size only)
-static size_t rescal_ws_layout(int P, int M, int d, void* base, RescalWs* ws) {
-  const int n = 2 * P, nchunks = (n + 63) / 64, tmax = rs_tmax(n, M);
+// n: triples in the batch (2P for pairs: positives then negatives; T for
+// labelled triples)
+static size_t rescal_ws_layout(int n, int M, int d, void* base, RescalWs* ws) {
+  const int nchunks = (n + 63) / 64, tmax = rs_tmax(n, M);
   size_t off = 0;
   char* b = (char*)base;
   auto take = [&](size_t bytes) {
@@ -87,9 +89,9 @@ static size_t rescal_ws_layout(int P, int M, int d, void* base, RescalWs* ws) {
   return off;
 }
 
-// triple k of the batch: positives 0..P-1, then negatives
-__device__ __forceinline__ const int* item_trip(const int* pos, const int* neg, int P, int k) {
-  return k < P ? pos + 3 * (size_t)k : neg + 3 * (size_t)(k - P);
+// triple k of the batch: list a (na triples: the positives), then list b
+__device__ __forceinline__ const int* item_trip(const int* a, const int* b, int na, int k) {
+  return k < na ? a + 3 * (size_t)k : b + 3 * (size_t)(k - na);
 }
 
 // ---------------------------------------------------------------------------
@@ -111,9 +113,9 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 }
 
 __global__ __launch_bounds__(256) void k_rs_count(const int* __restrict__ pos,
-                                                  const int* __restrict__ neg, int P, int M,
-                                                  RescalWs ws) {
-  const int n = 2 * P, nchunks = (n + 63) / 64, l = lane_id();
+                                                  const int* __restrict__ neg, int P, int n,
+                                                  int M, RescalWs ws) {
+  const int nchunks = (n + 63) / 64, l = lane_id();
   const int c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (c >= nchunks) return;
   const int k = c * 64 + l;
@@ -128,11 +130,11 @@ __global__ __launch_bounds__(256) void k_rs_count(const int* __restrict__ pos,
   }
 }
 
-__global__ __launch_bounds__(1024) void k_rs_scan(int P, int M, RescalWs ws) {
+__global__ __launch_bounds__(1024) void k_rs_scan(int n, int M, RescalWs ws) {
   extern __shared__ int lds[];   // cnt[M], tile_base[M+1]
   int* cnt = lds;
   int* tbase = lds + M;
-  const int n = 2 * P, nchunks = (n + 63) / 64;
+  const int nchunks = (n + 63) / 64;
   const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6, nw = blockDim.x >> 6;
   for (int p = wave; p < M; p += nw) {   // exclusive scan of relation p over the chunks
     int carry = 0;
@@ -183,9 +185,9 @@ __global__ __launch_bounds__(1024) void k_rs_scan(int P, int M, RescalWs ws) {
 }
 
 __global__ __launch_bounds__(256) void k_rs_scatter(const int* __restrict__ pos,
-                                                    const int* __restrict__ neg, int P, int M,
-                                                    RescalWs ws) {
-  const int n = 2 * P, nchunks = (n + 63) / 64, l = lane_id();
+                                                    const int* __restrict__ neg, int P, int n,
+                                                    int M, RescalWs ws) {
+  const int nchunks = (n + 63) / 64, l = lane_id();
   const int c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (c >= nchunks) return;
   const int k = c * 64 + l;
@@ -446,6 +448,49 @@ __global__ __launch_bounds__(256) void k_rescal_scatter(const int* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// logistic loss + entity contributions, one wave per labelled triple
+// (rescal.py:37-76): fs = -y sigmoid(-y f); E[s] += fs WE, E[o] += fs EW
+// ---------------------------------------------------------------------------
+template <int KM>
+__global__ __launch_bounds__(256) void k_rescal_logistic(const int* __restrict__ trip,
+                                                         const float* __restrict__ ys, int T,
+                                                         int d, RescalWs ws, Accum accE,
+                                                         float* score_out, float* loss) {
+  const int wpb = blockDim.x >> 6, ncb = (d + GC - 1) / GC;
+  float lsum = 0.0f;
+  for (int i = blockIdx.x * wpb + (threadIdx.x >> 6); i < T; i += gridDim.x * wpb) {
+    const int s = __builtin_amdgcn_readfirstlane(trip[3 * i]);
+    const int o = __builtin_amdgcn_readfirstlane(trip[3 * i + 1]);
+    float score = 0.0f;
+    for (int q = 0; q < ncb; ++q) score += ws.spart[(size_t)i * ncb + q];   // fixed order
+    const float y = ys[i];
+    const float ysc = y * score;
+    const float li = fmaxf(-ysc, 0.0f) + log1pf(expf(-fabsf(ysc)));   // logaddexp(0, -ys)
+    const float fs = -(y * (1.0f / (1.0f + expf(ysc))));                 // -(y sigmoid(-ys))
+    if (lane_id() == 0) {
+      if (score_out) score_out[i] = score;
+      ws.coef[ws.bpos[i]] = fs;
+    }
+    {
+      const int l = lane_id();   // entity occurrences (s, o): slots 2i, 2i+1
+      if (l < 2) commit_slot(accE, l == 0 ? s : o, s == o ? (l == 0 ? 2 : 0) : 1, 2 * i + l);
+    }
+    float we[KM], ew[KM], x[KM], yv[KM];
+    load_row<KM>(ws.WE, i, d, we);
+    load_row<KM>(ws.EW, i, d, ew);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {   // rescal.py:65-66 (fs WE over ss, fs EW over os)
+      x[k] = fs * we[k];
+      yv[k] = fs * ew[k];
+    }
+    acc_two<KM>(accE, s, x, o, yv, d);
+    lsum += li;
+  }
+  __shared__ float lds_loss;
+  if (loss) block_sum_add(loss, lsum, &lds_loss);
+}
+
+// ---------------------------------------------------------------------------
 // dW[p] = sum_items coef_i E[s_i] (x) E[o_i]: one workgroup per (relation,
 // 16-row strip, 4 x 16-column tiles); K = the relation's triples in bucket order
 // ---------------------------------------------------------------------------
@@ -526,59 +571,92 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
 
 using namespace skge;
 
-size_t skge_rescal_mfma_ws_bytes(int P, int M, int d) { return rescal_ws_layout(P, M, d, nullptr, nullptr); }
+size_t skge_rescal_mfma_ws_bytes(int n, int M, int d) {
+  return rescal_ws_layout(n, M, d, nullptr, nullptr);
+}
 
 bool skge_rescal_mfma_ok(int d, int M) {
   return d >= 1 && d <= RS_MAX_D && M >= 1 && M <= RS_MAX_M;
 }
 
-// the RESCAL pairwise gradient (entity accumulator, W accumulator, coef) on MFMA
-int skge_rescal_pair_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
-                               const skge_table_t* rel, int d, const int* pos, const int* neg,
-                               int P, float margin, void* workspace, size_t ws_bytes,
-                               float* pscore, float* nscore, int* nviol) {
+// bucket the n = na + nb triples (list a, then list b) by relation and run the
+// two GEMMs (WE^T, EW, partial scores)
+static int rescal_front(hipStream_t st, const skge_table_t* ent, const skge_table_t* rel, int d,
+                        const int* a, int na, const int* b, int n, const RescalWs& ws) {
   const int M = rel->rows;
-  RescalWs ws;
-  const size_t need = rescal_ws_layout(P, M, d, workspace, &ws);
-  SKGE_CHECK_ARG(workspace && ws_bytes >= need, "RESCAL workspace needs %zu bytes", need);
-  SKGE_CHECK_ARG(rel->acc_sum && rel->acc_cnt, "W accumulator missing");
-  const int nchunks = (2 * P + 63) / 64;
+  const int nchunks = (n + 63) / 64;
   SKGE_CHECK_HIP(hipMemsetAsync(ws.chunk, 0, (size_t)nchunks * M * sizeof(int), st));
   const int cblocks = (nchunks + 3) / 4;
-  hipLaunchKernelGGL(k_rs_count, dim3(cblocks), dim3(256), 0, st, pos, neg, P, M, ws);
-  hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(1024), (size_t)(2 * M + 1) * sizeof(int), st, P, M,
+  hipLaunchKernelGGL(k_rs_count, dim3(cblocks), dim3(256), 0, st, a, b, na, n, M, ws);
+  hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(1024), (size_t)(2 * M + 1) * sizeof(int), st, n, M,
                      ws);
-  hipLaunchKernelGGL(k_rs_scatter, dim3(cblocks), dim3(256), 0, st, pos, neg, P, M, ws);
+  hipLaunchKernelGGL(k_rs_scatter, dim3(cblocks), dim3(256), 0, st, a, b, na, n, M, ws);
   const int ncb = (d + GC - 1) / GC;
-  const dim3 ggrid((unsigned)(rs_tmax(2 * P, M) * 2 * ncb));
+  const dim3 ggrid((unsigned)(rs_tmax(n, M) * 2 * ncb));
   if ((d & 3) == 0)
     hipLaunchKernelGGL((k_rescal_gemm<true>), ggrid, dim3(256), 0, st, ent->param, rel->param, d,
                        ws);
   else
     hipLaunchKernelGGL((k_rescal_gemm<false>), ggrid, dim3(256), 0, st, ent->param, rel->param,
                        d, ws);
+  SKGE_CHECK_LAUNCH("rescal mfma front");
+  return SKGE_OK;
+}
+
+static void rescal_wgrad_launch(hipStream_t st, const skge_table_t* ent,
+                                const skge_table_t* rel, int d, const RescalWs& ws) {
+  const int dp = (d + 15) & ~15, ntd = dp / 16, ngrp = (ntd + 3) / 4;
+  hipLaunchKernelGGL(k_rescal_wgrad_mfma, dim3((unsigned)((long long)rel->rows * ntd * ngrp)),
+                     dim3(256), 0, st, ent->param, d, ws, accum_of(rel));
+}
+
+#define SKGE_KM_SWITCH(KERNEL, ...)                                             \
+  switch (km_for(d)) {                                                          \
+    case 1: hipLaunchKernelGGL((KERNEL<1>), __VA_ARGS__); break;                \
+    case 2: hipLaunchKernelGGL((KERNEL<2>), __VA_ARGS__); break;                \
+    case 3: hipLaunchKernelGGL((KERNEL<3>), __VA_ARGS__); break;                \
+    case 4: hipLaunchKernelGGL((KERNEL<4>), __VA_ARGS__); break;                \
+    case 8: hipLaunchKernelGGL((KERNEL<8>), __VA_ARGS__); break;                \
+    case 16: hipLaunchKernelGGL((KERNEL<16>), __VA_ARGS__); break;              \
+    default: set_error("d=%d unsupported on the MFMA path", d); return SKGE_ENOTSUP; \
+  }
+
+// the RESCAL pairwise gradient (entity accumulator, W accumulator) on MFMA
+int skge_rescal_pair_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
+                               const skge_table_t* rel, int d, const int* pos, const int* neg,
+                               int P, float margin, void* workspace, size_t ws_bytes,
+                               float* pscore, float* nscore, int* nviol) {
+  RescalWs ws;
+  const size_t need = rescal_ws_layout(2 * P, rel->rows, d, workspace, &ws);
+  SKGE_CHECK_ARG(workspace && ws_bytes >= need, "RESCAL workspace needs %zu bytes", need);
+  SKGE_CHECK_ARG(rel->acc_sum && rel->acc_cnt, "W accumulator missing");
+  int rc = rescal_front(st, ent, rel, d, pos, P, neg, 2 * P, ws);
+  if (rc) return rc;
   const int blocks = std::max(1, std::min((P + 3) / 4, 16384));
   const Accum aE = accum_of(ent);
-  switch (km_for(d)) {
-#define SKGE_RS(K)                                                                            \
-  case K:                                                                                     \
-    hipLaunchKernelGGL((k_rescal_scatter<K>), dim3(blocks), dim3(256), 0, st, pos, neg, P, d, \
-                       af, margin, ws, aE, pscore, nscore, nviol);                            \
-    break;
-    SKGE_RS(1)
-    SKGE_RS(2)
-    SKGE_RS(3)
-    SKGE_RS(4)
-    SKGE_RS(8)
-    SKGE_RS(16)
-#undef SKGE_RS
-    default:
-      set_error("d=%d unsupported on the MFMA path", d);
-      return SKGE_ENOTSUP;
-  }
-  const int dp = (d + 15) & ~15, ntd = dp / 16, ngrp = (ntd + 3) / 4;
-  hipLaunchKernelGGL(k_rescal_wgrad_mfma, dim3((unsigned)((long long)M * ntd * ngrp)), dim3(256),
-                     0, st, ent->param, d, ws, accum_of(rel));
+  SKGE_KM_SWITCH(k_rescal_scatter, dim3(blocks), dim3(256), 0, st, pos, neg, P, d, af, margin, ws,
+                 aE, pscore, nscore, nviol)
+  rescal_wgrad_launch(st, ent, rel, d, ws);
   SKGE_CHECK_LAUNCH("rescal mfma pair grad");
+  return SKGE_OK;
+}
+
+// the RESCAL logistic gradient (rescal.py:37-76) on MFMA
+int skge_rescal_triple_grad_mfma(hipStream_t st, const skge_table_t* ent,
+                                 const skge_table_t* rel, int d, const int* trip,
+                                 const float* ys, int T, void* workspace, size_t ws_bytes,
+                                 float* score, float* loss) {
+  RescalWs ws;
+  const size_t need = rescal_ws_layout(T, rel->rows, d, workspace, &ws);
+  SKGE_CHECK_ARG(workspace && ws_bytes >= need, "RESCAL workspace needs %zu bytes", need);
+  SKGE_CHECK_ARG(rel->acc_sum && rel->acc_cnt, "W accumulator missing");
+  int rc = rescal_front(st, ent, rel, d, trip, T, trip, T, ws);
+  if (rc) return rc;
+  const int blocks = std::max(1, std::min((T + 3) / 4, 16384));
+  const Accum aE = accum_of(ent);
+  SKGE_KM_SWITCH(k_rescal_logistic, dim3(blocks), dim3(256), 0, st, trip, ys, T, d, ws, aE, score,
+                 loss)
+  rescal_wgrad_launch(st, ent, rel, d, ws);
+  SKGE_CHECK_LAUNCH("rescal mfma triple grad");
   return SKGE_OK;
 }

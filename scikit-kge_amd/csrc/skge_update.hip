@@ -808,7 +808,11 @@ extern "C" int skge_accum_apply(void* stream, const skge_table_t* tables, int nt
 }
 
 // RESCAL on the matrix cores (skge_rescal.hip)
-size_t skge_rescal_mfma_ws_bytes(int P, int M, int d);
+size_t skge_rescal_mfma_ws_bytes(int n, int M, int d);
+int skge_rescal_triple_grad_mfma(hipStream_t st, const skge_table_t* ent,
+                                 const skge_table_t* rel, int d, const int* trip,
+                                 const float* ys, int T, void* workspace, size_t ws_bytes,
+                                 float* score, float* loss);
 bool skge_rescal_mfma_ok(int d, int M);
 int skge_rescal_pair_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
                                const skge_table_t* rel, int d, const int* pos, const int* neg,
@@ -824,7 +828,7 @@ static bool rescal_use_mfma(int d, int M) {
 extern "C" size_t skge_pair_step_workspace_bytes(int model, int P, int M, int d) {
   if (model != SKGE_RESCAL || P <= 0) return 0;
   const size_t coef = (size_t)2 * P * sizeof(float);   // coef of every pair (VALU path)
-  if (skge_rescal_mfma_ok(d, M)) return std::max(coef, skge_rescal_mfma_ws_bytes(P, M, d));
+  if (skge_rescal_mfma_ok(d, M)) return std::max(coef, skge_rescal_mfma_ws_bytes(2 * P, M, d));
   return coef;
 }
 
@@ -862,5 +866,44 @@ extern "C" int skge_pair_step(void* stream, int model, int af, const skge_table_
   t[0].gate = nviol;
   t[1].gate = nviol;
   const int ns[2] = {4 * P, model == SKGE_RESCAL ? rel->rows : 2 * P};
+  return skge_accum_apply(stream, t, 2, ns);
+}
+
+extern "C" size_t skge_triple_step_workspace_bytes(int model, int T, int M, int d) {
+  if (model != SKGE_RESCAL || T <= 0) return 0;
+  const size_t coef = (size_t)T * sizeof(float);   // fs of every triple (VALU path)
+  if (skge_rescal_mfma_ok(d, M)) return std::max(coef, skge_rescal_mfma_ws_bytes(T, M, d));
+  return coef;
+}
+
+extern "C" int skge_triple_step(void* stream, int model, const skge_table_t* ent,
+                                const skge_table_t* rel, int d, const int* trip, const float* ys,
+                                int T, void* workspace, size_t ws_bytes, float* loss) {
+  int rc;
+  if (model == SKGE_RESCAL && T > 0) {
+    const size_t need = skge_triple_step_workspace_bytes(model, T, rel->rows, d);
+    SKGE_CHECK_ARG(workspace && ws_bytes >= need, "RESCAL needs a %zu-byte workspace", need);
+    SKGE_CHECK_ARG(trip && ys, "trip/ys NULL");
+    if (rescal_use_mfma(d, rel->rows)) {
+      if ((rc = check_table(ent, "ent", true)) || (rc = check_table(rel, "rel", false)) ||
+          (rc = check_f32(ent, "ent")) || (rc = check_f32(rel, "rel")) ||
+          (rc = check_single(ent, "ent")) || (rc = check_single(rel, "rel")))
+        return rc;
+      SKGE_CHECK_ARG(ent->width == d && rel->width == d * d, "RESCAL table widths");
+      if ((rc = check_slots(ent, 2ll * T, "ent")) || (rc = check_slots(rel, rel->rows, "W")))
+        return rc;
+      rc = skge_rescal_triple_grad_mfma(as_stream(stream), ent, rel, d, trip, ys, T, workspace,
+                                        ws_bytes, nullptr, loss);
+    } else {
+      float* coef = (float*)workspace;
+      rc = skge_triple_grad(stream, model, ent, rel, d, trip, ys, T, nullptr, coef, loss);
+      if (!rc) rc = skge_rescal_wgrad(stream, ent, rel, d, trip, coef, T, nullptr, nullptr, 0);
+    }
+  } else {
+    rc = skge_triple_grad(stream, model, ent, rel, d, trip, ys, T, nullptr, nullptr, loss);
+  }
+  if (rc) return rc;
+  skge_table_t t[2] = {*ent, *rel};
+  const int ns[2] = {2 * T, model == SKGE_RESCAL ? rel->rows : T};
   return skge_accum_apply(stream, t, 2, ns);
 }

@@ -239,20 +239,16 @@ class Model(object):
         return ws
 
     def _logistic_step(self, trip, ys, updaters, loss):
-        dev = self.device
+        """score + grad + update for labelled triples in one skge_triple_step."""
         T = trip.shape[0]
-        coef = torch.empty(T, dtype=torch.float32, device=dev)
-        slots = self._triple_slots(T)
-        te, tr = self._tables("logistic", updaters, slots=slots)
         lib = L.lib()
-        st = L.stream_ptr()
-        L.check(lib.skge_triple_grad(st, self._kernel_model(), te, tr, self.d, L.ptr(trip),
-                                     L.ptr(ys), T, None, L.ptr(coef), L.ptr(loss)), "triple_grad")
-        if self.rel_id == "W":
-            L.check(lib.skge_rescal_wgrad(st, te, tr, self.d, L.ptr(trip), L.ptr(coef), T, None,
-                                          None, 0), "rescal_wgrad")
-        arr = (L.SkgeTable * 2)(te, tr)
-        L.check(lib.skge_accum_apply(st, arr, 2, L.int_array(*slots)), "apply")
+        nbytes = lib.skge_triple_step_workspace_bytes(self._kernel_model(), T,
+                                                      self.params[self.rel_id].rows, self.d)
+        ws = self._workspace(nbytes)
+        te, tr = self._tables("logistic", updaters, slots=self._triple_slots(T))
+        L.check(lib.skge_triple_step(L.stream_ptr(), self._kernel_model(), te, tr, self.d,
+                                     L.ptr(trip), L.ptr(ys), T, L.ptr(ws), nbytes, L.ptr(loss)),
+                "triple_step")
 
 
 class StochasticTrainer(object):

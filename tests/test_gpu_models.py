@@ -96,3 +96,43 @@ def test_rescal_mfma_relation_gradient_deterministic():
 @pytest.mark.parametrize("n_ent,n_rel,d,P", [(300, 7, 40, 600), (400, 18, 200, 500)])
 def test_hole_step_vs_oracle(n_ent, n_rel, d, P):
     _run("hole", n_ent, n_rel, d, P, nb=2)
+
+
+def _run_logistic(name, n_ent, n_rel, d, B, nb, rparam=0.0, seed=9):
+    """StochasticTrainer-style steps (B positives y=+1 and their two sampler
+    corruptions y=-1, skge/base.py:1293-1304) vs one oracle logistic step from
+    the device's state before each."""
+    m, upd = _model(name, n_ent, n_rel, d, rparam=rparam)
+    rs = np.random.RandomState(seed)
+    loss = torch.zeros(1, dtype=torch.float32, device=m.device)
+    for b in range(nb):
+        params = {pid: p.data.detach().cpu().numpy().astype(np.float64)
+                  for pid, p in m.params.items()}
+        state = {pid: upd[pid].p2.detach().cpu().numpy().astype(np.float64) for pid in m.params}
+        pos, neg = _batch(rs, n_ent, n_rel, B, diff_rel=0.0)
+        trip = np.concatenate([pos, neg]).astype(np.int32)
+        ys = np.concatenate([np.ones(B), -np.ones(B)]).astype(np.float32)
+        loss.zero_()
+        m._logistic_step(torch.as_tensor(trip, device=m.device),
+                         torch.as_tensor(ys, device=m.device), upd, loss)
+        _, want_loss, _ = O.logistic_step(name, params, state, trip, ys.astype(np.float64), 0.1,
+                                          "adagrad", rparam=rparam)
+        np.testing.assert_allclose(float(loss.item()), want_loss, rtol=1e-5)
+        for pid in m.params:
+            close_adagrad(m.params[pid].data, params[pid], state[pid], 0.1,
+                          "%s logistic b%d %s" % (name, b, pid))
+            close(upd[pid].p2, state[pid], "%s logistic b%d p2 %s" % (name, b, pid))
+
+
+@pytest.mark.parametrize("n_ent,n_rel,d,B", [(300, 7, 40, 300), (400, 18, 200, 350)])
+def test_rescal_logistic_mfma_vs_oracle(n_ent, n_rel, d, B):
+    _run_logistic("rescal", n_ent, n_rel, d, B, nb=2)
+
+
+def test_rescal_logistic_rparam():
+    _run_logistic("rescal", 300, 5, 32, 200, nb=2, rparam=0.05)
+
+
+@pytest.mark.parametrize("n_ent,n_rel,d,B", [(300, 7, 40, 300), (400, 18, 200, 250)])
+def test_hole_logistic_vs_oracle(n_ent, n_rel, d, B):
+    _run_logistic("hole", n_ent, n_rel, d, B, nb=2)
