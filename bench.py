@@ -146,7 +146,14 @@ def main():
     ap.add_argument("--reps", type=int, default=1, help="relation accumulator copies")
     ap.add_argument("--large-nb", type=int, default=2,
                     help="also time this nbatches (large-batch detail line); 0 = skip")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
+                    help="2: WN18 TransE d=200 (the headline); 5: synthetic |E|=50M |R|=10k "
+                         "d=512, B=131072 per GPU (BASELINE.json configs[4])")
+    ap.add_argument("--c5-scale", type=float, default=1.0,
+                    help="config 5 only: scale |E| and T (quick rehearsals)")
     args = ap.parse_args()
+    if args.config == 5:
+        return run_config5(args)
 
     import torch
     import torch.distributed as dist
@@ -204,7 +211,13 @@ def main():
     value = replica_value(positives, world, elapsed)
 
     # ---- per-kernel timing (HIP events on the runner stream, eager launches of
-    # one more epoch, outside the timed region) for the roofline ----
+    # one more epoch, outside the timed region) for the roofline.  The tables
+    # are rolled back to the initial state first, so the profiled epoch does
+    # the same work as the timed region's first epoch ----
+    for pid, p in model.params.items():
+        p.data.copy_(init[pid])
+        upd[pid].reset()
+    torch.cuda.synchronize()
     prof = pipe_profile(runner, kg, nb, d) if runner.pipelined else \
         kernel_profile(model, upd, kg, nb, d, st, runner)
 
@@ -287,11 +300,19 @@ def main():
         dist.destroy_process_group()
 
 
-def _score_bytes(d, cnt, V):
+def _score_bytes(d, cnt, V, packed=True):
     """Scoring part of a batch: gathers of s, o, p + 2
     corrupted rows, 20 B of index/hash traffic per positive, and the atomic row
-    adds of the violating positives (<= 5 rows each)."""
-    return 4 * d * (3 * cnt + 2 * cnt) + 20 * cnt + 4 * d * min(5 * cnt, 2 * V + 3 * cnt)
+    adds of the violating positives (<= 5 rows each; 2 B per element with the
+    exact int16x4 sums, 4 B with fp32)."""
+    ab = 2 * d if packed else 4 * d
+    return 4 * d * (3 * cnt + 2 * cnt) + 20 * cnt + ab * min(5 * cnt, 2 * V + 3 * cnt)
+
+
+def _apply_bytes(d, rows, packed=True):
+    """Per applied row: read param + AdaGrad state, write both (16d), read the
+    sums and write them back zeroed (4d packed, 8d fp32)."""
+    return (16 * d + (4 * d if packed else 8 * d)) * rows
 
 
 def pipe_profile(runner, kg, nb, d):
@@ -308,7 +329,7 @@ def pipe_profile(runner, kg, nb, d):
     b_pipe, t_pipe, total = 0.0, 0.0, 0.0
     for i, cnt in enumerate(counts, start=1):
         UE, UR, V = (int(x) for x in stats[i])
-        b = _score_bytes(d, cnt, V) + 24 * d * (UE + UR)
+        b = _score_bytes(d, cnt, V) + _apply_bytes(d, UE + UR)
         b_pipe += b
         t_pipe += float(us[i])
         if cnt:
@@ -323,6 +344,107 @@ def pipe_profile(runner, kg, nb, d):
                              "bytes_per_launch": 40.0 * T,
                              "achieved_gbs": 40.0 * T / (float(us[0]) * 1e-6) / 1e9}}
     return {"kernels": kern, "dominant": kern["pipe_batch"], "epoch_bytes": total}
+
+
+N5, M5, D5, T5, B5 = 50_000_000, 10_000, 512, 100_000_000, 131072
+
+
+def make_config5_kg(n_ent, n_rel, n_triples, dev, seed):
+    """Unique uniform (s, o, p) triples drawn on the device (torch generator)."""
+    import torch
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    out = None
+    while out is None or out.shape[0] < n_triples:
+        need = n_triples - (0 if out is None else out.shape[0])
+        m = need + need // 64 + 1024
+        cand = torch.stack([torch.randint(n_ent, (m,), device=dev, generator=g, dtype=torch.int32),
+                            torch.randint(n_ent, (m,), device=dev, generator=g, dtype=torch.int32),
+                            torch.randint(n_rel, (m,), device=dev, generator=g, dtype=torch.int32)],
+                           dim=1)
+        allt = cand if out is None else torch.cat([out, cand])
+        out = torch.unique(allt, dim=0)   # sorted order; the runner permutes per epoch
+        del cand, allt
+    out = out[:n_triples].contiguous()
+    torch.cuda.empty_cache()
+    return out
+
+
+def run_config5(args):
+    """BASELINE.json configs[4] on one GPU per rank: TransE-L1 d=512, |E|=50M,
+    |R|=10k, T=100M synthetic triples, B=131072 positives per batch, AdaGrad.
+    The tables (E 102 GB + AdaGrad state 102 GB + packed sums 51 GB) fit one
+    MI355X, so N GPUs run replicas (north_star: shard only past 288 GB)."""
+    import torch
+    import torch.distributed as dist
+    world, rank, local = dist_env()
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, EpochRunner
+    n_ent, T = int(N5 * args.c5_scale), int(T5 * args.c5_scale)
+    d, n_rel = D5, M5
+    t_build = time.perf_counter()
+    trip = make_config5_kg(n_ent, n_rel, T, dev, seed=rank)
+    model = S.TransE((n_ent, n_ent, n_rel), d, l1=True, init="device_nunif")
+    model.add_hyperparam("margin", 2.0)
+    upd = {pid: S.AdaGrad(p, 0.1) for pid, p in model.params.items()}
+    kg = DeviceKG(trip, dev)
+    del trip
+    nb = max(1, T // B5)
+    runner = EpochRunner(model, upd, kg, nbatches=nb, seed=99 + rank)
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t_build
+    runner.run(args.warmup)
+    runner.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    runner.run(args.steps)
+    runner.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(elapsed, world, dev)
+    value = replica_value(T * args.steps, world, elapsed)
+    prof = pipe_profile(runner, kg, nb, d) if runner.pipelined else \
+        kernel_profile(model, upd, kg, nb, d, runner.stream, runner)
+    k = prof["dominant"]
+    if rank == 0:
+        line = {
+            "metric": "triples/sec (score+grad+update), synthetic TransE |E|=50M |R|=10k d=512, "
+                      "B=131072 per GPU (BASELINE configs[4])",
+            "value": round(value, 1), "unit": "triples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic uniform KG (|E|=%d |R|=%d T=%d, torch generator seed rank); "
+                    "device-drawn nunif params" % (n_ent, n_rel, T),
+            "config": {"workload": "TransE-L1 d=%d PairwiseStochasticTrainer+AdaGrad, margin 2.0, "
+                                   "lr 0.1, device RandomModeSampler(1,[0,1]); step = 1 epoch of "
+                                   "%d batches" % (d, nb),
+                       "global_batch": T // nb * world, "parallelism": "replicas%d" % world},
+            "roofline": {"bound": "hbm", "kernel": k["name"],
+                         "achieved": round(k["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                         "traffic": None, "bytes_per_launch": round(k["bytes_per_launch"]),
+                         "avg_launch_us": round(k["avg_us"], 3)},
+            "cpu_baseline": None,
+            "detail": {"runner": "pipelined" if runner.pipelined else "two-launch",
+                       "accumulator": "int16x4 exact" if runner.packed else "fp32",
+                       "build_s": round(t_build, 1),
+                       "kernels": {n: {"avg_us": round(v["avg_us"], 3), "launches": v["launches"],
+                                       "GB_s": round(v["achieved_gbs"], 1)}
+                                   for n, v in prof["kernels"].items()},
+                       "gpu_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)},
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def kernel_profile(model, upd, kg, nb, d, st, runner):
@@ -364,8 +486,8 @@ def kernel_profile(model, upd, kg, nb, d, st, runner):
             times["transe_sample_grad"].append(e[0].elapsed_time(e[1]) * 1e3)
             times["accum_apply"].append(e[2].elapsed_time(e[3]) * 1e3)
             P = 2 * cnt
-            b_sg = _score_bytes(d, cnt, V)
-            b_ap = 24 * d * (UE + UR)     # read sum, param, state; write param, state, zero sum
+            b_sg = _score_bytes(d, cnt, V, runner.packed)
+            b_ap = _apply_bytes(d, UE + UR, runner.packed)
             bytes_["transe_sample_grad"] += b_sg
             bytes_["accum_apply"] += b_ap
             total += algorithmic_bytes(d, cnt, P, UE, UR)

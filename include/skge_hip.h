@@ -55,10 +55,12 @@ enum {
   SKGE_ACC_F32 = 0,    /* acc_sum: fp32 [rows][width] */
   SKGE_ACC_I16X4 = 1   /* acc_sum: exact integer sums of TransE-L1 sign contributions,
                           four elements per int64 (elements 4q..4q+3 in qword q, added
-                          with one 64-bit integer atomic; each 16-bit field's total
-                          stays within +-32767) -- produced only by
-                          skge_transe_sample_grad with l1 != 0, width % 4 == 0 and
-                          4 * count <= 32767 */
+                          with one 64-bit integer atomic; exact while each 16-bit
+                          field's total stays within +-32767, which a row whose
+                          per-batch count is <= 32767 guarantees: the apply kernels
+                          flag larger counts, skge_device_error bit 2) -- produced
+                          only by skge_transe_sample_grad / the pipelined runner with
+                          l1 != 0 and width % 4 == 0 */
 };
 
 /*
@@ -113,6 +115,10 @@ typedef struct skge_table {
 
 int skge_abi_version(void);
 const char *skge_last_error(void);
+/* Synchronizes the stream and returns the error bits raised by device kernels
+ * since the last reset (2 = a packed row's count exceeded 32767); reset != 0
+ * clears them. */
+int skge_device_error(void *stream, int reset);
 
 /*
  * Pairwise scoring + contribution scatter for P explicit (positive, negative)

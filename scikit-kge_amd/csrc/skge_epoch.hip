@@ -332,9 +332,9 @@ static int launch_sample(const SampleArgs& a, bool l1, hipStream_t st) {
   if (blocks < 1) blocks = 1;
   if (blocks > 16384) blocks = 16384;
   if (a.accE.mode == ACC_I16X4) {
-    if (!l1 || a.accR.mode != ACC_I16X4 || (a.d & 3) || a.d > 1024 || 4ll * a.count > 32767) {
+    if (!l1 || a.accR.mode != ACC_I16X4 || (a.d & 3) || a.d > 1024) {
       set_error("packed accumulators need TransE-L1, both tables packed, d %% 4 == 0, "
-                "d <= 1024, 4*count <= 32767");
+                "d <= 1024");
       return SKGE_EINVAL;
     }
     const int kq = (a.d / 4 + 63) / 64;

@@ -530,6 +530,7 @@ static void* dalloc(skge_pipe_runner* r, size_t bytes) {
 }
 
 static void pipe_free(skge_pipe_runner* r) {
+  (void)hipGetLastError();   // a failed allocation must not poison later launch checks
   if (!r) return;
   if (r->exec) (void)hipGraphExecDestroy(r->exec);
   if (r->graph) (void)hipGraphDestroy(r->graph);

@@ -11,6 +11,10 @@
 
 namespace skge {
 
+// error bits raised by apply kernels (read with skge_device_error):
+// 2 = a packed int16x4 row's count exceeded 32767 (its sums may have wrapped)
+__device__ int g_skge_dev_err = 0;
+
 struct TableDev {
   float* P;
   float* A;
@@ -198,6 +202,9 @@ __device__ __forceinline__ void apply_row_i16(const TableDev& t, int row, bool u
   }
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row, or a stale slot
+  // each occurrence adds a coefficient no larger than its count: c <= 32767
+  // means no 16-bit field can have wrapped
+  if (c > 32767 && l == 0) atomicOr(&g_skge_dev_err, 2);
   const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
   float ss = 0.0f;
 #pragma unroll
@@ -296,6 +303,7 @@ __device__ __forceinline__ void apply_row_rep_block(const TableDev& t, int row, 
   }
   __syncthreads();
   const int c = lds[dw];
+  if (MODE == ACC_I16X4 && c > 32767 && tid == 0) atomicOr(&g_skge_dev_err, 2);
   if (tid < 64 && c != 0) {
     const int l = tid;
     const bool ada = t.opt == OPT_ADAGRAD;
@@ -823,6 +831,18 @@ int skge_rescal_pair_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
 static bool rescal_use_mfma(int d, int M) {
   static const bool valu = getenv("SKGE_RESCAL_VALU") && atoi(getenv("SKGE_RESCAL_VALU")) != 0;
   return !valu && skge_rescal_mfma_ok(d, M);
+}
+
+extern "C" int skge_device_error(void* stream, int reset) {
+  int v = 0;
+  hipStream_t st = as_stream(stream);
+  SKGE_CHECK_HIP(hipStreamSynchronize(st));
+  SKGE_CHECK_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_skge_dev_err), sizeof(int)));
+  if (reset && v) {
+    const int z = 0;
+    SKGE_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_skge_dev_err), &z, sizeof(int)));
+  }
+  return v;
 }
 
 extern "C" size_t skge_pair_step_workspace_bytes(int model, int P, int M, int d) {

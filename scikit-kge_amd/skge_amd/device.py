@@ -58,11 +58,12 @@ class EpochRunner(object):
             torch.zeros(1, dtype=torch.int32, device=dev)
         bs = kg.T // nbatches
         # TransE-L1 sign contributions are small integers: exact packed int16x4
-        # sums.  The pipelined runner checks every row's count at run time (any
-        # batch size); the two-launch runner needs the static bound 4*batch <= 32767.
+        # sums at any batch size (the applies flag a row whose count could have
+        # wrapped a 16-bit field, checked by synchronize())
         can_pack = bool(model.l1) and model.d % 4 == 0 and not force_f32
         can_pipe = can_pack and replicas <= 1 and pipelined is not False
-        packed = can_pack and (can_pipe or 4 * bs <= 32767)
+        self._auto = pipelined is None
+        packed = can_pack
         mode = L.SKGE_ACC_I16X4 if packed else L.SKGE_ACC_F32
         from .param import Accumulator
         E, R = model.params["E"], model.params["R"]
@@ -72,6 +73,13 @@ class EpochRunner(object):
         self.accR = Accumulator(R.rows, R.width, dev, mode=mode, dense=True,
                                 replicas=replicas)
         self.packed = packed
+        if can_pipe and pipelined is None:
+            # the pipelined runner's scratch: a second entity accumulator copy,
+            # per-row marks and the epoch's records (auto mode: only if it fits)
+            torch.cuda.synchronize(dev)
+            torch.cuda.empty_cache()
+            extra = E.rows * E.width * 2 + E.rows * 12 + kg.T * 20 + (64 << 20)
+            can_pipe = extra < torch.cuda.mem_get_info(dev)[0] * 0.9
         self.te = updaters["E"].table(self.accE)
         self.tr = updaters["R"].table(self.accR)
         self.nbatches = nbatches
@@ -86,11 +94,14 @@ class EpochRunner(object):
                 L.stream_ptr(self.stream), self.te, self.tr, model.d, L.ptr(kg.trip), kg.T,
                 L.ptr(kg.slots), kg.capacity, int(nbatches), int(seed) & (2 ** 64 - 1),
                 L.ptr(self.epoch_key), float(model.margin), int(ntries), L.ptr(self.nviol_total))
-            if not h:
-                raise L.SkgeError("skge_pipe_runner_create: %s" % lib.skge_last_error().decode())
-            self.handle = h
-            self.nlaunches = lib.skge_pipe_runner_nlaunches(h)
-            return
+            if h:
+                self.handle = h
+                self.nlaunches = lib.skge_pipe_runner_nlaunches(h)
+                return
+            err = lib.skge_last_error().decode()
+            if not (self._auto and "allocation" in err):
+                raise L.SkgeError("skge_pipe_runner_create: %s" % err)
+            self.pipelined = False   # auto mode: out of device memory -> two-launch runner
         h = lib.skge_runner_create(L.stream_ptr(self.stream), int(bool(model.l1)),
                                    self.te, self.tr,
                                    model.d, L.ptr(kg.trip), kg.T, L.ptr(kg.slots), kg.capacity,
@@ -130,6 +141,11 @@ class EpochRunner(object):
 
     def synchronize(self):
         self.stream.synchronize()
+        if not self.pipelined and self.packed:
+            rc = L.lib().skge_device_error(L.stream_ptr(self.stream), 1)
+            if rc & 2:
+                raise L.SkgeError("epoch runner: a row's per-batch count exceeded 32767 "
+                                  "(packed sums may have wrapped); use force_f32=True")
         if self.pipelined:
             rc = L.lib().skge_pipe_runner_error(self.handle, L.stream_ptr(self.stream))
             if rc < 0:

@@ -99,6 +99,42 @@ def post_code(post):
                          "normalize / normless1)" % (post,))
 
 
+def _device_init(shape, method, dev):
+    """init_nunif / init_unif / init_randn (skge/param.py:23-54) drawn on the
+    device, fp32, in place."""
+    t = torch.empty(shape, dtype=torch.float32, device=dev)
+    rows, cols = shape[-2], shape[-1]
+    if method == "nunif":
+        bnd = float(np.sqrt(6) / np.sqrt(rows + cols))
+        t.uniform_(-bnd, bnd)
+    elif method == "unif":
+        bnd = float(np.sqrt(1.0 / rows))
+        t.uniform_(-bnd, bnd)
+    elif method == "randn":
+        t.normal_()
+    else:
+        raise ValueError("Unknown initialization (device_%s)" % method)
+    return t
+
+
+def _device_post_init(t, post, chunk=1 << 20):
+    """The model-construction projection (idx=None) on a device table, in
+    row chunks so no full-size temporary is made."""
+    if post is normalize:
+        for r0 in range(0, t.shape[0], chunk):
+            blk = t[r0:r0 + chunk]
+            blk.div_(blk.norm(dim=1, keepdim=True))
+    elif post is normless1:   # the column-wise quirk of normless1(M, None)
+        col = torch.zeros(t.shape[1], dtype=torch.float64, device=t.device)
+        for r0 in range(0, t.shape[0], chunk):
+            col += (t[r0:r0 + chunk].double() ** 2).sum(dim=0)
+        col = torch.where(col < 1, torch.ones_like(col), col).float()
+        for r0 in range(0, t.shape[0], chunk):
+            t[r0:r0 + chunk].div_(col)
+    else:
+        raise ValueError("unsupported post projection %r" % (post,))
+
+
 # --------------------------------------------------------------------------
 # Parameter
 # --------------------------------------------------------------------------
@@ -115,6 +151,14 @@ class Parameter(object):
         self.name = name
         self.post = post
         dev = device if device is not None else _device()
+        if value is None and method.startswith("device_"):
+            # tables too large for a host NumPy draw (e.g. 50M x 512): the same
+            # distribution drawn on the device with torch's generator -- not the
+            # reference's RNG stream
+            self.data = _device_init(tuple(shape), method[len("device_"):], dev)
+            if post is not None:
+                _device_post_init(self.data, post)
+            return
         if value is None:
             shape = tuple(shape)
             if len(shape) == 3:   # param.py:62-64: each d x d slice drawn independently
@@ -213,7 +257,9 @@ class Accumulator(object):
                  replicas=1):
         self.rows, self.width, self.mode = rows, width, mode
         self.replicas = replicas if dense else 1
-        self.sum = torch.zeros(self.replicas * rows * width, dtype=torch.float32, device=device)
+        # int16x4 mode packs four elements per 8 bytes: width / 2 dwords per row
+        dw = width // 2 if mode == L.SKGE_ACC_I16X4 else width
+        self.sum = torch.zeros(self.replicas * rows * dw, dtype=torch.float32, device=device)
         self.cnt = torch.zeros(self.replicas * rows, dtype=torch.int32, device=device)
         self.touched = None if dense else \
             torch.full((max(slots, 1),), -1, dtype=torch.int32, device=device)
