@@ -307,6 +307,26 @@ int skge_pipe_runner_profile(skge_pipe_runner_t *r, void *stream, float *us_out,
                              int n, int trace_launch, uint64_t *trace_out, int64_t trace_len);
 void skge_pipe_runner_destroy(skge_pipe_runner_t *r);
 
+/* ---------------- evaluation ---------------- */
+
+/*
+ * Filtered link-prediction ranks: FilteredRankingEval.positions
+ * (skge/base.py:913-1031) with TransEEval (skge/run_transe.py:15-29; the L1
+ * distance for either norm, as there) or HolEEval (skge/run_hole.py:12-19);
+ * RESCAL scores E_s W_p E_o the same way.  For each test triple i = (s, o, p)
+ * of queries[nq][3]: ranks_out[4i..4i+3] = tail rank of o given (s, p) raw and
+ * filtered, head rank of s given (o, p) raw and filtered, where rank = 1 +
+ * #entities scoring strictly higher (ties in the true entity's favour) and
+ * the filtered count skips entities forming a known triple (set: a triple set
+ * built by skge_triple_set_build over the known triples; NULL = no filter).
+ * E [N][d], R [M][d] (W [M][d][d] for RESCAL), d <= 1024; workspace of
+ * skge_rank_workspace_bytes(nq, d) bytes.
+ */
+size_t skge_rank_workspace_bytes(int nq, int d);
+int skge_rank(void *stream, int model, const float *E, const float *R, int N, int d,
+              const int *queries, int nq, const void *set, int64_t set_capacity,
+              void *workspace, size_t ws_bytes, int *ranks_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -416,3 +416,57 @@ def logistic_step(model, params, state, trip, ys, lr, opt="adagrad", rparam=0.0)
         sc, loss, g = rescal_gradients(params["E"], params["W"], trip, ys, rparam)
     apply_grads(model, params, state, g, lr, opt)
     return sc, loss, g
+
+
+# ----------------------------------------------------------------------------
+# filtered ranking evaluation  (skge/base.py:913-1031, skge/run_transe.py:15-29,
+# skge/run_hole.py:12-19)
+# ----------------------------------------------------------------------------
+
+def entity_scores(model, E, R, s, o, p, direction):
+    """Scores of every entity as the tail (direction 'tail': (s, p, ?)) or the
+    head ('head': (?, p, o)), as the reference's evaluators compute them:
+    TransEEval  scores_o = -sum|E[s] + R[p] - E|, scores_s = -sum|E + R[p] - E[o]|
+                (run_transe.py:24-29; the L1 form whatever the training norm)
+    HolEEval    ER = ccorr(R[p], E); scores_o = ER . E[s], scores_s = E . ER[o]
+                (run_hole.py:14-19)
+    RESCAL      (no reference evaluator) E[s] W[p] E^T / E W[p] E[o]."""
+    if model == "transe":
+        if direction == "tail":
+            return -np.sum(np.abs(E[s] + R[p] - E), axis=1)
+        return -np.sum(np.abs(E + R[p] - E[o]), axis=1)
+    if model == "hole":
+        ER = ccorr(R[p], E)
+        return ER.dot(E[s]) if direction == "tail" else E.dot(ER[o])
+    W = R[p]
+    return E.dot(E[s].dot(W)) if direction == "tail" else E.dot(W.dot(E[o]))
+
+
+def filtered_ranks(model, E, R, queries, known):
+    """FilteredRankingEval.positions for explicit queries (s, o, p): per query
+    (tail raw, tail filtered, head raw, head filtered) positions.  A position
+    is 1 + #entities scoring strictly higher than the true one -- the
+    reference's descending-argsort position whenever no other entity ties the
+    true score exactly; the filtered count skips known triples other than the
+    query itself (the reference's -inf masking, base.py:970-977, 1011-1017)."""
+    known = set(map(tuple, np.asarray(known).tolist()))
+    out = np.zeros((len(queries), 4), dtype=np.int64)
+    n = E.shape[0]
+    for i, (s, o, p) in enumerate(np.asarray(queries).tolist()):
+        for col, direction, target in ((0, "tail", o), (2, "head", s)):
+            sc = entity_scores(model, E, R, s, o, p, direction)
+            higher = sc > sc[target]
+            out[i, col] = 1 + int(higher.sum())
+            if direction == "tail":
+                mask = np.array([(s, j, p) in known and j != o for j in range(n)])
+            else:
+                mask = np.array([(j, o, p) in known and j != s for j in range(n)])
+            out[i, col + 1] = 1 + int((higher & ~mask).sum())
+    return out
+
+
+def compute_scores(pos, hits=10):
+    """(MRR, mean position, hits@k in percent) of a position array
+    (skge/base.py:1099-1103)."""
+    pos = np.asarray(pos, dtype=np.float64)
+    return float(np.mean(1.0 / pos)), float(np.mean(pos)), float(np.mean(pos <= hits) * 100)

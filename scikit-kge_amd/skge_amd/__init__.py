@@ -10,3 +10,4 @@ from .hole import HolE
 from .rescal import RESCAL
 from .param import Parameter, SGD, AdaGrad, normalize, normless1
 from .sample import RandomModeSampler
+from .eval import FilteredRankingEval, TransEEval, HolEEval, compute_scores, ranking_scores

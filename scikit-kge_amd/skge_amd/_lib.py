@@ -52,6 +52,8 @@ SIGNATURES = {
     "skge_update_rows": (c_i, [c_p, T_P, c_p, c_p, c_i]),
     "skge_accum_apply": (c_i, [c_p, T_P, c_i, ctypes.POINTER(c_i)]),
     "skge_device_error": (c_i, [c_p, c_i]),
+    "skge_rank_workspace_bytes": (c_sz, [c_i, c_i]),
+    "skge_rank": (c_i, [c_p, c_i, c_p, c_p, c_i, c_i, c_p, c_i, c_p, c_i64, c_p, c_sz, c_p]),
     "skge_pair_step_workspace_bytes": (c_sz, [c_i, c_i, c_i, c_i]),
     "skge_triple_step_workspace_bytes": (c_sz, [c_i, c_i, c_i, c_i]),
     "skge_triple_step": (c_i, [c_p, c_i, T_P, T_P, c_i, c_p, c_p, c_i, c_p, c_sz, c_p]),
