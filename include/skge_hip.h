@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SKGE_ABI_VERSION 1
+#define SKGE_ABI_VERSION 2
 
 enum {
   SKGE_OK = 0,
@@ -111,6 +111,11 @@ typedef struct skge_table {
   float rin, rout, fixed_div;
   const int *gate;     /* optional: if non-NULL and *gate == 0, the update is
                           skipped (the model returned None: no violations) */
+  int *upd_count;      /* optional [rows]: AdaGrad applies add 1 per updated row
+                          (Parameter.updateCounts, skge/param.py:149-150) */
+  int *violations;     /* optional [rows], entity table of a TransE pair launch:
+                          +1 per violating pair for each distinct entity of
+                          {sn, on, sp, op} (E.violations, skge/transe.py:78-83) */
 } skge_table_t;
 
 int skge_abi_version(void);

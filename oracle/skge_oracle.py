@@ -163,6 +163,25 @@ def transe_pairwise_gradients(E, R, pos, neg, margin, l1=True):
     ridx, rs, rn = segment_mean(np.concatenate([pp, pn]), np.vstack([pg, ng]))  # 158-160
     return ps, ns, nviol, {"E": (es / en[:, None], eidx), "R": (rs / rn[:, None], ridx)}
 
+def transe_violation_counts(violations, pos, neg, ind):
+    """E.violations bookkeeping of skge/transe.py:78-83: for every violating
+    pair i in ind, +1 for each distinct entity of {sn, on, sp, op}."""
+    sp, _, op = _split(pos)
+    sn, _, on = _split(neg)
+    for i in ind:
+        for u in set([sn[i], on[i], sp[i], op[i]]):
+            violations[u] += 1
+    return violations
+
+
+def adagrad_update_counts(counts, idx):
+    """Parameter.updateCounts of skge/param.py:149-150: +1 per row of an
+    AdaGrad update's idx."""
+    for i in idx:
+        counts[i] += 1
+    return counts
+
+
 # ----------------------------------------------------------------------------
 # HolE  (skge/hole.py)
 # ----------------------------------------------------------------------------

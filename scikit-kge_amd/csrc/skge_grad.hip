@@ -37,6 +37,7 @@ struct PairArgs {
   int* nviol;
   float* loss;
   int record;  // 0: score only (no contribution scatter, no slot writes)
+  int* eviol;  // optional per-entity violation counter (TransE pairs)
 };
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -463,6 +464,19 @@ __device__ __forceinline__ bool rescal_pair(const PairArgs& a, int i, float* sw,
   return true;
 }
 
+// E.violations[u] += 1 for each distinct u in {sn, on, sp, op} of a violating
+// pair (skge/transe.py:78-83): lane j < 4 takes one entity and counts it
+// unless an earlier lane holds the same id
+__device__ __forceinline__ void count_entity_violation(int* cnt, const int (&ix)[6]) {
+  const int l = lane_id();
+  const int sp = ix[0], op = ix[1], sn = ix[3], on = ix[4];
+  if (l < 4) {
+    const int u = l == 0 ? sn : (l == 1 ? on : (l == 2 ? sp : op));
+    const bool dup = (l >= 1 && u == sn) || (l >= 2 && u == on) || (l >= 3 && u == sp);
+    if (!dup) atomicAdd(cnt + u, 1);
+  }
+}
+
 template <int MODEL, int KM>
 __global__ __launch_bounds__(256) void k_pair_grad(PairArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -483,6 +497,8 @@ __global__ __launch_bounds__(256) void k_pair_grad(PairArgs a) {
     else
       v = rescal_pair<KM>(a, i, sw, ix);
     if (a.record) commit_pair(a.accE, MODEL == RESCAL ? nullptr : &a.accR, v, ix, i);
+    if ((MODEL == TRANSE_L1 || MODEL == TRANSE_L2) && a.eviol && v)
+      count_entity_violation(a.eviol, ix);
     nv += v ? 1 : 0;
   }
   __shared__ int lds_nv;
@@ -803,6 +819,7 @@ extern "C" int skge_pair_grad(void* stream, int model, int af, const skge_table_
   a.coef = coef;
   a.nviol = nviol;
   a.record = margin == -INFINITY ? 0 : 1;   // -inf margin: score only
+  if (a.record) a.eviol = ent->violations;
   if (a.record) {
     if ((rc = check_slots(ent, 4ll * P, "ent"))) return rc;
     if (model != SKGE_RESCAL && (rc = check_slots(rel, 2ll * P, "rel"))) return rc;

@@ -22,6 +22,7 @@ struct TableDev {
   int rows, width, opt, post;
   float lr, rin, rout, fdiv;
   const int* gate;
+  int* ucnt;   // optional AdaGrad update counter per row (skge/param.py:149-150)
 };
 
 static TableDev table_dev(const skge_table_t* t) {
@@ -38,6 +39,7 @@ static TableDev table_dev(const skge_table_t* t) {
   d.rout = t->rout;
   d.fdiv = t->fixed_div;
   d.gate = t->gate;
+  d.ucnt = t->upd_count;
   return d;
 }
 
@@ -51,6 +53,7 @@ __device__ __forceinline__ void update_row(const TableDev& t, int row, const flo
   float* arow = t.A ? t.A + (size_t)row * w : nullptr;
   const bool ada = t.opt == OPT_ADAGRAD;
   float p[KM], a[KM];
+  if (ada && t.ucnt && l == 0) t.ucnt[row] += 1;   // updateCounts[i] += 1  param.py:149-150
 #pragma unroll
   for (int k = 0; k < KM; ++k) {   // unconditional loads (see load_row)
     const int e = l + 64 * k;
@@ -142,6 +145,7 @@ __device__ __forceinline__ void apply_row(const TableDev& t, int row, bool upd) 
   }
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row, or a stale slot
+  if (upd && ada && t.ucnt && l == 0) t.ucnt[row] += 1;   // param.py:149-150
   const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
   float ss = 0.0f;
 #pragma unroll
@@ -202,6 +206,7 @@ __device__ __forceinline__ void apply_row_i16(const TableDev& t, int row, bool u
   }
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row, or a stale slot
+  if (upd && ada && t.ucnt && l == 0) t.ucnt[row] += 1;   // param.py:149-150
   // each occurrence adds a coefficient no larger than its count: c <= 32767
   // means no 16-bit field can have wrapped
   if (c > 32767 && l == 0) atomicOr(&g_skge_dev_err, 2);
@@ -349,6 +354,7 @@ __device__ __forceinline__ void apply_row_rep_block(const TableDev& t, int row, 
 #pragma unroll
       for (int k = 0; k < KR; ++k) p[k] = p[k] / nrm;
     }
+    if (upd && ada && t.ucnt && l == 0) t.ucnt[row] += 1;   // param.py:149-150
     if (upd) {
 #pragma unroll
       for (int k = 0; k < KR; ++k) {
@@ -421,6 +427,7 @@ __global__ __launch_bounds__(256) void k_apply_wide(TableDev t, int nslots) {
     const float g = (t.acc.sum[off] + t.rin * pv) / div + t.rout * pv;
     t.acc.sum[off] = 0.0f;
     if (gate) {
+      if (e == 0 && t.opt == OPT_ADAGRAD && t.ucnt) t.ucnt[row] += 1;   // param.py:149-150
       if (t.opt == OPT_ADAGRAD) {
         const float av = t.A[off] + g * g;
         t.A[off] = av;
@@ -469,6 +476,7 @@ __global__ __launch_bounds__(256) void k_update_rows_wide(TableDev t, const floa
     const long long e = q - i * w;
     const size_t off = (size_t)idx[i] * w + e;
     const float gv = g[q];
+    if (e == 0 && t.opt == OPT_ADAGRAD && t.ucnt) t.ucnt[idx[i]] += 1;   // param.py:149-150
     if (t.opt == OPT_ADAGRAD) {
       const float av = t.A[off] + gv * gv;
       t.A[off] = av;

@@ -33,7 +33,8 @@ class SkgeTable(ctypes.Structure):
     _fields_ = [("param", c_p), ("state", c_p), ("acc_sum", c_p), ("acc_cnt", c_p),
                 ("acc_touched", c_p), ("rows", c_i), ("width", c_i), ("touched_cap", c_i),
                 ("acc_mode", c_i), ("acc_replicas", c_i), ("opt", c_i), ("post", c_i), ("lr", c_f), ("rin", c_f), ("rout", c_f),
-                ("fixed_div", c_f), ("gate", c_p)]
+                ("fixed_div", c_f), ("gate", c_p), ("upd_count", c_p),
+                ("violations", c_p)]
 
 
 T_P = ctypes.POINTER(SkgeTable)
@@ -97,7 +98,7 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.skge_abi_version() != 1:
+    if lib.skge_abi_version() != 2:
         raise SkgeError("ABI version mismatch")
     _lib = lib
     return lib

@@ -129,6 +129,8 @@ class Model(object):
                 t = table_struct(self.params[pid], None, acc, rin=rin, rout=rout, fixed_div=fdiv,
                                  gate=gate)
             out.append(t)
+        if mode == "pairwise" and self._kernel_model() in (L.SKGE_TRANSE_L1, L.SKGE_TRANSE_L2):
+            out[0].violations = L.ptr(self.params["E"].counter("viol"))   # transe.py:78-83
         return out
 
     def _collect(self, pid, t):
@@ -405,10 +407,16 @@ class PairwiseStochasticTrainer(StochasticTrainer):
         for x in xs:
             neighbours[x[0]] += 1
             neighbours[x[1]] += 1
+        self.model.E.neighbours = neighbours
         if self.file_gradients is not None:
+            # E.violations / E.updateCounts: device counters of the per-batch
+            # paths (zero under device_loop, whose runners do not count)
+            viol = self.model.E.violations
+            upd = self.model.E.updateCounts
             self.file_gradients.write("Entity,Degree,#(violations),#(updates)\n")
-            for index in range(n):   # violation / update counters are not tracked on device
-                self.file_gradients.write("%d,%d,%d,%d\n" % (index, neighbours[index], 0, 0))
+            for index in range(n):
+                self.file_gradients.write("%d,%d,%d,%d\n" % (index, neighbours[index],
+                                                              viol[index], upd[index]))
             self.file_gradients.flush()
         E = np.asarray(self.model.E, dtype=np.float64)
         if self.file_embeddings is not None:

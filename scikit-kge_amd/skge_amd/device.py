@@ -80,8 +80,8 @@ class EpochRunner(object):
             torch.cuda.empty_cache()
             extra = E.rows * E.width * 2 + E.rows * 12 + kg.T * 20 + (64 << 20)
             can_pipe = extra < torch.cuda.mem_get_info(dev)[0] * 0.9
-        self.te = updaters["E"].table(self.accE)
-        self.tr = updaters["R"].table(self.accR)
+        self.te = updaters["E"].table(self.accE, counters=False)
+        self.tr = updaters["R"].table(self.accR, counters=False)
         self.nbatches = nbatches
         torch.cuda.current_stream().synchronize()
         lib = L.lib()

@@ -144,12 +144,18 @@ class Parameter(object):
 
     ``.data`` is the fp32 torch tensor ([rows, d] or [M, d, d]); ``.name``,
     ``.post`` as in the reference.  ``np.asarray(param)`` copies to the host.
-    The reference's per-row Python counter lists are not kept.
+    The reference's per-row counters (param.py:84-86) are device int32 arrays,
+    read as host copies: ``updateCounts`` (AdaGrad applies, param.py:149-150)
+    and ``violations`` (TransE violating pairs, transe.py:78-83) are counted
+    by the kernels of the per-batch paths (not by the device-loop runners);
+    ``neighbours`` (entity degree) is filled by PairwiseStochasticTrainer.fit.
     """
 
     def __init__(self, shape, method="nunif", name=None, post=None, value=None, device=None):
         self.name = name
         self.post = post
+        self._counters = {}
+        self.neighbours = None
         dev = device if device is not None else _device()
         if value is None and method.startswith("device_"):
             # tables too large for a host NumPy draw (e.g. 50M x 512): the same
@@ -172,6 +178,29 @@ class Parameter(object):
             value = value.data
         self.data = torch.as_tensor(np.asarray(value) if not torch.is_tensor(value) else value,
                                     dtype=torch.float32, device=dev).contiguous()
+
+    def counter(self, name):
+        """Device int32 [rows] counter `name` ('upd' or 'viol'), allocated zeroed
+        on first use."""
+        c = self._counters.get(name)
+        if c is None:
+            c = torch.zeros(self.rows, dtype=torch.int32, device=self.data.device)
+            self._counters[name] = c
+        return c
+
+    def _counts(self, name):
+        c = self._counters.get(name)
+        if c is None:
+            return np.zeros(self.rows, dtype=np.int64)
+        return c.cpu().numpy().astype(np.int64)
+
+    @property
+    def updateCounts(self):
+        return self._counts("upd")
+
+    @property
+    def violations(self):
+        return self._counts("viol")
 
     # array-ish conveniences
     @property
@@ -219,7 +248,7 @@ def as_rows(g, device):
 
 
 def table_struct(param, state=None, acc=None, opt=L.SKGE_SGD, post=L.SKGE_POST_NONE, lr=0.0,
-                 rin=0.0, rout=0.0, fixed_div=0.0, gate=None):
+                 rin=0.0, rout=0.0, fixed_div=0.0, gate=None, upd_count=None, violations=None):
     t = L.SkgeTable()
     t.param = L.ptr(param.data)
     t.state = L.ptr(state)
@@ -234,6 +263,8 @@ def table_struct(param, state=None, acc=None, opt=L.SKGE_SGD, post=L.SKGE_POST_N
     t.opt, t.post, t.lr = opt, post, lr
     t.rin, t.rout, t.fixed_div = rin, rout, fixed_div
     t.gate = L.ptr(gate)
+    t.upd_count = L.ptr(upd_count)
+    t.violations = L.ptr(violations)
     return t
 
 
@@ -288,7 +319,11 @@ class ParameterUpdate(object):
     def state(self):
         return None
 
-    def table(self, acc=None, **kw):
+    def table(self, acc=None, counters=True, **kw):
+        """skge_table_t of this updater; counters=True lets the apply kernels
+        count AdaGrad row updates into param.updateCounts."""
+        if counters and self.opt == L.SKGE_ADAGRAD:
+            kw.setdefault("upd_count", self.param.counter("upd"))
         return table_struct(self.param, self.state(), acc, opt=self.opt,
                             post=post_code(self.param.post), lr=float(self.learning_rate), **kw)
 

@@ -32,14 +32,15 @@ def test_library_loads_and_exports_every_declared_symbol():
     missing = [f for f in fns if not hasattr(lib, f)]
     assert not missing, missing
     assert set(L.SIGNATURES) == set(fns)
-    assert lib.skge_abi_version() == 1
+    assert lib.skge_abi_version() == 2
 
 
 def test_table_struct_layout():
     from skge_amd import _lib as L
-    # 5 pointers, 7 ints, 4 floats, pad, 1 pointer (natural alignment) = 96 bytes
-    assert ctypes.sizeof(L.SkgeTable) == 96
+    # 5 pointers, 7 ints, 4 floats, pad, 3 pointers (natural alignment) = 112 bytes
+    assert ctypes.sizeof(L.SkgeTable) == 112
     assert L.SkgeTable.gate.offset == 88
+    assert L.SkgeTable.violations.offset == 104
 
 
 def test_errors_are_reported_without_a_gpu():
