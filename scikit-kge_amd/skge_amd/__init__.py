@@ -11,3 +11,4 @@ from .rescal import RESCAL
 from .param import Parameter, SGD, AdaGrad, normalize, normless1
 from .sample import RandomModeSampler
 from .eval import FilteredRankingEval, TransEEval, HolEEval, compute_scores, ranking_scores
+from .checkpoint import save_reference, load_reference, read_reference_state

@@ -45,6 +45,7 @@ class Model(object):
     of each table (see skge_table_t)."""
     model_code = None
     rel_id = "R"
+    default_posts = {}
 
     def __init__(self, *args, **kwargs):
         self.params = {}
@@ -76,11 +77,17 @@ class Model(object):
         self.params = {}
         self.hyperparams = {}
         self._acc = {}
-        posts = st.get("posts", {})
+        posts = st.get("posts", type(self).default_posts)
         for pid, p in st["params"].items():
             self.add_param(pid, None, posts.get(pid), value=p)
         for pid, p in st["hyperparams"].items():
             self.add_hyperparam(pid, p)
+
+    def save_reference(self, fname, updaters=None):
+        """Write the reference's model pickle (skge.<module>.<Class>, float64
+        params) -- readable by skge's Model.load; see checkpoint.py."""
+        from .checkpoint import save_reference
+        save_reference(self, fname, updaters=updaters)
 
     def save(self, fname, protocol=pickle.HIGHEST_PROTOCOL):
         with open(fname, "wb") as fout:

@@ -10,6 +10,7 @@ from .param import normless1
 
 
 class HolE(Model):
+    default_posts = {"E": normless1}   # posts restored when loading a reference file
     model_code = L.SKGE_HOLE
     rel_id = "R"
 

@@ -13,6 +13,7 @@ log = logging.getLogger("EX-KG")
 
 class TransE(Model):
     """Translational Embeddings of Knowledge Graphs (skge/transe.py:9-23)."""
+    default_posts = {"E": normalize}   # posts restored when loading a reference file
     rel_id = "R"
 
     def __init__(self, *args, **kwargs):

@@ -11,7 +11,7 @@ def case_names(prefix=""):
     out = []
     for p in sorted(glob.glob(os.path.join(GOLDEN, prefix + "*.npz"))):
         n = os.path.basename(p)[:-4]
-        if n != "init_quirks" and not n.startswith("eval_"):   # eval_*: test_oracle_eval.py
+        if n != "init_quirks" and not n.startswith(("eval_", "ckpt_")):   # own tests
             out.append(n)
     return out
 
