@@ -91,17 +91,24 @@ def algorithmic_bytes(d, B, P, U_E, U_R, opt_k=12):
     return 4 * d * (3 * B + P) + opt_k * d * (U_E + U_R) + 20 * B
 
 
-def cpu_baseline(trip, d, nb, seconds=12.0):
+def cpu_baseline(trip, d, nb, seconds=12.0, model="transe", margin=2.0):
     """The oracle (fp64 NumPy restatement, oracle/skge_oracle.py) on a bounded
     sample of the same workload: consecutive nb=100 batches of epoch 1,
     negatives from the reference-semantics host sampler (not timed)."""
     from oracle import skge_oracle as O
     rs = np.random.RandomState(42)
     np.random.seed(42)
-    bnd = np.sqrt(6) / np.sqrt(N_ENT + d)
-    E = O.normalize(rs.uniform(-bnd, bnd, size=(N_ENT, d)), None)
-    R = rs.uniform(-np.sqrt(6) / np.sqrt(N_REL + d), np.sqrt(6) / np.sqrt(N_REL + d), size=(N_REL, d))
-    params = {"E": E, "R": R}
+
+    def nunif(rows, cols):
+        bnd = np.sqrt(6) / np.sqrt(rows + cols)
+        return rs.uniform(-bnd, bnd, size=(rows, cols))
+
+    if model == "transe":
+        params = {"E": O.normalize(nunif(N_ENT, d), None), "R": nunif(N_REL, d)}
+    elif model == "hole":
+        params = {"E": O.normless1(nunif(N_ENT, d), None), "R": nunif(N_REL, d)}
+    else:
+        params = {"E": nunif(N_ENT, d), "W": np.array([nunif(d, d) for _ in range(N_REL)])}
     state = {k: np.zeros_like(v) for k, v in params.items()}
     tset = set(map(tuple, trip.tolist()))
     idx = np.arange(len(trip))
@@ -117,7 +124,7 @@ def cpu_baseline(trip, d, nb, seconds=12.0):
         pos = np.array([p for p, _ in pairs])
         neg = np.array([n for _, n in pairs])
         t1 = time.perf_counter()
-        O.pairwise_step("transe", params, state, pos, neg, 0.1, 2.0, "adagrad", l1=True)
+        O.pairwise_step(model, params, state, pos, neg, 0.1, margin, "adagrad", l1=True)
         t2 = time.perf_counter()
         t_step += t2 - t1
         t_all += t2 - t0
@@ -126,9 +133,11 @@ def cpu_baseline(trip, d, nb, seconds=12.0):
         if t_all > seconds:
             break
     return {"value": npos / t_step, "unit": "triples/s", "cores": 1, "kind": "port",
-            "sample": "%d nb=100 batches (%d positives) of epoch 1, WN18-shaped KG, TransE-L1 "
-                      "d=%d AdaGrad margin 2.0; oracle/skge_oracle.py fp64 NumPy, 1 thread; "
-                      "score+grad+update only (host sampler untimed)" % (nb_done, npos, d),
+            "sample": "%d nb=100 batches (%d positives) of epoch 1, WN18-shaped KG, %s "
+                      "d=%d AdaGrad margin %g; oracle/skge_oracle.py fp64 NumPy, 1 thread; "
+                      "score+grad+update only (host sampler untimed)"
+                      % (nb_done, npos, {"transe": "TransE-L1", "hole": "HolE",
+                                         "rescal": "RESCAL"}[model], d, margin),
             "e2e_value": npos / t_all}
 
 
@@ -146,14 +155,17 @@ def main():
     ap.add_argument("--reps", type=int, default=1, help="relation accumulator copies")
     ap.add_argument("--large-nb", type=int, default=2,
                     help="also time this nbatches (large-batch detail line); 0 = skip")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
-                    help="2: WN18 TransE d=200 (the headline); 5: synthetic |E|=50M |R|=10k "
-                         "d=512, B=131072 per GPU (BASELINE.json configs[4])")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
+                    help="2: WN18 TransE d=200 (the headline); 3: WN18 HolE d=200; 4: WN18 "
+                         "RESCAL d=200 (pairwise, device pair loop); 5: synthetic |E|=50M "
+                         "|R|=10k d=512, B=131072 per GPU (BASELINE.json configs[4])")
     ap.add_argument("--c5-scale", type=float, default=1.0,
                     help="config 5 only: scale |E| and T (quick rehearsals)")
     args = ap.parse_args()
     if args.config == 5:
         return run_config5(args)
+    if args.config in (3, 4):
+        return run_config34(args)
 
     import torch
     import torch.distributed as dist
@@ -441,6 +453,98 @@ def run_config5(args):
                                        "GB_s": round(v["achieved_gbs"], 1)}
                                    for n, v in prof["kernels"].items()},
                        "gpu_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)},
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+FP32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 matrix (MFMA) peak
+
+
+def model_flops(kind, d, P, V):
+    """Algorithmic FLOPs of one batch of P pairs with V violators:
+    HolE: 2 scoring correlations per pair + 6 gradient correlations per
+    violating pair, 2d^2 each (direct form); RESCAL: W E_o for the 4 triples of
+    a positive's 2 pairs, E_s W for the violators' entity gradients (computed
+    for all 4 by the GEMM) and the 4 dW outer products: 24 d^2 per positive."""
+    if kind == "hole":
+        return 2.0 * d * d * (2 * P + 6 * V)
+    return 24.0 * d * d * (P / 2.0)
+
+
+def run_config34(args):
+    """BASELINE.json configs[2] / configs[3]: HolE (Sigmoid, margin 0.2) or
+    RESCAL (Linear, margin 0.2) d=200, pairwise, AdaGrad lr 0.1, on the WN18
+    shape at nb=100 -- whole epochs on the device pair loop (device sampler +
+    explicit pairs + skge_pair_step per batch, one hipGraph per epoch)."""
+    import torch
+    import torch.distributed as dist
+    world, rank, local = dist_env()
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner, batch_sizes
+    kind = "hole" if args.config == 3 else "rescal"
+    d, nb, margin = args.d, args.nb, 0.2
+    trip = make_wn18_kg(seed=rank)
+    np.random.seed(42 + rank)
+    model = (S.HolE if kind == "hole" else S.RESCAL)((N_ENT, N_ENT, N_REL), d)
+    model.add_hyperparam("margin", margin)
+    upd = {pid: S.AdaGrad(p, 0.1) for pid, p in model.params.items()}
+    kg = DeviceKG(trip, dev)
+    runner = PairLoopRunner(model, upd, kg, nb, seed=1234 + rank)
+    init = {pid: p.data.clone() for pid, p in model.params.items()}
+    runner.run(args.warmup)
+    runner.synchronize()
+    for pid, p in model.params.items():
+        p.data.copy_(init[pid])
+        upd[pid].reset()
+    runner.nviol_total.zero_()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    runner.run(args.steps)
+    runner.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(elapsed, world, dev)
+    V = int(runner.nviol_total.item())
+    value = replica_value(N_TRIPLES * args.steps, world, elapsed)
+    P = 2 * N_TRIPLES * args.steps
+    flops = model_flops(kind, d, P, V)
+    tfs = flops / elapsed / 1e12 * world
+    if rank == 0:
+        cpu = None if args.no_cpu else cpu_baseline(trip, d, nb, args.cpu_seconds, kind, margin)
+        name = {"hole": "HolE", "rescal": "RESCAL"}[kind]
+        line = {
+            "metric": "triples/sec (score+grad+update), WN18 %s d=%d pairwise, 1 MI355X "
+                      "(BASELINE configs[%d])" % (name, d, args.config - 1),
+            "value": round(value, 1), "unit": "triples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442 uniform, "
+                    "RandomState(rank)); random-init params (nunif, seed 42)",
+            "config": {"workload": "%s d=%d PairwiseStochasticTrainer+AdaGrad, %s, margin %g, "
+                                   "lr 0.1, nb=%d (B=%d), device RandomModeSampler(1,[0,1]); "
+                                   "step = 1 epoch on the device pair loop"
+                                   % (name, d, "Sigmoid" if kind == "hole" else "Linear",
+                                      margin, nb, N_TRIPLES // nb),
+                       "global_batch": N_TRIPLES // nb, "parallelism": "replicas%d" % world},
+            "roofline": {"bound": "valu" if kind == "hole" else "mfma", "kernel": "whole step",
+                         "achieved": round(tfs, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": round(tfs / FP32_PEAK_TFS, 4), "traffic": None},
+            "cpu_baseline": cpu,
+            "detail": {"violations_per_pair": round(V / float(P), 4),
+                       "graph_nodes_per_step": runner.nlaunches,
+                       "batches": len(batch_sizes(N_TRIPLES, nb))},
         }
         print(json.dumps(line))
     if world > 1:

@@ -137,6 +137,11 @@ int skge_device_error(void *stream, int reset);
  * contribution rows into ent->acc_* / rel->acc_* (segment sum + counts).
  * coef (RESCAL only, [2P]): gp for every pair, then gn for every pair.
  * margin == -INFINITY: score only (nothing accumulated, no slots written).
+ * A pair whose positive has relation -1 is SKIPPED (no score, no violation,
+ * no contribution, coef 0; its negative is not read): the device pair loop
+ * (skge_pair_runner_*) marks so a positive whose sampler found no negative
+ * in ntries draws (skge/sample.py:41-46 drops that pair).  The same holds for
+ * skge_pair_step.
  */
 int skge_pair_grad(void *stream, int model, int af, const skge_table_t *ent,
                    const skge_table_t *rel, int d, const int *pos, const int *neg, int P,
@@ -268,6 +273,34 @@ skge_runner_t *skge_runner_create(void *stream, int l1, const skge_table_t *ent,
 int skge_runner_run(skge_runner_t *r, void *stream, int nepochs);
 int skge_runner_nlaunches(const skge_runner_t *r);
 void skge_runner_destroy(skge_runner_t *r);
+
+/*
+ * Device pair loop for any model (TransE L1/L2, HolE, RESCAL): one epoch of
+ * PairwiseStochasticTrainer with RandomModeSampler(1, [0, 1])
+ * (skge/base.py:1242-1291, 1394-1427; skge/sample.py:28-46) captured into a
+ * hipGraph: the epoch's permutation and negatives (the same keyed draws as
+ * the TransE runners), then per batch the explicit pairs (positive j ->
+ * pairs 2j: s-corrupted, 2j+1: o-corrupted; a negative not found in ntries
+ * draws -> a skipped pair) and one skge_pair_step.  ent needs 8 * batch_size
+ * touched slots, rel (if it records slots) 4 * batch_size.  *nviol_total
+ * accumulates the violations.  nlaunches reports the graph's node count.
+ */
+typedef struct skge_pair_runner skge_pair_runner_t;
+/* The epoch's draws as the pair loop (and the pipelined TransE runner) make
+ * them: rec [T][4] = (s, o, p, s' or -1), rec_n1 [T] = o' or -1, for
+ * position j of the epoch's order (tests / host-side replay). */
+int skge_epoch_sample(void *stream, const int *trip, int64_t T, const void *set,
+                      int64_t set_capacity, int n_ent, uint64_t seed, const uint64_t *epoch_key,
+                      int ntries, int *rec, int *rec_n1);
+skge_pair_runner_t *skge_pair_runner_create(void *stream, int model, int af,
+                                            const skge_table_t *ent, const skge_table_t *rel,
+                                            int d, const int *trip, int64_t T, const void *set,
+                                            int64_t set_capacity, int nbatches, uint64_t seed,
+                                            uint64_t *epoch_key, float margin, int ntries,
+                                            int *nviol_total);
+int skge_pair_runner_run(skge_pair_runner_t *r, void *stream, int nepochs);
+int skge_pair_runner_nlaunches(const skge_pair_runner_t *r);
+void skge_pair_runner_destroy(skge_pair_runner_t *r);
 
 /*
  * Pipelined epoch runner for TransE-L1 with packed accumulators (the

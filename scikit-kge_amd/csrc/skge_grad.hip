@@ -487,8 +487,13 @@ __global__ __launch_bounds__(256) void k_pair_grad(PairArgs a) {
   for (int i = blockIdx.x * wpb + wave; i < a.P; i += gridDim.x * wpb) {
     const int ix[6] = {uni(a.pos[3 * i]), uni(a.pos[3 * i + 1]), uni(a.pos[3 * i + 2]),
                        uni(a.neg[3 * i]), uni(a.neg[3 * i + 1]), uni(a.neg[3 * i + 2])};
-    bool v;
-    if (MODEL == TRANSE_L1)
+    bool v = false;
+    if (ix[2] < 0) {   // skipped pair (no negative drawn): no score, no contribution
+      if (a.coef && lane_id() == 0) {
+        a.coef[i] = 0.0f;
+        a.coef[a.P + i] = 0.0f;
+      }
+    } else if (MODEL == TRANSE_L1)
       v = transe_pair<KM, true>(a, i, ix);
     else if (MODEL == TRANSE_L2)
       v = transe_pair<KM, false>(a, i, ix);
@@ -517,7 +522,7 @@ __global__ __launch_bounds__(256) void k_hole_pair_fast(PairArgs a) {
   for (int i = blockIdx.x * wpb + wave; i < a.P; i += gridDim.x * wpb) {
     const int ix[6] = {uni(a.pos[3 * i]), uni(a.pos[3 * i + 1]), uni(a.pos[3 * i + 2]),
                        uni(a.neg[3 * i]), uni(a.neg[3 * i + 1]), uni(a.neg[3 * i + 2])};
-    const bool v = hole_pair_fast<KM>(a, i, sw, ix);
+    const bool v = ix[2] >= 0 && hole_pair_fast<KM>(a, i, sw, ix);   // p < 0: skipped pair
     if (a.record) commit_pair(a.accE, &a.accR, v, ix, i);
     nv += v ? 1 : 0;
   }

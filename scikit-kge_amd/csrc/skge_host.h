@@ -101,4 +101,20 @@ inline int check_slots(const skge_table_t* t, long long nslots, const char* name
   return SKGE_OK;
 }
 
+inline TripleSet triple_set_view(const void* set, int64_t capacity) {
+  TripleSet ts;
+  ts.slots = (const int4*)set;
+  ts.filter = (const uint32_t*)((const int4*)set + capacity);
+  ts.mask = (uint64_t)(capacity - 1);
+  ts.fmask = (uint64_t)(8 * capacity - 1);
+  return ts;
+}
+
+// skge_pipeline.hip: draw every negative of the epoch whose key is *epoch_key
+// (rec[j] = (s, o, p, s' or -1), rec_n1[j] = o' or -1 for positive j of the
+// epoch's order)
+int launch_epoch_sample(hipStream_t st, const int* trip, long long T, uint64_t seed,
+                        const uint64_t* epoch_key, TripleSet set, int n_ent, int ntries,
+                        int4* rec, int* rec_n1);
+
 }  // namespace skge

@@ -496,6 +496,17 @@ __global__ void k_epoch_sample(const int* __restrict__ trip, long long T, int ha
   }
 }
 
+int launch_epoch_sample(hipStream_t st, const int* trip, long long T, uint64_t seed,
+                        const uint64_t* epoch_key, TripleSet set, int n_ent, int ntries,
+                        int4* rec, int* rec_n1) {
+  long long blocks = (T + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_epoch_sample, dim3((unsigned)blocks), dim3(256), 0, st, trip, T,
+                     perm_half(T), seed, epoch_key, set, n_ent, ntries, rec, rec_n1);
+  SKGE_CHECK_LAUNCH("epoch sample");
+  return SKGE_OK;
+}
+
 }  // namespace skge
 
 using namespace skge;

@@ -404,6 +404,10 @@ __global__ __launch_bounds__(256) void k_rescal_scatter(const int* __restrict__ 
                        __builtin_amdgcn_readfirstlane(neg[3 * i]),
                        __builtin_amdgcn_readfirstlane(neg[3 * i + 1]),
                        __builtin_amdgcn_readfirstlane(neg[3 * i + 2])};
+    if (ix[2] < 0) {   // skipped pair: never bucketed (relation -1), no contribution
+      commit_pair(accE, nullptr, false, ix, i);
+      continue;
+    }
     const int ncb = (d + GC - 1) / GC;
     float praw = 0.0f, nraw = 0.0f;
     for (int q = 0; q < ncb; ++q) {   // fixed order: deterministic

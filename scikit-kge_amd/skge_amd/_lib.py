@@ -69,6 +69,12 @@ SIGNATURES = {
     "skge_runner_run": (c_i, [c_p, c_p, c_i]),
     "skge_runner_nlaunches": (c_i, [c_p]),
     "skge_runner_destroy": (None, [c_p]),
+    "skge_pair_runner_create": (c_p, [c_p, c_i, c_i, T_P, T_P, c_i, c_p, c_i64, c_p, c_i64, c_i,
+                                      c_u64, c_p, c_f, c_i, c_p]),
+    "skge_pair_runner_run": (c_i, [c_p, c_p, c_i]),
+    "skge_epoch_sample": (c_i, [c_p, c_p, c_i64, c_p, c_i64, c_i, c_u64, c_p, c_i, c_p, c_p]),
+    "skge_pair_runner_nlaunches": (c_i, [c_p]),
+    "skge_pair_runner_destroy": (None, [c_p]),
     "skge_pipe_runner_create": (c_p, [c_p, T_P, T_P, c_i, c_p, c_i64, c_p, c_i64, c_i, c_u64, c_p,
                                       c_f, c_i, c_p]),
     "skge_pipe_runner_run": (c_i, [c_p, c_p, c_i]),

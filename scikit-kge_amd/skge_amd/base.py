@@ -9,9 +9,9 @@ numeric step of a batch runs as HIP kernels through libskgehip.so:
 * ``fused=False``: the reference protocol step by step --
   ``model._pairwise_gradients`` returns ``{pid: (rows, sorted idx)}`` and the
   updaters are called by ``_batch_step`` (skge/base.py:1306-1316);
-* ``device_loop=True`` (TransE, PairwiseStochasticTrainer): the whole epoch
-  runs on the device -- permutation, negative sampling, score, scatter,
-  update -- captured once into a hipGraph by the native runner.
+* ``device_loop=True`` (PairwiseStochasticTrainer, every model): the whole
+  epoch runs on the device -- permutation, negative sampling, score,
+  scatter, update -- captured once into a hipGraph by a native runner.
 """
 import logging
 import pickle
@@ -354,11 +354,13 @@ class StochasticTrainer(object):
 class PairwiseStochasticTrainer(StochasticTrainer):
     """Stochastic gradient descent trainer with pairwise ranking loss
     (skge/base.py:1320-1427).  Extra kwargs: ``fused`` (default True),
-    ``device_loop`` (TransE only: device-resident epoch, see module doc),
-    ``seed`` (device sampler / permutation key)."""
+    ``device_loop`` (device-resident epochs, see module doc), ``device_runner``
+    ('auto', 'epoch': TransE's fused runners, 'pairs': the any-model pair
+    loop), ``seed`` (device sampler / permutation key), ``ntries``."""
 
     def __init__(self, *args, **kwargs):
         self.device_loop = kwargs.pop("device_loop", False)
+        self.device_runner = kwargs.pop("device_runner", "auto")
         self.seed = kwargs.pop("seed", 0)
         self.ntries = kwargs.pop("ntries", 100)
         super(PairwiseStochasticTrainer, self).__init__(*args, **kwargs)

@@ -1,8 +1,10 @@
-"""Device-resident training data and the native epoch runner.
+"""Device-resident training data and the native epoch runners.
 
 DeviceKG holds the training triples on the GPU ([T, 3] int32, (s, o, p)) and
 the open-addressing triple set the device sampler rejects against.
-EpochRunner wraps skge_runner_* (csrc/skge_epoch.hip): one epoch of
+EpochRunner wraps the TransE runners (skge_pipe_runner_* / skge_runner_*,
+csrc/skge_pipeline.hip, skge_epoch.hip) and PairLoopRunner the any-model pair
+loop (skge_pair_runner_*, csrc/skge_pairloop.hip): one epoch of
 PairwiseStochasticTrainer batches (nbatches full batches + the remainder,
 skge/base.py:1246-1268), captured once into a hipGraph and replayed."""
 import timeit
@@ -168,6 +170,95 @@ class EpochRunner(object):
             self.handle = None
 
 
+def batch_sizes(T, nbatches):
+    """Batch sizes of StochasticTrainer._optim's np.split (skge/base.py:1246-1268)."""
+    bs = T // nbatches
+    return [min(bs, T - s0) for s0 in range(0, T, bs)]
+
+
+class PairLoopRunner(object):
+    """Native hipGraph epoch of the device pair loop for any model
+    (skge_pair_runner_*, csrc/skge_pairloop.hip): the epoch's permutation and
+    negatives drawn on the device (the same keyed draws as EpochRunner), then
+    per batch the explicit pairs and one skge_pair_step -- the kernels of the
+    explicit-pair path, so a device epoch trains like feeding those pairs to
+    model._pairwise_step.  The per-row counters (updateCounts, TransE
+    violations) are kept as on that path."""
+
+    pipelined = False
+
+    def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, stream=None,
+                 nviol_total=None):
+        dev = model.device
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=dev)
+        self.kg = kg
+        self.model = model
+        self.nbatches = nbatches
+        self.epoch_key = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.nviol_total = nviol_total if nviol_total is not None else \
+            torch.zeros(1, dtype=torch.int32, device=dev)
+        P = 2 * max(batch_sizes(kg.T, nbatches))
+        self.te, self.tr = model._tables("pairwise", updaters, slots=model._pair_slots(P))
+        torch.cuda.current_stream().synchronize()
+        lib = L.lib()
+        h = lib.skge_pair_runner_create(
+            L.stream_ptr(self.stream), model._kernel_model(), model._af_code(), self.te, self.tr,
+            model.d, L.ptr(kg.trip), kg.T, L.ptr(kg.slots), kg.capacity, int(nbatches),
+            int(seed) & (2 ** 64 - 1), L.ptr(self.epoch_key), float(model.margin), int(ntries),
+            L.ptr(self.nviol_total))
+        if not h:
+            raise L.SkgeError("skge_pair_runner_create: %s" % lib.skge_last_error().decode())
+        self.handle = h
+        self.nlaunches = lib.skge_pair_runner_nlaunches(h)
+
+    def run(self, nepochs=1):
+        L.check(L.lib().skge_pair_runner_run(self.handle, L.stream_ptr(self.stream),
+                                             int(nepochs)), "pair runner run")
+
+    def synchronize(self):
+        self.stream.synchronize()
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                self.stream.synchronize()
+                L.lib().skge_pair_runner_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+def epoch_records(kg, n_ent, seed, epoch_key, ntries=100, stream=None):
+    """The epoch's positives and draws as the device loops make them:
+    (rec [T, 4] = (s, o, p, s' or -1), rec_n1 [T] = o' or -1) on the device."""
+    dev = kg.trip.device
+    rec = torch.empty((kg.T, 4), dtype=torch.int32, device=dev)
+    rec_n1 = torch.empty(kg.T, dtype=torch.int32, device=dev)
+    ek = torch.tensor([int(epoch_key)], dtype=torch.int64, device=dev)
+    L.check(L.lib().skge_epoch_sample(L.stream_ptr(stream), L.ptr(kg.trip), kg.T, L.ptr(kg.slots),
+                                      kg.capacity, int(n_ent), int(seed) & (2 ** 64 - 1),
+                                      L.ptr(ek), int(ntries), L.ptr(rec), L.ptr(rec_n1)),
+            "epoch sample")
+    return rec, rec_n1
+
+
+def make_runner(model, updaters, kg, nbatches, seed=0, ntries=100, nviol_total=None,
+                runner="auto"):
+    """runner: 'auto' (TransE -> EpochRunner, the fused sampler/score runners;
+    HolE / RESCAL -> PairLoopRunner), 'epoch' or 'pairs'."""
+    from .transe import TransE
+    if runner == "auto":
+        runner = "epoch" if isinstance(model, TransE) else "pairs"
+    if runner == "epoch":
+        return EpochRunner(model, updaters, kg, nbatches, seed=seed, ntries=ntries,
+                           nviol_total=nviol_total)
+    if runner == "pairs":
+        return PairLoopRunner(model, updaters, kg, nbatches, seed=seed, ntries=ntries,
+                              nviol_total=nviol_total)
+    raise ValueError("unknown device runner %r" % (runner,))
+
+
 def device_optim(trainer, xs):
     """PairwiseStochasticTrainer.fit with device_loop=True."""
     model = trainer.model
@@ -175,8 +266,9 @@ def device_optim(trainer, xs):
     if trainer._nviol_dev is None:
         trainer._nviol_dev = torch.zeros(1, dtype=torch.int32, device=dev)
     kg = DeviceKG(xs, dev)
-    runner = EpochRunner(model, trainer._updaters, kg, trainer.nbatches, seed=trainer.seed,
-                         ntries=trainer.ntries, nviol_total=trainer._nviol_dev)
+    runner = make_runner(model, trainer._updaters, kg, trainer.nbatches, seed=trainer.seed,
+                         ntries=trainer.ntries, nviol_total=trainer._nviol_dev,
+                         runner=trainer.device_runner)
     trainer._runner = runner
     with torch.cuda.stream(runner.stream):
         for trainer.epoch in range(1, trainer.max_epochs + 1):

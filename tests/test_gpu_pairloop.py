@@ -1,0 +1,182 @@
+"""Device pair loop (skge_pair_runner_*, GPU) for every model.
+
+The runner draws the epoch's permutation and negatives on the device; the
+same draws are exposed by skge_epoch_sample, so each test replays them on the
+host the way PairwiseStochasticTrainer._process_batch builds its pairs
+(skge/base.py:1394-1427: positive x, then its s-corrupted and o-corrupted
+negatives, a negative missing after ntries draws dropping that pair,
+skge/sample.py:41-46) and feeds them to model._pairwise_step on a twin model.
+SGD keeps the comparison linear: only float-atomic summation order differs,
+so |diff| <= 1e-5 + 1e-5 |want|; violation totals are compared exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ATOL = RTOL = 1e-5
+
+
+def make_kg(n_ent, n_rel, T, seed=0):
+    rs = np.random.RandomState(seed)
+    seen, out = set(), []
+    while len(out) < T:
+        t = (int(rs.randint(n_ent)), int(rs.randint(n_ent)), int(rs.randint(n_rel)))
+        if t not in seen:
+            seen.add(t)
+            out.append(t)
+    return out
+
+
+def make_model(kind, sz, d):
+    import skge_amd as S
+    np.random.seed(42)
+    if kind == "transe_l1":
+        return S.TransE(sz, d, l1=True)
+    if kind == "transe_l2":
+        return S.TransE(sz, d, l1=False)
+    if kind == "hole":
+        return S.HolE(sz, d, rparam=0.05)
+    return S.RESCAL(sz, d, rparam=0.05)
+
+
+def host_pairs(rec, n1, start, count):
+    pos, neg = [], []
+    for j in range(start, start + count):
+        s, o, p, a = (int(x) for x in rec[j])
+        b = int(n1[j])
+        if a >= 0:
+            pos.append((s, o, p))
+            neg.append((a, o, p))
+        if b >= 0:
+            pos.append((s, o, p))
+            neg.append((s, b, p))
+    return pos, neg
+
+
+def replay(model, upd, kg, n_ent, nbatches, epochs, seed, ntries):
+    from skge_amd.device import batch_sizes, epoch_records
+    dev = model.device
+    nv = torch.zeros(1, dtype=torch.int32, device=dev)
+    total = 0
+    for e in range(epochs):
+        rec, n1 = epoch_records(kg, n_ent, seed, e, ntries)
+        rec, n1 = rec.cpu().numpy(), n1.cpu().numpy()
+        start = 0
+        for c in batch_sizes(kg.T, nbatches):
+            pos, neg = host_pairs(rec, n1, start, c)
+            start += c
+            if not pos:
+                continue
+            nv.zero_()
+            model._pairwise_step(torch.tensor(pos, dtype=torch.int32, device=dev),
+                                 torch.tensor(neg, dtype=torch.int32, device=dev), upd, nv)
+            total += int(nv.item())
+    return total
+
+
+@pytest.mark.parametrize("kind,d,dense", [("transe_l1", 32, False), ("transe_l2", 24, False),
+                                          ("hole", 32, False), ("rescal", 16, False),
+                                          ("hole", 16, True), ("rescal", 8, True)])
+def test_pair_loop_matches_host_replay(kind, d, dense):
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    if dense:   # 70% of all triples: many negatives not found in 3 draws -> skipped pairs
+        n_ent, n_rel, T, ntries = 12, 2, 200, 3
+    else:
+        n_ent, n_rel, T, ntries = 300, 7, 2000, 100
+    xs = make_kg(n_ent, n_rel, T)
+    sz = (n_ent, n_ent, n_rel)
+    nb, epochs, seed, margin = 7, 2, 11, 0.5
+    a = make_model(kind, sz, d)
+    b = make_model(kind, sz, d)
+    for m in (a, b):
+        m.add_hyperparam("margin", margin)
+    upd_a = {pid: S.SGD(p, 0.05) for pid, p in a.params.items()}
+    upd_b = {pid: S.SGD(p, 0.05) for pid, p in b.params.items()}
+    kg = DeviceKG(xs, a.device)
+    r = PairLoopRunner(a, upd_a, kg, nb, seed=seed, ntries=ntries)
+    with torch.cuda.stream(r.stream):
+        r.run(epochs)
+    r.synchronize()
+    want_nv = replay(b, upd_b, kg, n_ent, nb, epochs, seed, ntries)
+    torch.cuda.synchronize()
+    assert int(r.nviol_total.item()) == want_nv
+    assert want_nv > 0
+    for pid in a.params:
+        np.testing.assert_allclose(a.params[pid].data.cpu().numpy(),
+                                   b.params[pid].data.cpu().numpy(), rtol=RTOL, atol=ATOL,
+                                   err_msg="%s %s" % (kind, pid))
+    for acc in a._acc.values():   # accumulators drained after every batch
+        assert int(acc.cnt.abs().sum().item()) == 0
+
+
+def test_dense_kg_skips_pairs():
+    """The dense case really exercises skipped pairs: some negatives are
+    missing (-1) in the draws the runner uses."""
+    from skge_amd.device import DeviceKG, epoch_records
+    xs = make_kg(12, 2, 200)
+    import skge_amd as S
+    m = make_model("hole", (12, 12, 2), 16)
+    kg = DeviceKG(xs, m.device)
+    rec, n1 = epoch_records(kg, 12, 11, 0, 3)
+    rec, n1 = rec.cpu().numpy(), n1.cpu().numpy()
+    assert (rec[:, 3] < 0).sum() > 0 and (n1 < 0).sum() > 0
+    assert (rec[:, 3] >= 0).sum() > 0
+    # accepted negatives are never training triples
+    known = set(xs)
+    for (s, o, p, a), b in zip(rec.tolist(), n1.tolist()):
+        assert a < 0 or (a, o, p) not in known
+        assert b < 0 or (s, b, p) not in known
+    assert sorted(map(tuple, rec[:, :3].tolist())) == sorted(xs)   # a permutation
+    del S
+
+
+def test_pair_loop_transe_agrees_with_epoch_runner():
+    """TransE-L1 through the pair loop and through the fused two-launch
+    runner (fp32 sums): same draws, same batches -> same parameters."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, EpochRunner, PairLoopRunner
+    n_ent, n_rel, T = 400, 9, 3000
+    xs = make_kg(n_ent, n_rel, T)
+    models = [make_model("transe_l1", (n_ent, n_ent, n_rel), 32) for _ in range(2)]
+    runners = []
+    for i, m in enumerate(models):
+        m.add_hyperparam("margin", 1.0)
+        upd = {pid: S.SGD(p, 0.05) for pid, p in m.params.items()}
+        kg = DeviceKG(xs, m.device)
+        if i == 0:
+            r = PairLoopRunner(m, upd, kg, 10, seed=3)
+        else:
+            r = EpochRunner(m, upd, kg, 10, seed=3, force_f32=True, pipelined=False)
+        with torch.cuda.stream(r.stream):
+            r.run(2)
+        r.synchronize()
+        runners.append(r)
+    assert int(runners[0].nviol_total.item()) == int(runners[1].nviol_total.item())
+    for pid in ("E", "R"):
+        np.testing.assert_allclose(models[0].params[pid].data.cpu().numpy(),
+                                   models[1].params[pid].data.cpu().numpy(), rtol=RTOL,
+                                   atol=ATOL, err_msg=pid)
+
+
+@pytest.mark.parametrize("kind", ["hole", "rescal"])
+def test_trainer_device_loop_any_model(kind):
+    """PairwiseStochasticTrainer(device_loop=True) trains HolE / RESCAL with
+    AdaGrad through the pair loop; callbacks see per-epoch violations."""
+    import skge_amd as S
+    n_ent, n_rel = 200, 5
+    xs = make_kg(n_ent, n_rel, 1500)
+    m = make_model(kind, (n_ent, n_ent, n_rel), 16)
+    E0 = m.E.data.clone()
+    seen = []
+    tr = S.PairwiseStochasticTrainer(m, nbatches=10, max_epochs=3, learning_rate=0.1,
+                                     margin=0.2, device_loop=True, file_grad=None,
+                                     file_embed=None,
+                                     post_epoch=[lambda t: seen.append(t.nviolations) or True])
+    tr.fit(xs, [1] * len(xs))
+    assert len(seen) == 3 and all(v > 0 for v in seen)
+    assert not torch.equal(E0, m.E.data)
+    assert np.isfinite(m.E.data.cpu().numpy()).all()
+    assert int(m.E.updateCounts.sum()) > 0
