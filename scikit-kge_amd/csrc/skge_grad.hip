@@ -250,7 +250,7 @@ __device__ __forceinline__ bool transe_pair(const PairArgs& a, int i, const int 
   acc_two<KM>(a.accE, sp, gp, sn, gn, d);
   acc_two<KM>(a.accE, op, ngp, on, ngn, d);
   // relation rows (pp, pn) -> (gp, gn)                      (transe.py:158-160)
-  acc_two<KM>(a.accR, pp, gp, pn, gn, d);
+  acc_two<KM>(replica(a.accR, i), pp, gp, pn, gn, d);
   return true;
 }
 
@@ -308,7 +308,7 @@ __device__ __forceinline__ bool hole_pair(const PairArgs& a, int i, float* sw, c
   // relation rows (pp, pn): (gp ccorr(E[sp],E[op]), gn ccorr(E[sn],E[on]))  hole.py:76-82
   scale<KM>(x, cp, gp);
   scale<KM>(y, cn, gn);
-  acc_two<KM>(a.accR, pp, x, pn, y, d);
+  acc_two<KM>(replica(a.accR, i), pp, x, pn, y, d);
   // entity rows (sp, sn): gp ccorr(R[pp],E[op]), gn ccorr(R[pn],E[on])   hole.py:93-94
   ccorr_lds<KM>(sRp, sEo, d, t);
   scale<KM>(x, t, gp);
@@ -383,19 +383,29 @@ __device__ __forceinline__ bool hole_pair_fast(const PairArgs& a, int i, float* 
   // relation rows (pp, pn): (gp ccorr(E[sp],E[op]), gn ccorr(E[sn],E[on]))  hole.py:76-82
   scale<KM>(x, cp, gp);
   scale<KM>(y, cn, gn);
-  acc_two<KM>(a.accR, pp, x, pn, y, d);
+#ifndef SKGE_ABL_HOLE_NO_RATOM   // timing-only ablation builds (tools/ablate.sh)
+  acc_two<KM>(replica(a.accR, i), pp, x, pn, y, d);
+#endif
+#ifndef SKGE_ABL_HOLE_NO_GCORR
   // entity rows (sp, sn): gp ccorr(R[pp],E[op]), gn ccorr(R[pn],E[on])   hole.py:93-94
   corr_fast<KM>(sRp, sEo, sout, d, t);
   scale<KM>(x, t, gp);
   corr_fast<KM>(sRn, sFo, sout, d, t);
   scale<KM>(y, t, gn);
+#endif
+#ifndef SKGE_ABL_HOLE_NO_EATOM
   acc_two<KM>(a.accE, sp, x, sn, y, d);
+#endif
+#ifndef SKGE_ABL_HOLE_NO_GCORR
   // entity rows (op, on): gp cconv(E[sp],R[pp]), gn cconv(E[sn],R[pn])    hole.py:95-96
   corr_fast<KM>(rEs, sRp, sout, d, t);
   scale<KM>(x, t, gp);
   corr_fast<KM>(rFs, sRn, sout, d, t);
   scale<KM>(y, t, gn);
+#endif
+#ifndef SKGE_ABL_HOLE_NO_EATOM
   acc_two<KM>(a.accE, op, x, on, y, d);
+#endif
   __builtin_amdgcn_wave_barrier();
   return true;
 }
@@ -501,7 +511,8 @@ __global__ __launch_bounds__(256) void k_pair_grad(PairArgs a) {
       v = hole_pair<KM>(a, i, sw, ix);
     else
       v = rescal_pair<KM>(a, i, sw, ix);
-    if (a.record) commit_pair(a.accE, MODEL == RESCAL ? nullptr : &a.accR, v, ix, i);
+    const Accum aR = replica(a.accR, i);   // dense relation tables may spread over copies
+    if (a.record) commit_pair(a.accE, MODEL == RESCAL ? nullptr : &aR, v, ix, i);
     if ((MODEL == TRANSE_L1 || MODEL == TRANSE_L2) && a.eviol && v)
       count_entity_violation(a.eviol, ix);
     nv += v ? 1 : 0;
@@ -523,7 +534,8 @@ __global__ __launch_bounds__(256) void k_hole_pair_fast(PairArgs a) {
     const int ix[6] = {uni(a.pos[3 * i]), uni(a.pos[3 * i + 1]), uni(a.pos[3 * i + 2]),
                        uni(a.neg[3 * i]), uni(a.neg[3 * i + 1]), uni(a.neg[3 * i + 2])};
     const bool v = ix[2] >= 0 && hole_pair_fast<KM>(a, i, sw, ix);   // p < 0: skipped pair
-    if (a.record) commit_pair(a.accE, &a.accR, v, ix, i);
+    const Accum aR = replica(a.accR, i);
+    if (a.record) commit_pair(a.accE, &aR, v, ix, i);
     nv += v ? 1 : 0;
   }
   __shared__ int lds_nv;
@@ -579,8 +591,8 @@ __global__ __launch_bounds__(256) void k_triple_grad(PairArgs a) {
       score = wave_sum(acc);
       logistic(y, score, &li, &fs);
       scale<KM>(x, c, fs);  // R: fs ccorr(E[s],E[o])   hole.py:32
-      acc_row<KM>(a.accR, p, x, d);
-      if (lane_id() == 2) commit_slot(a.accR, p, 1, i);
+      acc_row<KM>(replica(a.accR, i), p, x, d);
+      if (lane_id() == 2) commit_slot(replica(a.accR, i), p, 1, i);
       corr_fast<KM>(fRp2, fEo2, fout, d, t);  // E[s]: fs ccorr(R[p],E[o])
       scale<KM>(x, t, fs);
       corr_fast<KM>(fEsr, fRp2, fout, d, t);  // E[o]: fs cconv(E[s],R[p])
@@ -601,8 +613,8 @@ __global__ __launch_bounds__(256) void k_triple_grad(PairArgs a) {
       score = wave_sum(acc);
       logistic(y, score, &li, &fs);
       scale<KM>(x, c, fs);  // R: fs ccorr(E[s],E[o])   hole.py:32
-      acc_row<KM>(a.accR, p, x, d);
-      if (lane_id() == 2) commit_slot(a.accR, p, 1, i);
+      acc_row<KM>(replica(a.accR, i), p, x, d);
+      if (lane_id() == 2) commit_slot(replica(a.accR, i), p, 1, i);
       ccorr_lds<KM>(sRp, sEo, d, t);  // E[s]: fs ccorr(R[p],E[o])   hole.py:37
       scale<KM>(x, t, fs);
       cconv_lds<KM>(sEs, sRp, d, t);  // E[o]: fs cconv(E[s],R[p])   hole.py:38
@@ -787,7 +799,11 @@ static int check_model_tables(int model, const skge_table_t* ent, const skge_tab
   if ((rc = check_table(ent, "ent", true)) != SKGE_OK) return rc;
   if ((rc = check_table(rel, "rel", model != SKGE_RESCAL)) != SKGE_OK) return rc;
   if ((rc = check_f32(ent, "ent")) || (rc = check_f32(rel, "rel"))) return rc;
-  if ((rc = check_single(ent, "ent")) || (rc = check_single(rel, "rel"))) return rc;
+  // a dense TransE / HolE relation table may hold several accumulator copies
+  // (contributions of pair i go to copy i mod replicas; the apply folds them)
+  if ((rc = check_single(ent, "ent")) ||
+      (model == SKGE_RESCAL && (rc = check_single(rel, "rel"))))
+    return rc;
   SKGE_CHECK_ARG(model >= 0 && model <= 3, "unknown model %d", model);
   SKGE_CHECK_ARG(d > 0 && ent->width == d, "entity width %d != d %d", ent->width, d);
   if (model == SKGE_RESCAL)

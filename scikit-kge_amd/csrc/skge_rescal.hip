@@ -20,8 +20,9 @@
 //   k_rescal_scatter  one wave per pair: activation, strict margin test, the
 //                     entity contributions (gp WE_p, gn WE_n over s; gp EW_p,
 //                     gn EW_n over o) into the entity accumulator, coef
-//   k_rescal_wgrad_mfma  one workgroup per (relation, 16-row strip, 64-col
-//                     group): dW[p] tiles written with plain stores
+//   k_rescal_wgrad_mfma  one workgroup per (relation, 64x64 tile of dW[p]):
+//                     the tile is applied to W[p] in place by its owner (the
+//                     W updater) or written with plain stores
 // Scores, WE, EW and dW have fixed summation orders (stable buckets, fixed
 // MFMA k order, fixed cross-wave reduction order), so the relation gradient
 // is bitwise reproducible; the entity sums use float atomics, as elsewhere.
@@ -33,7 +34,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int RT_ITEMS = 64;    // triples per GEMM tile
 constexpr int GC = 64;          // output columns per GEMM tile
-constexpr int KS = 16;          // k per staged step
+#ifndef SKGE_RS_KS
+#define SKGE_RS_KS 32
+#endif
+constexpr int KS = SKGE_RS_KS;  // k per staged step
 constexpr int RS_MAX_D = 1024;  // d of the MFMA path
 constexpr int RS_MAX_M = 8192;  // relations (k_rs_scan keeps 2M+1 ints in LDS)
 
@@ -120,7 +124,16 @@ __global__ __launch_bounds__(256) void k_rs_count(const int* __restrict__ pos,
   if (c >= nchunks) return;
   const int k = c * 64 + l;
   const int b = k < n ? item_trip(pos, neg, P, k)[2] : -1;
-  uint64_t act = __ballot(b >= 0);
+  if (M <= 64) {   // lane p owns relation p: the whole row is written, no memset
+    int mine = 0;
+    for (int p = 0; p < M; ++p) {
+      const int cp = __popcll(__ballot(b == p));
+      if (l == p) mine = cp;
+    }
+    if (l < M) ws.chunk[(size_t)c * M + l] = mine;
+    return;
+  }
+  uint64_t act = __ballot(b >= 0);   // the table was zeroed by a memset
   while (act) {
     const int leader = __ffsll((unsigned long long)act) - 1;
     const int bl = __builtin_amdgcn_readlane(b, leader);
@@ -210,18 +223,126 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const int* __restrict__ pos,
   }
 }
 
+// Small batches (n <= SB_MAXN triples, M <= SB_MAXM relations): the same
+// stable bucketing in ONE workgroup -- totals, scans and tile list, then the
+// items in rounds of 1024 (wave-ordered ranks through LDS), so the batch
+// pays one launch instead of a memset and three.
+constexpr int SB_MAXM = 256;
+constexpr int SB_ITEMS = 1;              // items per thread, held in registers
+constexpr int SB_MAXN = 1024 * SB_ITEMS;
+
+__global__ __launch_bounds__(1024) void k_rs_bucket_small(const int* __restrict__ pos,
+                                                          const int* __restrict__ neg, int P,
+                                                          int n, int M, RescalWs ws) {
+  __shared__ int cw[16][SB_MAXM];   // per-wave counts of the current round
+  __shared__ int cnt[SB_MAXM];      // relation totals
+  __shared__ int base[SB_MAXM];     // next free position of each relation
+  __shared__ int tbase[SB_MAXM + 1];
+  const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
+  // every item of the batch is loaded once, up front (one memory round trip)
+  int rs[SB_ITEMS], ss[SB_ITEMS], os[SB_ITEMS];
+#pragma unroll
+  for (int u = 0; u < SB_ITEMS; ++u) {
+    const int k = u * 1024 + tid;
+    const int* tr = item_trip(pos, neg, P, k < n ? k : 0);
+    ss[u] = tr[0];
+    os[u] = tr[1];
+    rs[u] = k < n ? tr[2] : -1;
+  }
+  for (int i = tid; i < M; i += blockDim.x) cnt[i] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < SB_ITEMS; ++u) {   // totals
+    const int r = rs[u];
+    uint64_t act = __ballot(r >= 0);
+    while (act) {
+      const int leader = __ffsll((unsigned long long)act) - 1;
+      const int rl = __builtin_amdgcn_readlane(r, leader);
+      const uint64_t m = __ballot(r == rl) & act;
+      if (l == leader) atomicAdd(&cnt[rl], __popcll(m));
+      act &= ~m;
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {   // relation offsets and tile bases (exclusive scans over p)
+    int off = 0, toff = 0;
+    for (int p0 = 0; p0 < M; p0 += 64) {
+      const int p = p0 + l;
+      const int v = p < M ? cnt[p] : 0, tv = (v + RT_ITEMS - 1) / RT_ITEMS;
+      const int inc = wave_incl_scan(v), tinc = wave_incl_scan(tv);
+      if (p < M) {
+        ws.rel_off[p] = off + inc - v;
+        base[p] = off + inc - v;
+        tbase[p] = toff + tinc - tv;
+      }
+      off += __shfl(inc, 63, 64);
+      toff += __shfl(tinc, 63, 64);
+    }
+    if (l == 0) {
+      ws.rel_off[M] = off;
+      tbase[M] = toff;
+      *ws.ntiles = toff;
+    }
+  }
+  __syncthreads();
+  for (int t = tid; t < tbase[M]; t += blockDim.x) {   // tile t: relation p, tbase[p] <= t
+    int lo = 0, hi = M - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tbase[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    const int st = (t - tbase[lo]) * RT_ITEMS;
+    ws.tile_rel[t] = lo;
+    ws.tile_start[t] = base[lo] + st;
+    ws.tile_cnt[t] = min(RT_ITEMS, cnt[lo] - st);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < SB_ITEMS; ++u) {   // stable scatter, one round of 1024 items
+    if (u * 1024 >= n) break;
+    for (int i = tid; i < 16 * M; i += blockDim.x) cw[i / M][i % M] = 0;
+    __syncthreads();
+    const int k = u * 1024 + tid;
+    const int ts = ss[u], to = os[u], r = rs[u];
+    int rank = 0;
+    uint64_t act = __ballot(r >= 0);
+    while (act) {
+      const int leader = __ffsll((unsigned long long)act) - 1;
+      const int rl = __builtin_amdgcn_readlane(r, leader);
+      const uint64_t m = __ballot(r == rl) & act;
+      if (r == rl) rank = __popcll(m & ((1ull << l) - 1ull));
+      if (l == leader) cw[wave][rl] = __popcll(m);
+      act &= ~m;
+    }
+    __syncthreads();
+    if (r >= 0) {
+      int at = base[r] + rank;
+      for (int w2 = 0; w2 < wave; ++w2) at += cw[w2][r];
+      ws.items[at] = k;
+      ws.sorted_s[at] = ts;
+      ws.sorted_o[at] = to;
+      ws.bpos[k] = at;
+    }
+    __syncthreads();
+    for (int p = tid; p < M; p += blockDim.x) {
+      int add = 0;
+      for (int w2 = 0; w2 < 16; ++w2) add += cw[w2][p];
+      base[p] += add;
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Relation-grouped GEMMs, one workgroup per (64-triple tile, 64-column block,
 // product):  WE^T[i][r] = sum_k Eo[i][k] W[r][k]   (product 0)
 //            EW[i][j]   = sum_k Es[i][k] W[k][j]   (product 1)
-// K advances 16 at a time through double-buffered LDS tiles (A: 64 triples x
-// 16, B: 16 x 64 columns), the next step's global loads in flight while the
-// current step's MFMAs run.  Wave w owns triples 16w..16w+15 and four 16x16
+// K advances 64 at a time through double-buffered LDS tiles (A: 64 triples x
+// 64, B: 64 x 64 columns), the next step's global loads in flight while the
+// current step's 64 MFMAs per wave run.  Wave w owns triples 16w..16w+15 and four 16x16
 // accumulators (independent chains hide the MFMA latency).  Product-0 blocks
 // also write each triple's partial score E[s_i] . WE_i over their 64 columns.
 // ---------------------------------------------------------------------------
-constexpr int PF = 6;   // k-steps of global loads kept in flight (registers)
-
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E,
                                                      const float* __restrict__ W, int d,
@@ -247,117 +368,110 @@ __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E
   __syncthreads();
   const float* Wp = W + (size_t)p * d * d;
   const int nk = (d + KS - 1) / KS;
-  // staging map: thread -> one float4 of A and one float4 of B per k-step
-  const int ai = tid >> 2, ak = (tid & 3) * 4;            // A[ai][ak..ak+3]
+  // staging map, 16 consecutive floats of A and of B per thread and k-step:
+  //   A[ai][ak..ak+15] = E[row ai][k + ak ..]
+  //   product 0: B[k + bk ..][bq] = W[c0 + bq][k + bk ..]   (transposed into LDS)
+  //   product 1: B[bq][bk ..]     = W[k + bq][c0 + bk ..]
+  constexpr int SPT = KS / 4;   // floats per thread and operand per k-step
+  const int ai = tid >> 2, ak = (tid & 3) * SPT;
   const float* arow = E + (size_t)s_row[ai] * d;
   const bool a_ok = ai < cnt;
-  // B for product 0: W[c0 + bi][k..k+3] (stored transposed); product 1: W[k + bk][c0 + bj..+3]
-  const int bi = tid >> 2, bk = (tid & 3) * 4;            // product 0
-  const int bkr = tid >> 4, bj = (tid & 15) * 4;          // product 1
-  auto load_step = [&](int ks, float4& av, float4& bv) {
+  // product 0: thread -> W row c0 + bq, k offsets bk..; product 1: W row
+  // k + bq, columns c0 + bk.. (256 / KS threads share a row of 64 columns)
+  const int bq = prod == 0 ? tid >> 2 : tid / (256 / KS);
+  const int bk = prod == 0 ? (tid & 3) * SPT : (tid % (256 / KS)) * SPT;
+  float ra[SPT], rb[SPT];
+  // raw loads from clamped in-range addresses; masks are applied when the
+  // values are staged (a select right after a load would wait for it)
+  auto load_step = [&](int ks) {
     const int k = ks * KS;
-#ifdef SKGE_RS_ABL_NOLOADW   // timing-only ablation builds (tools/ablate.sh)
-    av = make_float4(k, k, k, k);
-    bv = av;
-    return;
-#endif
-    if (VEC) {   // d % 4 == 0: every 4-float group is inside or outside together
-      const int kk = k + ak;
-      const float4 x = *reinterpret_cast<const float4*>(arow + (kk < d ? kk : 0));
-      av = (a_ok && kk < d) ? x : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      if (prod == 0) {
-        const int r = c0 + bi, kb2 = k + bk;
-        const float4 y = *reinterpret_cast<const float4*>(
-            Wp + (size_t)(r < d ? r : 0) * d + (kb2 < d ? kb2 : 0));
-        bv = (r < d && kb2 < d) ? y : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      } else {
-        const int kr = k + bkr, j = c0 + bj;
-        const float4 y = *reinterpret_cast<const float4*>(
-            Wp + (size_t)(kr < d ? kr : 0) * d + (j < d ? j : 0));
-        bv = (kr < d && j < d) ? y : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      }
-      return;
-    }
-    {
-      float v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int kk = k + ak + u;
-        const float x = arow[kk < d ? kk : 0];
-        v[u] = (a_ok && kk < d) ? x : 0.0f;
-      }
-      av = make_float4(v[0], v[1], v[2], v[3]);
-    }
-    float v[4];
+    const float* brow;
+    int boff;
     if (prod == 0) {
-      const int r = c0 + bi, rc = r < d ? r : 0;
+      brow = Wp + (size_t)(c0 + bq < d ? c0 + bq : 0) * d;
+      boff = k + bk;
+    } else {
+      brow = Wp + (size_t)(k + bq < d ? k + bq : 0) * d;
+      boff = c0 + bk;
+    }
+    if (VEC) {   // d % 4 == 0: each 4-float group is inside or outside together
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int kk = k + bk + u;
-        const float x = Wp[(size_t)rc * d + (kk < d ? kk : 0)];
-        v[u] = (r < d && kk < d) ? x : 0.0f;
+      for (int m = 0; m < SPT / 4; ++m) {
+        const int ka = k + ak + 4 * m, kb = boff + 4 * m;
+        const float4 x = *reinterpret_cast<const float4*>(arow + (ka < d ? ka : 0));
+        const float4 y = *reinterpret_cast<const float4*>(brow + (kb < d ? kb : 0));
+        ra[4 * m] = x.x, ra[4 * m + 1] = x.y, ra[4 * m + 2] = x.z, ra[4 * m + 3] = x.w;
+        rb[4 * m] = y.x, rb[4 * m + 1] = y.y, rb[4 * m + 2] = y.z, rb[4 * m + 3] = y.w;
       }
     } else {
-      const int kk = k + bkr, kc = kk < d ? kk : 0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = c0 + bj + u;
-        const float x = Wp[(size_t)kc * d + (j < d ? j : 0)];
-        v[u] = (kk < d && j < d) ? x : 0.0f;
+      for (int e = 0; e < SPT; ++e) {
+        const int ka = k + ak + e, kb = boff + e;
+        ra[e] = arow[ka < d ? ka : 0];
+        rb[e] = brow[kb < d ? kb : 0];
       }
     }
-    bv = make_float4(v[0], v[1], v[2], v[3]);
   };
-  auto store_step = [&](int buf, const float4& av, const float4& bv) {
-    *reinterpret_cast<float4*>(&sA[buf][ai][ak]) = av;
+  auto store_step = [&](int buf, int ks) {
+    const int k = ks * KS;
+#pragma unroll
+    for (int m = 0; m < SPT / 4; ++m) {
+      float4 v;
+      v.x = (a_ok && k + ak + 4 * m + 0 < d) ? ra[4 * m + 0] : 0.0f;
+      v.y = (a_ok && k + ak + 4 * m + 1 < d) ? ra[4 * m + 1] : 0.0f;
+      v.z = (a_ok && k + ak + 4 * m + 2 < d) ? ra[4 * m + 2] : 0.0f;
+      v.w = (a_ok && k + ak + 4 * m + 3 < d) ? ra[4 * m + 3] : 0.0f;
+      *reinterpret_cast<float4*>(&sA[buf][ai][ak + 4 * m]) = v;
+    }
     if (prod == 0) {   // B[k][r] = W[r][k]
-      sB[buf][bk + 0][bi] = bv.x;
-      sB[buf][bk + 1][bi] = bv.y;
-      sB[buf][bk + 2][bi] = bv.z;
-      sB[buf][bk + 3][bi] = bv.w;
+      const bool rok = c0 + bq < d;
+#pragma unroll
+      for (int e = 0; e < SPT; ++e) sB[buf][bk + e][bq] = (rok && k + bk + e < d) ? rb[e] : 0.0f;
     } else {
-      *reinterpret_cast<float4*>(&sB[buf][bkr][bj]) = bv;
+      const bool kok = k + bq < d;
+#pragma unroll
+      for (int m = 0; m < SPT / 4; ++m) {
+        float4 v;
+        v.x = (kok && c0 + bk + 4 * m + 0 < d) ? rb[4 * m + 0] : 0.0f;
+        v.y = (kok && c0 + bk + 4 * m + 1 < d) ? rb[4 * m + 1] : 0.0f;
+        v.z = (kok && c0 + bk + 4 * m + 2 < d) ? rb[4 * m + 2] : 0.0f;
+        v.w = (kok && c0 + bk + 4 * m + 3 < d) ? rb[4 * m + 3] : 0.0f;
+        *reinterpret_cast<float4*>(&sB[buf][bq][bk + 4 * m]) = v;
+      }
     }
   };
   f32x4 acc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-  // PF steps of loads in flight: regs[u] holds step ks0 + u until it is staged
-  float4 ra[PF], rb[PF];
-#pragma unroll
-  for (int u = 0; u < PF; ++u)
-    if (u < nk) load_step(u, ra[u], rb[u]);
   const int row = wave * 16 + (l & 15), kq = l >> 4;
-  for (int ks0 = 0; ks0 < nk; ks0 += PF) {
+  load_step(0);
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    store_step(buf, ks);
+    __syncthreads();   // (also: every wave is done with buf's previous use, step ks - 2)
+    if (ks + 1 < nk) load_step(ks + 1);   // in flight during this step's MFMAs
 #pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      const int ks = ks0 + u;
-      if (ks >= nk) break;
-      const int buf = ks & 1;
-      store_step(buf, ra[u], rb[u]);
-      __syncthreads();
-      if (ks + PF < nk) load_step(ks + PF, ra[u], rb[u]);
-#ifndef SKGE_RS_ABL_NOMFMA
+    for (int k4 = 0; k4 < KS; k4 += 4) {
+      const float a = sA[buf][row][k4 + kq];
 #pragma unroll
-      for (int k4 = 0; k4 < KS; k4 += 4) {
-        const float a = sA[buf][row][k4 + kq];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, sB[buf][k4 + kq][q * 16 + (l & 15)],
-                                                        acc[q], 0, 0, 0);
-      }
-#else
-      acc[0][0] += sA[buf][row][kq] + sB[buf][kq][l & 15];
-#endif
+      for (int q = 0; q < 4; ++q)
+        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, sB[buf][k4 + kq][q * 16 + (l & 15)],
+                                                      acc[q], 0, 0, 0);
     }
   }
   // epilogue: D[row 4g + reg][col] of accumulator q -> triple 16w + 4g + reg, column c0 + 16q + c
-#ifdef SKGE_RS_ABL_NOEPI
-  if (acc[0][0] == 12345.0f) ws.WE[0] = acc[1][1] + acc[2][2] + acc[3][3];
-  return;
-#endif
   float* out = prod == 0 ? ws.WE : ws.EW;
   const int g = l >> 4, c = l & 15;
+  float ev[4][4];
+  if (prod == 0) {   // E[s_i] over the block's columns, all loads issued together
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int col = c0 + q * 16 + c;
+        ev[q][reg] = E[(size_t)s_es[wave * 16 + 4 * g + reg] * d + (col < d ? col : 0)];
+      }
+  }
   float ps[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -366,10 +480,7 @@ __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E
     for (int reg = 0; reg < 4; ++reg) {
       const int it = wave * 16 + 4 * g + reg;
       if (it < cnt && col < d) out[(size_t)s_gid[it] * d + col] = acc[q][reg];
-      if (prod == 0) {
-        const float e = E[(size_t)s_es[it] * d + (col < d ? col : 0)];
-        ps[reg] += (col < d) ? acc[q][reg] * e : 0.0f;
-      }
+      if (prod == 0) ps[reg] += (col < d) ? acc[q][reg] * ev[q][reg] : 0.0f;
     }
   }
   if (prod == 0) {
@@ -498,76 +609,166 @@ __global__ __launch_bounds__(256) void k_rescal_logistic(const int* __restrict__
 // dW[p] = sum_items coef_i E[s_i] (x) E[o_i]: one workgroup per (relation,
 // 16-row strip, 4 x 16-column tiles); K = the relation's triples in bucket order
 // ---------------------------------------------------------------------------
-constexpr int WG_CHUNK = 128;
+// the W updater, applied by the workgroup that owns each dW tile (APPLY):
+// the same g = (sum + rin W)/div + rout W, AdaGrad / SGD step as k_apply_wide
+// (skge/param.py:115-155), with sum = the tile's dW straight from registers
+struct WApply {
+  float* W;
+  float* A;          // AdaGrad state or nullptr
+  int opt;
+  float lr, rin, rout, fdiv;
+  const int* gate;   // skip the update when *gate == 0 (no violations)
+  int* ucnt;         // optional updateCounts
+};
 
+// dW[p] = sum_i coef_i E[s_i]^T E[o_i] over relation p's items.  One
+// workgroup per (relation, 64-row tile, 64-col tile); wave w owns rows
+// 16w..16w+15 and all 64 columns (four 16x16 accumulators); items are staged
+// 64 at a time (coef-scaled E[s] and E[o] row segments, one memory round
+// trip per chunk) and contracted with v_mfma_f32_16x16x4_f32.
+constexpr int WG_T = 64;    // rows / columns of a dW tile
+constexpr int WG_CH = 64;   // items staged per step
+constexpr int WG_TPI = 256 / WG_CH;       // threads per item
+constexpr int WG_FPT = WG_T / WG_TPI;     // row floats per thread and operand
+
+template <bool APPLY, bool VEC>
 __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restrict__ E, int d,
-                                                           RescalWs ws, Accum accW) {
-  const int dp = (d + 15) & ~15, ntd = dp / 16, ngrp = (ntd + 3) / 4;
+                                                           RescalWs ws, Accum accW, WApply wa) {
+  const int nt = (d + WG_T - 1) / WG_T;
   const int blk = blockIdx.x;
-  const int p = blk / (ntd * ngrp);
-  const int rem = blk - p * ntd * ngrp;
-  const int rt = rem / ngrp, cg = rem - (rem / ngrp) * ngrp;
+  const int p = blk / (nt * nt);
+  const int rem = blk - p * nt * nt;
+  const int rt = rem / nt, ct = rem - (rem / nt) * nt;
   const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
   const int off = ws.rel_off[p], cnt = ws.rel_off[p + 1] - off;
-  if (rem == 0 && tid == 0) {   // slot p (skge_hip.h slot map)
+  if (!APPLY && rem == 0 && tid == 0) {   // slot p (skge_hip.h slot map)
     if (accW.touched) accW.touched[p] = cnt > 0 ? p : -1;
     accW.cnt[p] = cnt;
   }
   if (cnt == 0) return;
-  __shared__ float sEs[WG_CHUNK][16];
-  __shared__ float sEo[WG_CHUNK][64 + 4];
-  __shared__ int s_s[WG_CHUNK], s_o[WG_CHUNK];
-  __shared__ float s_c[WG_CHUNK];
-  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-  const int r0 = rt * 16, c0 = cg * 64;
-  for (int b0 = 0; b0 < cnt; b0 += WG_CHUNK) {
-    const int m = min(WG_CHUNK, cnt - b0);
-    if (tid < WG_CHUNK) {
-      const int at = off + b0 + (tid < m ? tid : 0);
-      s_s[tid] = ws.sorted_s[at];
-      s_o[tid] = ws.sorted_o[at];
-      s_c[tid] = tid < m ? ws.coef[at] : 0.0f;
+  const bool upd = !APPLY || wa.gate == nullptr || *wa.gate != 0;
+  if (APPLY && !upd) return;   // the model returned None: no update
+  if (APPLY && rem == 0 && tid == 0 && wa.opt == OPT_ADAGRAD && wa.ucnt)
+    wa.ucnt[p] += 1;   // updateCounts, skge/param.py:149-150
+  __shared__ float sEs[2][WG_CH][WG_T + 4];
+  __shared__ float sEo[2][WG_CH][WG_T + 4];
+  const int r0 = rt * WG_T, c0 = ct * WG_T;
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  // thread -> item it of a chunk, WG_FPT columns from h of its
+  // E[s] segment (rows r0..) and E[o] segment (columns c0..).  Software
+  // pipeline: chunk b+1's rows are in flight during chunk b's MFMAs and chunk
+  // b+2's item ids behind them.
+  const int it = tid / WG_TPI, h = (tid % WG_TPI) * WG_FPT;
+  int nxt_s = 0, nxt_o = 0;
+  float nxt_c = 0.0f;
+  auto load_idx = [&](int b0) {
+    const int i = b0 + it;
+    const int at = off + (i < cnt ? i : cnt - 1);
+    nxt_s = ws.sorted_s[at];
+    nxt_o = ws.sorted_o[at];
+    nxt_c = i < cnt ? ws.coef[at] : 0.0f;
+  };
+  float4 es[WG_FPT / 4], eo[WG_FPT / 4];
+  float cur_c = 0.0f;
+  auto load_rows = [&]() {   // raw loads from clamped in-range addresses
+    const float* srow = E + (size_t)nxt_s * d;
+    const float* orow = E + (size_t)nxt_o * d;
+#pragma unroll
+    for (int m = 0; m < WG_FPT / 4; ++m) {
+      const int cs = r0 + h + 4 * m, co = c0 + h + 4 * m;
+      if (VEC) {
+        es[m] = *reinterpret_cast<const float4*>(srow + (cs < d ? cs : 0));
+        eo[m] = *reinterpret_cast<const float4*>(orow + (co < d ? co : 0));
+      } else {
+        es[m] = make_float4(srow[cs < d ? cs : 0], srow[cs + 1 < d ? cs + 1 : 0],
+                            srow[cs + 2 < d ? cs + 2 : 0], srow[cs + 3 < d ? cs + 3 : 0]);
+        eo[m] = make_float4(orow[co < d ? co : 0], orow[co + 1 < d ? co + 1 : 0],
+                            orow[co + 2 < d ? co + 2 : 0], orow[co + 3 < d ? co + 3 : 0]);
+      }
     }
-    __syncthreads();
-    {   // every gather of this thread issued before the LDS stores wait on them
-      float vs[WG_CHUNK * 16 / 256], vo[WG_CHUNK * 64 / 256];
+    cur_c = nxt_c;
+  };
+  const int nch = (cnt + WG_CH - 1) / WG_CH;
+  load_idx(0);
+  load_rows();
+  if (nch > 1) load_idx(WG_CH);
+  for (int b = 0; b < nch; ++b) {
+    const int buf = b & 1;
 #pragma unroll
-      for (int u = 0; u < WG_CHUNK * 16 / 256; ++u) {
-        const int q = tid + u * 256, i = q >> 4, cc = q & 15;
-        vs[u] = E[(size_t)s_s[i] * d + (r0 + cc < d ? r0 + cc : 0)];
-      }
-#pragma unroll
-      for (int u = 0; u < WG_CHUNK * 64 / 256; ++u) {
-        const int q = tid + u * 256, i = q >> 6, cc = q & 63;
-        vo[u] = E[(size_t)s_o[i] * d + (c0 + cc < d ? c0 + cc : 0)];
-      }
-#pragma unroll
-      for (int u = 0; u < WG_CHUNK * 16 / 256; ++u) {
-        const int q = tid + u * 256, i = q >> 4, cc = q & 15;
-        sEs[i][cc] = (i < m && r0 + cc < d) ? s_c[i] * vs[u] : 0.0f;
-      }
-#pragma unroll
-      for (int u = 0; u < WG_CHUNK * 64 / 256; ++u) {
-        const int q = tid + u * 256, i = q >> 6, cc = q & 63;
-        sEo[i][cc] = (i < m && c0 + cc < d) ? vo[u] : 0.0f;
-      }
+    for (int m = 0; m < WG_FPT / 4; ++m) {   // coef-scaled E[s], E[o]; zero past d
+      const int cs = r0 + h + 4 * m, co = c0 + h + 4 * m;
+      float4 a = es[m], o = eo[m];
+      a.x = cs + 0 < d ? cur_c * a.x : 0.0f;
+      a.y = cs + 1 < d ? cur_c * a.y : 0.0f;
+      a.z = cs + 2 < d ? cur_c * a.z : 0.0f;
+      a.w = cs + 3 < d ? cur_c * a.w : 0.0f;
+      o.x = co + 0 < d ? o.x : 0.0f;
+      o.y = co + 1 < d ? o.y : 0.0f;
+      o.z = co + 2 < d ? o.z : 0.0f;
+      o.w = co + 3 < d ? o.w : 0.0f;
+      *reinterpret_cast<float4*>(&sEs[buf][it][h + 4 * m]) = a;
+      *reinterpret_cast<float4*>(&sEo[buf][it][h + 4 * m]) = o;
     }
-    __syncthreads();
-    // A[row r][k = item] = coef Es[item][r], B[k = item][col] = Eo[item][col]
+    __syncthreads();   // (also: every wave is done with buf's use two chunks ago)
+    if (b + 1 < nch) {
+      load_rows();                                        // chunk b+1
+      if (b + 2 < nch) load_idx((b + 2) * WG_CH);         // chunk b+2's ids
+    }
+    const int m = min(WG_CH, cnt - b * WG_CH);   // items past m are zero (coef 0)
+    // A[row i][k = item] = coef Es[item][i], B[k = item][col j] = Eo[item][j]
     for (int k0 = 0; k0 < m; k0 += 4) {
-      const int it = k0 + (l >> 4);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(sEs[it][l & 15], sEo[it][wave * 16 + (l & 15)],
-                                                  acc, 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  const int ct = cg * 4 + wave;
-  if (ct >= ntd) return;
-  float* out = accW.sum + (size_t)p * d * d;
+      const int ik = k0 + (l >> 4);
+      const float a = sEs[buf][ik][16 * wave + (l & 15)];
 #pragma unroll
-  for (int reg = 0; reg < 4; ++reg) {   // D[row 4g + reg][col]
-    const int r = r0 + 4 * (l >> 4) + reg, cc = ct * 16 + (l & 15);
-    if (r < d && cc < d) out[(size_t)r * d + cc] = acc[reg];
+      for (int j = 0; j < 4; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, sEo[buf][ik][16 * j + (l & 15)], acc[j],
+                                                      0, 0, 0);
+    }
+  }
+  // D[row 4g + reg][col] of accumulator j; out-of-range elements read a
+  // clamped in-range address and are not stored
+  size_t os[16];
+  bool in[16];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int r = r0 + 16 * wave + 4 * (l >> 4) + reg, cc = c0 + 16 * j + (l & 15);
+      in[4 * j + reg] = r < d && cc < d;
+      os[4 * j + reg] = (size_t)p * d * d + (size_t)(r < d ? r : 0) * d + (cc < d ? cc : 0);
+    }
+  if (!APPLY) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      if (in[e]) accW.sum[os[e]] = acc[e >> 2][e & 3];
+    return;
+  }
+  // same step as k_apply_wide (skge/param.py:115-155); every load of the
+  // tile issued before any of it is used
+  const float div = wa.fdiv > 0.0f ? wa.fdiv : (float)cnt;
+  const bool ada = wa.opt == OPT_ADAGRAD;
+  float pv[16], av[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    pv[e] = wa.W[os[e]];
+    av[e] = ada ? wa.A[os[e]] : 0.0f;
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const float g = (acc[e >> 2][e & 3] + wa.rin * pv[e]) / div + wa.rout * pv[e];
+    float w;
+    if (ada) {
+      av[e] = av[e] + g * g;
+      w = pv[e] - (wa.lr * g) / fmaxf(sqrtf(av[e]), 1e-7f);
+    } else {
+      w = pv[e] - wa.lr * g;
+    }
+    if (in[e]) {
+      wa.W[os[e]] = w;
+      if (ada) wa.A[os[e]] = av[e];
+    }
   }
 }
 
@@ -588,13 +789,18 @@ bool skge_rescal_mfma_ok(int d, int M) {
 static int rescal_front(hipStream_t st, const skge_table_t* ent, const skge_table_t* rel, int d,
                         const int* a, int na, const int* b, int n, const RescalWs& ws) {
   const int M = rel->rows;
-  const int nchunks = (n + 63) / 64;
-  SKGE_CHECK_HIP(hipMemsetAsync(ws.chunk, 0, (size_t)nchunks * M * sizeof(int), st));
-  const int cblocks = (nchunks + 3) / 4;
-  hipLaunchKernelGGL(k_rs_count, dim3(cblocks), dim3(256), 0, st, a, b, na, n, M, ws);
-  hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(1024), (size_t)(2 * M + 1) * sizeof(int), st, n, M,
-                     ws);
-  hipLaunchKernelGGL(k_rs_scatter, dim3(cblocks), dim3(256), 0, st, a, b, na, n, M, ws);
+  if (M <= SB_MAXM && n <= SB_MAXN) {
+    hipLaunchKernelGGL(k_rs_bucket_small, dim3(1), dim3(1024), 0, st, a, b, na, n, M, ws);
+  } else {
+    const int nchunks = (n + 63) / 64;
+    if (M > 64)   // (k_rs_count writes whole rows itself for M <= 64)
+      SKGE_CHECK_HIP(hipMemsetAsync(ws.chunk, 0, (size_t)nchunks * M * sizeof(int), st));
+    const int cblocks = (nchunks + 3) / 4;
+    hipLaunchKernelGGL(k_rs_count, dim3(cblocks), dim3(256), 0, st, a, b, na, n, M, ws);
+    hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(1024), (size_t)(2 * M + 1) * sizeof(int), st, n,
+                       M, ws);
+    hipLaunchKernelGGL(k_rs_scatter, dim3(cblocks), dim3(256), 0, st, a, b, na, n, M, ws);
+  }
   const int ncb = (d + GC - 1) / GC;
   const dim3 ggrid((unsigned)(rs_tmax(n, M) * 2 * ncb));
   if ((d & 3) == 0)
@@ -607,11 +813,39 @@ static int rescal_front(hipStream_t st, const skge_table_t* ent, const skge_tabl
   return SKGE_OK;
 }
 
+// dW per relation; apply_gate != nullptr: also the W update of rel's updater
+// (fused apply, gated on *apply_gate unless it points at a constant 1 --
+// pass rel->gate semantics through `gate`)
 static void rescal_wgrad_launch(hipStream_t st, const skge_table_t* ent,
-                                const skge_table_t* rel, int d, const RescalWs& ws) {
-  const int dp = (d + 15) & ~15, ntd = dp / 16, ngrp = (ntd + 3) / 4;
-  hipLaunchKernelGGL(k_rescal_wgrad_mfma, dim3((unsigned)((long long)rel->rows * ntd * ngrp)),
-                     dim3(256), 0, st, ent->param, d, ws, accum_of(rel));
+                                const skge_table_t* rel, int d, const RescalWs& ws, bool apply,
+                                const int* gate) {
+  const int nt = (d + WG_T - 1) / WG_T;
+  const dim3 grid((unsigned)((long long)rel->rows * nt * nt));
+  WApply wa = {};
+  if (apply) {
+    wa.W = rel->param;
+    wa.A = rel->state;
+    wa.opt = rel->opt;
+    wa.lr = rel->lr;
+    wa.rin = rel->rin;
+    wa.rout = rel->rout;
+    wa.fdiv = rel->fixed_div;
+    wa.gate = gate;
+    wa.ucnt = rel->upd_count;
+    if ((d & 3) == 0)
+      hipLaunchKernelGGL((k_rescal_wgrad_mfma<true, true>), grid, dim3(256), 0, st, ent->param, d,
+                         ws, accum_of(rel), wa);
+    else
+      hipLaunchKernelGGL((k_rescal_wgrad_mfma<true, false>), grid, dim3(256), 0, st, ent->param,
+                         d, ws, accum_of(rel), wa);
+  } else {
+    if ((d & 3) == 0)
+      hipLaunchKernelGGL((k_rescal_wgrad_mfma<false, true>), grid, dim3(256), 0, st, ent->param,
+                         d, ws, accum_of(rel), wa);
+    else
+      hipLaunchKernelGGL((k_rescal_wgrad_mfma<false, false>), grid, dim3(256), 0, st, ent->param,
+                         d, ws, accum_of(rel), wa);
+  }
 }
 
 #define SKGE_KM_SWITCH(KERNEL, ...)                                             \
@@ -629,18 +863,19 @@ static void rescal_wgrad_launch(hipStream_t st, const skge_table_t* ent,
 int skge_rescal_pair_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
                                const skge_table_t* rel, int d, const int* pos, const int* neg,
                                int P, float margin, void* workspace, size_t ws_bytes,
-                               float* pscore, float* nscore, int* nviol) {
+                               float* pscore, float* nscore, int* nviol, bool apply_w) {
   RescalWs ws;
   const size_t need = rescal_ws_layout(2 * P, rel->rows, d, workspace, &ws);
   SKGE_CHECK_ARG(workspace && ws_bytes >= need, "RESCAL workspace needs %zu bytes", need);
-  SKGE_CHECK_ARG(rel->acc_sum && rel->acc_cnt, "W accumulator missing");
+  SKGE_CHECK_ARG(apply_w || (rel->acc_sum && rel->acc_cnt), "W accumulator missing");
+  SKGE_CHECK_ARG(!apply_w || nviol, "the fused W update is gated on nviol");
   int rc = rescal_front(st, ent, rel, d, pos, P, neg, 2 * P, ws);
   if (rc) return rc;
   const int blocks = std::max(1, std::min((P + 3) / 4, 16384));
   const Accum aE = accum_of(ent);
   SKGE_KM_SWITCH(k_rescal_scatter, dim3(blocks), dim3(256), 0, st, pos, neg, P, d, af, margin, ws,
                  aE, pscore, nscore, nviol)
-  rescal_wgrad_launch(st, ent, rel, d, ws);
+  rescal_wgrad_launch(st, ent, rel, d, ws, apply_w, nviol);
   SKGE_CHECK_LAUNCH("rescal mfma pair grad");
   return SKGE_OK;
 }
@@ -649,18 +884,18 @@ int skge_rescal_pair_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
 int skge_rescal_triple_grad_mfma(hipStream_t st, const skge_table_t* ent,
                                  const skge_table_t* rel, int d, const int* trip,
                                  const float* ys, int T, void* workspace, size_t ws_bytes,
-                                 float* score, float* loss) {
+                                 float* score, float* loss, bool apply_w) {
   RescalWs ws;
   const size_t need = rescal_ws_layout(T, rel->rows, d, workspace, &ws);
   SKGE_CHECK_ARG(workspace && ws_bytes >= need, "RESCAL workspace needs %zu bytes", need);
-  SKGE_CHECK_ARG(rel->acc_sum && rel->acc_cnt, "W accumulator missing");
+  SKGE_CHECK_ARG(apply_w || (rel->acc_sum && rel->acc_cnt), "W accumulator missing");
   int rc = rescal_front(st, ent, rel, d, trip, T, trip, T, ws);
   if (rc) return rc;
   const int blocks = std::max(1, std::min((T + 3) / 4, 16384));
   const Accum aE = accum_of(ent);
   SKGE_KM_SWITCH(k_rescal_logistic, dim3(blocks), dim3(256), 0, st, trip, ys, T, d, ws, aE, score,
                  loss)
-  rescal_wgrad_launch(st, ent, rel, d, ws);
+  rescal_wgrad_launch(st, ent, rel, d, ws, apply_w, rel->gate);
   SKGE_CHECK_LAUNCH("rescal mfma triple grad");
   return SKGE_OK;
 }

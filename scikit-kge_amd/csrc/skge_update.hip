@@ -269,41 +269,48 @@ __device__ __forceinline__ void apply_row_rep_block(const TableDev& t, int row, 
                                                     int* lds) {
   const int tid = threadIdx.x, R = t.acc.replicas, rows = t.rows, w = t.width;
   const int dw = acc_row_dwords(MODE, w);             // accumulator dwords per row
-  for (int i = tid; i <= dw; i += blockDim.x) lds[i] = 0;   // lds[dw]: the count
-  __syncthreads();
-  for (int k = tid; k < R; k += blockDim.x) {
-    int* cp = t.acc.cnt + (size_t)k * rows + row;
-    const int c = *cp;
-    if (c) {
-      atomicAdd(lds + dw, c);
-      *cp = 0;
-    }
+  // fold the copies: each thread owns one accumulator word (or the count) and
+  // loads it from every copy with the loads in flight together, summing in
+  // copy order (fixed order: deterministic), then clears the copies
+  if (tid < 64) {   // counts: lane k holds copy k (R <= 32), one wave sum
+    int v = 0;
+    int* cp = t.acc.cnt + (size_t)tid * rows + row;
+    if (tid < R) v = *cp;
+    if (v) *cp = 0;
+    v = wave_sum_int(v);
+    if (tid == 0) lds[dw] = v;
   }
-  if (MODE == ACC_I16X4) {   // fold qwords: packed sums are linear under integer adds
-    const int nq = w >> 2, total = R * nq;
+  if (MODE == ACC_I16X4) {   // qwords: packed sums are linear under integer adds
+    const int nq = w >> 2;
     unsigned long long* l64 = reinterpret_cast<unsigned long long*>(lds);
-#pragma unroll 4
-    for (int f = tid; f < total; f += blockDim.x) {
-      const int k = f / nq, q = f - k * nq;
-      unsigned long long* sp =
-          reinterpret_cast<unsigned long long*>(t.acc.sum) + ((size_t)k * rows + row) * nq + q;
-      const unsigned long long v = *sp;
-      if (v) {
-        atomicAdd(l64 + q, v);
-        *sp = 0ull;
+    for (int q = tid; q < nq; q += blockDim.x) {
+      unsigned long long* sp = reinterpret_cast<unsigned long long*>(t.acc.sum) + (size_t)row * nq + q;
+      const size_t stride = (size_t)rows * nq;
+      unsigned long long v[32];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) v[k] = k < R ? sp[k * stride] : 0ull;
+      unsigned long long acc = 0ull;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        acc += v[k];
+        if (k < R && v[k]) sp[k * stride] = 0ull;
       }
+      l64[q] = acc;
     }
   } else {
-    const int total = R * dw;
-#pragma unroll 4
-    for (int f = tid; f < total; f += blockDim.x) {
-      const int k = f / dw, q = f - k * dw;
-      float* sp = t.acc.sum + ((size_t)k * rows + row) * dw + q;
-      const float v = *sp;
-      if (v != 0.0f) {
-        atomicAdd(reinterpret_cast<float*>(lds) + q, v);
-        *sp = 0.0f;
+    for (int q = tid; q < dw; q += blockDim.x) {
+      float* sp = t.acc.sum + (size_t)row * dw + q;
+      const size_t stride = (size_t)rows * dw;
+      float v[32];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) v[k] = k < R ? sp[k * stride] : 0.0f;
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        acc += v[k];
+        if (k < R && v[k] != 0.0f) sp[k * stride] = 0.0f;
       }
+      reinterpret_cast<float*>(lds)[q] = acc;
     }
   }
   __syncthreads();
@@ -593,6 +600,32 @@ __global__ __launch_bounds__(256) void k_gather_mean_wide(TableDev t, const int*
 }
 
 // zero the counts of the listed rows
+// fold the copies of a replicated fp32 accumulator into copy 0 (collect path)
+__global__ __launch_bounds__(256) void k_fold_replicas(float* __restrict__ sum,
+                                                       int* __restrict__ cnt, int reps, int rows,
+                                                       int width) {
+  const long long n = (long long)rows * width;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (long long)gridDim.x * blockDim.x) {
+    float v = sum[e];
+    for (int k = 1; k < reps; ++k) {
+      float* q = sum + (size_t)k * n + e;
+      v += *q;
+      *q = 0.0f;
+    }
+    sum[e] = v;
+    if (e < rows) {
+      int c = cnt[e];
+      for (int k = 1; k < reps; ++k) {
+        int* q = cnt + (size_t)k * rows + e;
+        c += *q;
+        *q = 0;
+      }
+      cnt[e] = c;
+    }
+  }
+}
+
 __global__ void k_zero_counts(int* __restrict__ cnt, const int* __restrict__ idx,
                               const int* __restrict__ Up) {
   const int U = *Up;
@@ -647,6 +680,12 @@ extern "C" int skge_accum_collect(void* stream, const skge_table_t* t, int* idx_
   int* bsum = (int*)workspace;
   int* boff = bsum + nb;
   TableDev td = table_dev(t);
+  if (t->acc_replicas > 1) {   // one copy first (the fold order is fixed: copy 0, 1, ...)
+    hipLaunchKernelGGL(k_fold_replicas, dim3(grid_for_elems((long long)t->rows * t->width)),
+                       dim3(256), 0, st, t->acc_sum, t->acc_cnt, t->acc_replicas, t->rows,
+                       t->width);
+    td.acc.replicas = 1;
+  }
   hipLaunchKernelGGL(k_count_nz, dim3(nb), dim3(256), 0, st, t->acc_cnt, t->rows, bsum);
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(256), 0, st, bsum, nb, boff, U_out);
   hipLaunchKernelGGL(k_compact, dim3(nb), dim3(256), 0, st, t->acc_cnt, t->rows, boff, idx_out);
@@ -828,12 +867,12 @@ size_t skge_rescal_mfma_ws_bytes(int n, int M, int d);
 int skge_rescal_triple_grad_mfma(hipStream_t st, const skge_table_t* ent,
                                  const skge_table_t* rel, int d, const int* trip,
                                  const float* ys, int T, void* workspace, size_t ws_bytes,
-                                 float* score, float* loss);
+                                 float* score, float* loss, bool apply_w);
 bool skge_rescal_mfma_ok(int d, int M);
 int skge_rescal_pair_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
                                const skge_table_t* rel, int d, const int* pos, const int* neg,
                                int P, float margin, void* workspace, size_t ws_bytes,
-                               float* pscore, float* nscore, int* nviol);
+                               float* pscore, float* nscore, int* nviol, bool apply_w);
 
 // SKGE_RESCAL_VALU=1 forces the per-pair GEMV path (A/B comparisons)
 static bool rescal_use_mfma(int d, int M) {
@@ -877,8 +916,16 @@ extern "C" int skge_pair_step(void* stream, int model, int af, const skge_table_
       SKGE_CHECK_ARG(af >= 0 && af <= 3, "unknown activation %d", af);
       if ((rc = check_slots(ent, 4ll * P, "ent")) || (rc = check_slots(rel, rel->rows, "W")))
         return rc;
+      SKGE_CHECK_ARG(rel->opt == SKGE_SGD || rel->state, "AdaGrad needs state");
+      // W is updated inside the dW kernel (its owner workgroup per tile):
+      // only the entity table is left for skge_accum_apply
       rc = skge_rescal_pair_grad_mfma(as_stream(stream), af, ent, rel, d, pos, neg, P, margin,
-                                      workspace, ws_bytes, nullptr, nullptr, nviol);
+                                      workspace, ws_bytes, nullptr, nullptr, nviol, true);
+      if (rc) return rc;
+      skge_table_t te = *ent;
+      te.gate = nviol;
+      const int ns = 4 * P;
+      return skge_accum_apply(stream, &te, 1, &ns);
     } else {
       float* coef = (float*)workspace;
       rc = skge_pair_grad(stream, model, af, ent, rel, d, pos, neg, P, margin, nullptr, nullptr,
@@ -920,8 +967,12 @@ extern "C" int skge_triple_step(void* stream, int model, const skge_table_t* ent
       SKGE_CHECK_ARG(ent->width == d && rel->width == d * d, "RESCAL table widths");
       if ((rc = check_slots(ent, 2ll * T, "ent")) || (rc = check_slots(rel, rel->rows, "W")))
         return rc;
+      SKGE_CHECK_ARG(rel->opt == SKGE_SGD || rel->state, "AdaGrad needs state");
       rc = skge_rescal_triple_grad_mfma(as_stream(stream), ent, rel, d, trip, ys, T, workspace,
-                                        ws_bytes, nullptr, loss);
+                                        ws_bytes, nullptr, loss, true);   // W updated in place
+      if (rc) return rc;
+      const int ns = 2 * T;
+      return skge_accum_apply(stream, ent, 1, &ns);
     } else {
       float* coef = (float*)workspace;
       rc = skge_triple_grad(stream, model, ent, rel, d, trip, ys, T, nullptr, coef, loss);

@@ -108,10 +108,19 @@ class Model(object):
         return int(self.ncomp)
 
     def accumulator(self, pid):
+        """The device accumulator of table pid.  A narrow relation table is
+        dense (no slot records; its apply is one wave or workgroup per row):
+        each of its few rows is hit by most pairs of a batch, and per-slot
+        claims -- or atomics -- on the same rows would serialise."""
         acc = self._acc.get(pid)
         if acc is None:
             p = self.params[pid]
-            acc = Accumulator(p.rows, p.width, p.data.device)
+            dense = pid == "R" and p.width <= 1024 and p.rows <= 65536   # not RESCAL W
+            # and spread over copies when rows are very few (pair i adds into
+            # copy i mod replicas; the apply / collect fold them)
+            reps = 16 if p.rows <= 256 else (4 if p.rows <= 4096 else 1)
+            acc = Accumulator(p.rows, p.width, p.data.device, dense=dense,
+                              replicas=reps if dense else 1)
             self._acc[pid] = acc
         return acc
 
