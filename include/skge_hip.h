@@ -345,6 +345,52 @@ int skge_pipe_runner_profile(skge_pipe_runner_t *r, void *stream, float *us_out,
                              int n, int trace_launch, uint64_t *trace_out, int64_t trace_len);
 void skge_pipe_runner_destroy(skge_pipe_runner_t *r);
 
+/* ---------------- row-sharded TransE-L1 step ----------------
+ *
+ * The entity table split by row over G ranks (rank g owns rows r % G == g at
+ * local index r / G), the relation table replicated.  One mini-batch of
+ * PairwiseStochasticTrainer (skge/base.py:1394-1427, TransE._pairwise_gradients
+ * skge/transe.py:48-165, AdaGrad + normalize skge/param.py:140-167) over the
+ * union of every rank's positives is, on each rank:
+ *   skge_shard_route   -> exchange request ids (all-to-all) ->
+ *   skge_shard_gather  -> exchange rows back (all-to-all) ->
+ *   skge_shard_score   -> exchange contributions (all-to-all) ->
+ *   skge_shard_accum   -> all-reduce the relation sums and counts ->
+ *   skge_accum_apply({entity shard: nslots = requests received}, {rel: dense}).
+ * The exchanges belong to the caller (RCCL via torch.distributed).  All sums
+ * are exact integers, so the result equals one GPU's step on the union batch
+ * bit for bit.  Positives come from skge_epoch_sample records (rec, rec_n1).
+ */
+
+/* Bucket the requests (s, o, s', o') of positives [start, start+count) by
+ * owner: send_ids [4*count] (owner-major, request order within a bucket),
+ * req_pos [4*count] = slot of request 4j+k in send_ids (-1: skipped negative),
+ * counts [G] int64 = bucket sizes.  G <= 64. */
+size_t skge_shard_route_workspace_bytes(int count, int G);
+int skge_shard_route(void *stream, const int *rec, const int *rec_n1, int64_t start, int count,
+                     int G, int *send_ids, int *req_pos, long long *counts, void *workspace,
+                     size_t ws_bytes);
+/* Owner side: rows_out[i] = E_shard[ids[i] / G] for i < n ([n][d] fp32). */
+int skge_shard_gather(void *stream, const float *E_shard, int d, int G, const int *ids, int64_t n,
+                      float *rows_out);
+/* Contribution record of one request: int32 count, pad to 16 B, int8[d]. */
+long long skge_shard_contrib_stride(int d);
+/* Requester side: score both pairs of every positive from the fetched rows
+ * (fetched[req_pos[4j+k]]) and rel (dense packed accumulator, replicated
+ * table), apply the strict margin test, write one contribution record per
+ * request into contrib [n_send][stride] and add the relation contributions
+ * into rel's accumulator; violations into the 64 sharded counters vshards
+ * (64 x 32 ints, folded by skge_shard_fold_violations). */
+int skge_shard_score(void *stream, const skge_table_t *rel, int d, const int *rec,
+                     const int *rec_n1, int64_t start, int count, const float *fetched,
+                     const int *req_pos, float margin, void *contrib, int *vshards);
+/* Owner side: add the n received records into ent_shard's packed sums (local
+ * row ids[i] / G), touched slot i per record; touched_cap >= n. */
+int skge_shard_accum(void *stream, const skge_table_t *ent_shard, int G, const int *ids,
+                     const void *contrib, int64_t n);
+/* *nviol_total += the violation shards, which are cleared. */
+int skge_shard_fold_violations(void *stream, int *vshards, int *nviol_total);
+
 /* ---------------- evaluation ---------------- */
 
 /*

@@ -1,0 +1,178 @@
+"""Row-sharded TransE-L1 step on the GPU (skge_amd.shard, csrc/skge_shard.hip).
+
+* the HIP routing equals the NumPy layout of tests/shard_numpy.py exactly;
+* one rank (G = 1): the sharded runner trains, bit for bit, like the
+  two-launch device runner (same epoch draws, exact packed sums, same apply);
+* one sharded batch against the oracle replaying its recorded pairs (1e-5);
+* two ranks on one GPU over gloo: the assembled entity table after a batch is
+  the oracle's union-batch step (1e-5) and the relation replicas agree bit
+  for bit.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle import skge_oracle as O
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("G,count,start", [(1, 37, 0), (2, 1000, 3), (3, 257, 10), (8, 4096, 0),
+                                           (5, 1, 0), (2, 0, 0)])
+def test_route_matches_numpy_layout(G, count, start):
+    from skge_amd import _lib as L
+    from shard_numpy import random_records, route
+    rec, rec_n1 = random_records(np.random.RandomState(G + count), 5000, 997, 9, skip=0.2)
+    dev = torch.device("cuda", 0)
+    r = torch.as_tensor(rec, device=dev)
+    r1 = torch.as_tensor(rec_n1, device=dev)
+    n = max(4 * count, 1)
+    ids = torch.full((n,), -9, dtype=torch.int32, device=dev)
+    pos = torch.full((n,), -9, dtype=torch.int32, device=dev)
+    counts = torch.full((G,), -9, dtype=torch.int64, device=dev)
+    wsb = int(L.lib().skge_shard_route_workspace_bytes(count, G))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    L.check(L.lib().skge_shard_route(L.stream_ptr(), L.ptr(r), L.ptr(r1), start, count, G,
+                                     L.ptr(ids), L.ptr(pos), L.ptr(counts), L.ptr(ws), wsb))
+    want_ids, want_pos, want_counts = route(rec, rec_n1, start, count, G)
+    c = counts.cpu().numpy()
+    assert c.tolist() == want_counts.tolist()
+    nsend = int(c.sum())
+    assert np.array_equal(ids.cpu().numpy()[:nsend], want_ids)
+    assert np.array_equal(pos.cpu().numpy()[:4 * count], want_pos)
+
+
+def _init_tables(n_ent, n_rel, d, seed):
+    rs = np.random.RandomState(seed)
+    E = rs.uniform(-0.3, 0.3, size=(n_ent, d))
+    E /= np.sqrt((E ** 2).sum(axis=1))[:, None]
+    R = rs.uniform(-0.3, 0.3, size=(n_rel, d))
+    return E.astype(np.float32), R.astype(np.float32)
+
+
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb", [
+    (500, 7, 3001, 200, 7),     # ragged remainder batch
+    (40, 3, 1200, 52, 4),       # tiny graph: every row in every batch
+    (2000, 11, 8000, 512, 20),  # config-5 width
+])
+def test_single_rank_bitwise_equals_device_runner(n_ent, n_rel, T, d, nb):
+    from test_gpu_device_loop import _runner_result
+    from skge_amd.shard import ShardedRunner
+    a, trip = _runner_result(n_ent, n_rel, T, d, nb, pipelined=False, seed=11)
+    import skge_amd as S
+    np.random.seed(11)
+    m = S.TransE((n_ent, n_ent, n_rel), d)   # the same initial tables as _runner_result
+    dev = m.device
+    r = ShardedRunner(n_ent, m.E.data.clone(), m.R.data.clone(), torch.as_tensor(trip, device=dev),
+                      nb, lr=0.1, margin=2.0, seed=11)
+    r.run(2)
+    r.synchronize()
+    assert int(r.epoch_key.item()) == 2
+    assert int(r.nviol_total.item()) == a["nviol"] > 0
+    assert np.array_equal(r.E.data.cpu().numpy(), a["E"])
+    assert np.array_equal(r.R.data.cpu().numpy(), a["R"])
+    assert np.array_equal(r.updE.p2.cpu().numpy(), a["pE"])
+    assert np.array_equal(r.updR.p2.cpu().numpy(), a["pR"])
+    for acc in (r.accE, r.accR):
+        assert int(acc.cnt.abs().sum().item()) == 0
+        assert float(acc.sum.abs().sum().item()) == 0.0
+
+
+def _oracle_union(E, R, recs, batches, lr=0.1, margin=2.0):
+    from shard_numpy import union_pairs
+    params = {"E": E.astype(np.float64), "R": R.astype(np.float64)}
+    state = {k: np.zeros_like(v) for k, v in params.items()}
+    nv = 0
+    for start, count in batches:
+        pos, neg = union_pairs([(rec, rec_n1, start, count) for rec, rec_n1 in recs])
+        nv += O.pairwise_step("transe", params, state, pos, neg, lr, margin, "adagrad", l1=True)[2]
+    return params, state, nv
+
+
+def test_single_rank_batches_match_oracle():
+    from skge_amd.shard import ShardedRunner
+    from test_gpu_device_loop import make_kg
+    n_ent, n_rel, d = 300, 5, 200
+    trip, _ = make_kg(n_ent, n_rel, 2000)
+    E, R = _init_tables(n_ent, n_rel, d, 1)
+    dev = torch.device("cuda", 0)
+    r = ShardedRunner(n_ent, torch.as_tensor(E, device=dev), torch.as_tensor(R, device=dev),
+                      torch.as_tensor(trip, device=dev), 8, seed=5)
+    r.sample_epoch()
+    batches = [(0, 250), (250, 250)]
+    for b in batches:
+        r.step(*b)
+    r.fold_violations()
+    r.synchronize()
+    params, state, nv = _oracle_union(E, R, [(r.rec.cpu().numpy(), r.rec_n1.cpu().numpy())],
+                                      batches)
+    assert int(r.nviol_total.item()) == nv > 0
+    np.testing.assert_allclose(r.E.data.cpu().numpy(), params["E"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(r.R.data.cpu().numpy(), params["R"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(r.updE.p2.cpu().numpy(), state["E"], rtol=1e-5, atol=1e-5)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+N2, M2, D2, T2 = 400, 6, 128, 3000
+BATCHES2 = [(0, 300), (300, 300)]
+
+
+def _two_rank_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank))
+    for p in (ROOT, os.path.join(ROOT, "scikit-kge_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    from skge_amd.shard import ShardedRunner
+    from test_gpu_device_loop import make_kg
+    dist.init_process_group("gloo", init_method="env://")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    trip, _ = make_kg(N2, M2, T2, seed=4)
+    E, R = _init_tables(N2, M2, D2, 2)
+    r = ShardedRunner(N2, torch.as_tensor(E[rank::world], device=dev),
+                      torch.as_tensor(R, device=dev),
+                      torch.as_tensor(trip[rank::world], device=dev), 5, seed=20 + rank)
+    r.sample_epoch()
+    for b in BATCHES2:
+        r.step(*b)
+    r.fold_violations()
+    r.synchronize()
+    full = r.gather_full_E().cpu().numpy()
+    out.put((rank, r.rec.cpu().numpy(), r.rec_n1.cpu().numpy(), full,
+             r.R.data.cpu().numpy(), int(r.nviol_total.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_on_one_gpu_match_union_oracle():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_two_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=100) for _ in procs), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    E, R = _init_tables(N2, M2, D2, 2)
+    params, state, nv = _oracle_union(E, R, [(x[1], x[2]) for x in res], BATCHES2)
+    assert res[0][5] + res[1][5] == nv > 0
+    assert np.array_equal(res[0][3], res[1][3])          # both ranks assembled the same table
+    assert np.array_equal(res[0][4], res[1][4])          # relation replicas identical
+    np.testing.assert_allclose(res[0][3], params["E"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(res[0][4], params["R"], rtol=1e-5, atol=1e-5)

@@ -1,0 +1,121 @@
+"""The sharded step's exchange protocol (skge_amd.shard.sharded_step) over a
+world-size-2 (and 3) gloo job on CPU, with the NumPy rank compute of
+tests/shard_numpy.py: after each step the assembled entity table and every
+rank's relation replica equal one process's reference step
+(oracle.pairwise_step: skge/transe.py:48-165 + AdaGrad + normalize) over the
+union of the ranks' batches.  Rows are shared across ranks on purpose (a
+30-entity graph), so the reduce-scatter really sums contributions from
+several ranks into one owner row."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N_ENT, N_REL, D, T_R = 30, 4, 8, 24
+MARGIN, LR = 2.0, 0.1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _problem(world):
+    rs = np.random.RandomState(7)
+    E = rs.uniform(-0.5, 0.5, size=(N_ENT, D))
+    E /= np.sqrt((E ** 2).sum(axis=1))[:, None]
+    R = rs.uniform(-0.5, 0.5, size=(N_REL, D))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from shard_numpy import random_records
+    recs = [random_records(np.random.RandomState(100 + r), T_R, N_ENT, N_REL) for r in range(world)]
+    return E, R, recs
+
+
+def _worker(rank, world, port, batches, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank))
+    for p in (ROOT, os.path.join(ROOT, "scikit-kge_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    from skge_amd.shard import Exchange, sharded_step
+    from shard_numpy import NumpyShardOps
+    dist.init_process_group("gloo", init_method="env://")
+    E, R, recs = _problem(world)
+    rec, rec_n1 = recs[rank]
+    ops = NumpyShardOps(rec, rec_n1, E[rank::world], R, world, MARGIN, LR)
+    ex = Exchange()
+    snaps = []
+    for start, count in batches:
+        sharded_step(ops, ex, start, count)
+        snaps.append((ops.E.copy(), ops.R.copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+    out.put((rank, snaps, ops.nviol))
+
+
+def _run(world, batches):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, batches, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=180) for _ in procs), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world,batches", [(2, [(0, 24)]), (2, [(0, 10), (10, 10), (20, 4)]),
+                                           (3, [(0, 12), (12, 12)])])
+def test_sharded_protocol_matches_union_batch(world, batches):
+    from oracle import skge_oracle as O
+    from shard_numpy import union_pairs
+    res = _run(world, batches)
+    E, R, recs = _problem(world)
+    params = {"E": E.copy(), "R": R.copy()}
+    state = {k: np.zeros_like(v) for k, v in params.items()}
+    nviol = 0
+    for b, (start, count) in enumerate(batches):
+        pos, neg = union_pairs([(rec, rec_n1, start, count) for rec, rec_n1 in recs])
+        _, _, nv, _ = O.pairwise_step("transe", params, state, pos, neg, LR, MARGIN, "adagrad",
+                                      l1=True)
+        nviol += nv
+        full = np.zeros_like(E)
+        for rank, snaps, _ in res:
+            full[rank::world] = snaps[b][0]
+            # every rank's relation replica is the union-batch relation table
+            np.testing.assert_allclose(snaps[b][1], params["R"], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(full, params["E"], rtol=0, atol=1e-12)
+    assert sum(r[2] for r in res) == nviol
+
+
+def test_route_layout_is_owner_major_and_stable():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from shard_numpy import route
+    rec = np.array([[0, 1, 0, 2], [3, 4, 1, -1], [5, 0, 0, 1]], dtype=np.int32)
+    rec_n1 = np.array([7, 2, -1], dtype=np.int32)
+    ids, pos, counts = route(rec, rec_n1, 0, 3, 2)
+    # requests: 0 1 2 7 | 3 4 -1 2 | 5 0 1 -1
+    assert counts.tolist() == [5, 5]
+    assert ids.tolist() == [0, 2, 4, 2, 0, 1, 7, 3, 5, 1]
+    assert pos.tolist() == [0, 5, 1, 6, 7, 2, -1, 3, 8, 4, 9, -1]
+    for k, p in enumerate(pos):
+        if p >= 0:
+            assert ids[p] == [0, 1, 2, 7, 3, 4, -1, 2, 5, 0, 1, -1][k]
+
+
+def test_owned_rows_partition():
+    from skge_amd.shard import owned_rows
+    for n in (1, 7, 30, 50):
+        for G in (1, 2, 3, 8):
+            assert sum(owned_rows(n, G, g) for g in range(G)) == n
+            assert all(owned_rows(n, G, g) == len(range(g, n, G)) for g in range(G))
