@@ -161,7 +161,13 @@ def main():
                          "|R|=10k d=512, B=131072 per GPU (BASELINE.json configs[4])")
     ap.add_argument("--c5-scale", type=float, default=1.0,
                     help="config 5 only: scale |E| and T (quick rehearsals)")
+    ap.add_argument("--shard", action="store_true",
+                    help="config 5 only: row-shard E and its AdaGrad state over the ranks "
+                         "(skge_amd.shard; RCCL all-to-all row fetch + contribution "
+                         "reduce-scatter, relation sums all-reduced) instead of replicas")
     args = ap.parse_args()
+    if args.config == 5 and args.shard:
+        return run_config5_sharded(args)
     if args.config == 5:
         return run_config5(args)
     if args.config in (3, 4):
@@ -457,6 +463,159 @@ def run_config5(args):
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_config5_sharded(args):
+    """BASELINE.json configs[4] as named there: the |E|=50M x d=512 entity
+    table (and its AdaGrad state) row-sharded over the ranks, R replicated,
+    T=100M triples split over the ranks, B=131072 positives per rank per
+    batch (global batch = G x 131072), TransE-L1 + AdaGrad, margin 2.0.
+    The dataset and tables are fixed as G grows: scaling "strong"."""
+    import torch
+    import torch.distributed as dist
+    world, rank, local = dist_env()
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from skge_amd.shard import ShardedRunner, owned_rows
+    n_ent, T = int(N5 * args.c5_scale), int(T5 * args.c5_scale)
+    d, n_rel = D5, M5
+    t_build = time.perf_counter()
+    T_r = T // world + (1 if rank < T % world else 0)
+    trip = make_config5_kg(n_ent, n_rel, T_r, dev, seed=rank)
+    bnd = float(np.sqrt(6) / np.sqrt(n_ent + d))      # init_nunif of the FULL table
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    E = torch.empty((owned_rows(n_ent, world, rank), d), dtype=torch.float32, device=dev)
+    E.uniform_(-bnd, bnd, generator=g)
+    for r0 in range(0, E.shape[0], 1 << 20):            # TransE's post=normalize at init
+        blk = E[r0:r0 + (1 << 20)]
+        blk.div_(blk.norm(dim=1, keepdim=True))
+    g.manual_seed(7)                                     # the same R on every rank
+    R = torch.empty((n_rel, d), dtype=torch.float32, device=dev)
+    R.uniform_(-float(np.sqrt(6) / np.sqrt(n_rel + d)), float(np.sqrt(6) / np.sqrt(n_rel + d)),
+               generator=g)
+    nb = max(1, T_r // B5)
+    runner = ShardedRunner(n_ent, E, R, trip, nb, lr=0.1, margin=2.0, seed=99 + rank)
+    del E, R
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t_build
+    runner.run(args.warmup)
+    runner.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    runner.run(args.steps)
+    runner.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(elapsed, world, dev)
+    value = T * args.steps / elapsed
+    prof = shard_profile(runner, d)
+    nviol = int(runner.nviol_total.item())
+    if rank == 0:
+        k = prof["dominant"]
+        line = {
+            "metric": "triples/sec (score+grad+update), synthetic TransE |E|=50M |R|=10k d=512, "
+                      "table row-sharded over the GPUs (BASELINE configs[4])",
+            "value": round(value, 1), "unit": "triples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic uniform KG (|E|=%d |R|=%d T=%d split over ranks, torch generator "
+                    "seed rank); device-drawn nunif params" % (n_ent, n_rel, T),
+            "config": {"workload": "TransE-L1 d=%d PairwiseStochasticTrainer+AdaGrad, margin 2.0, "
+                                   "lr 0.1, device RandomModeSampler(1,[0,1]); E and AdaGrad state "
+                                   "row-sharded (row %% G), R replicated; step = 1 epoch of %d "
+                                   "batches of %d positives per rank" % (d, len(runner.batches), B5),
+                       "global_batch": B5 * world, "parallelism": "rowshard%d" % world},
+            "roofline": {"bound": "hbm", "kernel": k["name"],
+                         "achieved": round(k["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                         "traffic": None, "bytes_per_launch": round(k["bytes_per_launch"]),
+                         "avg_launch_us": round(k["avg_us"], 3)},
+            "cpu_baseline": None,
+            "detail": {"runner": "row-sharded (skge_amd.shard)",
+                       "build_s": round(t_build, 1),
+                       "violations_per_pair": round(nviol / (2.0 * T_r * (args.warmup + args.steps)), 4),
+                       "phases_ms_per_batch": {n: round(v, 4) for n, v in prof["phases_ms"].items()},
+                       "kernels": {n: {"avg_us": round(v["avg_us"], 3),
+                                       "GB_s": round(v["achieved_gbs"], 1)}
+                                   for n, v in prof["kernels"].items()},
+                       "gpu_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)},
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def shard_profile(runner, d, nbatch=6):
+    """The phases of `nbatch` sharded steps (skge_amd.shard.sharded_step,
+    replayed here with HIP events on the runner stream between phases; the
+    collectives' time shows in the phases that wait for them) and the
+    algorithmic bytes of each HIP kernel: route 52 B per positive (record +
+    request ids + slots), gather 8d + 4 B per row served, score 20d + 20 B per
+    positive (4 fetched rows + R row) + d + 16 B per contribution record + 2d
+    per violating positive's R row, accum d + 20 B per record + 4d per
+    non-empty record (packed sums read+written), apply 20d per applied row."""
+    import torch
+    ops, ex, st = runner.ops, runner.ex, runner.stream
+    names = ["route", "split_sizes", "a2a_ids", "gather", "a2a_rows", "score", "a2a_contrib",
+             "accum", "allreduce_R", "apply"]
+    ms = {n: 0.0 for n in names}
+    kb = {n: 0.0 for n in ("route", "gather", "score", "accum", "apply")}
+    batches = [b for b in runner.batches if b[1] > 0][:nbatch]
+    with torch.cuda.stream(st):
+        runner.sample_epoch()
+        for start, count in batches:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
+            ev[0].record(st)
+            send_ids, req_pos, cnts = ops.route(start, count, ex.G)
+            ev[1].record(st)
+            send, recv = ex.split_sizes(cnts)
+            ev[2].record(st)
+            recv_ids = ex.all_to_all(send_ids, send, recv)
+            ev[3].record(st)
+            rows = ops.gather(recv_ids)
+            ev[4].record(st)
+            fetched = ex.all_to_all(rows, recv, send)
+            ev[5].record(st)
+            contrib = ops.score(start, count, fetched, req_pos)
+            ev[6].record(st)
+            rc = ex.all_to_all(contrib, send, recv)
+            ev[7].record(st)
+            ops.accum(recv_ids, rc)
+            ev[8].record(st)
+            for t in ops.rel_sums():
+                ex.all_reduce_(t)
+            ev[9].record(st)
+            nz = int((rc[:, :4].contiguous().view(torch.int32)[:, 0] > 0).sum().item())
+            touched = int((runner.accE.cnt != 0).sum().item()) + int((runner.accR.cnt != 0).sum().item())
+            e_apply = torch.cuda.Event(enable_timing=True)
+            e_apply.record(st)
+            ops.apply(int(sum(recv)))
+            ev[10].record(st)
+            st.synchronize()
+            for i, n in enumerate(names):
+                ms[n] += (e_apply if n == "apply" else ev[i]).elapsed_time(ev[i + 1])
+            nrecv = int(sum(recv))
+            kb["route"] += 52.0 * count
+            kb["gather"] += (8.0 * d + 4) * nrecv
+            kb["score"] += (20.0 * d + 20) * count + (d + 16.0) * int(sum(send)) + 2.0 * d * count
+            kb["accum"] += (d + 20.0) * nrecv + 4.0 * d * nz
+            kb["apply"] += 20.0 * d * touched
+    n = max(len(batches), 1)
+    kern = {}
+    for k in kb:
+        us = 1000.0 * ms[k] / n
+        kern[k] = {"name": k, "avg_us": us, "bytes_per_launch": kb[k] / n,
+                   "achieved_gbs": (kb[k] / n) / (us * 1e-6) / 1e9 if us > 0 else 0.0}
+    return {"phases_ms": {k: v / n for k, v in ms.items()}, "kernels": kern,
+            "dominant": max(kern.values(), key=lambda v: v["avg_us"])}
 
 
 FP32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 matrix (MFMA) peak
