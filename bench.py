@@ -58,6 +58,10 @@ def pmc_traffic(kernel_substr):
     data = json.load(open(files[-1]))
     for name, e in data.items():
         if kernel_substr in name and "traffic_bytes_per_launch" in e:
+            grids = [g for g in e.get("by_grid", {}).values() if "traffic_bytes_per_launch" in g]
+            if grids:   # the geometry launched most (the nb=100 epochs, not the detail lines)
+                g = max(grids, key=lambda x: x["calls"])
+                return g["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
             return e["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
     return None, None
 
@@ -161,6 +165,8 @@ def main():
                          "|R|=10k d=512, B=131072 per GPU (BASELINE.json configs[4])")
     ap.add_argument("--c5-scale", type=float, default=1.0,
                     help="config 5 only: scale |E| and T (quick rehearsals)")
+    ap.add_argument("--no-roofline", action="store_true",
+                    help="skip the measured gather roofline (skge_roofline_gather)")
     ap.add_argument("--shard", action="store_true",
                     help="config 5 only: row-shard E and its AdaGrad state over the ranks "
                          "(skge_amd.shard; RCCL all-to-all row fetch + contribution "
@@ -236,8 +242,31 @@ def main():
         p.data.copy_(init[pid])
         upd[pid].reset()
     torch.cuda.synchronize()
-    prof = pipe_profile(runner, kg, nb, d) if runner.pipelined else \
+    prof = pipe_profile(runner, kg, nb, d, epochs=args.steps,
+                        gpu_ms_per_epoch=gpu_ms / args.steps) if runner.pipelined else \
         kernel_profile(model, upd, kg, nb, d, st, runner)
+    meas = None
+    if runner.pipelined and not args.no_roofline:
+        # the same per-launch row traffic without the path's
+        # dependencies, and the streaming random-row gather rate of the table
+        geo = prof["geometry"]
+        npos = int(round(geo["positives"]))
+        m_us, m_b, m_gbs = measured_roofline(dev, N_ENT, d, npos, 5,
+                                             int(round(geo["atomic_rows"] / max(npos, 1))),
+                                             int(round(geo["applied_rows"])))
+        s_us, s_b, s_gbs = measured_roofline(dev, N_ENT, d, 262144, 5, 0, 0, launches=10, reps=3)
+        h_us, h_b, h_gbs = measured_roofline(dev, 5_000_000, d, 262144, 5, 0, 0, launches=10,
+                                             reps=3)
+        meas = {"kernel": "k_roofline (skge_roofline_gather)",
+                "geometry": "per launch: %d waves x 5 random %d-B row gathers + %d atomic rows "
+                            "each, %d rows read+written (20d B), WN18 table"
+                            % (npos, 4 * d, int(round(geo["atomic_rows"] / max(npos, 1))),
+                               int(round(geo["applied_rows"]))),
+                "avg_launch_us": round(m_us, 3), "bytes_per_launch": round(m_b),
+                "GB_s": round(m_gbs, 1),
+                "frac": round(prof["dominant"]["achieved_gbs"] / m_gbs, 4),
+                "streaming_gather_GB_s": {"wn18_table_33MB": round(s_gbs, 1),
+                                          "table_4GB": round(h_gbs, 1)}}
 
     # ---- detail: the same path at a large batch ("throughput at
     # nb=100 and at a stated larger batch"), not the headline value ----
@@ -251,12 +280,23 @@ def main():
         r2.run(1)
         r2.synchronize()
         e2 = 5
+        for pid, p in model.params.items():   # the timed and profiled epochs start fresh
+            p.data.copy_(init[pid])
+            upd[pid].reset()
         torch.cuda.synchronize()
         t2 = time.perf_counter()
+        f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        f0.record(r2.stream)
         r2.run(e2)
+        f1.record(r2.stream)
         r2.synchronize()
         t2 = time.perf_counter() - t2
-        p2 = pipe_profile(r2, kg, args.large_nb, d) if r2.pipelined else \
+        for pid, p in model.params.items():
+            p.data.copy_(init[pid])
+            upd[pid].reset()
+        torch.cuda.synchronize()
+        p2 = pipe_profile(r2, kg, args.large_nb, d, epochs=e2,
+                          gpu_ms_per_epoch=f0.elapsed_time(f1) / e2) if r2.pipelined else \
             kernel_profile(model, upd, kg, args.large_nb, d, r2.stream, r2)
         k2 = p2["dominant"]
         large = {"nbatches": args.large_nb, "batch": N_TRIPLES // args.large_nb,
@@ -298,7 +338,11 @@ def main():
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,
                          "bytes_per_launch": round(k["bytes_per_launch"]),
-                         "avg_launch_us": round(k["avg_us"], 3)},
+                         "avg_launch_us": round(k["avg_us"], 3),
+                         "avg_launch_source": "timed-region HIP events (graph replays) minus "
+                                              "the draw/advance launches, per batch launch",
+                         "eager_avg_launch_us": round(k.get("eager_avg_us", k["avg_us"]), 3),
+                         "measured": meas},
             "cpu_baseline": cpu,
             "detail": {
                 "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
@@ -333,35 +377,96 @@ def _apply_bytes(d, rows, packed=True):
     return (16 * d + (4 * d if packed else 8 * d)) * rows
 
 
-def pipe_profile(runner, kg, nb, d):
-    """Pipelined runner: one eager epoch with HIP events around every launch
-    (skge_pipe_runner_profile, on the runner's stream).  Launch i >= 1 scores
-    batch i-1 and applies batch i-2: its algorithmic bytes are the scoring
-    bytes of its batch plus 24 B/element for each row it applied (read sum,
-    param, state; write param, state, zero sum), with the applied-row and
-    violation counts the kernel itself recorded."""
-    us, stats = runner.profile()
+def pipe_profile(runner, kg, nb, d, epochs=1, gpu_ms_per_epoch=None):
+    """Pipelined runner: `epochs` eager epochs with HIP events around every
+    launch and the kernel's own per-launch counters (skge_pipe_runner_profile,
+    on the runner's stream), started from the same state as the timed region.
+    Launch i >= 1 scores batch i-1 and applies batch i-2: its algorithmic
+    bytes are the scoring bytes of its batch plus 20 B/element for each row it
+    applied (read sum, param, state; write param, state, zero sum), with the
+    applied-row and violation counts the kernel itself recorded.
+
+    avg_us: with gpu_ms_per_epoch (the timed region's HIP-event time per
+    epoch, graph replays) the batch launches' share of it -- the epoch minus
+    the draw and key-advance launches, over the batch launches; else the
+    eager per-launch event times (which include per-launch event overhead)."""
     T = kg.T
     bs = T // nb
     counts = [min(bs, T - s) for s in range(0, T, bs)] + [0]   # + the flush launch
-    b_pipe, t_pipe, total = 0.0, 0.0, 0.0
-    for i, cnt in enumerate(counts, start=1):
-        UE, UR, V = (int(x) for x in stats[i])
-        b = _score_bytes(d, cnt, V) + _apply_bytes(d, UE + UR)
-        b_pipe += b
-        t_pipe += float(us[i])
-        if cnt:
-            total += algorithmic_bytes(d, cnt, 2 * cnt, 0, 0)
-        total += 12 * d * (UE + UR)
     n = len(counts)
-    kern = {"pipe_batch": {"name": "pipe_batch", "avg_us": t_pipe / n, "launches": n,
-                           "bytes_per_launch": b_pipe / n,
-                           "achieved_gbs": b_pipe / (t_pipe * 1e-6) / 1e9},
+    b_pipe, t_pipe, total, t_other = 0.0, 0.0, 0.0, 0.0
+    geo = np.zeros(4)   # positives, atomic rows, applied rows, launches
+    us0 = 0.0
+    for _ in range(epochs):
+        us, stats = runner.profile()
+        us0 += float(us[0])
+        t_other += float(us[0]) + float(us[n + 1])
+        for i, cnt in enumerate(counts, start=1):
+            UE, UR, V = (int(x) for x in stats[i])
+            b = _score_bytes(d, cnt, V) + _apply_bytes(d, UE + UR)
+            b_pipe += b
+            t_pipe += float(us[i])
+            if cnt:
+                total += algorithmic_bytes(d, cnt, 2 * cnt, 0, 0)
+            total += 12 * d * (UE + UR)
+            geo += (cnt, min(5 * cnt, 2 * V + 3 * cnt), UE + UR, 1)
+    eager_us = t_pipe / (n * epochs)
+    avg_us = eager_us
+    if gpu_ms_per_epoch is not None:
+        avg_us = (1000.0 * gpu_ms_per_epoch - t_other / epochs) / n
+    bpl = b_pipe / (n * epochs)
+    kern = {"pipe_batch": {"name": "pipe_batch", "avg_us": avg_us, "launches": n,
+                           "eager_avg_us": eager_us, "bytes_per_launch": bpl,
+                           "achieved_gbs": bpl / (avg_us * 1e-6) / 1e9},
             # per positive: triple 12 B, two filter words 8 B, record 20 B
-            "epoch_sample": {"name": "epoch_sample", "avg_us": float(us[0]), "launches": 1,
+            "epoch_sample": {"name": "epoch_sample", "avg_us": us0 / epochs, "launches": 1,
                              "bytes_per_launch": 40.0 * T,
-                             "achieved_gbs": 40.0 * T / (float(us[0]) * 1e-6) / 1e9}}
-    return {"kernels": kern, "dominant": kern["pipe_batch"], "epoch_bytes": total}
+                             "achieved_gbs": 40.0 * T / (us0 / epochs * 1e-6) / 1e9}}
+    g = geo / geo[3]
+    return {"kernels": kern, "dominant": kern["pipe_batch"], "epoch_bytes": total / epochs,
+            "geometry": {"positives": g[0], "atomic_rows": g[1], "applied_rows": g[2]}}
+
+
+def measured_roofline(dev, rows, d, n_gather, rows_per_wave, atom_rows, n_rmw, launches=101,
+                      reps=5):
+    """skge_roofline_gather (csrc/skge_roofline.hip): the same row traffic as
+    one training launch without its dependencies, `launches` launches
+    captured in one graph like an epoch; returns (us per launch, bytes per
+    launch, GB/s).  Scratch tables of the training table's shape."""
+    import torch
+    from skge_amd import _lib as L
+    P = torch.rand((rows, d), dtype=torch.float32, device=dev)
+    A = torch.rand((rows, d), dtype=torch.float32, device=dev)
+    S = torch.zeros(rows * d // 4, dtype=torch.int64, device=dev)
+    out = torch.empty(max(n_gather, 1), dtype=torch.float32, device=dev)
+    lib = L.lib()
+
+    def launch_all():
+        for i in range(launches):
+            L.check(lib.skge_roofline_gather(L.stream_ptr(), L.ptr(P), L.ptr(A), L.ptr(S), rows, d,
+                                             n_gather, rows_per_wave, atom_rows, n_rmw,
+                                             (i * 7919 + 13) & 0xFFFFFFFF, L.ptr(out)), "roofline")
+
+    st = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(st):
+        launch_all()                      # warm (eager)
+    st.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        launch_all()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    with torch.cuda.stream(st):
+        for _ in range(reps):
+            g.replay()
+    e1.record(st)
+    torch.cuda.synchronize()
+    us = 1000.0 * e0.elapsed_time(e1) / (reps * launches)
+    b = n_gather * (rows_per_wave * 4.0 * d + atom_rows * 2.0 * d) + n_rmw * 20.0 * d
+    del P, A, S, out, g
+    return us, b, b / (us * 1e-6) / 1e9
 
 
 N5, M5, D5, T5, B5 = 50_000_000, 10_000, 512, 100_000_000, 131072

@@ -391,6 +391,20 @@ int skge_shard_accum(void *stream, const skge_table_t *ent_shard, int G, const i
 /* *nviol_total += the violation shards, which are cleared. */
 int skge_shard_fold_violations(void *stream, int *vshards, int *nviol_total);
 
+/* ---------------- measurement ----------------
+ *
+ * Measured gather + RMW-scatter roofline: one launch of the same row traffic
+ * as a training launch without its dependencies.  n_rmw waves each read and
+ * write back one random row of P, A (fp32 [rows][d]) and S (packed sums,
+ * u64 [rows][d/4]) = 20d bytes; then n_gather waves each gather
+ * rows_per_wave random rows of P (4d bytes each) and add atom_rows_per_wave
+ * rows of 64-bit atomics into S (2d bytes each).  out [n_gather] receives a
+ * per-wave checksum.  The values of P, A, S are left unchanged.  Not part of
+ * the training path (bench.py times it beside the training kernels). */
+int skge_roofline_gather(void *stream, float *P, float *A, void *S, int rows, int d, int n_gather,
+                         int rows_per_wave, int atom_rows_per_wave, int n_rmw, uint32_t salt,
+                         float *out);
+
 /* ---------------- evaluation ---------------- */
 
 /*

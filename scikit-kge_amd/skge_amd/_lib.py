@@ -89,6 +89,8 @@ SIGNATURES = {
     "skge_shard_score": (c_i, [c_p, T_P, c_i, c_p, c_p, c_i64, c_i, c_p, c_p, c_f, c_p, c_p]),
     "skge_shard_accum": (c_i, [c_p, T_P, c_i, c_p, c_p, c_i64]),
     "skge_shard_fold_violations": (c_i, [c_p, c_p, c_p]),
+    "skge_roofline_gather": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i,
+                                   ctypes.c_uint32, c_p]),
 }
 
 _lib = None

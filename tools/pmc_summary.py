@@ -21,21 +21,46 @@ def one(pattern):
     return f[0] if f else None
 
 
-def counters(d, name):
+def grid_of(r):
+    for key in ("Grid_Size_X", "Grid_Size", "Grid_Size_x"):
+        if key in r and r[key] not in (None, ""):
+            return int(float(r[key]))
+    return None
+
+
+def counters(d, name, by_grid=None):
     f = one(os.path.join(d, "**", "*counter_collection.csv"))
     out = defaultdict(list)
     if not f:
         return out
     per_dispatch = defaultdict(float)
     kname = {}
+    kgrid = {}
     for r in csv.DictReader(open(f)):
         if r.get("Counter_Name") != name:
             continue
         key = r["Dispatch_Id"]
         per_dispatch[key] += float(r["Counter_Value"])
         kname[key] = r["Kernel_Name"]
+        kgrid[key] = grid_of(r)
     for k, v in per_dispatch.items():
         out[kname[k]].append(v)
+        if by_grid is not None:
+            by_grid[(kname[k], kgrid[k])].append(v)
+    return out
+
+
+def trace_by_grid(d):
+    """(kernel, grid size) -> list of durations (us) from the kernel trace: the
+    same kernel launched at two geometries (e.g. the nb=100 epochs and the
+    large-batch detail) is reported per geometry."""
+    f = one(os.path.join(d, "**", "*kernel_trace.csv"))
+    out = defaultdict(list)
+    if not f:
+        return out
+    for r in csv.DictReader(open(f)):
+        dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        out[(r["Kernel_Name"], grid_of(r))].append(dur)
     return out
 
 
@@ -46,8 +71,10 @@ def main(d):
         for r in csv.DictReader(open(f)):
             stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
                                 "pct": float(r["Percentage"])}
-    fetch = counters(os.path.join(d, "fetch"), "FETCH_SIZE")
-    write = counters(os.path.join(d, "write"), "WRITE_SIZE")
+    gfetch, gwrite = defaultdict(list), defaultdict(list)
+    fetch = counters(os.path.join(d, "fetch"), "FETCH_SIZE", gfetch)
+    write = counters(os.path.join(d, "write"), "WRITE_SIZE", gwrite)
+    gtrace = trace_by_grid(os.path.join(d, "stats"))
     res = {}
     for k in set(stats) | set(fetch) | set(write):
         e = dict(stats.get(k, {}))
@@ -58,6 +85,18 @@ def main(d):
         if "fetch_kb_per_launch" in e and "write_kb_per_launch" in e:
             e["traffic_bytes_per_launch"] = 1024.0 * (2 * e["fetch_kb_per_launch"] +
                                                       e["write_kb_per_launch"])
+        grids = sorted(g for (n, g) in gtrace if n == k)
+        if len(grids) > 1:
+            e["by_grid"] = {}
+            for g in grids:
+                t = gtrace[(k, g)]
+                ge = {"calls": len(t), "avg_us": sum(t) / len(t)}
+                if gfetch.get((k, g)) and gwrite.get((k, g)):
+                    fk = sum(gfetch[(k, g)]) / len(gfetch[(k, g)])
+                    wk = sum(gwrite[(k, g)]) / len(gwrite[(k, g)])
+                    ge.update(fetch_kb_per_launch=fk, write_kb_per_launch=wk,
+                              traffic_bytes_per_launch=1024.0 * (2 * fk + wk))
+                e["by_grid"][str(g)] = ge
         res[k] = e
     print(json.dumps(res, indent=1, sort_keys=True))
 
