@@ -726,6 +726,13 @@ def shard_profile(runner, d, nbatch=6):
 FP32_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 matrix (MFMA) peak
 
 
+def hole_positive_path(d):
+    """The device pair loop runs HolE on k_hole_pos (one positive and both of
+    its pairs per wave: 3 scores + 4 gradient correlations, computed for every
+    positive) unless SKGE_HOLE_PAIRS=1 or d is outside its range."""
+    return d % 4 == 0 and 4 <= d <= 256 and os.environ.get("SKGE_HOLE_PAIRS", "0") in ("", "0")
+
+
 def model_flops(kind, d, P, V):
     """Algorithmic FLOPs of one batch of P pairs with V violators:
     HolE: 2 scoring correlations per pair + 6 gradient correlations per
@@ -733,6 +740,8 @@ def model_flops(kind, d, P, V):
     a positive's 2 pairs, E_s W for the violators' entity gradients (computed
     for all 4 by the GEMM) and the 4 dW outer products: 24 d^2 per positive."""
     if kind == "hole":
+        if hole_positive_path(d):   # k_hole_pos: 7 correlations per positive (P / 2)
+            return 2.0 * d * d * 7 * (P / 2.0)
         return 2.0 * d * d * (2 * P + 6 * V)
     return 24.0 * d * d * (P / 2.0)
 

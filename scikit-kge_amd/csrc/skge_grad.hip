@@ -543,6 +543,281 @@ __global__ __launch_bounds__(256) void k_hole_pair_fast(PairArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// HolE pairwise, one positive and BOTH of its pairs per wave (device pair
+// loop).  Record j = (s, o, p, s'), o' gives pair 2j = ((s,o,p), (s',o,p)) and
+// pair 2j+1 = ((s,o,p), (s,o',p)) (skge/sample.py:41-46, base.py:1411-1416).
+// The two pairs share operands, so the 12 correlations of two
+// k_hole_pair_fast waves reduce to 7, in three loops that each slide ONE
+// window of their common second operand b (ccorr(a,b)_k = sum_j a_j b_{j+k}):
+//   b = E[o] : X = ccorr(E[s],E[o])   Y = ccorr(E[s'],E[o])   A = ccorr(R[p],E[o])
+//   b = E[o']: Z = ccorr(E[s],E[o'])  B = ccorr(R[p],E[o'])
+//   b = R[p] : C = cconv(E[s],R[p])   D = cconv(E[s'],R[p])
+// Scores R[p].X, R[p].Y, R[p].Z (hole.py:20) with k_hole_pair_fast's exact
+// arithmetic, so the margin decisions (hole.py:56) are the pair path's;
+// gp = -g(f(p)), gn = g(f(n)) (hole.py:66-67).  Per violating pair (v0, v1)
+// the contributions of hole.py:76-96, summed per row before the atomics:
+//   R[p] : v0 (gp X + g0 Y) + v1 (gp X + g1 Z)
+//   E[s] : v0 gp A + v1 (gp A + g1 B)          E[s']: v0 g0 A
+//   E[o] : v0 (gp C + g0 D) + v1 gp C          E[o']: v1 g1 C
+// with the occurrence counts grad_sum_matrix gives those lists (s: v0 + 2 v1,
+// o: 2 v0 + v1, s': v0, o': v1, p: 2 (v0 + v1)).  Entity slots 4j..4j+3 name
+// (s, o, s', o'), relation slot j names p.  Rows are held in the quad layout
+// (lane l: elements 4l..4l+3), so d % 4 == 0 and d <= 256.
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ int hole_pos_lds_floats(int d) { return 10 * d + 12; }
+
+__device__ __forceinline__ void q_lds(float* s, const float4& v, int d) {
+  const int base = 4 * lane_id();
+  if (base < d) *reinterpret_cast<float4*>(s + base) = v;
+}
+
+// doubled row (b operand): s2[e] = s2[e + d] = v_e, 4 zeros after
+__device__ __forceinline__ void q_lds_dbl(float* s2, const float4& v, int d) {
+  const int l = lane_id(), base = 4 * l;
+  if (base < d) {
+    *reinterpret_cast<float4*>(s2 + base) = v;
+    *reinterpret_cast<float4*>(s2 + base + d) = v;
+  }
+  if (l < 4) s2[2 * d + l] = 0.0f;
+}
+
+// reversed row a'_m = a_{-m mod d}: cconv(a, b) = ccorr(a', b)
+__device__ __forceinline__ void q_lds_rev(float* s, const float4& v, int d) {
+  const int base = 4 * lane_id();
+  if (base < d) {
+    s[base == 0 ? 0 : d - base] = v.x;
+    s[d - base - 1] = v.y;
+    s[d - base - 2] = v.z;
+    s[d - base - 3] = v.w;
+  }
+}
+
+// NA correlations against one second operand: out[n] (quad layout) =
+// ccorr(sa[n], b) with b doubled in sb2; per output the FMA sequence of corr_fast
+template <int NA>
+__device__ __forceinline__ void corr_quad(const float* const (&sa)[NA], const float* sb2, int d,
+                                          float4 (&out)[NA]) {
+  const int base = 4 * lane_id();
+  f2 c01[NA], c23[NA], e01[NA], e23[NA];
+#pragma unroll
+  for (int n = 0; n < NA; ++n) {
+    c01[n] = f2{0.0f, 0.0f};
+    c23[n] = f2{0.0f, 0.0f};
+    e01[n] = f2{0.0f, 0.0f};
+    e23[n] = f2{0.0f, 0.0f};
+  }
+  if (base < d) {
+    float4 lo = *reinterpret_cast<const float4*>(sb2 + base);
+    float4 hi = *reinterpret_cast<const float4*>(sb2 + base + 4);
+    for (int j0 = 0; j0 < d; j0 += 4) {
+      const float4 nx = *reinterpret_cast<const float4*>(sb2 + j0 + 8 + base);
+      const f2 w01 = {lo.x, lo.y}, w12 = {lo.y, lo.z}, w23 = {lo.z, lo.w}, w34 = {lo.w, hi.x};
+      const f2 w45 = {hi.x, hi.y}, w56 = {hi.y, hi.z};
+#pragma unroll
+      for (int n = 0; n < NA; ++n) {
+        const float4 a = *reinterpret_cast<const float4*>(sa[n] + j0);   // broadcast
+        const f2 ax = {a.x, a.x}, ay = {a.y, a.y}, az = {a.z, a.z}, aw = {a.w, a.w};
+        c01[n] = __builtin_elementwise_fma(ax, w01, c01[n]);
+        c23[n] = __builtin_elementwise_fma(ax, w23, c23[n]);
+        e01[n] = __builtin_elementwise_fma(ay, w12, e01[n]);
+        e23[n] = __builtin_elementwise_fma(ay, w34, e23[n]);
+        c01[n] = __builtin_elementwise_fma(az, w23, c01[n]);
+        c23[n] = __builtin_elementwise_fma(az, w45, c23[n]);
+        e01[n] = __builtin_elementwise_fma(aw, w34, e01[n]);
+        e23[n] = __builtin_elementwise_fma(aw, w56, e23[n]);
+      }
+      lo = hi;
+      hi = nx;
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NA; ++n) {
+    const f2 u = c01[n] + e01[n], v = c23[n] + e23[n];
+    out[n] = make_float4(u.x, u.y, v.x, v.y);
+  }
+}
+
+// score R . c with k_hole_pair_fast's arithmetic: lane-strided products
+// summed over k, then the wave sum (c staged through the wave's LDS)
+template <int KM>
+__device__ __forceinline__ float score_q(const float4& c, const float* sR, int d, float* stage) {
+  q_lds(stage, c, d);
+  __builtin_amdgcn_wave_barrier();
+  const int l = lane_id();
+  float ps = 0.0f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k;
+    const float r = e < d ? sR[e] : 0.0f, x = e < d ? stage[e] : 0.0f;
+    ps += r * x;
+  }
+  __builtin_amdgcn_wave_barrier();
+  return wave_sum(ps);
+}
+
+// a quad-layout contribution row, re-laid lane-strided through the wave's LDS
+// stage so every float-atomic wave-instruction covers contiguous bytes
+// (MI355X_MICROARCH.md "Global float atomics": scattered lanes are far slower)
+template <int KM>
+__device__ __forceinline__ void acc_q(const Accum& acc, int row, const float4& v, int d,
+                                      float* stage) {
+  q_lds(stage, v, d);
+  __builtin_amdgcn_wave_barrier();
+  float x[KM];
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k;
+    x[k] = e < d ? stage[e] : 0.0f;
+  }
+  __builtin_amdgcn_wave_barrier();
+  acc_row<KM>(acc, row, x, d);
+}
+
+struct HolePosArgs {
+  const float* E;
+  const float* R;
+  Accum accE, accR;
+  const int4* rec;   // the epoch's records (s, o, p, s' or -1)
+  const int* rec_n1; // o' or -1
+  long long start;   // this batch: positives [start, start + count)
+  int count, d, af;
+  float margin;
+  int* nviol;        // this batch's gate word: += violating pairs
+  int* fold;         // the previous batch's gate word: added to *total, then cleared
+  int* total;
+};
+
+template <int KM>
+__global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wave = threadIdx.x >> 6, wpb = blockDim.x >> 6, l = lane_id();
+  const int d = a.d;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.fold) {
+    if (a.total) *a.total += *a.fold;
+    *a.fold = 0;
+  }
+  float* sEs = smem + wave * hole_pos_lds_floats(d);   // a operands
+  float* sFs = sEs + d;
+  float* rEs = sEs + 2 * d;
+  float* rFs = sEs + 3 * d;
+  float* sR2 = sEs + 4 * d;                            // doubled b operands
+  float* sO2 = sR2 + 2 * d + 4;
+  float* sQ2 = sO2 + 2 * d + 4;
+  int nv = 0;
+  for (int j = blockIdx.x * wpb + wave; j < a.count; j += gridDim.x * wpb) {
+    const int4 r4 = a.rec[a.start + j];
+    const int s = uni(r4.x), o = uni(r4.y), p = uni(r4.z), neg0 = uni(r4.w);
+    const int neg1 = uni(a.rec_n1[a.start + j]);
+    const int n0r = neg0 >= 0 ? neg0 : s, n1r = neg1 >= 0 ? neg1 : o;
+    float4 es[1], eo[1], rp[1], fs[1], fo[1];
+    load_row4<1>(a.E, s, d, es);
+    load_row4<1>(a.E, o, d, eo);
+    load_row4<1>(a.R, p, d, rp);
+    load_row4<1>(a.E, n0r, d, fs);
+    load_row4<1>(a.E, n1r, d, fo);
+    q_lds(sEs, es[0], d);
+    q_lds(sFs, fs[0], d);
+    q_lds_rev(rEs, es[0], d);
+    q_lds_rev(rFs, fs[0], d);
+    q_lds_dbl(sR2, rp[0], d);
+    q_lds_dbl(sO2, eo[0], d);
+    q_lds_dbl(sQ2, fo[0], d);
+    __builtin_amdgcn_wave_barrier();
+    float4 c1[3], c2[2], c3[2];
+    {
+      const float* const a1[3] = {sEs, sFs, sR2};
+      corr_quad<3>(a1, sO2, d, c1);
+      const float* const a2[2] = {sEs, sR2};
+      corr_quad<2>(a2, sQ2, d, c2);
+      const float* const a3[2] = {rEs, rFs};
+      corr_quad<2>(a3, sR2, d, c3);
+    }
+    __builtin_amdgcn_wave_barrier();   // sEs is reused as the stage below
+    const float4 X = c1[0], Y = c1[1], A = c1[2], Z = c2[0], B = c2[1], C = c3[0], D = c3[1];
+    const float praw = score_q<KM>(X, sR2, d, sEs);
+    const float raw0 = score_q<KM>(Y, sR2, d, sEs), raw1 = score_q<KM>(Z, sR2, d, sEs);
+    const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
+    const int v0 = (neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0;   // hole.py:56
+    const int v1 = (neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0;
+    const Accum aR = replica(a.accR, j);
+    if (l < 4)
+      commit_slot(a.accE, sel4(l, s, o, neg0, neg1), sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1),
+                  4 * j + l);
+    else if (l == 4)
+      commit_slot(aR, p, 2 * (v0 + v1), j);
+    if (v0 + v1 == 0) continue;
+    nv += v0 + v1;
+    const float gp = -af_g_given_f(a.af, pf);   // hole.py:66
+    const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
+    const float fv0 = (float)v0, fv1 = (float)v1;
+    float4 cs, co, c0, cq, cr;
+#define SKGE_HC(M)                                                \
+  cs.M = fv0 * (gp * A.M) + fv1 * (gp * A.M + g1 * B.M);          \
+  co.M = fv0 * (gp * C.M + g0 * D.M) + fv1 * (gp * C.M);          \
+  c0.M = g0 * A.M;                                                \
+  cq.M = g1 * C.M;                                                \
+  cr.M = fv0 * (gp * X.M + g0 * Y.M) + fv1 * (gp * X.M + g1 * Z.M);
+    SKGE_HC(x)
+    SKGE_HC(y)
+    SKGE_HC(z)
+    SKGE_HC(w)
+#undef SKGE_HC
+    acc_q<KM>(aR, p, cr, d, sEs);
+    acc_q<KM>(a.accE, s, cs, d, sEs);
+    acc_q<KM>(a.accE, o, co, d, sEs);
+    if (v0) acc_q<KM>(a.accE, neg0, c0, d, sEs);
+    if (v1) acc_q<KM>(a.accE, neg1, cq, d, sEs);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __shared__ int lds_nv;
+  block_count_add(a.nviol, nv, &lds_nv);   // one atomic per workgroup
+}
+
+bool hole_pos_ok(int af, const skge_table_t* ent, const skge_table_t* rel, int d) {
+  return af >= 0 && af <= 3 && d % 4 == 0 && d >= 4 && d <= 256 && ent && rel &&
+         ent->width == d && rel->width == d && ent->acc_mode == SKGE_ACC_F32 &&
+         rel->acc_mode == SKGE_ACC_F32 && ent->acc_replicas <= 1 && ent->acc_sum &&
+         ent->acc_cnt && rel->acc_sum && rel->acc_cnt;
+}
+
+// one batch of the HolE device pair loop (slots: 4 * count entity, count relation)
+int launch_hole_pos(hipStream_t st, int af, const skge_table_t* ent, const skge_table_t* rel,
+                    int d, const int4* rec, const int* rec_n1, long long start, int count,
+                    float margin, int* nviol, int* fold, int* total) {
+  int rc;
+  if ((rc = check_table(ent, "ent", true)) || (rc = check_table(rel, "rel", true)) ||
+      (rc = check_slots(ent, 4ll * count, "ent")) || (rc = check_slots(rel, count, "rel")))
+    return rc;
+  SKGE_CHECK_ARG(hole_pos_ok(af, ent, rel, d), "HolE positive kernel: unsupported tables");
+  HolePosArgs a = {};
+  a.E = ent->param;
+  a.R = rel->param;
+  a.accE = accum_of(ent);
+  a.accR = accum_of(rel);
+  a.rec = rec;
+  a.rec_n1 = rec_n1;
+  a.start = start;
+  a.count = count;
+  a.d = d;
+  a.af = af;
+  a.margin = margin;
+  a.nviol = nviol;
+  a.fold = fold;
+  a.total = total;
+  const int blocks = std::max(1, std::min((count + 3) / 4, 8192));
+  const size_t lds = (size_t)4 * hole_pos_lds_floats(d) * sizeof(float);
+  switch (km_for(d)) {
+    case 1: hipLaunchKernelGGL((k_hole_pos<1>), dim3(blocks), dim3(256), lds, st, a); break;
+    case 2: hipLaunchKernelGGL((k_hole_pos<2>), dim3(blocks), dim3(256), lds, st, a); break;
+    case 3: hipLaunchKernelGGL((k_hole_pos<3>), dim3(blocks), dim3(256), lds, st, a); break;
+    default: hipLaunchKernelGGL((k_hole_pos<4>), dim3(blocks), dim3(256), lds, st, a); break;
+  }
+  SKGE_CHECK_LAUNCH("hole positive kernel");
+  return SKGE_OK;
+}
+
+// ---------------------------------------------------------------------------
 // logistic loss: HolE skge/hole.py:22-42, RESCAL skge/rescal.py:37-76
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void logistic(float y, float score, float* loss_i, float* fs) {

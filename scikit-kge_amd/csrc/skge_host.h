@@ -117,4 +117,10 @@ int launch_epoch_sample(hipStream_t st, const int* trip, long long T, uint64_t s
                         const uint64_t* epoch_key, TripleSet set, int n_ent, int ntries,
                         int4* rec, int* rec_n1);
 
+// skge_grad.hip: HolE pairwise, one positive (both of its pairs) per wave
+bool hole_pos_ok(int af, const skge_table_t* ent, const skge_table_t* rel, int d);
+int launch_hole_pos(hipStream_t st, int af, const skge_table_t* ent, const skge_table_t* rel,
+                    int d, const int4* rec, const int* rec_n1, long long start, int count,
+                    float margin, int* nviol, int* fold, int* total);
+
 }  // namespace skge

@@ -16,6 +16,10 @@
 //
 // The per-batch kernels are the ones of the explicit-pair API, so a device
 // epoch trains exactly like feeding the same pairs through skge_pair_step.
+// Exception: HolE (d % 4 == 0, d <= 256) scores both pairs of a positive in
+// one wave straight from the records (k_hole_pos, skge_grad.hip): the same
+// pairs, contributions and counts, 7 correlations per positive instead of 12.
+#include <cstdlib>
 #include <vector>
 
 #include "skge_host.h"
@@ -56,9 +60,11 @@ __global__ __launch_bounds__(256) void k_pairs_of_records(const int4* __restrict
   }
 }
 
-__global__ void k_pairs_epoch_end(int* nviol, int* nviol_total, uint64_t* ek) {
-  if (nviol_total) *nviol_total += *nviol;
+// nviol2: the second gate word of the HolE positive path (batch parity), or null
+__global__ void k_pairs_epoch_end(int* nviol, int* nviol2, int* nviol_total, uint64_t* ek) {
+  if (nviol_total) *nviol_total += *nviol + (nviol2 ? *nviol2 : 0);
   *nviol = 0;
+  if (nviol2) *nviol2 = 0;
   *ek += 1;
 }
 
@@ -139,11 +145,32 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
     pair_runner_free(r);
     return fail("%s", "hipStreamBeginCapture failed");
   }
+  // HolE with the register-tiled correlations: both pairs of a positive in
+  // one wave straight from the records, 4 entity slots and 1 relation slot per
+  // positive (SKGE_HOLE_PAIRS=1 keeps the explicit pairs).  Its gate words
+  // alternate by batch parity: each batch's kernel folds the previous batch's
+  // word into the epoch total.
+  const char* hp = getenv("SKGE_HOLE_PAIRS");
+  const bool hpos = model == SKGE_HOLE && !(hp && atoi(hp)) && hole_pos_ok(af, ent, rel, d);
+  int* gate[2] = {r->nviol, r->nviol + 32};   // separate 128-B lines
   int rc = launch_epoch_sample(st, trip, (long long)T, seed, epoch_key, ts, ent->rows, ntries,
                                r->rec, r->rec_n1);
   r->nlaunch = 1;
   for (size_t k = 0; k < batches.size() && !rc; ++k) {
     const int count = (int)batches[k].second;
+    if (hpos) {
+      rc = launch_hole_pos(st, af, ent, rel, d, r->rec, r->rec_n1, (long long)batches[k].first,
+                           count, margin, gate[k & 1], gate[(k + 1) & 1], nviol_total);
+      if (!rc) {
+        skge_table_t t[2] = {*ent, *rel};
+        t[0].gate = gate[k & 1];
+        t[1].gate = gate[k & 1];
+        const int ns[2] = {4 * count, count};
+        rc = skge_accum_apply(stream, t, 2, ns);
+      }
+      r->nlaunch += 1;
+      continue;
+    }
     const int blocks = std::max(1, std::min((count + 255) / 256, 1024));
     hipLaunchKernelGGL(k_pairs_of_records, dim3(blocks), dim3(256), 0, st, r->rec, r->rec_n1,
                        (long long)batches[k].first, count, pos, neg, r->nviol, nviol_total);
@@ -157,8 +184,8 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
     r->nlaunch += 1;
   }
   if (!rc) {
-    hipLaunchKernelGGL(k_pairs_epoch_end, dim3(1), dim3(1), 0, st, r->nviol, nviol_total,
-                       epoch_key);
+    hipLaunchKernelGGL(k_pairs_epoch_end, dim3(1), dim3(1), 0, st, r->nviol,
+                       hpos ? r->nviol + 32 : nullptr, nviol_total, epoch_key);
     r->nlaunch += 1;
   }
   hipGraph_t g = nullptr;

@@ -78,7 +78,9 @@ def replay(model, upd, kg, n_ent, nbatches, epochs, seed, ntries):
 
 @pytest.mark.parametrize("kind,d,dense", [("transe_l1", 32, False), ("transe_l2", 24, False),
                                           ("hole", 32, False), ("rescal", 16, False),
-                                          ("hole", 16, True), ("rescal", 8, True)])
+                                          ("hole", 16, True), ("rescal", 8, True),
+                                          ("hole", 100, False), ("hole", 200, False),
+                                          ("hole", 30, False)])
 def test_pair_loop_matches_host_replay(kind, d, dense):
     import skge_amd as S
     from skge_amd.device import DeviceKG, PairLoopRunner
@@ -180,3 +182,31 @@ def test_trainer_device_loop_any_model(kind):
     assert not torch.equal(E0, m.E.data)
     assert np.isfinite(m.E.data.cpu().numpy()).all()
     assert int(m.E.updateCounts.sum()) > 0
+
+
+@pytest.mark.parametrize("d", [32, 200])
+def test_hole_positive_kernel_matches_explicit_pairs(d, monkeypatch):
+    """The HolE pair loop's positive kernel (k_hole_pos: both pairs of a
+    positive per wave) against the explicit-pair kernels (SKGE_HOLE_PAIRS=1)
+    on the same draws: equal violation totals (the scores use the same
+    arithmetic), parameters within the fp32 tolerance."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    n_ent, n_rel, T = 300, 7, 2000
+    xs = make_kg(n_ent, n_rel, T)
+    out = []
+    for pairs in ("0", "1"):
+        monkeypatch.setenv("SKGE_HOLE_PAIRS", pairs)
+        m = make_model("hole", (n_ent, n_ent, n_rel), d)
+        m.add_hyperparam("margin", 0.5)
+        upd = {pid: S.SGD(p, 0.05) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), 7, seed=5)
+        with torch.cuda.stream(r.stream):
+            r.run(2)
+        r.synchronize()
+        out.append((int(r.nviol_total.item()),
+                    {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}))
+    assert out[0][0] == out[1][0] > 0
+    for pid in out[0][1]:
+        np.testing.assert_allclose(out[0][1][pid], out[1][1][pid], rtol=RTOL, atol=ATOL,
+                                   err_msg=pid)

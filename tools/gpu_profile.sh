@@ -6,7 +6,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
 TAG=${TAG:-r01}
-ARGS=${ARGS:---steps 5 --warmup 1 --no-cpu}
+ARGS=${ARGS:---steps 20 --warmup 3 --no-cpu}   # the default bench workload (no CPU leg)
 export TMPDIR=/tmp
 D=gpurun_out/prof_$TAG
 mkdir -p $D
@@ -14,8 +14,8 @@ timeout -k 10 300 python3 bench.py $ARGS > $D/bench.log 2>&1 || { tail $D/bench.
 grep '^{' $D/bench.log > $D/bench.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $D/stats -o run -- python3 bench.py $ARGS > $D/stats.log 2>&1 || exit $?
 grep '^{' $D/stats.log > $D/bench_under_rocprof.json
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d $D/fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $D/fetch.log 2>&1 || exit $?
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv -d $D/write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $D/write.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d $D/fetch -o run -- python3 bench.py $ARGS > $D/fetch.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv -d $D/write -o run -- python3 bench.py $ARGS > $D/write.log 2>&1 || exit $?
 python3 tools/pmc_summary.py $D > $D/pmc.json && cat $D/bench.json && python3 -c "
 import json; d=json.load(open('$D/pmc.json'))
 for k,v in d.items():
