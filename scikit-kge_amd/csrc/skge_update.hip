@@ -396,17 +396,22 @@ template <int K, int MODE, int KR>
 __global__ __launch_bounds__(256) void k_apply(TableDev t0, int n0, TableDev t1, int n1,
                                                int nblk0) {
   __shared__ int lds[1025];
+  int blk = (int)blockIdx.x;
   if (t1.acc.replicas > 1) {
-    if ((int)blockIdx.x >= nblk0) {
-      for (int r = blockIdx.x - nblk0; r < n1; r += gridDim.x - nblk0)
+    // the replicated rows' workgroups come FIRST in dispatch order: each runs
+    // a fold -> update chain, so as the grid's tail they set its length
+    const int nrep = (int)gridDim.x - nblk0;
+    if (blk < nrep) {
+      for (int r = blk; r < n1; r += nrep)
         apply_row_rep_block<MODE, KR>(t1, r, t1.gate == nullptr || *t1.gate != 0, lds);
       return;
     }
+    blk -= nrep;
     n1 = 0;   // table 1 is not a wave-per-slot table
   }
   const int wpb = blockDim.x >> 6;
   const int nw = (t1.acc.replicas > 1 ? nblk0 : gridDim.x) * wpb;
-  for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < n0 + n1; w += nw) {
+  for (int w = blk * wpb + (threadIdx.x >> 6); w < n0 + n1; w += nw) {
     if (w < n0)
       apply_slot<K, MODE>(t0, w);
     else
