@@ -725,6 +725,7 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
     q_lds_dbl(sQ2, fo[0], d);
     __builtin_amdgcn_wave_barrier();
     float4 c1[3], c2[2], c3[2];
+#ifndef SKGE_ABL_HPOS_NO_CORR   // timing-only ablation builds (tools/ablate.sh)
     {
       const float* const a1[3] = {sEs, sFs, sR2};
       corr_quad<3>(a1, sO2, d, c1);
@@ -733,6 +734,9 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
       const float* const a3[2] = {rEs, rFs};
       corr_quad<2>(a3, sR2, d, c3);
     }
+#else
+    c1[0] = c1[1] = c1[2] = c2[0] = c2[1] = c3[0] = c3[1] = eo[0];
+#endif
     __builtin_amdgcn_wave_barrier();   // sEs is reused as the stage below
     const float4 X = c1[0], Y = c1[1], A = c1[2], Z = c2[0], B = c2[1], C = c3[0], D = c3[1];
     const float praw = score_q<KM>(X, sR2, d, sEs);
@@ -763,11 +767,13 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
     SKGE_HC(z)
     SKGE_HC(w)
 #undef SKGE_HC
+#ifndef SKGE_ABL_HPOS_NO_ATOM
     acc_q<KM>(aR, p, cr, d, sEs);
     acc_q<KM>(a.accE, s, cs, d, sEs);
     acc_q<KM>(a.accE, o, co, d, sEs);
     if (v0) acc_q<KM>(a.accE, neg0, c0, d, sEs);
     if (v1) acc_q<KM>(a.accE, neg1, cq, d, sEs);
+#endif
     __builtin_amdgcn_wave_barrier();
   }
   __shared__ int lds_nv;
