@@ -4,15 +4,16 @@
 //
 //   k_epoch_sample (skge_pipeline.hip)  the epoch's permutation and every
 //       negative, one thread per positive: records (s, o, p, s'), o'
+//   k_pairs_of_epoch  every batch's explicit pairs at once, in the reference's
+//       order (the records do not depend on the parameters) -- positive j
+//       gives pair 2j (s-corrupted) and 2j+1 (o-corrupted); a negative the
+//       sampler did not find in ntries draws becomes a SKIPPED pair (positive
+//       relation -1, see skge_pair_grad) -- and clears the batches' gate words
 //   per batch b (the reference's np.split geometry):
-//     k_pairs_of_records  the batch's explicit pairs in the reference's order
-//       -- positive j gives pair 2j (s-corrupted) and 2j+1 (o-corrupted); a
-//       negative the sampler did not find in ntries draws becomes a SKIPPED
-//       pair (positive relation -1, see skge_pair_grad) -- and folds the
-//       previous batch's violation count into the epoch total
 //     skge_pair_step  score + margin test + contributions (+ RESCAL dW) +
 //       segment mean + updater + projection, gated on the batch's violations
-//   k_pairs_epoch_end  last fold, epoch key + 1
+//       (its own gate word)
+//   k_pairs_epoch_end  the gate words' total into the caller's count, key + 1
 //
 // The per-batch kernels are the ones of the explicit-pair API, so a device
 // epoch trains exactly like feeding the same pairs through skge_pair_step.
@@ -27,20 +28,17 @@
 
 namespace skge {
 
-__global__ __launch_bounds__(256) void k_pairs_of_records(const int4* __restrict__ rec,
-                                                          const int* __restrict__ rec_n1,
-                                                          long long start, int count,
-                                                          int* __restrict__ pos,
-                                                          int* __restrict__ neg, int* nviol,
-                                                          int* nviol_total) {
-  const int j0 = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j0 == 0) {   // the previous batch's gate word -> epoch total, then re-arm
-    if (nviol_total) *nviol_total += *nviol;
-    *nviol = 0;
-  }
-  for (int j = j0; j < count; j += gridDim.x * blockDim.x) {
-    const int4 r = rec[start + j];
-    const int n1 = rec_n1[start + j];
+__global__ __launch_bounds__(256) void k_pairs_of_epoch(const int4* __restrict__ rec,
+                                                        const int* __restrict__ rec_n1,
+                                                        long long T, int* __restrict__ pos,
+                                                        int* __restrict__ neg,
+                                                        int* __restrict__ gates, int nb) {
+  for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < T;
+       j += (long long)gridDim.x * blockDim.x) {
+    if (j < nb) gates[j] = 0;
+    if (pos == nullptr) continue;   // HolE positive path: the records are its input
+    const int4 r = rec[j];
+    const int n1 = rec_n1[j];
     int* pp = pos + 6 * (size_t)j;
     int* nn = neg + 6 * (size_t)j;
     // pair 2j: mode 0 corrupts s; pair 2j+1: mode 1 corrupts o (sample.py:41-46)
@@ -60,12 +58,18 @@ __global__ __launch_bounds__(256) void k_pairs_of_records(const int4* __restrict
   }
 }
 
-// nviol2: the second gate word of the HolE positive path (batch parity), or null
-__global__ void k_pairs_epoch_end(int* nviol, int* nviol2, int* nviol_total, uint64_t* ek) {
-  if (nviol_total) *nviol_total += *nviol + (nviol2 ? *nviol2 : 0);
-  *nviol = 0;
-  if (nviol2) *nviol2 = 0;
-  *ek += 1;
+__global__ __launch_bounds__(256) void k_pairs_epoch_end(const int* __restrict__ gates, int nb,
+                                                         int* nviol_total, uint64_t* ek) {
+  __shared__ int part[4];
+  int v = 0;
+  for (int k = threadIdx.x; k < nb; k += blockDim.x) v += gates[k];
+  v = wave_sum_int(v);
+  if (lane_id() == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (nviol_total) *nviol_total += part[0] + part[1] + part[2] + part[3];
+    *ek += 1;
+  }
 }
 
 }  // namespace skge
@@ -78,8 +82,8 @@ struct skge_pair_runner {
   int nlaunch = 0;
   int4* rec = nullptr;
   int* rec_n1 = nullptr;
-  int* pairs = nullptr;   // pos [2*bs][3], then neg [2*bs][3]
-  int* nviol = nullptr;   // the batch's gate word
+  int* pairs = nullptr;   // the epoch's pairs: pos [2T][3], then neg [2T][3]
+  int* nviol = nullptr;   // [nbatches]: each batch's gate word (its violations)
   void* ws = nullptr;
   size_t ws_bytes = 0;
 };
@@ -126,67 +130,68 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
   const int Pmax = (int)(2 * maxb);
   if ((long long)4 * Pmax > ent->touched_cap && ent->acc_touched)
     return fail("%s", "entity accumulator needs 8 * batch_size touched slots");
+  // HolE with the register-tiled correlations: both pairs of a positive in
+  // one wave straight from the records, 4 entity slots and 1 relation slot per
+  // positive (SKGE_HOLE_PAIRS=1 keeps the explicit pairs)
+  const char* hp = getenv("SKGE_HOLE_PAIRS");
+  const bool hpos = model == SKGE_HOLE && !(hp && atoi(hp)) && hole_pos_ok(af, ent, rel, d);
+  const int nb = (int)batches.size();
   skge_pair_runner_t* r = new skge_pair_runner_t();
   r->ws_bytes = skge_pair_step_workspace_bytes(model, Pmax, rel->rows, d);
   if (hipMalloc(&r->rec, (size_t)T * sizeof(int4)) != hipSuccess ||
       hipMalloc(&r->rec_n1, (size_t)T * sizeof(int)) != hipSuccess ||
-      hipMalloc(&r->pairs, (size_t)Pmax * 6 * sizeof(int)) != hipSuccess ||
-      hipMalloc(&r->nviol, 256) != hipSuccess ||
+      (!hpos && hipMalloc(&r->pairs, (size_t)T * 12 * sizeof(int)) != hipSuccess) ||
+      hipMalloc(&r->nviol, (size_t)nb * sizeof(int)) != hipSuccess ||
       (r->ws_bytes && hipMalloc(&r->ws, r->ws_bytes) != hipSuccess) ||
-      hipMemset(r->nviol, 0, 256) != hipSuccess) {
+      hipMemset(r->nviol, 0, (size_t)nb * sizeof(int)) != hipSuccess) {
     pair_runner_free(r);
     return fail("%s", "pair runner: device allocation failed");
   }
   int* pos = r->pairs;
-  int* neg = r->pairs + (size_t)Pmax * 3;
+  int* neg = r->pairs ? r->pairs + (size_t)T * 6 : nullptr;
   const TripleSet ts = triple_set_view(set, set_capacity);
   if (hipStreamSynchronize(st) != hipSuccess ||
       hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
     pair_runner_free(r);
     return fail("%s", "hipStreamBeginCapture failed");
   }
-  // HolE with the register-tiled correlations: both pairs of a positive in
-  // one wave straight from the records, 4 entity slots and 1 relation slot per
-  // positive (SKGE_HOLE_PAIRS=1 keeps the explicit pairs).  Its gate words
-  // alternate by batch parity: each batch's kernel folds the previous batch's
-  // word into the epoch total.
-  const char* hp = getenv("SKGE_HOLE_PAIRS");
-  const bool hpos = model == SKGE_HOLE && !(hp && atoi(hp)) && hole_pos_ok(af, ent, rel, d);
-  int* gate[2] = {r->nviol, r->nviol + 32};   // separate 128-B lines
   int rc = launch_epoch_sample(st, trip, (long long)T, seed, epoch_key, ts, ent->rows, ntries,
                                r->rec, r->rec_n1);
-  r->nlaunch = 1;
-  for (size_t k = 0; k < batches.size() && !rc; ++k) {
-    const int count = (int)batches[k].second;
-    if (hpos) {
-      rc = launch_hole_pos(st, af, ent, rel, d, r->rec, r->rec_n1, (long long)batches[k].first,
-                           count, margin, gate[k & 1], gate[(k + 1) & 1], nviol_total);
-      if (!rc) {
-        skge_table_t t[2] = {*ent, *rel};
-        t[0].gate = gate[k & 1];
-        t[1].gate = gate[k & 1];
-        const int ns[2] = {4 * count, count};
-        rc = skge_accum_apply(stream, t, 2, ns);
-      }
-      r->nlaunch += 1;
-      continue;
-    }
-    const int blocks = std::max(1, std::min((count + 255) / 256, 1024));
-    hipLaunchKernelGGL(k_pairs_of_records, dim3(blocks), dim3(256), 0, st, r->rec, r->rec_n1,
-                       (long long)batches[k].first, count, pos, neg, r->nviol, nviol_total);
+  if (!rc) {
+    const int64_t blocks = std::max((int64_t)1, std::min((T + 255) / 256, (int64_t)4096));
+    hipLaunchKernelGGL(k_pairs_of_epoch, dim3((unsigned)blocks), dim3(256), 0, st, r->rec,
+                       r->rec_n1, (long long)T, pos, neg, r->nviol, nb);
     if (hipGetLastError() != hipSuccess) {
       set_error("pairs launch failed");
       rc = SKGE_EHIP;
-      break;
     }
-    rc = skge_pair_step(stream, model, af, ent, rel, d, pos, neg, 2 * count, margin, r->ws,
-                        r->ws_bytes, r->nviol);
-    r->nlaunch += 1;
+  }
+  for (int k = 0; k < nb && !rc; ++k) {
+    const long long start = batches[k].first;
+    const int count = (int)batches[k].second;
+    int* gate = r->nviol + k;
+    if (hpos) {
+      rc = launch_hole_pos(st, af, ent, rel, d, r->rec, r->rec_n1, start, count, margin, gate,
+                           nullptr, nullptr);
+      if (!rc) {
+        skge_table_t t[2] = {*ent, *rel};
+        t[0].gate = gate;
+        t[1].gate = gate;
+        const int ns[2] = {4 * count, count};
+        rc = skge_accum_apply(stream, t, 2, ns);
+      }
+    } else {
+      rc = skge_pair_step(stream, model, af, ent, rel, d, pos + 6 * start, neg + 6 * start,
+                          2 * count, margin, r->ws, r->ws_bytes, gate);
+    }
   }
   if (!rc) {
-    hipLaunchKernelGGL(k_pairs_epoch_end, dim3(1), dim3(1), 0, st, r->nviol,
-                       hpos ? r->nviol + 32 : nullptr, nviol_total, epoch_key);
-    r->nlaunch += 1;
+    hipLaunchKernelGGL(k_pairs_epoch_end, dim3(1), dim3(256), 0, st, r->nviol, nb, nviol_total,
+                       epoch_key);
+    if (hipGetLastError() != hipSuccess) {
+      set_error("epoch end launch failed");
+      rc = SKGE_EHIP;
+    }
   }
   hipGraph_t g = nullptr;
   hipError_t e = hipStreamEndCapture(st, &g);
