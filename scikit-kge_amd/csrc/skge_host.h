@@ -124,3 +124,10 @@ int launch_hole_pos(hipStream_t st, int af, const skge_table_t* ent, const skge_
                     float margin, int* nviol, int* fold, int* total);
 
 }  // namespace skge
+
+// skge_rescal.hip / skge_update.hip: the device pair loop's RESCAL batch
+bool rescal_pair_mfma_selected(int d, int M);
+int skge_rescal_pos_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
+                              const skge_table_t* rel, int d, const int* pos, const int* neg,
+                              const int4* rec, const int* rec_n1, long long start, int count,
+                              float margin, void* workspace, size_t ws_bytes, int* nviol);

@@ -32,13 +32,29 @@ __global__ __launch_bounds__(256) void k_pairs_of_epoch(const int4* __restrict__
                                                         const int* __restrict__ rec_n1,
                                                         long long T, int* __restrict__ pos,
                                                         int* __restrict__ neg,
-                                                        int* __restrict__ gates, int nb) {
+                                                        int* __restrict__ gates, int nb,
+                                                        int dedup) {
   for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < T;
        j += (long long)gridDim.x * blockDim.x) {
     if (j < nb) gates[j] = 0;
     if (pos == nullptr) continue;   // HolE positive path: the records are its input
     const int4 r = rec[j];
     const int n1 = rec_n1[j];
+    if (dedup) {   // RESCAL: each positive once ([T][3]), its two negatives ([T][2][3])
+      const bool k0 = r.w >= 0, k1 = n1 >= 0;
+      int* pp = pos + 3 * (size_t)j;
+      int* nn = neg + 6 * (size_t)j;
+      pp[0] = r.x;
+      pp[1] = r.y;
+      pp[2] = (k0 || k1) ? r.z : -1;
+      nn[0] = k0 ? r.w : r.x;
+      nn[1] = r.y;
+      nn[2] = k0 ? r.z : -1;
+      nn[3] = r.x;
+      nn[4] = k1 ? n1 : r.y;
+      nn[5] = k1 ? r.z : -1;
+      continue;
+    }
     int* pp = pos + 6 * (size_t)j;
     int* nn = neg + 6 * (size_t)j;
     // pair 2j: mode 0 corrupts s; pair 2j+1: mode 1 corrupts o (sample.py:41-46)
@@ -135,6 +151,12 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
   // positive (SKGE_HOLE_PAIRS=1 keeps the explicit pairs)
   const char* hp = getenv("SKGE_HOLE_PAIRS");
   const bool hpos = model == SKGE_HOLE && !(hp && atoi(hp)) && hole_pos_ok(af, ent, rel, d);
+  // RESCAL on the matrix cores: each positive once in the GEMMs and dW, both
+  // of its pairs per scatter wave (k_rescal_pos_scatter; SKGE_RESCAL_PAIRS=1
+  // keeps the explicit pairs)
+  const char* rp = getenv("SKGE_RESCAL_PAIRS");
+  const bool rpos = model == SKGE_RESCAL && !(rp && atoi(rp)) &&
+                    rescal_pair_mfma_selected(d, rel->rows);
   const int nb = (int)batches.size();
   skge_pair_runner_t* r = new skge_pair_runner_t();
   r->ws_bytes = skge_pair_step_workspace_bytes(model, Pmax, rel->rows, d);
@@ -160,7 +182,7 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
   if (!rc) {
     const int64_t blocks = std::max((int64_t)1, std::min((T + 255) / 256, (int64_t)4096));
     hipLaunchKernelGGL(k_pairs_of_epoch, dim3((unsigned)blocks), dim3(256), 0, st, r->rec,
-                       r->rec_n1, (long long)T, pos, neg, r->nviol, nb);
+                       r->rec_n1, (long long)T, pos, neg, r->nviol, nb, rpos ? 1 : 0);
     if (hipGetLastError() != hipSuccess) {
       set_error("pairs launch failed");
       rc = SKGE_EHIP;
@@ -179,6 +201,16 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
         t[1].gate = gate;
         const int ns[2] = {4 * count, count};
         rc = skge_accum_apply(stream, t, 2, ns);
+      }
+    } else if (rpos) {
+      rc = skge_rescal_pos_grad_mfma(st, af, ent, rel, d, pos + 3 * start, neg + 6 * start,
+                                     r->rec, r->rec_n1, start, count, margin, r->ws, r->ws_bytes,
+                                     gate);
+      if (!rc) {   // the entity table's apply (W was updated by the dW kernel)
+        skge_table_t te = *ent;
+        te.gate = gate;
+        const int ns = 4 * count;
+        rc = skge_accum_apply(stream, &te, 1, &ns);
       }
     } else {
       rc = skge_pair_step(stream, model, af, ent, rel, d, pos + 6 * start, neg + 6 * start,

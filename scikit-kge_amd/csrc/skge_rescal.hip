@@ -563,6 +563,84 @@ __global__ __launch_bounds__(256) void k_rescal_scatter(const int* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// The device pair loop's form: one wave per POSITIVE and both of its pairs.
+// The batch's triples are deduplicated -- list a holds each positive once
+// (item j), list b its two negatives (items count + 2j: (s', o, p), count +
+// 2j + 1: (s, o', p)) -- so the GEMMs and dW see 3 items per positive instead
+// of the explicit pairs' 4 (the positive appears in both pairs).  Scores come
+// from the same per-item partial sums (bitwise the pair path's); dW gets the
+// positive once with coefficient gp (k0 + k1) (rescal.py:113-125 sums gp over
+// every pair it is in); the entity rows get the two pairs' contributions
+// (rescal.py:296-301) summed per row, with the occurrence counts of the
+// lists (s: v0 + 2 v1, o: 2 v0 + v1, s': v0, o': v1; slots 4j..4j+3).
+// ---------------------------------------------------------------------------
+template <int KM>
+__global__ __launch_bounds__(256) void k_rescal_pos_scatter(const int4* __restrict__ rec,
+                                                            const int* __restrict__ rec_n1,
+                                                            long long start, int count, int d,
+                                                            int af, float margin, RescalWs ws,
+                                                            Accum accE, int* nviol) {
+  const int wpb = blockDim.x >> 6, l = lane_id(), ncb = (d + GC - 1) / GC;
+  int nv = 0;
+  for (int j = blockIdx.x * wpb + (threadIdx.x >> 6); j < count; j += gridDim.x * wpb) {
+    const int4 r4 = rec[start + j];
+    const int s = __builtin_amdgcn_readfirstlane(r4.x), o = __builtin_amdgcn_readfirstlane(r4.y);
+    const int neg0 = __builtin_amdgcn_readfirstlane(r4.w);
+    const int neg1 = __builtin_amdgcn_readfirstlane(rec_n1[start + j]);
+    const int k0 = neg0 >= 0 ? 1 : 0, k1 = neg1 >= 0 ? 1 : 0;
+    const int i0 = count + 2 * j, i1 = i0 + 1;   // the negatives' items
+    float praw = 0.0f, raw0 = 0.0f, raw1 = 0.0f;
+    for (int q = 0; q < ncb; ++q) {   // fixed order: deterministic
+      praw += ws.spart[(size_t)j * ncb + q];
+      raw0 += ws.spart[(size_t)i0 * ncb + q];
+      raw1 += ws.spart[(size_t)i1 * ncb + q];
+    }
+    const float pf = af_f(af, praw), f0 = af_f(af, raw0), f1 = af_f(af, raw1);
+    const float gp = -af_g_given_f(af, pf);   // rescal.py:275 (all pairs)
+    const float g0 = af_g_given_f(af, f0), g1 = af_g_given_f(af, f1);
+    if (l == 0 && k0 + k1 > 0) {
+      ws.coef[ws.bpos[j]] = gp * (float)(k0 + k1);
+      if (k0) ws.coef[ws.bpos[i0]] = g0;
+      if (k1) ws.coef[ws.bpos[i1]] = g1;
+    }
+    const int v0 = (k0 && f0 + margin > pf) ? 1 : 0;   // rescal.py:269
+    const int v1 = (k1 && f1 + margin > pf) ? 1 : 0;
+    if (l < 4)
+      commit_slot(accE, sel4(l, s, o, neg0, neg1), sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1),
+                  4 * j + l);
+    if (v0 + v1 == 0) continue;
+    nv += v0 + v1;
+    // every row loaded (stale rows of absent negatives are not used)
+    float wep[KM], ewp[KM], we0[KM], ew0[KM], we1[KM], ew1[KM], x[KM];
+    load_row<KM>(ws.WE, j, d, wep);
+    load_row<KM>(ws.EW, j, d, ewp);
+    load_row<KM>(ws.WE, i0, d, we0);
+    load_row<KM>(ws.EW, i0, d, ew0);
+    load_row<KM>(ws.WE, i1, d, we1);
+    load_row<KM>(ws.EW, i1, d, ew1);
+    const float fv0 = (float)v0, fv1 = (float)v1;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) x[k] = fv0 * (gp * wep[k]) + fv1 * (gp * wep[k] + g1 * we1[k]);
+    acc_row<KM>(accE, s, x, d);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) x[k] = fv0 * (gp * ewp[k] + g0 * ew0[k]) + fv1 * (gp * ewp[k]);
+    acc_row<KM>(accE, o, x, d);
+    if (v0) {
+#pragma unroll
+      for (int k = 0; k < KM; ++k) x[k] = g0 * we0[k];
+      acc_row<KM>(accE, neg0, x, d);
+    }
+    if (v1) {
+#pragma unroll
+      for (int k = 0; k < KM; ++k) x[k] = g1 * ew1[k];
+      acc_row<KM>(accE, neg1, x, d);
+    }
+  }
+  __shared__ int lds_nv;
+  if (nviol) block_count_add(nviol, nv, &lds_nv);
+}
+
+// ---------------------------------------------------------------------------
 // logistic loss + entity contributions, one wave per labelled triple
 // (rescal.py:37-76): fs = -y sigmoid(-y f); E[s] += fs WE, E[o] += fs EW
 // ---------------------------------------------------------------------------
@@ -877,6 +955,36 @@ int skge_rescal_pair_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
                  aE, pscore, nscore, nviol)
   rescal_wgrad_launch(st, ent, rel, d, ws, apply_w, nviol);
   SKGE_CHECK_LAUNCH("rescal mfma pair grad");
+  return SKGE_OK;
+}
+
+// the device pair loop's RESCAL batch (k_rescal_pos_scatter): lists a = the
+// count positives, b = their 2 count negatives (k_pairs_of_epoch's RESCAL
+// form), records for the scatter; W updated in place, entity rows accumulated
+int skge_rescal_pos_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
+                              const skge_table_t* rel, int d, const int* pos, const int* neg,
+                              const int4* rec, const int* rec_n1, long long start, int count,
+                              float margin, void* workspace, size_t ws_bytes, int* nviol) {
+  int rc;
+  if ((rc = check_table(ent, "ent", true)) || (rc = check_table(rel, "rel", false)) ||
+      (rc = check_f32(ent, "ent")) || (rc = check_f32(rel, "rel")) ||
+      (rc = check_single(ent, "ent")) || (rc = check_single(rel, "rel")) ||
+      (rc = check_slots(ent, 4ll * count, "ent")) || (rc = check_slots(rel, rel->rows, "W")))
+    return rc;
+  SKGE_CHECK_ARG(ent->width == d && rel->width == d * d, "RESCAL table widths");
+  SKGE_CHECK_ARG(af >= 0 && af <= 3, "unknown activation %d", af);
+  SKGE_CHECK_ARG(rel->opt == SKGE_SGD || rel->state, "AdaGrad needs state");
+  SKGE_CHECK_ARG(nviol, "the fused W update is gated on nviol");
+  RescalWs ws;
+  const size_t need = rescal_ws_layout(3 * count, rel->rows, d, workspace, &ws);
+  SKGE_CHECK_ARG(workspace && ws_bytes >= need, "RESCAL workspace needs %zu bytes", need);
+  rc = rescal_front(st, ent, rel, d, pos, count, neg, 3 * count, ws);
+  if (rc) return rc;
+  const int blocks = std::max(1, std::min((count + 3) / 4, 16384));
+  SKGE_KM_SWITCH(k_rescal_pos_scatter, dim3(blocks), dim3(256), 0, st, rec, rec_n1, start, count,
+                 d, af, margin, ws, accum_of(ent), nviol)
+  rescal_wgrad_launch(st, ent, rel, d, ws, true, nviol);
+  SKGE_CHECK_LAUNCH("rescal positive grad");
   return SKGE_OK;
 }
 

@@ -884,6 +884,7 @@ static bool rescal_use_mfma(int d, int M) {
   static const bool valu = getenv("SKGE_RESCAL_VALU") && atoi(getenv("SKGE_RESCAL_VALU")) != 0;
   return !valu && skge_rescal_mfma_ok(d, M);
 }
+bool rescal_pair_mfma_selected(int d, int M) { return rescal_use_mfma(d, M); }
 
 extern "C" int skge_device_error(void* stream, int reset) {
   int v = 0;

@@ -210,3 +210,31 @@ def test_hole_positive_kernel_matches_explicit_pairs(d, monkeypatch):
     for pid in out[0][1]:
         np.testing.assert_allclose(out[0][1][pid], out[1][1][pid], rtol=RTOL, atol=ATOL,
                                    err_msg=pid)
+
+
+@pytest.mark.parametrize("d", [16, 64])
+def test_rescal_positive_path_matches_explicit_pairs(d, monkeypatch):
+    """The RESCAL pair loop's deduplicated form (each positive once in the
+    GEMMs and dW, both pairs per scatter wave) against the explicit pairs
+    (SKGE_RESCAL_PAIRS=1) on the same draws: equal violation totals (the scores
+    are the same per-item sums), parameters within the fp32 tolerance."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    n_ent, n_rel, T = 300, 7, 2000
+    xs = make_kg(n_ent, n_rel, T)
+    out = []
+    for pairs in ("0", "1"):
+        monkeypatch.setenv("SKGE_RESCAL_PAIRS", pairs)
+        m = make_model("rescal", (n_ent, n_ent, n_rel), d)
+        m.add_hyperparam("margin", 0.5)
+        upd = {pid: S.SGD(p, 0.05) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), 7, seed=5)
+        with torch.cuda.stream(r.stream):
+            r.run(2)
+        r.synchronize()
+        out.append((int(r.nviol_total.item()),
+                    {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}))
+    assert out[0][0] == out[1][0] > 0
+    for pid in out[0][1]:
+        np.testing.assert_allclose(out[0][1][pid], out[1][1][pid], rtol=RTOL, atol=ATOL,
+                                   err_msg=pid)
