@@ -796,6 +796,9 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
     }
     const int m = min(WG_CH, cnt - b * WG_CH);   // items past m are zero (coef 0)
     // A[row i][k = item] = coef Es[item][i], B[k = item][col j] = Eo[item][j]
+#ifdef SKGE_ABL_WG_NOMFMA   // timing-only ablation (tools/ablate.sh): no contraction
+    if (m < 0)
+#endif
     for (int k0 = 0; k0 < m; k0 += 4) {
       const int ik = k0 + (l >> 4);
       const float a = sEs[buf][ik][16 * wave + (l & 15)];
@@ -823,6 +826,14 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
       if (in[e]) accW.sum[os[e]] = acc[e >> 2][e & 3];
     return;
   }
+#ifdef SKGE_ABL_WG_NOAPPLY   // timing-only ablation: dW written, W not updated
+  if (os[0] != (size_t)-1) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      if (in[e]) accW.sum[os[e]] = acc[e >> 2][e & 3];
+    return;
+  }
+#endif
   // same step as k_apply_wide (skge/param.py:115-155); every load of the
   // tile issued before any of it is used
   const float div = wa.fdiv > 0.0f ? wa.fdiv : (float)cnt;
