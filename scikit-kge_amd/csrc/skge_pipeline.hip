@@ -266,6 +266,17 @@ __device__ __forceinline__ void rel_row(const RelTab& t, int row, int d, int rd,
 
 __device__ __forceinline__ unsigned long long now_10ns() { return __builtin_amdgcn_s_memrealtime(); }
 
+// A kernel argument made opaque to the compiler (kept in SGPRs, or spilled to
+// VGPR lanes): under SGPR pressure hipcc otherwise re-loads argument fields
+// from the kernarg segment where they are used, and the scoring wave's
+// scatter section paid one dependent scalar-memory round trip per pointer.
+template <typename T>
+__device__ __forceinline__ T* opaque_ptr(T* p) {
+  unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  asm volatile("" : "+s"(v));
+  return reinterpret_cast<T*>(v);
+}
+
 #ifdef SKGE_PIPE_WAVES_PER_EU
 #define SKGE_PIPE_OCC __attribute__((amdgpu_waves_per_eu(SKGE_PIPE_WAVES_PER_EU, 8)))
 #else
@@ -337,6 +348,11 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
     return;
   }
   // ---- B role: score batch b, scatter into accumulator copies cp / ra_cur ----
+  int* const cnt_cp = opaque_ptr(a.E.cnt[cp]);
+  int* const tch_cp = opaque_ptr(a.E.touched[cp]);
+  int* const pend_cp = opaque_ptr(a.E.pend[cp]);
+  unsigned long long* const racc = opaque_ptr(a.R.acc[ra_cur]);
+  unsigned long long* const esum = opaque_ptr(a.E.sum[cp]);
   int nv = 0;
   for (int w = blk_b * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
     const long long j = a.start + w;
@@ -414,10 +430,10 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
       const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
       const int rE = sel4(l, s, o, neg0, neg1);
       if (l < 4) {
-        commit_slot(a.E.cnt[cp], a.E.touched[cp], rE, cE, 4 * w + l);
-        if (cE > 0) a.E.pend[cp][rE] = g;
+        commit_slot(cnt_cp, tch_cp, rE, cE, 4 * w + l);
+        if (cE > 0) pend_cp[rE] = g;
       } else if (l == 4 && v0 + v1 > 0) {
-        atomicAdd(a.R.acc[ra_cur] + (size_t)p * a.R.rw + nq, (unsigned long long)(2 * (v0 + v1)));
+        atomicAdd(racc + (size_t)p * a.R.rw + nq, (unsigned long long)(2 * (v0 + v1)));
       }
     }
     if (v0 + v1 > 0) {
@@ -439,13 +455,13 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
 #undef SKGE_CO
       }
       Accum aE, aR;
-      aE.sum = reinterpret_cast<float*>(a.E.sum[cp]);
+      aE.sum = reinterpret_cast<float*>(esum);
       acc_row4_i16<KQ>(aE, s, cs, d);
       acc_row4_i16<KQ>(aE, o, co, d);
       if (v0) acc_row4_i16<KQ>(aE, neg0, c0, d);
       if (v1) acc_row4_i16<KQ>(aE, neg1, c1, d);
       // relation sums: rows of rw words (acc_row4_i16 indexes rows of d/4 words)
-      aR.sum = reinterpret_cast<float*>(a.R.acc[ra_cur] + (size_t)p * a.R.rw);
+      aR.sum = reinterpret_cast<float*>(racc + (size_t)p * a.R.rw);
       acc_row4_i16<KQ>(aR, 0, cr, d);
     }
     if (a.trace) {   // stamp after issue (no drain: the trace must not slow the launch)
