@@ -179,11 +179,15 @@ def batch_sizes(T, nbatches):
 class PairLoopRunner(object):
     """Native hipGraph epoch of the device pair loop for any model
     (skge_pair_runner_*, csrc/skge_pairloop.hip): the epoch's permutation and
-    negatives drawn on the device (the same keyed draws as EpochRunner), then
-    per batch the explicit pairs and one skge_pair_step -- the kernels of the
-    explicit-pair path, so a device epoch trains like feeding those pairs to
-    model._pairwise_step.  The per-row counters (updateCounts, TransE
-    violations) are kept as on that path."""
+    negatives drawn on the device (the same keyed draws as EpochRunner), every
+    batch's explicit pairs built once per epoch, then per batch one
+    skge_pair_step -- the kernels of the explicit-pair path, so a device epoch
+    trains like feeding those pairs to model._pairwise_step.  HolE and RESCAL
+    (MFMA) run both pairs of a positive together instead (k_hole_pos,
+    k_rescal_pos_scatter: the same pairs, contributions and counts; the env
+    switches SKGE_HOLE_PAIRS=1 / SKGE_RESCAL_PAIRS=1 select the explicit
+    pairs).  The per-row counters (updateCounts, TransE violations) are kept
+    as on that path."""
 
     pipelined = False
 
