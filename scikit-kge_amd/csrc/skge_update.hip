@@ -181,22 +181,27 @@ __device__ __forceinline__ void apply_row(const TableDev& t, int row, bool upd) 
   }
 }
 
-// ACC_I16X4 form of apply_row: the accumulator holds exact integer sums,
-// four per qword; rows in the quad layout (see load_row4): one 16-byte load /
-// store per lane per 1 KB of row
+// (the accumulator holds exact integer sums, four per qword)
+// ACC_I16X4 form of apply_row, in two halves so one wave can keep several
+// rows' claims and loads in flight (apply_slots2_i16): i16_load claims row
+// (lane 0 swaps its count out) and loads its packed sums, parameters and
+// state in the same memory round trip; i16_finish applies the update if the
+// claim was won.  Rows in the quad layout (see load_row4): one 16-byte load /
+// store per lane per 1 KB of row.
 template <int KQ>
-__device__ __forceinline__ void apply_row_i16(const TableDev& t, int row, bool upd) {
+__device__ __forceinline__ void i16_load(const TableDev& t, int row, int& c,
+                                         unsigned long long (&sv)[KQ], float4 (&p)[KQ],
+                                         float4 (&a)[KQ]) {
   const int l = lane_id();
   const int w = t.width, nq = w >> 2;
-  int c = 0;
-  if (l == 0) c = atomicExch(t.acc.cnt + row, 0);
+  c = 0;
+  if (l == 0 && row >= 0) c = atomicExch(t.acc.cnt + row, 0);
+  row = row >= 0 ? row : 0;   // a stale (-1) row still loads from a valid address
   unsigned long long* __restrict__ srow =
       reinterpret_cast<unsigned long long*>(t.acc.sum) + (size_t)row * nq;
   float4* __restrict__ prow = reinterpret_cast<float4*>(t.P + (size_t)row * w);
   float4* __restrict__ arow = t.A ? reinterpret_cast<float4*>(t.A + (size_t)row * w) : nullptr;
   const bool ada = t.opt == OPT_ADAGRAD;
-  unsigned long long sv[KQ];
-  float4 p[KQ], a[KQ];
 #pragma unroll
   for (int m = 0; m < KQ; ++m) {
     const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
@@ -204,6 +209,19 @@ __device__ __forceinline__ void apply_row_i16(const TableDev& t, int row, bool u
     p[m] = prow[qc];
     a[m] = ada ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
+}
+
+template <int KQ>
+__device__ __forceinline__ void i16_finish(const TableDev& t, int row, bool upd, int c,
+                                           unsigned long long (&sv)[KQ], float4 (&p)[KQ],
+                                           float4 (&a)[KQ]) {
+  const int l = lane_id();
+  const int w = t.width, nq = w >> 2;
+  unsigned long long* __restrict__ srow =
+      reinterpret_cast<unsigned long long*>(t.acc.sum) + (size_t)row * nq;
+  float4* __restrict__ prow = reinterpret_cast<float4*>(t.P + (size_t)row * w);
+  float4* __restrict__ arow = t.A ? reinterpret_cast<float4*>(t.A + (size_t)row * w) : nullptr;
+  const bool ada = t.opt == OPT_ADAGRAD;
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row, or a stale slot
   if (upd && ada && t.ucnt && l == 0) t.ucnt[row] += 1;   // param.py:149-150
@@ -257,6 +275,34 @@ __device__ __forceinline__ void apply_row_i16(const TableDev& t, int row, bool u
       }
     }
   }
+}
+
+
+template <int KQ>
+__device__ __forceinline__ void apply_row_i16(const TableDev& t, int row, bool upd) {
+  int c;
+  unsigned long long sv[KQ];
+  float4 p[KQ], a[KQ];
+  i16_load<KQ>(t, row, c, sv, p, a);
+  i16_finish<KQ>(t, row, upd, c, sv, p, a);
+}
+
+// two slot-recorded rows per wave, both rows' claims and loads in flight
+// together (a slot-per-wave apply is bound by its claim -> load -> store
+// chain, not by bandwidth, on large random tables); row -1 = empty slot
+template <int KQ>
+__device__ __forceinline__ void apply_slots2_i16(const TableDev& t, int s0, int s1) {
+  const int r0 = __builtin_amdgcn_readfirstlane(t.acc.touched[s0]);
+  const int r1 = s1 >= 0 ? __builtin_amdgcn_readfirstlane(t.acc.touched[s1]) : -1;
+  if (r0 < 0 && r1 < 0) return;
+  const bool upd = t.gate == nullptr || *t.gate != 0;
+  int c0, c1;
+  unsigned long long v0[KQ], v1[KQ];
+  float4 p0[KQ], a0[KQ], p1[KQ], a1[KQ];
+  i16_load<KQ>(t, r0, c0, v0, p0, a0);
+  i16_load<KQ>(t, r1, c1, v1, p1, a1);
+  if (r0 >= 0) i16_finish<KQ>(t, r0, upd, c0, v0, p0, a0);
+  if (r1 >= 0) i16_finish<KQ>(t, r1, upd, c1, v1, p1, a1);
 }
 
 // Dense table with replicated accumulators: one WORKGROUP per row.  Its 256
@@ -411,11 +457,16 @@ __global__ __launch_bounds__(256) void k_apply(TableDev t0, int n0, TableDev t1,
   }
   const int wpb = blockDim.x >> 6;
   const int nw = (t1.acc.replicas > 1 ? nblk0 : gridDim.x) * wpb;
-  for (int w = blk * wpb + (threadIdx.x >> 6); w < n0 + n1; w += nw) {
-    if (w < n0)
-      apply_slot<K, MODE>(t0, w);
+  // a slot-recorded packed table 0 is applied two slots per wave
+  const bool two = MODE == ACC_I16X4 && t0.acc.touched != nullptr;
+  const int w0 = two ? (n0 + 1) / 2 : n0;
+  for (int w = blk * wpb + (threadIdx.x >> 6); w < w0 + n1; w += nw) {
+    if (w >= w0)
+      apply_slot<K, MODE>(t1, w - w0);
+    else if (two)
+      apply_slots2_i16<K>(t0, 2 * w, 2 * w + 1 < n0 ? 2 * w + 1 : -1);
     else
-      apply_slot<K, MODE>(t1, w - n0);
+      apply_slot<K, MODE>(t0, w);
   }
 }
 
@@ -796,12 +847,15 @@ extern "C" int skge_accum_apply(void* stream, const skge_table_t* tables, int nt
     const int mode = tables[i >= 0 ? i : j].acc_mode;
     const int na = i >= 0 ? slots_of(i) : 0;
     const int nb = j >= 0 ? slots_of(j) : 0;
+    // waves of table i: two slots per wave for a slot-recorded packed table (k_apply)
+    const int wa = (i >= 0 && tables[i].acc_mode == SKGE_ACC_I16X4 && tables[i].acc_touched)
+                       ? (na + 1) / 2 : na;
     int nblk0, grid;
     if (j >= 0 && reps(j) > 1) {
-      nblk0 = std::max(1, std::min((na + 3) / 4, 16384));
+      nblk0 = std::max(1, std::min((wa + 3) / 4, 16384));
       grid = nblk0 + std::min(nb, 4096);
     } else {
-      nblk0 = grid = grid_for_waves((long long)na + nb);
+      nblk0 = grid = grid_for_waves((long long)wa + nb);
     }
     TableDev b = j >= 0 ? table_dev(tables + j) : table_dev(tables + i);
     TableDev a = i >= 0 ? table_dev(tables + i) : b;
