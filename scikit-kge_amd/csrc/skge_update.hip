@@ -183,7 +183,7 @@ __device__ __forceinline__ void apply_row(const TableDev& t, int row, bool upd) 
 
 // (the accumulator holds exact integer sums, four per qword)
 // ACC_I16X4 form of apply_row, in two halves so one wave can keep several
-// rows' claims and loads in flight (apply_slots2_i16): i16_load claims row
+// rows' claims and loads in flight (apply_slots_i16): i16_load claims row
 // (lane 0 swaps its count out) and loads its packed sums, parameters and
 // state in the same memory round trip; i16_finish applies the update if the
 // claim was won.  Rows in the quad layout (see load_row4): one 16-byte load /
@@ -287,22 +287,35 @@ __device__ __forceinline__ void apply_row_i16(const TableDev& t, int row, bool u
   i16_finish<KQ>(t, row, upd, c, sv, p, a);
 }
 
-// two slot-recorded rows per wave, both rows' claims and loads in flight
-// together (a slot-per-wave apply is bound by its claim -> load -> store
-// chain, not by bandwidth, on large random tables); row -1 = empty slot
+// APPLY_SLOTS slot-recorded rows per wave, all their claims and loads in
+// flight together; row -1 = empty slot.  Measured on config 5 (|E| = 50M,
+// d = 512) in one run: one slot per wave is fastest -- the chip already has
+// enough waves in flight, and a multi-row wave holds its slot for the
+// slowest of its rows -- so the default is 1.
+#ifndef SKGE_APPLY_SLOTS
+#define SKGE_APPLY_SLOTS 1   // A/B on config 5 (same run): 1 slot 302 us, 2 slots 323, 4 slots 347
+#endif
+constexpr int APPLY_SLOTS = SKGE_APPLY_SLOTS;
+
 template <int KQ>
-__device__ __forceinline__ void apply_slots2_i16(const TableDev& t, int s0, int s1) {
-  const int r0 = __builtin_amdgcn_readfirstlane(t.acc.touched[s0]);
-  const int r1 = s1 >= 0 ? __builtin_amdgcn_readfirstlane(t.acc.touched[s1]) : -1;
-  if (r0 < 0 && r1 < 0) return;
+__device__ __forceinline__ void apply_slots_i16(const TableDev& t, int s0, int n) {
+  int r[APPLY_SLOTS];
+  bool any = false;
+#pragma unroll
+  for (int k = 0; k < APPLY_SLOTS; ++k) {
+    r[k] = s0 + k < n ? __builtin_amdgcn_readfirstlane(t.acc.touched[s0 + k]) : -1;
+    any = any || r[k] >= 0;
+  }
+  if (!any) return;
   const bool upd = t.gate == nullptr || *t.gate != 0;
-  int c0, c1;
-  unsigned long long v0[KQ], v1[KQ];
-  float4 p0[KQ], a0[KQ], p1[KQ], a1[KQ];
-  i16_load<KQ>(t, r0, c0, v0, p0, a0);
-  i16_load<KQ>(t, r1, c1, v1, p1, a1);
-  if (r0 >= 0) i16_finish<KQ>(t, r0, upd, c0, v0, p0, a0);
-  if (r1 >= 0) i16_finish<KQ>(t, r1, upd, c1, v1, p1, a1);
+  int c[APPLY_SLOTS];
+  unsigned long long v[APPLY_SLOTS][KQ];
+  float4 p[APPLY_SLOTS][KQ], a[APPLY_SLOTS][KQ];
+#pragma unroll
+  for (int k = 0; k < APPLY_SLOTS; ++k) i16_load<KQ>(t, r[k], c[k], v[k], p[k], a[k]);
+#pragma unroll
+  for (int k = 0; k < APPLY_SLOTS; ++k)
+    if (r[k] >= 0) i16_finish<KQ>(t, r[k], upd, c[k], v[k], p[k], a[k]);
 }
 
 // Dense table with replicated accumulators: one WORKGROUP per row.  Its 256
@@ -457,14 +470,14 @@ __global__ __launch_bounds__(256) void k_apply(TableDev t0, int n0, TableDev t1,
   }
   const int wpb = blockDim.x >> 6;
   const int nw = (t1.acc.replicas > 1 ? nblk0 : gridDim.x) * wpb;
-  // a slot-recorded packed table 0 is applied two slots per wave
+  // a slot-recorded packed table 0 is applied APPLY_SLOTS slots per wave
   const bool two = MODE == ACC_I16X4 && t0.acc.touched != nullptr;
-  const int w0 = two ? (n0 + 1) / 2 : n0;
+  const int w0 = two ? (n0 + APPLY_SLOTS - 1) / APPLY_SLOTS : n0;
   for (int w = blk * wpb + (threadIdx.x >> 6); w < w0 + n1; w += nw) {
     if (w >= w0)
       apply_slot<K, MODE>(t1, w - w0);
     else if (two)
-      apply_slots2_i16<K>(t0, 2 * w, 2 * w + 1 < n0 ? 2 * w + 1 : -1);
+      apply_slots_i16<K>(t0, APPLY_SLOTS * w, n0);
     else
       apply_slot<K, MODE>(t0, w);
   }
@@ -847,9 +860,9 @@ extern "C" int skge_accum_apply(void* stream, const skge_table_t* tables, int nt
     const int mode = tables[i >= 0 ? i : j].acc_mode;
     const int na = i >= 0 ? slots_of(i) : 0;
     const int nb = j >= 0 ? slots_of(j) : 0;
-    // waves of table i: two slots per wave for a slot-recorded packed table (k_apply)
+    // waves of table i: APPLY_SLOTS slots per wave for a slot-recorded packed table
     const int wa = (i >= 0 && tables[i].acc_mode == SKGE_ACC_I16X4 && tables[i].acc_touched)
-                       ? (na + 1) / 2 : na;
+                       ? (na + APPLY_SLOTS - 1) / APPLY_SLOTS : na;
     int nblk0, grid;
     if (j >= 0 && reps(j) > 1) {
       nblk0 = std::max(1, std::min((wa + 3) / 4, 16384));
