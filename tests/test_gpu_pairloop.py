@@ -238,3 +238,31 @@ def test_rescal_positive_path_matches_explicit_pairs(d, monkeypatch):
     for pid in out[0][1]:
         np.testing.assert_allclose(out[0][1][pid], out[1][1][pid], rtol=RTOL, atol=ATOL,
                                    err_msg=pid)
+
+
+@pytest.mark.parametrize("kind,env", [("hole", "SKGE_HOLE_PAIRS"), ("rescal", "SKGE_RESCAL_PAIRS")])
+def test_per_positive_paths_at_wn18_batch_geometry(kind, env, monkeypatch):
+    """WN18's entity count, relation count, d=200 and batch size (1414
+    positives, 10 batches): the per-positive kernels against the explicit-pair
+    kernels on the same draws -- equal violation totals, parameters within the
+    fp32 tolerance (SGD, margin 0.2 as in the reference's HolE/RESCAL runs)."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    n_ent, n_rel, T, nb = 40943, 18, 14140, 10
+    xs = make_kg(n_ent, n_rel, T, seed=3)
+    out = []
+    for pairs in ("0", "1"):
+        monkeypatch.setenv(env, pairs)
+        m = make_model(kind, (n_ent, n_ent, n_rel), 200)
+        m.add_hyperparam("margin", 0.2)
+        upd = {pid: S.SGD(p, 0.1) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), nb, seed=9)
+        with torch.cuda.stream(r.stream):
+            r.run(1)
+        r.synchronize()
+        out.append((int(r.nviol_total.item()),
+                    {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}))
+    assert out[0][0] == out[1][0] > 0
+    for pid in out[0][1]:
+        np.testing.assert_allclose(out[0][1][pid], out[1][1][pid], rtol=RTOL, atol=ATOL,
+                                   err_msg="%s %s" % (kind, pid))
