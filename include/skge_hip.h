@@ -53,7 +53,7 @@ enum { SKGE_POST_NONE = 0, SKGE_POST_NORMALIZE = 1, SKGE_POST_NORMLESS1 = 2 };
 /* accumulator encodings */
 enum {
   SKGE_ACC_F32 = 0,    /* acc_sum: fp32 [rows][width] */
-  SKGE_ACC_I16X4 = 1   /* acc_sum: exact integer sums of TransE-L1 sign contributions,
+  SKGE_ACC_I16X4 = 1,  /* acc_sum: exact integer sums of TransE-L1 sign contributions,
                           four elements per int64 (elements 4q..4q+3 in qword q, added
                           with one 64-bit integer atomic; exact while each 16-bit
                           field's total stays within +-32767, which a row whose
@@ -61,6 +61,10 @@ enum {
                           flag larger counts, skge_device_error bit 2) -- produced
                           only by skge_transe_sample_grad / the pipelined runner with
                           l1 != 0 and width % 4 == 0 */
+  SKGE_ACC_I32X2 = 2   /* pipelined runner's RELATION table only: the same exact sums
+                          with 32-bit fields, two elements per int64 (a hot
+                          relation's per-batch count passes 32767 long before any
+                          entity row's does); the runner keeps these sums itself */
 };
 
 /*
@@ -309,12 +313,14 @@ void skge_pair_runner_destroy(skge_pair_runner_t *r);
  * one launch, then each mini-batch is ONE launch that scores batch b while
  * applying batch b-1's updates (accumulators double-buffered by batch parity;
  * a scoring wave that reads a row batch b-1 touched applies it first or waits
- * for its publisher).  Needs ent/rel in SKGE_ACC_I16X4 mode, d % 4 == 0, an
- * entity table with slot records (capacity >= 4 * batch), a dense
- * single-copy relation table and no gates.  Any batch size: a row's packed
- * sums are exact while its per-batch count is <= 32767 (each occurrence adds
- * a coefficient no larger than the count it adds), and the apply reports a
- * larger count through skge_pipe_runner_error (bit 2).  Allocates
+ * for its publisher).  Needs ent in SKGE_ACC_I16X4 mode, rel in
+ * SKGE_ACC_I16X4 or SKGE_ACC_I32X2 mode (the encoding of the relation sums
+ * the runner keeps), d % 4 == 0, an entity table with slot records (capacity
+ * >= 4 * batch), a dense single-copy relation table and no gates.  Any batch
+ * size: a row's 16-bit packed sums are exact while its per-batch count is
+ * <= 32767 (each occurrence adds a coefficient no larger than the count it
+ * adds), and the apply reports a larger count through skge_pipe_runner_error
+ * (bit 2); 32-bit relation sums are exact below 2^29 positives.  Allocates
  * the second accumulator copy and per-row batch marks itself (freed by
  * destroy).  *epoch_key must only advance (the runner advances it once per
  * epoch).  Replaces the per-batch loop of skge/base.py:1268-1284.

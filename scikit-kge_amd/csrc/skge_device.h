@@ -73,7 +73,7 @@ struct Accum {
   int rows;
 };
 
-enum AccMode : int { ACC_F32 = 0, ACC_I16X4 = 1 };
+enum AccMode : int { ACC_F32 = 0, ACC_I16X4 = 1, ACC_I32X2 = 2 };
 
 // accumulator dwords per row
 __device__ __host__ __forceinline__ int acc_row_dwords(int mode, int width) {
@@ -267,6 +267,19 @@ __device__ __forceinline__ float4 unpack_i16x4(unsigned long long u) {
   const long long f2 = (short)(x & 0xFFFF);
   x = (x - f2) >> 16;
   return make_float4((float)f0, (float)f1, (float)f2, (float)x);
+}
+
+// two int32 fields per int64 (the same carry/borrow scheme, 32-bit fields):
+// the relation rows' sums, which every positive of a batch with that relation
+// adds into, so a 16-bit field would bound the batch by the relation's
+// frequency; 32-bit fields are exact for any batch below 2^29 positives
+__device__ __forceinline__ unsigned long long pack_i32x2(float lo, float hi) {
+  return (unsigned long long)((long long)hi * 4294967296ll + (long long)lo);
+}
+__device__ __forceinline__ float2 unpack_i32x2(unsigned long long u) {
+  const long long x = (long long)u;
+  const long long f0 = (int)(x & 0xFFFFFFFFll);
+  return make_float2((float)f0, (float)((x - f0) >> 32));
 }
 
 template <int KQ>

@@ -38,11 +38,14 @@
 
 namespace skge {
 
-// Packed int16x4 sums are exact while every field's total stays within
+// Packed int16x4 entity sums are exact while every field's total stays within
 // +-32767.  Each occurrence adds a coefficient no larger in magnitude than the
-// count it adds (s: |v0 gp + v1 (gp + g1)| <= v0 + 2 v1, relation:
-// |v0 (gp + g0) + v1 (gp + g1)| <= 2 (v0 + v1), ...), so a row whose count c
-// is <= 32767 cannot have wrapped; the apply flags any larger count.
+// count it adds (s: |v0 gp + v1 (gp + g1)| <= v0 + 2 v1, ...), so a row whose
+// count c is <= 32767 cannot have wrapped; the apply flags any larger count
+// (the host picks packed sums only when its bound keeps counts below that,
+// skge_amd/device.py packed_count_bound).  Relation rows use int32x2 sums
+// (|v0 (gp + g0) + v1 (gp + g1)| <= 2 (v0 + v1) per positive): exact for any
+// batch size this runner accepts.
 constexpr int PACKED_MAX = 32767;
 enum : int { ERR_WAIT = 1, ERR_PACKED = 2 };
 
@@ -68,6 +71,7 @@ struct RelTab {                // relation table
   float* P[2];                 // P[0]: the caller's parameters; P[1]: the other buffer
   float* A[2];                 // AdaGrad state, likewise (nullptr: SGD)
   unsigned long long* acc[3];  // [rows][rw]: int16x4 sums in words [0, d/4), count in word d/4
+                               // (w32: int32x2 sums in words [0, d/2), count in word d/2)
   int rows, rw;
   UpdParams u;
   int* updated;                // profile only: rows with a nonzero count (sharded)
@@ -150,13 +154,15 @@ __device__ __forceinline__ void load_upd_row(const float* P, const float* A,
   }
 }
 
-// One row's update from its packed sums and occurrence count c > 0: segment
+// One row's update from its exact packed sums (W32: int32x2 in sv / sw, else
+// int16x4 in sv) and occurrence count c > 0: segment
 // mean + AdaGrad / SGD + projection; the same arithmetic as apply_row_i16
 // (skge_update.hip) and the reference (skge/param.py:130, 147-155;
 // skge/transe.py normalize).  Lanes past the row end with zeros.
-template <int KQ>
+template <int KQ, bool W32>
 __device__ __forceinline__ void row_update(const UpdParams& t, int c, int d,
-                                           const unsigned long long (&sv)[KQ], float4 (&p)[KQ],
+                                           const unsigned long long (&sv)[KQ],
+                                           const unsigned long long (&sw)[KQ], float4 (&p)[KQ],
                                            float4 (&a)[KQ]) {
   const int l = lane_id(), nq = d >> 2;
   const bool ada = t.opt == OPT_ADAGRAD;
@@ -165,7 +171,13 @@ __device__ __forceinline__ void row_update(const UpdParams& t, int c, int d,
 #pragma unroll
   for (int m = 0; m < KQ; ++m) {
     const bool in = 64 * m + l < nq;
-    const float4 sm = unpack_i16x4(in ? sv[m] : 0ull);
+    float4 sm;
+    if (W32) {   // int32x2 sums: quad q in words sv (elements 0, 1) and sw (2, 3)
+      const float2 lo = unpack_i32x2(in ? sv[m] : 0ull), hi = unpack_i32x2(in ? sw[m] : 0ull);
+      sm = make_float4(lo.x, lo.y, hi.x, hi.y);
+    } else {     // int16x4 sums
+      sm = unpack_i16x4(in ? sv[m] : 0ull);
+    }
 #define SKGE_UP(X)                                                      \
   {                                                                     \
     const float g = (sm.X + t.rin * p[m].X) / div + t.rout * p[m].X;    \
@@ -216,7 +228,7 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row
   if (c > PACKED_MAX && l == 0) atomicOr(t.err, ERR_PACKED);   // a 16-bit field may have wrapped
-  row_update<KQ>(t.u, c, d, sv, p, a);
+  row_update<KQ, false>(t.u, c, d, sv, sv, p, a);
 #pragma unroll
   for (int m = 0; m < KQ; ++m) {
     const int q = 64 * m + l;
@@ -252,16 +264,45 @@ __device__ __forceinline__ void ensure_applied(const PipeTab& t, int pp, int row
 }
 
 // relation row R_b[row] (the value batch b scores with): R_{b-1}[row] from
-// buffer rd updated with batch b-1's sums (accumulator copy ra)
-template <int KQ>
+// buffer rd updated with batch b-1's sums (accumulator copy ra).  W32: int32x2
+// sums, words 2q, 2q+1 hold quad q and word 2 nq the count; else int16x4
+// sums, word q holds quad q and word nq the count.  Every load is issued
+// before the count is read (kept in load_upd_row's shape: hipcc would sink
+// loads used only under `if (c)` below the count's wait).  Lanes past the row
+// end with zeros whether or not the row was updated (they enter the scores).
+template <int KQ, bool W32>
 __device__ __forceinline__ void rel_row(const RelTab& t, int row, int d, int rd, int ra,
                                         float4 (&p)[KQ], float4 (&a)[KQ], int& c) {
-  unsigned long long sv[KQ];
+  const int l = lane_id(), nq = d >> 2;
   const unsigned long long* acc = t.acc[ra] + (size_t)row * t.rw;
-  load_upd_row<KQ>(t.P[rd] + (size_t)row * d, t.A[rd] ? t.A[rd] + (size_t)row * d : nullptr, acc,
-                   d, p, a, sv);
-  c = __builtin_amdgcn_readfirstlane((int)acc[d >> 2]);
-  if (c) row_update<KQ>(t.u, c, d, sv, p, a);
+  unsigned long long sv[KQ], sw[KQ];
+  if (W32) {
+    const float4* prow = reinterpret_cast<const float4*>(t.P[rd] + (size_t)row * d);
+    const float4* arow = reinterpret_cast<const float4*>(t.A[rd] + (size_t)row * d);
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+      const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
+      const ulonglong2 w = reinterpret_cast<const ulonglong2*>(acc)[qc];
+      sv[m] = w.x;
+      sw[m] = w.y;
+      p[m] = prow[qc];
+      a[m] = t.A[rd] ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+  } else {
+    load_upd_row<KQ>(t.P[rd] + (size_t)row * d, t.A[rd] ? t.A[rd] + (size_t)row * d : nullptr,
+                     acc, d, p, a, sv);
+  }
+  c = __builtin_amdgcn_readfirstlane((int)acc[W32 ? 2 * nq : nq]);
+  if (c) {
+    row_update<KQ, W32>(t.u, c, d, sv, sw, p, a);   // (zeroes the lanes past the row)
+  }
+#ifndef SKGE_PIPE_ABL_NO_RELZERO   // timing-only ablation
+  else {
+#pragma unroll
+    for (int m = 0; m < KQ; ++m)
+      if (64 * m + l >= nq) p[m] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+#endif
 }
 
 __device__ __forceinline__ unsigned long long now_10ns() { return __builtin_amdgcn_s_memrealtime(); }
@@ -285,11 +326,12 @@ __device__ __forceinline__ T* opaque_ptr(T* p) {
 #ifndef SKGE_PIPE_WG
 #define SKGE_PIPE_WG 256   // threads per workgroup
 #endif
-template <int KQ>
+template <int KQ, bool W32>
 __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
   const int d = a.d, nq = d >> 2;
+  const int rcw = W32 ? 2 * nq : nq;   // relation accumulator: the count word
   const int g = launch_id(a), gp = g - 1;
   const int cp = a.b & 1, pp = cp ^ 1;   // entity accumulator copies: this / previous batch
   const int rd = a.b & 1;                // relation buffer holding R_{b-1}
@@ -311,7 +353,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
       if (w < nR) {
         float4 p[KQ], av[KQ];
         int c;
-        rel_row<KQ>(a.R, w, d, rd, ra_prev, p, av, c);
+        rel_row<KQ, W32>(a.R, w, d, rd, ra_prev, p, av, c);
         float4* prow = reinterpret_cast<float4*>(a.R.P[rw] + (size_t)w * d);
         float4* arow = a.R.A[rw] ? reinterpret_cast<float4*>(a.R.A[rw] + (size_t)w * d) : nullptr;
         unsigned long long* old = a.R.acc[ra_old] + (size_t)w * a.R.rw;
@@ -325,12 +367,12 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
             if (arow) arow[q] = av[m];
           }
         }
-        for (int q = l; q <= nq; q += 64) {
+        for (int q = l; q <= rcw; q += 64) {
           old[q] = 0ull;
           if (flush) prev[q] = 0ull;
         }
         if (c && a.R.updated && l == 0) atomicAdd(shard_of(a.R.updated), 1);
-        if (c > PACKED_MAX && l == 0) atomicOr(a.err, ERR_PACKED);
+        if (!W32 && c > PACKED_MAX && l == 0) atomicOr(a.err, ERR_PACKED);
       } else {
         const int row = __builtin_amdgcn_readfirstlane(a.E.touched[pp][w - nR]);
 #ifndef SKGE_PIPE_ABL_NOAPPLY_E   // timing-only ablation: entity rows never updated
@@ -353,17 +395,27 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
   int* const pend_cp = opaque_ptr(a.E.pend[cp]);
   unsigned long long* const racc = opaque_ptr(a.R.acc[ra_cur]);
   unsigned long long* const esum = opaque_ptr(a.E.sum[cp]);
+  // the batch's records through buffer descriptors built once (not pointers
+  // re-loaded from the kernarg segment on the wave's first dependent chain)
+  const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int4*>(a.rec + a.start), 0, a.count * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rec1_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int*>(a.rec_n1 + a.start), 0, a.count * 4, 0x00020000);
   int nv = 0;
   for (int w = blk_b * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
-    const long long j = a.start + w;
     unsigned long long tt[4];
     if (a.trace) tt[0] = now_10ns();
-    const int4 r4 = a.rec[j];
+    const u32x4 rx = __builtin_amdgcn_raw_buffer_load_b128(rec_rs, w * 16, 0, 0);
+    const int r1 = (int)__builtin_amdgcn_raw_buffer_load_b32(rec1_rs, w * 4, 0, 0);
+    const int4 r4 = make_int4((int)rx.x, (int)rx.y, (int)rx.z, (int)rx.w);
+    // both record loads in one memory round trip (left alone, the scheduler
+    // may put the first load's wait before the second load)
+    __builtin_amdgcn_sched_barrier(0);
     const int s = __builtin_amdgcn_readfirstlane(r4.x);
     const int o = __builtin_amdgcn_readfirstlane(r4.y);
     const int p = __builtin_amdgcn_readfirstlane(r4.z);
     const int neg0 = __builtin_amdgcn_readfirstlane(r4.w);
-    const int neg1 = __builtin_amdgcn_readfirstlane(a.rec_n1[j]);
+    const int neg1 = __builtin_amdgcn_readfirstlane(r1);
     const int n0r = neg0 >= 0 ? neg0 : s, n1r = neg1 >= 0 ? neg1 : o;
     // entity rows as of the launch start (plain loads), their pending marks,
     // and the relation row this batch scores with
@@ -377,7 +429,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
     {
       float4 ra[KQ];
       int c;
-      rel_row<KQ>(a.R, p, d, rd, ra_prev, rp, ra, c);
+      rel_row<KQ, W32>(a.R, p, d, rd, ra_prev, rp, ra, c);
     }
 #ifdef SKGE_PIPE_ABL_NOENSURE   // timing-only ablation (tools/ablate.sh): ignore pending rows
     const uint64_t pend = 0ull * __ballot(mark == gp);
@@ -433,7 +485,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
         commit_slot(cnt_cp, tch_cp, rE, cE, 4 * w + l);
         if (cE > 0) pend_cp[rE] = g;
       } else if (l == 4 && v0 + v1 > 0) {
-        atomicAdd(racc + (size_t)p * a.R.rw + nq, (unsigned long long)(2 * (v0 + v1)));
+        atomicAdd(racc + (size_t)p * a.R.rw + rcw, (unsigned long long)(2 * (v0 + v1)));
       }
     }
     if (v0 + v1 > 0) {
@@ -454,15 +506,27 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
         SKGE_CO(w)
 #undef SKGE_CO
       }
-      Accum aE, aR;
+      Accum aE;
       aE.sum = reinterpret_cast<float*>(esum);
       acc_row4_i16<KQ>(aE, s, cs, d);
       acc_row4_i16<KQ>(aE, o, co, d);
       if (v0) acc_row4_i16<KQ>(aE, neg0, c0, d);
       if (v1) acc_row4_i16<KQ>(aE, neg1, c1, d);
-      // relation sums: rows of rw words (acc_row4_i16 indexes rows of d/4 words)
-      aR.sum = reinterpret_cast<float*>(racc + (size_t)p * a.R.rw);
-      acc_row4_i16<KQ>(aR, 0, cr, d);
+      // relation sums: rows of rw words; int32x2 (two words per quad) when a
+      // hot relation's batch total could pass 16 bits
+      unsigned long long* rrow = racc + (size_t)p * a.R.rw;
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) {
+        const int q = 64 * m + l;
+        if (q < nq) {
+          if (W32) {
+            atomicAdd(rrow + 2 * q, pack_i32x2(cr[m].x, cr[m].y));
+            atomicAdd(rrow + 2 * q + 1, pack_i32x2(cr[m].z, cr[m].w));
+          } else {
+            atomicAdd(rrow + q, pack_i16x4(cr[m]));
+          }
+        }
+      }
     }
     if (a.trace) {   // stamp after issue (no drain: the trace must not slow the launch)
       if (l == 0) {
@@ -545,6 +609,7 @@ struct skge_pipe_runner {
   int* rec_n1 = nullptr;
   std::vector<PipeArgs> batch;     // nb1 batches + the flush
   std::vector<int> grid;
+  bool w32 = false;                // int32x2 relation sums
   int nlaunch() const { return (int)batch.size() + 2; }
 };
 
@@ -590,8 +655,13 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
       a.stats_viol = stats + (3 * i + 2) * sh;
     }
     if (trace && i == trace_launch) a.trace = trace;
-#define SKGE_PB(K) \
-  hipLaunchKernelGGL((k_pipe_batch<K>), dim3(r->grid[k]), dim3(SKGE_PIPE_WG), 0, st, a)
+#define SKGE_PB(K)                                                                              \
+  do {                                                                                          \
+    if (r->w32)                                                                                 \
+      hipLaunchKernelGGL((k_pipe_batch<K, true>), dim3(r->grid[k]), dim3(SKGE_PIPE_WG), 0, st, a); \
+    else                                                                                        \
+      hipLaunchKernelGGL((k_pipe_batch<K, false>), dim3(r->grid[k]), dim3(SKGE_PIPE_WG), 0, st, a); \
+  } while (0)
     if (r->kq <= 1) SKGE_PB(1);
     else if (r->kq <= 2) SKGE_PB(2);
     else SKGE_PB(4);
@@ -610,13 +680,17 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
                                                        float margin, int ntries,
                                                        int* nviol_total) {
   // the pipelined loop is the packed TransE-L1 path
-  if (check_table(ent, "ent", true) || check_table(rel, "rel", true)) return nullptr;
-  if (ent->acc_mode != SKGE_ACC_I16X4 || rel->acc_mode != SKGE_ACC_I16X4 || d % 4 || d > 1024 ||
+  skge_table_t relc = *rel;   // the relation encoding is the runner's own (checked below)
+  if (relc.acc_mode == SKGE_ACC_I32X2) relc.acc_mode = SKGE_ACC_I16X4;
+  if (check_table(ent, "ent", true) || check_table(&relc, "rel", true)) return nullptr;
+  if (ent->acc_mode != SKGE_ACC_I16X4 ||
+      (rel->acc_mode != SKGE_ACC_I16X4 && rel->acc_mode != SKGE_ACC_I32X2) || d % 4 || d > 1024 ||
       ent->width != d || rel->width != d || ent->acc_touched == nullptr ||
       rel->acc_touched != nullptr || rel->acc_replicas > 1 || ent->acc_replicas > 1 ||
       ent->gate || rel->gate) {
-    set_error("pipelined runner: needs packed (SKGE_ACC_I16X4) tables, d %% 4 == 0, an entity "
-              "table with slot records and a dense single-copy relation table, no gates");
+    set_error("pipelined runner: needs a packed (SKGE_ACC_I16X4) entity table with slot "
+              "records, a dense single-copy SKGE_ACC_I16X4 / SKGE_ACC_I32X2 relation table, "
+              "d %% 4 == 0, no gates");
     return nullptr;
   }
   if (!trip || !set || !epoch_key || T <= 0 || nbatches < 1 || nbatches > T || !stream ||
@@ -667,7 +741,8 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
     const int M = rel->rows;
     const bool ada = rel->opt == SKGE_ADAGRAD;
     q.rows = M;
-    q.rw = (nq + 1 + 15) / 16 * 16;   // sums + count, rows on whole 128-B lines
+    r->w32 = rel->acc_mode == SKGE_ACC_I32X2;
+    q.rw = ((r->w32 ? 2 * nq : nq) + 1 + 15) / 16 * 16;   // sums + count, whole 128-B lines
     q.u = upd(rel);
     q.updated = nullptr;
     q.P[0] = rel->param;

@@ -336,25 +336,35 @@ __device__ __forceinline__ void apply_row_rep_block(const TableDev& t, int row, 
     int* cp = t.acc.cnt + (size_t)tid * rows + row;
     if (tid < R) v = *cp;
     if (v) *cp = 0;
+    // each copy's 16-bit fields are exact while that copy's count is <= 32767
+    // (producers spread over copies by position, so a copy sees at most
+    // ceil(batch / R) of a hot row's occurrences)
+    if (MODE == ACC_I16X4 && v > 32767) atomicOr(&g_skge_dev_err, 2);
     v = wave_sum_int(v);
-    if (tid == 0) lds[dw] = v;
+    if (tid == 0) lds[w] = v;
   }
-  if (MODE == ACC_I16X4) {   // qwords: packed sums are linear under integer adds
+  if (MODE == ACC_I16X4) {   // every copy decoded on its own, summed as int32 per element
     const int nq = w >> 2;
-    unsigned long long* l64 = reinterpret_cast<unsigned long long*>(lds);
     for (int q = tid; q < nq; q += blockDim.x) {
       unsigned long long* sp = reinterpret_cast<unsigned long long*>(t.acc.sum) + (size_t)row * nq + q;
       const size_t stride = (size_t)rows * nq;
       unsigned long long v[32];
 #pragma unroll
       for (int k = 0; k < 32; ++k) v[k] = k < R ? sp[k * stride] : 0ull;
-      unsigned long long acc = 0ull;
+      int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
 #pragma unroll
       for (int k = 0; k < 32; ++k) {
-        acc += v[k];
+        const float4 f = unpack_i16x4(v[k]);
+        s0 += (int)f.x;
+        s1 += (int)f.y;
+        s2 += (int)f.z;
+        s3 += (int)f.w;
         if (k < R && v[k]) sp[k * stride] = 0ull;
       }
-      l64[q] = acc;
+      lds[4 * q] = s0;
+      lds[4 * q + 1] = s1;
+      lds[4 * q + 2] = s2;
+      lds[4 * q + 3] = s3;
     }
   } else {
     for (int q = tid; q < dw; q += blockDim.x) {
@@ -373,8 +383,7 @@ __device__ __forceinline__ void apply_row_rep_block(const TableDev& t, int row, 
     }
   }
   __syncthreads();
-  const int c = lds[dw];
-  if (MODE == ACC_I16X4 && c > 32767 && tid == 0) atomicOr(&g_skge_dev_err, 2);
+  const int c = lds[w];
   if (tid < 64 && c != 0) {
     const int l = tid;
     const bool ada = t.opt == OPT_ADAGRAD;
@@ -393,9 +402,7 @@ __device__ __forceinline__ void apply_row_rep_block(const TableDev& t, int row, 
         const int ec = e < w ? e : w - 1;
         float sv;
         if (MODE == ACC_I16X4) {
-          const float4 q4 = unpack_i16x4(reinterpret_cast<unsigned long long*>(lds)[ec >> 2]);
-          const int r4 = ec & 3;
-          sv = r4 == 0 ? q4.x : (r4 == 1 ? q4.y : (r4 == 2 ? q4.z : q4.w));
+          sv = (float)lds[ec];
         } else {
           sv = __int_as_float(lds[ec]);
         }

@@ -16,6 +16,7 @@ numeric step of a batch runs as HIP kernels through libskgehip.so:
 import logging
 import pickle
 import timeit
+import warnings
 
 import numpy as np
 import torch
@@ -35,6 +36,11 @@ _DEF_MAX_EPOCHS = 1000
 _DEF_MARGIN = 1.0
 _FILE_GRADIENTS = "gradients.txt"
 _FILE_EMBEDDINGS = "embeddings.txt"
+
+
+def _epoch_runner_type():
+    from .device import EpochRunner
+    return EpochRunner
 
 
 class Model(object):
@@ -401,9 +407,18 @@ class PairwiseStochasticTrainer(StochasticTrainer):
             self._nviol_dev.zero_()
 
     def fit(self, xs, ys):
+        use_device = False
         if self.device_loop:
+            from .device import device_sampler_args
+            use_device, ntries, why = device_sampler_args(self, xs, ys)
+            if not use_device:
+                # the device loop draws RandomModeSampler(1, [0, 1]) negatives
+                # itself; anything else trains on the per-batch path instead
+                warnings.warn("device_loop: %s; training on the per-batch path" % why)
+        self._on_device = use_device
+        if use_device:
             from .device import device_optim
-            device_optim(self, xs)
+            device_optim(self, xs, ntries=ntries)
         elif self.samplef is None:
             pidx = np.where(np.array(ys) == 1)[0]
             nidx = np.where(np.array(ys) != 1)[0]
@@ -412,23 +427,28 @@ class PairwiseStochasticTrainer(StochasticTrainer):
             self.pxs = int(len(self.nxs) / len(pxs)) * pxs
             xys = list(range(min(len(pxs), len(self.nxs))))
             self._optim(xys)
+            return   # the labelled-negatives branch writes no files (skge/base.py:1350-1357)
         else:
             self._optim(list(zip(xs, ys)))
-        self._write_outputs(xs)
+        self._write_outputs(xs, use_device)
 
-    def _write_outputs(self, xs):
-        """Post-fit files of the reference (skge/base.py:1364-1386)."""
-        if self.file_gradients is None and self.file_embeddings is None:
-            return
+    def _write_outputs(self, xs, device=False):
+        """Post-fit counters and files of the reference's samplef branch
+        (skge/base.py:1364-1386): E.neighbours accumulates over fits."""
         n = self.model.E.rows
-        neighbours = np.zeros(n, dtype=np.int64)
-        for x in xs:
-            neighbours[x[0]] += 1
-            neighbours[x[1]] += 1
-        self.model.E.neighbours = neighbours
+        if self.model.E.neighbours is None:
+            self.model.E.neighbours = np.zeros(n, dtype=np.int64)
+        neighbours = self.model.E.neighbours
+        x = np.asarray(xs, dtype=np.int64).reshape(-1, 3)
+        np.add.at(neighbours, x[:, 0], 1)
+        np.add.at(neighbours, x[:, 1], 1)
         if self.file_gradients is not None:
             # E.violations / E.updateCounts: device counters of the per-batch
-            # paths (zero under device_loop, whose runners do not count)
+            # paths and the device pair loop; the TransE epoch runners keep none
+            if device and isinstance(self._runner, _epoch_runner_type()):
+                warnings.warn("device_loop (TransE epoch runner) keeps no per-row counters: "
+                              "the #(violations) and #(updates) columns of file_grad are zero; "
+                              "use device_runner='pairs' to count them")
             viol = self.model.E.violations
             upd = self.model.E.updateCounts
             self.file_gradients.write("Entity,Degree,#(violations),#(updates)\n")
@@ -447,7 +467,7 @@ class PairwiseStochasticTrainer(StochasticTrainer):
 
     def _pre_epoch(self):
         self.nviolations = 0
-        if self.samplef is None and not self.device_loop:
+        if self.samplef is None and not getattr(self, "_on_device", False):
             shuffle(self.pxs)
             shuffle(self.nxs)
 

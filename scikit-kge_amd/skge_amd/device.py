@@ -7,7 +7,9 @@ csrc/skge_pipeline.hip, skge_epoch.hip) and PairLoopRunner the any-model pair
 loop (skge_pair_runner_*, csrc/skge_pairloop.hip): one epoch of
 PairwiseStochasticTrainer batches (nbatches full batches + the remainder,
 skge/base.py:1246-1268), captured once into a hipGraph and replayed."""
+import math
 import timeit
+import warnings
 
 import numpy as np
 import torch
@@ -36,6 +38,45 @@ class DeviceKG(object):
                                               L.ptr(self.slots), self.capacity), "triple set build")
 
 
+PACKED_MAX = 32767   # a 16-bit packed field's bound (csrc/skge_pipeline.hip PACKED_MAX)
+
+
+def _bincount_max(col, n):
+    return torch.bincount(col.long(), minlength=n)
+
+
+def packed_count_bound(kg, n_ent, batch):
+    """Upper bound on an ENTITY row's per-batch occurrence count in the
+    TransE-L1 device loops (the count bounds every 16-bit field of its packed
+    sums, csrc/skge_pipeline.hip).  A positive adds at most 3 to each of its s
+    and o (skge/transe.py:103-136: s is sp of both pairs and sn of the
+    tail-corrupted one) and 1 to each accepted corruption.  The first part is
+    exact from the training triples; the corruptions are uniform draws over
+    the entities (skge/sample.py:41-46), bounded by their Poisson tail
+    (lambda + 12 sqrt(lambda) + 40, lambda = 2 batch / n_ent).  The applies
+    still check every row's count at run time (ERR_PACKED), and device_optim
+    reads that flag after every epoch."""
+    occ = _bincount_max(kg.trip[:, 0], n_ent) + _bincount_max(kg.trip[:, 1], n_ent)
+    det = 3 * min(int(occ.max().item()), 2 * int(batch))
+    lam = 2.0 * batch / max(n_ent, 1)
+    corr = min(2 * int(batch), int(math.ceil(lam + 12.0 * math.sqrt(lam) + 40)))
+    return det + corr
+
+
+def relation_replicas(kg, n_rel, batch, max_reps=32):
+    """Accumulator copies the two-launch runner's packed relation sums need:
+    positive j adds into copy j mod reps, so a copy holds at most
+    ceil(batch / reps) positives, each adding <= 4 to its relation's count.
+    Returns 0 when even max_reps copies cannot keep the count <= PACKED_MAX."""
+    top = int(_bincount_max(kg.trip[:, 2], n_rel).max().item())
+    reps = 1
+    while 4 * min(top, -(-int(batch) // reps)) > PACKED_MAX:
+        reps *= 2
+        if reps > max_reps:
+            return 0
+    return reps
+
+
 class EpochRunner(object):
     """Native hipGraph epoch of the TransE device batch loop.
 
@@ -44,10 +85,16 @@ class EpochRunner(object):
     single-copy relation accumulator) and the two-launch runner otherwise;
     True demands it, False forces the two-launch runner.  Both give identical
     parameters.
+
+    Packed (exact int16x4) entity sums are used for TransE-L1 unless
+    force_f32, or unless packed_count_bound() says a row's per-batch count
+    could pass 32767 (then fp32 sums: packed=None decides, packed=True
+    insists).  The pipelined runner keeps relation sums as int32x2; the
+    two-launch runner spreads them over relation_replicas() copies.
     """
 
     def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, stream=None,
-                 nviol_total=None, force_f32=False, replicas=1, pipelined=None):
+                 nviol_total=None, force_f32=False, replicas=1, pipelined=None, packed=None):
         from .transe import TransE
         if not isinstance(model, TransE):
             raise NotImplementedError("device_loop supports TransE (the north-star path) only")
@@ -59,22 +106,27 @@ class EpochRunner(object):
         self.nviol_total = nviol_total if nviol_total is not None else \
             torch.zeros(1, dtype=torch.int32, device=dev)
         bs = kg.T // nbatches
-        # TransE-L1 sign contributions are small integers: exact packed int16x4
-        # sums at any batch size (the applies flag a row whose count could have
-        # wrapped a 16-bit field, checked by synchronize())
-        can_pack = bool(model.l1) and model.d % 4 == 0 and not force_f32
-        can_pipe = can_pack and replicas <= 1 and pipelined is not False
+        self.nbatches = nbatches
         self._auto = pipelined is None
-        packed = can_pack
-        mode = L.SKGE_ACC_I16X4 if packed else L.SKGE_ACC_F32
-        from .param import Accumulator
+        # TransE-L1 sign contributions are small integers: exact packed int16x4
+        # sums while every row's per-batch count stays <= 32767 (the applies
+        # flag a larger count, checked by synchronize())
+        can_pack = bool(model.l1) and model.d % 4 == 0 and not force_f32
+        self.count_bound = packed_count_bound(kg, model.E.rows, bs) if can_pack else 0
+        auto_packed = packed is None
+        if packed is None:
+            packed = can_pack and self.count_bound <= PACKED_MAX
+        elif packed and not can_pack:
+            raise ValueError("packed sums need TransE-L1, d % 4 == 0 and no force_f32")
+        packed = bool(packed)
+        # the two-launch runner's packed relation sums: hot relations spread
+        # over accumulator copies (0: not even 32 copies suffice)
+        rel_reps = relation_replicas(kg, model.R.rows, bs) if packed else 1
         E, R = model.params["E"], model.params["R"]
-        self.accE = Accumulator(E.rows, E.width, dev, slots=4 * bs, mode=mode)
-        # relation rows are hot (every positive adds to one of |R| rows):
-        # `replicas` > 1 spreads the adds over accumulator copies (dense apply sums them)
-        self.accR = Accumulator(R.rows, R.width, dev, mode=mode, dense=True,
-                                replicas=replicas)
-        self.packed = packed
+        can_pipe = packed and replicas <= 1 and pipelined is not False
+        if pipelined and not can_pipe:
+            raise ValueError("pipelined runner needs TransE-L1, d % 4 == 0, packed sums "
+                             "and replicas == 1")
         if can_pipe and pipelined is None:
             # the pipelined runner's scratch: a second entity accumulator copy,
             # per-row marks and the epoch's records (auto mode: only if it fits)
@@ -82,28 +134,32 @@ class EpochRunner(object):
             torch.cuda.empty_cache()
             extra = E.rows * E.width * 2 + E.rows * 12 + kg.T * 20 + (64 << 20)
             can_pipe = extra < torch.cuda.mem_get_info(dev)[0] * 0.9
-        self.te = updaters["E"].table(self.accE, counters=False)
-        self.tr = updaters["R"].table(self.accR, counters=False)
-        self.nbatches = nbatches
         torch.cuda.current_stream().synchronize()
         lib = L.lib()
-        if pipelined and not can_pipe:
-            raise ValueError("pipelined runner needs TransE-L1, d % 4 == 0, "
-                             "no forced f32 and replicas == 1")
-        self.pipelined = can_pipe if pipelined is None else bool(pipelined)
-        if self.pipelined:
+        if can_pipe:
+            # relation sums in 16-bit fields while a relation's per-batch count
+            # fits them (faster: half the atomics), else int32x2
+            self._tables(model, updaters, packed, 1, rel_w32=rel_reps != 1)
             h = lib.skge_pipe_runner_create(
                 L.stream_ptr(self.stream), self.te, self.tr, model.d, L.ptr(kg.trip), kg.T,
                 L.ptr(kg.slots), kg.capacity, int(nbatches), int(seed) & (2 ** 64 - 1),
                 L.ptr(self.epoch_key), float(model.margin), int(ntries), L.ptr(self.nviol_total))
             if h:
+                self.pipelined = True
                 self.handle = h
                 self.nlaunches = lib.skge_pipe_runner_nlaunches(h)
                 return
             err = lib.skge_last_error().decode()
             if not (self._auto and "allocation" in err):
                 raise L.SkgeError("skge_pipe_runner_create: %s" % err)
-            self.pipelined = False   # auto mode: out of device memory -> two-launch runner
+            # auto mode: out of device memory -> two-launch runner
+        self.pipelined = False
+        if packed and rel_reps == 0:
+            if not auto_packed:
+                raise ValueError("packed sums: a relation's per-batch count exceeds what 32 "
+                                 "accumulator copies hold; use packed=None or force_f32=True")
+            packed = False
+        self._tables(model, updaters, packed, max(int(replicas), rel_reps) if packed else replicas)
         h = lib.skge_runner_create(L.stream_ptr(self.stream), int(bool(model.l1)),
                                    self.te, self.tr,
                                    model.d, L.ptr(kg.trip), kg.T, L.ptr(kg.slots), kg.capacity,
@@ -113,6 +169,24 @@ class EpochRunner(object):
             raise L.SkgeError("skge_runner_create: %s" % lib.skge_last_error().decode())
         self.handle = h
         self.nlaunches = lib.skge_runner_nlaunches(h)
+
+    def _tables(self, model, updaters, packed, rel_replicas, rel_w32=False):
+        """The runner's own accumulators (captured by its graph) and tables."""
+        from .param import Accumulator
+        dev = model.device
+        E, R = model.params["E"], model.params["R"]
+        mode = L.SKGE_ACC_I16X4 if packed else L.SKGE_ACC_F32
+        bs = self.kg.T // self.nbatches
+        self.accE = Accumulator(E.rows, E.width, dev, slots=4 * bs, mode=mode)
+        # relation rows are hot (every positive adds to one of |R| rows): the
+        # two-launch runner spreads the adds over `rel_replicas` copies, the
+        # pipelined one keeps 32-bit fields (rel_w32)
+        self.accR = Accumulator(R.rows, R.width, dev, mode=L.SKGE_ACC_I32X2 if rel_w32 else mode,
+                                dense=True, replicas=rel_replicas)
+        self.rel_w32 = rel_w32
+        self.packed = packed
+        self.te = updaters["E"].table(self.accE, counters=False)
+        self.tr = updaters["R"].table(self.accR, counters=False)
 
     def run(self, nepochs=1):
         lib = L.lib()
@@ -203,6 +277,11 @@ class PairLoopRunner(object):
             torch.zeros(1, dtype=torch.int32, device=dev)
         P = 2 * max(batch_sizes(kg.T, nbatches))
         self.te, self.tr = model._tables("pairwise", updaters, slots=model._pair_slots(P))
+        # the graph captures raw pointers to the model's accumulators and
+        # counters: hold the tensors, so a later per-batch call that grows the
+        # model's slot arrays cannot free what this runner still writes
+        self._captured = [(a.sum, a.cnt, a.touched) for a in model._acc.values()] + \
+            [p._counters.copy() for p in model.params.values()]
         torch.cuda.current_stream().synchronize()
         lib = L.lib()
         h = lib.skge_pair_runner_create(
@@ -263,23 +342,52 @@ def make_runner(model, updaters, kg, nbatches, seed=0, ntries=100, nviol_total=N
     raise ValueError("unknown device runner %r" % (runner,))
 
 
-def device_optim(trainer, xs):
-    """PairwiseStochasticTrainer.fit with device_loop=True."""
+def device_sampler_args(trainer, xs, ys):
+    """(eligible, ntries, reason): whether PairwiseStochasticTrainer.fit with
+    device_loop=True may run the device loop, whose sampler draws what
+    RandomModeSampler(1, [0, 1], xs, sz).sample would (skge/sample.py:28-46,
+    skge/base.py:426): every y must be +1 (the labelled-negatives branch,
+    samplef None with y = -1 rows, skge/base.py:1350-1357, pairs given
+    negatives instead) and samplef must be None or such a sampler's sample."""
+    if ys is not None and not np.all(np.asarray(ys) == 1):
+        return False, trainer.ntries, "labelled negatives (y != 1)"
+    f = trainer.samplef
+    if f is None:
+        return True, trainer.ntries, ""
+    from .sample import RandomModeSampler
+    smp = getattr(f, "__self__", None)
+    if not isinstance(smp, RandomModeSampler) or getattr(f, "__func__", None) is not \
+            RandomModeSampler.sample:
+        return False, trainer.ntries, "samplef is not RandomModeSampler.sample"
+    if smp.n != 1 or list(smp.modes) != [0, 1]:
+        return False, trainer.ntries, "RandomModeSampler(n=%r, modes=%r) is not (1, [0, 1])" % (
+            smp.n, smp.modes)
+    n_ent = trainer.model.E.rows
+    if tuple(smp.sz[:2]) != (n_ent, n_ent):
+        return False, trainer.ntries, "sampler sizes %r differ from the model's" % (smp.sz,)
+    return True, smp.ntries, ""
+
+
+def device_optim(trainer, xs, ntries=None):
+    """PairwiseStochasticTrainer.fit with device_loop=True.  The runner's
+    error word (packed-sum overflow, cross-workgroup wait timeout) is read
+    after every epoch, before the post_epoch callbacks, so no callback ever
+    sees parameters from a failed epoch."""
     model = trainer.model
     dev = model.device
     if trainer._nviol_dev is None:
         trainer._nviol_dev = torch.zeros(1, dtype=torch.int32, device=dev)
     kg = DeviceKG(xs, dev)
     runner = make_runner(model, trainer._updaters, kg, trainer.nbatches, seed=trainer.seed,
-                         ntries=trainer.ntries, nviol_total=trainer._nviol_dev,
-                         runner=trainer.device_runner)
+                         ntries=trainer.ntries if ntries is None else ntries,
+                         nviol_total=trainer._nviol_dev, runner=trainer.device_runner)
     trainer._runner = runner
     with torch.cuda.stream(runner.stream):
         for trainer.epoch in range(1, trainer.max_epochs + 1):
             trainer._pre_epoch()
             trainer.epoch_start = timeit.default_timer()
             runner.run(1)
+            runner.synchronize()   # raises on the epoch's error bits
             for f in trainer.post_epoch:
                 if not f(trainer):
                     break
-    runner.synchronize()

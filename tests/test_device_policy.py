@@ -1,0 +1,64 @@
+"""Host-side accumulator policy of the TransE device loops (CPU): the bound
+that decides exact packed int16x4 entity sums vs fp32 sums, and the number
+of relation accumulator copies the two-launch runner needs.  Counts follow
+the kernels' occurrence counting (skge/transe.py:73-136 via
+csrc/skge_pipeline.hip): s and o of a positive <= 3 each, an accepted
+corruption 1."""
+import types
+
+import numpy as np
+import torch
+
+from skge_amd.device import PACKED_MAX, packed_count_bound, relation_replicas
+
+
+def _kg(trip):
+    return types.SimpleNamespace(trip=torch.as_tensor(np.asarray(trip, dtype=np.int32)))
+
+
+def test_bound_uniform_wn18_shape_fits_even_at_two_batches():
+    rs = np.random.RandomState(0)
+    trip = np.stack([rs.randint(40943, size=141442), rs.randint(40943, size=141442),
+                     rs.randint(18, size=141442)], axis=1)
+    kg = _kg(trip)
+    occ = np.bincount(trip[:, 0], minlength=40943) + np.bincount(trip[:, 1], minlength=40943)
+    for batch in (1414, 70721):
+        b = packed_count_bound(kg, 40943, batch)
+        assert b >= 3 * occ.max()
+        assert b <= PACKED_MAX
+    # WN18-shaped relations at nb=2: 4 * ~7.9k positives per relation fits one copy
+    assert relation_replicas(kg, 18, 1414) == 1
+
+
+def test_bound_hub_entity_forces_fp32():
+    # entity 0 is the subject of 12000 triples: 3 * 12000 > 32767 at nb=1
+    n = 20000
+    o = np.arange(1, 12001)
+    trip = np.stack([np.zeros_like(o), o, o % 7], axis=1)
+    kg = _kg(trip)
+    assert packed_count_bound(kg, n, len(trip)) > PACKED_MAX
+    # small batches bound the hub's per-batch count instead
+    assert packed_count_bound(kg, n, 1000) <= PACKED_MAX
+
+
+def test_corruption_term_tiny_graph():
+    # 10 entities, one batch of 40000: ~8000 occurrences per row (24000
+    # counted) and corruptions concentrate (lambda = 8000 per row)
+    rs = np.random.RandomState(1)
+    trip = np.stack([rs.randint(10, size=40000), rs.randint(10, size=40000),
+                     rs.randint(3, size=40000)], axis=1)
+    kg = _kg(trip)
+    assert packed_count_bound(kg, 10, 40000) > PACKED_MAX   # -> fp32 sums
+    assert packed_count_bound(kg, 10, 4000) > 3 * 8000   # the triples' part is not batch-bound
+
+
+def test_relation_replicas_dominant_relation():
+    rs = np.random.RandomState(2)
+    T = 141442
+    p = np.where(rs.rand(T) < 0.5, 0, rs.randint(1, 18, size=T))   # relation 0: half the triples
+    trip = np.stack([rs.randint(40943, size=T), rs.randint(40943, size=T), p], axis=1)
+    kg = _kg(trip)
+    assert relation_replicas(kg, 18, 1414) == 1          # 4 * 1414 fits
+    r = relation_replicas(kg, 18, 70721)                   # ~35k positives of relation 0
+    assert r > 1 and 4 * -(-70721 // r) <= PACKED_MAX
+    assert relation_replicas(kg, 18, 70721, max_reps=4) == 0
