@@ -331,6 +331,21 @@ skge_pipe_runner_t *skge_pipe_runner_create(void *stream, const skge_table_t *en
                                             int64_t T, const void *set, int64_t set_capacity,
                                             int nbatches, uint64_t seed, uint64_t *epoch_key,
                                             float margin, int ntries, int *nviol_total);
+/* flags of skge_pipe_runner_create_ex */
+enum {
+  SKGE_PIPE_LAZY = 1   /* lazy apply: no entity apply waves; the first wave of a later batch
+                          to read a row applies its pending update (claimed with an atomicMax
+                          on a per-row launch id, published write-through), the epoch's flush
+                          launch applies the rest.  One entity accumulator copy (the caller's;
+                          no slot records needed), two int words per entity row.  Same
+                          parameters, bit for bit. */
+};
+skge_pipe_runner_t *skge_pipe_runner_create_ex(void *stream, const skge_table_t *ent,
+                                               const skge_table_t *rel, int d, const int *trip,
+                                               int64_t T, const void *set, int64_t set_capacity,
+                                               int nbatches, uint64_t seed, uint64_t *epoch_key,
+                                               float margin, int ntries, int *nviol_total,
+                                               int flags);
 int skge_pipe_runner_run(skge_pipe_runner_t *r, void *stream, int nepochs);
 /* synchronizes the stream; returns 0, or a bit set (results then invalid):
  * 1 = a bounded cross-workgroup wait gave up, 2 = a row's per-batch count

@@ -62,6 +62,8 @@ struct PipeTab {               // entity table
   int* touched[2];             // slot records of the batch
   int* pend[2];                // [rows]: id of the launch that last accumulated into the row
   int* done;                   // [rows]: id of the launch whose update of the row was last applied
+                               // (lazy: whose first reader of the row has published it)
+  int* claim;                  // lazy only, [rows]: id of the last launch that claimed the row
   UpdParams u;
   int* claims;                 // profile only: rows applied in this launch (sharded)
   int* err;                    // ERR_* bits
@@ -88,6 +90,7 @@ struct PipeArgs {
   int b, nb1;                  // batch index in the epoch (nb1: the flush), batches per epoch
   const uint64_t* epoch_key;
   int d, nA;                   // nA: workgroups of the A role
+  int n_ent;                   // entity rows (the lazy flush scans them all)
   float margin;
   int* nviol_total;            // the caller's counter: += the epoch's violations, at the flush
   int* nviol_shards;           // [NSHARD][SHARD_STRIDE]: this epoch's violations so far
@@ -241,6 +244,54 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
   if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
 }
 
+// Two slot-recorded rows per A wave (SKGE_PIPE_ASLOTS 2): both claims (lanes 0
+// and 1 of one atomic instruction) and both rows' loads in one round trip, the
+// claimed rows applied and stored write-through, ONE drain, then both done
+// words.  Halves the A role's waves: the launch's waves then fit the chip's
+// residency (6 waves per SIMD here), so no scoring workgroup waits for an
+// apply workgroup to retire before it can start.
+template <int KQ>
+__device__ __forceinline__ void claim_and_apply2(const PipeTab& t, int pp, int r0, int r1, int d,
+                                                 int gp) {
+  const int l = lane_id(), nq = d >> 2;
+  int c = 0;
+  const int rl = l == 0 ? r0 : r1;
+  if (l < 2 && rl >= 0) c = atomicExch(t.cnt[pp] + rl, 0);
+  const int q0 = r0 >= 0 ? r0 : r1, q1 = r1 >= 0 ? r1 : r0;   // valid addresses for the loads
+  unsigned long long sv0[KQ], sv1[KQ];
+  float4 p0[KQ], a0[KQ], p1[KQ], a1[KQ];
+  load_upd_row<KQ>(t.P + (size_t)q0 * d, t.A ? t.A + (size_t)q0 * d : nullptr,
+                   t.sum[pp] + (size_t)q0 * nq, d, p0, a0, sv0);
+  load_upd_row<KQ>(t.P + (size_t)q1 * d, t.A ? t.A + (size_t)q1 * d : nullptr,
+                   t.sum[pp] + (size_t)q1 * nq, d, p1, a1, sv1);
+  const int c0 = __builtin_amdgcn_readlane(c, 0), c1 = __builtin_amdgcn_readlane(c, 1);
+  if (c0 == 0 && c1 == 0) return;   // other waves own the rows (or empty slots)
+  if (c0) {
+    if (c0 > PACKED_MAX && l == 0) atomicOr(t.err, ERR_PACKED);
+    row_update<KQ, false>(t.u, c0, d, sv0, sv0, p0, a0);
+    unsigned long long* srow = t.sum[pp] + (size_t)r0 * nq;
+#pragma unroll
+    for (int m = 0; m < KQ; ++m)
+      if (64 * m + l < nq) srow[64 * m + l] = 0ull;
+    store_row4_sc1<KQ>(t.P, r0, d, p0);
+    if (t.A) store_row4_sc1<KQ>(t.A, r0, d, a0);
+  }
+  if (c1) {
+    if (c1 > PACKED_MAX && l == 0) atomicOr(t.err, ERR_PACKED);
+    row_update<KQ, false>(t.u, c1, d, sv1, sv1, p1, a1);
+    unsigned long long* srow = t.sum[pp] + (size_t)r1 * nq;
+#pragma unroll
+    for (int m = 0; m < KQ; ++m)
+      if (64 * m + l < nq) srow[64 * m + l] = 0ull;
+    store_row4_sc1<KQ>(t.P, r1, d, p1);
+    if (t.A) store_row4_sc1<KQ>(t.A, r1, d, a1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+  if (l < 2 && (l == 0 ? c0 : c1))
+    __hip_atomic_store(t.done + rl, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t.claims && l == 0) atomicAdd(shard_of(t.claims), (c0 != 0) + (c1 != 0));
+}
+
 // B role: make sure launch gp's update of entity `row` (pending at launch
 // start) has landed -- apply it if nobody has claimed it yet, else wait for
 // its publisher
@@ -318,6 +369,38 @@ __device__ __forceinline__ T* opaque_ptr(T* p) {
   return reinterpret_cast<T*>(v);
 }
 
+// A role, relation row w: write R_b[w] (from R_{b-1} and batch b-1's sums) to
+// buffer rw for the next launch, clear the accumulator copy two launches old
+// (at the flush also the previous one: no scoring wave reads it any more)
+template <int KQ, bool W32>
+__device__ __forceinline__ void rel_publish(const PipeArgs& a, int w, int rd, int rw, int ra_prev,
+                                            int ra_old) {
+  const int l = lane_id(), d = a.d, nq = d >> 2;
+  const int rcw = W32 ? 2 * nq : nq;
+  float4 p[KQ], av[KQ];
+  int c;
+  rel_row<KQ, W32>(a.R, w, d, rd, ra_prev, p, av, c);
+  float4* prow = reinterpret_cast<float4*>(a.R.P[rw] + (size_t)w * d);
+  float4* arow = a.R.A[rw] ? reinterpret_cast<float4*>(a.R.A[rw] + (size_t)w * d) : nullptr;
+  unsigned long long* old = a.R.acc[ra_old] + (size_t)w * a.R.rw;
+  unsigned long long* prev = a.R.acc[ra_prev] + (size_t)w * a.R.rw;
+  const bool flush = a.b == a.nb1;
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l;
+    if (q < nq) {
+      prow[q] = p[m];
+      if (arow) arow[q] = av[m];
+    }
+  }
+  for (int q = l; q <= rcw; q += 64) {
+    old[q] = 0ull;
+    if (flush) prev[q] = 0ull;
+  }
+  if (c && a.R.updated && l == 0) atomicAdd(shard_of(a.R.updated), 1);
+  if (!W32 && c > PACKED_MAX && l == 0) atomicOr(a.err, ERR_PACKED);
+}
+
 #ifdef SKGE_PIPE_WAVES_PER_EU
 #define SKGE_PIPE_OCC __attribute__((amdgpu_waves_per_eu(SKGE_PIPE_WAVES_PER_EU, 8)))
 #else
@@ -326,6 +409,10 @@ __device__ __forceinline__ T* opaque_ptr(T* p) {
 #ifndef SKGE_PIPE_WG
 #define SKGE_PIPE_WG 256   // threads per workgroup
 #endif
+#ifndef SKGE_PIPE_ASLOTS
+#define SKGE_PIPE_ASLOTS 1   // entity slots per A-role wave (1 or 2)
+#endif
+constexpr int ASLOTS = SKGE_PIPE_ASLOTS;
 template <int KQ, bool W32>
 __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
@@ -344,42 +431,29 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
   if ((int)blockIdx.x < a.nA) {
     // ---- A role: write R_b, then apply the previous batch's entity rows ----
     const int nR = a.R.rows;
-    const int total = nR + a.prev_slots;   // relation rows, then entity slots
+    const int total = nR + (a.prev_slots + ASLOTS - 1) / ASLOTS;   // relation rows, slot groups
     const int wa = blk_a * wpb + (threadIdx.x >> 6);
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
     if (a.b == a.nb1 && wa == 0)   // the flush: fold the epoch's violation count
       fold_shards(a.nviol_shards, a.nviol_total);
     for (int w = wa; w < total; w += a.nA * wpb) {
       if (w < nR) {
-        float4 p[KQ], av[KQ];
-        int c;
-        rel_row<KQ, W32>(a.R, w, d, rd, ra_prev, p, av, c);
-        float4* prow = reinterpret_cast<float4*>(a.R.P[rw] + (size_t)w * d);
-        float4* arow = a.R.A[rw] ? reinterpret_cast<float4*>(a.R.A[rw] + (size_t)w * d) : nullptr;
-        unsigned long long* old = a.R.acc[ra_old] + (size_t)w * a.R.rw;
-        unsigned long long* prev = a.R.acc[ra_prev] + (size_t)w * a.R.rw;
-        const bool flush = a.b == a.nb1;   // no scoring waves read copy ra_prev any more
-#pragma unroll
-        for (int m = 0; m < KQ; ++m) {
-          const int q = 64 * m + l;
-          if (q < nq) {
-            prow[q] = p[m];
-            if (arow) arow[q] = av[m];
-          }
-        }
-        for (int q = l; q <= rcw; q += 64) {
-          old[q] = 0ull;
-          if (flush) prev[q] = 0ull;
-        }
-        if (c && a.R.updated && l == 0) atomicAdd(shard_of(a.R.updated), 1);
-        if (!W32 && c > PACKED_MAX && l == 0) atomicOr(a.err, ERR_PACKED);
+        rel_publish<KQ, W32>(a, w, rd, rw, ra_prev, ra_old);
       } else {
-        const int row = __builtin_amdgcn_readfirstlane(a.E.touched[pp][w - nR]);
+        if (ASLOTS == 2) {
+          const int i0 = 2 * (w - nR);
+          const int r0 = __builtin_amdgcn_readfirstlane(a.E.touched[pp][i0]);
+          const int r1 = i0 + 1 < a.prev_slots
+                             ? __builtin_amdgcn_readfirstlane(a.E.touched[pp][i0 + 1]) : -1;
+          if (r0 >= 0 || r1 >= 0) claim_and_apply2<KQ>(a.E, pp, r0, r1, d, gp);
+        } else {
+          const int row = __builtin_amdgcn_readfirstlane(a.E.touched[pp][w - nR]);
 #ifndef SKGE_PIPE_ABL_NOAPPLY_E   // timing-only ablation: entity rows never updated
-        if (row >= 0) claim_and_apply<KQ>(a.E, pp, row, d, gp);
+          if (row >= 0) claim_and_apply<KQ>(a.E, pp, row, d, gp);
 #else
-        if (row >= 0 && l == 0) a.E.cnt[pp][row] = 0;
+          if (row >= 0 && l == 0) a.E.cnt[pp][row] = 0;
 #endif
+        }
       }
     }
     if (a.trace && l == 0) {
@@ -542,6 +616,309 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
   }
 }
 
+// ---- lazy apply (skge_pipe_runner_create_ex with SKGE_PIPE_LAZY) ----
+//
+// Entity rows keep ONE accumulator (sum, cnt): the contributions of the last
+// batch that touched the row, not yet applied.  A launch has no entity apply
+// waves; instead the first scoring wave of batch b to read a row applies the
+// row's pending update before scoring with it: lane k of the wave claims its
+// row with atomicMax(claim[row], g) (old < g: first reader in this launch), in
+// the same memory round trip as the row's parameters, AdaGrad state, sums and
+// count; the claimer updates the row (row_update, the same code as every other
+// apply), writes it back write-through, zeroes the sums, drains and publishes
+// done[row] = g.  Other readers of the row in the same batch wait for that and
+// re-read it (sc1).  Rows nobody reads again are applied by the epoch's flush
+// launch.  Every batch's sums of a row are applied once, before any later read
+// of the row, by the same arithmetic: bitwise the two-launch loop's result.
+
+// 8-B write-through stores of zeros over a packed sum row (lanes past the row
+// fall outside the descriptor: dropped)
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+template <int KQ>
+__device__ __forceinline__ void zero_sum_row_sc1(unsigned long long* S, int row, int nq) {
+  row = __builtin_amdgcn_readfirstlane(row);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(S + (size_t)row * nq, 0, nq * 8, 0x00020000);
+  const u32x2 z = {0u, 0u};
+#pragma unroll
+  for (int m = 0; m < KQ; ++m)
+    __builtin_amdgcn_raw_buffer_store_b64(z, rs, (64 * m + lane_id()) * 8, 0, AUX_SC1);
+}
+
+// parameters, AdaGrad state (P again when A is null: discarded) and packed sums
+// of one row, unconditional 16-B / 8-B loads; P and A zero past the row
+template <int KQ>
+__device__ __forceinline__ void load_lazy_row(const float* P, const float* A,
+                                              const unsigned long long* S, int row, int d,
+                                              float4 (&p)[KQ], float4 (&a)[KQ],
+                                              unsigned long long (&sv)[KQ]) {
+  const int l = lane_id(), nq = d >> 2;
+  const float4* prow = reinterpret_cast<const float4*>(P + (size_t)row * d);
+  const float4* arow = reinterpret_cast<const float4*>((A ? A : P) + (size_t)row * d);
+  const unsigned long long* srow = S + (size_t)row * nq;
+  const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
+    const float4 pv = prow[qc], av = arow[qc];
+    sv[m] = srow[qc];
+    p[m] = q < nq ? pv : z;
+    a[m] = q < nq && A ? av : z;
+  }
+}
+
+// the claimer's apply of one row: update, write back, zero the sums (not the
+// count: lane `lane` of the caller does that)
+template <int KQ>
+__device__ __forceinline__ void lazy_apply(const PipeTab& t, int row, int c, int d,
+                                           const unsigned long long (&sv)[KQ], float4 (&p)[KQ],
+                                           float4 (&a)[KQ]) {
+  row_update<KQ, false>(t.u, c, d, sv, sv, p, a);
+  store_row4_sc1<KQ>(t.P, row, d, p);
+  if (t.A) store_row4_sc1<KQ>(t.A, row, d, a);
+  zero_sum_row_sc1<KQ>(t.sum[0], row, d >> 2);
+}
+
+template <int KQ, bool W32>
+__global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_lazy_batch(PipeArgs a) {
+  const int wpb = blockDim.x >> 6;
+  const int l = lane_id();
+  const int d = a.d, nq = d >> 2;
+  const int rcw = W32 ? 2 * nq : nq;
+  const int g = launch_id(a);
+  const int rd = a.b & 1;
+  const int rw = a.b < a.nb1 ? rd ^ 1 : 0;
+  const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
+  const int nB = gridDim.x - a.nA;
+  if ((int)blockIdx.x < a.nA) {
+    // ---- A role: write R_b; at the flush also apply every pending entity row ----
+    const int nR = a.R.rows;
+    const bool flush = a.b == a.nb1;
+    const int nchunk = flush ? (a.n_ent + 63) / 64 : 0;
+    const int wa = (int)blockIdx.x * wpb + (threadIdx.x >> 6);
+    if (flush && wa == 0) fold_shards(a.nviol_shards, a.nviol_total);
+    for (int w = wa; w < nR + nchunk; w += a.nA * wpb) {
+      if (w < nR) {
+        rel_publish<KQ, W32>(a, w, rd, rw, ra_prev, ra_old);
+        continue;
+      }
+      const int r0 = (w - nR) * 64;
+      const int cv = r0 + l < a.n_ent ? a.E.cnt[0][r0 + l] : 0;
+      uint64_t mask = __ballot(cv != 0);
+      int napplied = 0;
+      while (mask) {
+        const int k = (int)__builtin_ctzll(mask);
+        mask &= mask - 1;
+        const int row = r0 + k;
+        const int c = __builtin_amdgcn_readlane(cv, k);
+        unsigned long long sv[KQ];
+        float4 p[KQ], av[KQ];
+        load_lazy_row<KQ>(a.E.P, a.E.A, a.E.sum[0], row, d, p, av, sv);
+        if (c > PACKED_MAX && l == 0) atomicOr(a.err, ERR_PACKED);
+        row_update<KQ, false>(a.E.u, c, d, sv, sv, p, av);
+        float4* prow = reinterpret_cast<float4*>(a.E.P + (size_t)row * d);
+        float4* arow = a.E.A ? reinterpret_cast<float4*>(a.E.A + (size_t)row * d) : nullptr;
+        unsigned long long* srow = a.E.sum[0] + (size_t)row * nq;
+#pragma unroll
+        for (int m = 0; m < KQ; ++m) {
+          const int q = 64 * m + l;
+          if (q < nq) {
+            prow[q] = p[m];
+            if (arow) arow[q] = av[m];
+            srow[q] = 0ull;
+          }
+        }
+        if (l == 0) a.E.cnt[0][row] = 0;
+        ++napplied;
+      }
+      if (a.E.claims && l == 0 && napplied) atomicAdd(shard_of(a.E.claims), napplied);
+    }
+    return;
+  }
+  // ---- B role: claim/apply/score/scatter batch b ----
+  unsigned long long* const esum = opaque_ptr(a.E.sum[0]);
+  int* const ecnt = opaque_ptr(a.E.cnt[0]);
+  int* const eclaim = opaque_ptr(a.E.claim);
+  int* const edone = opaque_ptr(a.E.done);
+  unsigned long long* const racc = opaque_ptr(a.R.acc[ra_cur]);
+  const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int4*>(a.rec + a.start), 0, a.count * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rec1_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int*>(a.rec_n1 + a.start), 0, a.count * 4, 0x00020000);
+  int nv = 0, napplied = 0;
+  const int blk_b = (int)blockIdx.x - a.nA;
+  for (int w = blk_b * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
+    unsigned long long tt[4];
+    if (a.trace) tt[0] = now_10ns();
+    const u32x4 rx = __builtin_amdgcn_raw_buffer_load_b128(rec_rs, w * 16, 0, 0);
+    const int r1 = (int)__builtin_amdgcn_raw_buffer_load_b32(rec1_rs, w * 4, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    const int s = __builtin_amdgcn_readfirstlane((int)rx.x);
+    const int o = __builtin_amdgcn_readfirstlane((int)rx.y);
+    const int p = __builtin_amdgcn_readfirstlane((int)rx.z);
+    const int neg0 = __builtin_amdgcn_readfirstlane((int)rx.w);
+    const int neg1 = __builtin_amdgcn_readfirstlane(r1);
+    const int n0r = neg0 >= 0 ? neg0 : s, n1r = neg1 >= 0 ? neg1 : o;
+    // a row the wave reads twice is claimed / waited for by its first lane only
+    const int dupm = (o == s ? 2 : 0) | (n0r == s || n0r == o ? 4 : 0) |
+                     (n1r == s || n1r == o || n1r == n0r ? 8 : 0);
+    const int myrow = sel4(l, s, o, n0r, n1r);
+    const bool own = l < 4 && !((dupm >> l) & 1);
+    // one round trip: claims, counts, rows, AdaGrad states, sums, relation row
+    int old = g, cv = 0;
+    if (own) {
+      old = atomicMax(eclaim + myrow, g);
+      cv = ecnt[myrow];
+    }
+    float4 es[KQ], eo[KQ], fs[KQ], fo[KQ], as_[KQ], ao[KQ], a0[KQ], a1[KQ], rp[KQ];
+    unsigned long long ss[KQ], so[KQ], s0[KQ], s1[KQ];
+    load_lazy_row<KQ>(a.E.P, a.E.A, esum, s, d, es, as_, ss);
+    load_lazy_row<KQ>(a.E.P, a.E.A, esum, o, d, eo, ao, so);
+    load_lazy_row<KQ>(a.E.P, a.E.A, esum, n0r, d, fs, a0, s0);
+    load_lazy_row<KQ>(a.E.P, a.E.A, esum, n1r, d, fo, a1, s1);
+    {
+      float4 ra[KQ];
+      int c;
+      rel_row<KQ, W32>(a.R, p, d, rd, ra_prev, rp, ra, c);
+    }
+    const int clm = (int)(__ballot(own && old < g) & 0xfull);   // rows this wave claims
+    const int cnz = (int)(__ballot(own && old < g && cv != 0) & 0xfull);   // ... with sums
+    if (a.trace) tt[1] = now_10ns();
+    if (cnz) {
+      if (cnz & 1) lazy_apply<KQ>(a.E, s, __builtin_amdgcn_readlane(cv, 0), d, ss, es, as_);
+      if (cnz & 2) lazy_apply<KQ>(a.E, o, __builtin_amdgcn_readlane(cv, 1), d, so, eo, ao);
+      if (cnz & 4) lazy_apply<KQ>(a.E, n0r, __builtin_amdgcn_readlane(cv, 2), d, s0, fs, a0);
+      if (cnz & 8) lazy_apply<KQ>(a.E, n1r, __builtin_amdgcn_readlane(cv, 3), d, s1, fo, a1);
+      if (l < 4 && ((cnz >> l) & 1))
+        __hip_atomic_store(ecnt + myrow, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+      napplied += __builtin_popcount(cnz);
+    }
+    if (l < 4 && ((clm >> l) & 1))
+      __hip_atomic_store(edone + myrow, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.trace) tt[2] = now_10ns();
+    // rows another wave of this batch claimed: wait for their publication, re-read
+    const int wt = (int)(__ballot(own && old >= g) & 0xfull);
+    if (wt) {
+      unsigned spins = 0;
+      for (;;) {
+        const bool ready = !(l < 4 && ((wt >> l) & 1)) ||
+                           __hip_atomic_load(edone + myrow, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) == g;
+        if (__ballot(!ready) == 0ull) break;
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 22)) {   // ~0.5 s: never hang the GPU; report instead
+          if (l == 0) atomicOr(a.err, ERR_WAIT);
+          break;
+        }
+        if ((spins & 1023u) == 0 &&
+            __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+          break;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the re-reads below the poll
+      if (wt & 1) load_row4_sc1<KQ>(a.E.P, s, d, es);
+      if (wt & 2) load_row4_sc1<KQ>(a.E.P, o, d, eo);
+      if (wt & 4) load_row4_sc1<KQ>(a.E.P, n0r, d, fs);
+      if (wt & 8) load_row4_sc1<KQ>(a.E.P, n1r, d, fo);
+    }
+    if (dupm) {   // duplicates take the first equal row's (updated) values
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) {
+        if (dupm & 2) eo[m] = es[m];
+        if (dupm & 4) fs[m] = n0r == s ? es[m] : eo[m];
+        if (dupm & 8) fo[m] = n1r == s ? es[m] : (n1r == o ? eo[m] : fs[m]);
+      }
+    }
+    float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
+    float4 gp4[KQ], g0[KQ], g1[KQ];
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+#define SKGE_EL(X)                                                                    \
+  {                                                                                   \
+    const float vp = (es[m].X + rp[m].X) - eo[m].X;   /* transe.py:32 */              \
+    const float v0 = (fs[m].X + rp[m].X) - eo[m].X;                                   \
+    const float v1 = (es[m].X + rp[m].X) - fo[m].X;                                   \
+    ps += fabsf(vp);                                                                  \
+    n0 += fabsf(v0);                                                                  \
+    n1 += fabsf(v1);                                                                  \
+    gp4[m].X = signf_np(-((eo[m].X - rp[m].X) - es[m].X)); /* transe.py:103,115 */    \
+    g0[m].X = signf_np((eo[m].X - rp[m].X) - fs[m].X);     /* transe.py:104,117 */    \
+    g1[m].X = signf_np((fo[m].X - rp[m].X) - es[m].X);                                \
+  }
+      SKGE_EL(x)
+      SKGE_EL(y)
+      SKGE_EL(z)
+      SKGE_EL(w)
+#undef SKGE_EL
+    }
+    const float pscore = -wave_sum(ps);
+    const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
+    const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // strict >, transe.py:73
+    const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
+    if (a.trace) tt[3] = now_10ns();
+    {
+      const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
+      const int rE = sel4(l, s, o, neg0, neg1);
+      if (l < 4) {
+        if (cE > 0) atomicAdd(ecnt + rE, cE);
+      } else if (l == 4 && v0 + v1 > 0) {
+        atomicAdd(racc + (size_t)p * a.R.rw + rcw, (unsigned long long)(2 * (v0 + v1)));
+      }
+    }
+    if (v0 + v1 > 0) {
+      nv += v0 + v1;
+      const float fv0 = (float)v0, fv1 = (float)v1;
+      float4 cs[KQ], co[KQ], c0[KQ], c1[KQ], cr[KQ];
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) {
+#define SKGE_CO(X)                                                   \
+  cs[m].X = fv0 * gp4[m].X + fv1 * (gp4[m].X + g1[m].X);             \
+  co[m].X = -(fv0 * (gp4[m].X + g0[m].X) + fv1 * gp4[m].X);          \
+  c0[m].X = g0[m].X;                                                 \
+  c1[m].X = -g1[m].X;                                                \
+  cr[m].X = fv0 * (gp4[m].X + g0[m].X) + fv1 * (gp4[m].X + g1[m].X);
+        SKGE_CO(x)
+        SKGE_CO(y)
+        SKGE_CO(z)
+        SKGE_CO(w)
+#undef SKGE_CO
+      }
+      Accum aE;
+      aE.sum = reinterpret_cast<float*>(esum);
+      acc_row4_i16<KQ>(aE, s, cs, d);
+      acc_row4_i16<KQ>(aE, o, co, d);
+      if (v0) acc_row4_i16<KQ>(aE, neg0, c0, d);
+      if (v1) acc_row4_i16<KQ>(aE, neg1, c1, d);
+      unsigned long long* rrow = racc + (size_t)p * a.R.rw;
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) {
+        const int q = 64 * m + l;
+        if (q < nq) {
+          if (W32) {
+            atomicAdd(rrow + 2 * q, pack_i32x2(cr[m].x, cr[m].y));
+            atomicAdd(rrow + 2 * q + 1, pack_i32x2(cr[m].z, cr[m].w));
+          } else {
+            atomicAdd(rrow + q, pack_i16x4(cr[m]));
+          }
+        }
+      }
+    }
+    if (a.trace && l == 0) {   // stamp after issue (no drain)
+      unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
+      tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
+      tr[5] = (unsigned long long)(cnz | (wt << 4) | (clm << 12)) |
+              ((unsigned long long)(v0 + v1 > 0) << 8);
+    }
+  }
+  if (l == 0) {
+    if (nv) {
+      atomicAdd(shard_of(a.nviol_shards), nv);
+      if (a.stats_viol) atomicAdd(shard_of(a.stats_viol), nv);
+    }
+    if (napplied && a.E.claims) atomicAdd(shard_of(a.E.claims), napplied);
+  }
+}
+
 __global__ void k_pipe_advance(uint64_t* ek) { *ek += 1; }
 
 // draw every negative of the epoch: one thread per positive, the same draws and
@@ -610,6 +987,7 @@ struct skge_pipe_runner {
   std::vector<PipeArgs> batch;     // nb1 batches + the flush
   std::vector<int> grid;
   bool w32 = false;                // int32x2 relation sums
+  bool lazy = false;               // SKGE_PIPE_LAZY: entity rows applied by their next reader
   int nlaunch() const { return (int)batch.size() + 2; }
 };
 
@@ -655,12 +1033,16 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
       a.stats_viol = stats + (3 * i + 2) * sh;
     }
     if (trace && i == trace_launch) a.trace = trace;
-#define SKGE_PB(K)                                                                              \
-  do {                                                                                          \
-    if (r->w32)                                                                                 \
-      hipLaunchKernelGGL((k_pipe_batch<K, true>), dim3(r->grid[k]), dim3(SKGE_PIPE_WG), 0, st, a); \
-    else                                                                                        \
-      hipLaunchKernelGGL((k_pipe_batch<K, false>), dim3(r->grid[k]), dim3(SKGE_PIPE_WG), 0, st, a); \
+#define SKGE_PB(K)                                                                               \
+  do {                                                                                           \
+    const dim3 gr(r->grid[k]), bl(SKGE_PIPE_WG);                                                 \
+    if (r->lazy) {                                                                               \
+      if (r->w32) hipLaunchKernelGGL((k_lazy_batch<K, true>), gr, bl, 0, st, a);                 \
+      else hipLaunchKernelGGL((k_lazy_batch<K, false>), gr, bl, 0, st, a);                       \
+    } else {                                                                                     \
+      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true>), gr, bl, 0, st, a);                 \
+      else hipLaunchKernelGGL((k_pipe_batch<K, false>), gr, bl, 0, st, a);                       \
+    }                                                                                            \
   } while (0)
     if (r->kq <= 1) SKGE_PB(1);
     else if (r->kq <= 2) SKGE_PB(2);
@@ -672,20 +1054,22 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
   if (ev) (void)hipEventRecord(ev[i + 1], st);
 }
 
-extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_table_t* ent,
-                                                       const skge_table_t* rel, int d,
-                                                       const int* trip, int64_t T, const void* set,
-                                                       int64_t set_capacity, int nbatches,
-                                                       uint64_t seed, uint64_t* epoch_key,
-                                                       float margin, int ntries,
-                                                       int* nviol_total) {
+extern "C" skge_pipe_runner_t* skge_pipe_runner_create_ex(
+    void* stream, const skge_table_t* ent, const skge_table_t* rel, int d, const int* trip,
+    int64_t T, const void* set, int64_t set_capacity, int nbatches, uint64_t seed,
+    uint64_t* epoch_key, float margin, int ntries, int* nviol_total, int flags) {
+  const bool lazy = (flags & SKGE_PIPE_LAZY) != 0;
+  if (flags & ~SKGE_PIPE_LAZY) {
+    set_error("pipelined runner: unknown flags %d", flags);
+    return nullptr;
+  }
   // the pipelined loop is the packed TransE-L1 path
   skge_table_t relc = *rel;   // the relation encoding is the runner's own (checked below)
   if (relc.acc_mode == SKGE_ACC_I32X2) relc.acc_mode = SKGE_ACC_I16X4;
   if (check_table(ent, "ent", true) || check_table(&relc, "rel", true)) return nullptr;
   if (ent->acc_mode != SKGE_ACC_I16X4 ||
       (rel->acc_mode != SKGE_ACC_I16X4 && rel->acc_mode != SKGE_ACC_I32X2) || d % 4 || d > 1024 ||
-      ent->width != d || rel->width != d || ent->acc_touched == nullptr ||
+      ent->width != d || rel->width != d || (ent->acc_touched == nullptr && !lazy) ||
       rel->acc_touched != nullptr || rel->acc_replicas > 1 || ent->acc_replicas > 1 ||
       ent->gate || rel->gate) {
     set_error("pipelined runner: needs a packed (SKGE_ACC_I16X4) entity table with slot "
@@ -700,7 +1084,7 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
   }
   // batch geometry of StochasticTrainer._optim (skge/base.py:1246-1268)
   const int64_t bs = T / nbatches;
-  if (4 * bs > ent->touched_cap || 4 * bs > (1ll << 30)) {
+  if ((!lazy && 4 * bs > ent->touched_cap) || 4 * bs > (1ll << 30)) {
     set_error("pipelined runner: batch too large for the slot capacity");
     return nullptr;
   }
@@ -708,6 +1092,7 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
   for (int64_t s0 = 0; s0 < T; s0 += bs) batches.push_back({s0, (s0 + bs <= T) ? bs : T - s0});
   const int nb1 = (int)batches.size();
   skge_pipe_runner* r = new skge_pipe_runner();
+  r->lazy = lazy;
   const int nq = d / 4;
   PipeArgs a = {};
   auto upd = [](const skge_table_t* s) {
@@ -731,12 +1116,19 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
     t.sum[0] = reinterpret_cast<unsigned long long*>(ent->acc_sum);
     t.cnt[0] = ent->acc_cnt;
     t.touched[0] = ent->acc_touched;
-    t.sum[1] = (unsigned long long*)dalloc(r, (size_t)N * nq * 8);
-    t.cnt[1] = (int*)dalloc(r, (size_t)N * 4);
-    t.touched[1] = (int*)dalloc(r, (size_t)4 * bs * 4);
-    t.pend[0] = (int*)dalloc(r, (size_t)N * 4);
-    t.pend[1] = (int*)dalloc(r, (size_t)N * 4);
     t.done = (int*)dalloc(r, (size_t)N * 4);
+    bool ok = t.done != nullptr;
+    if (lazy) {   // one accumulator copy (the caller's), claim words
+      t.claim = (int*)dalloc(r, (size_t)N * 4);
+      ok = ok && t.claim;
+    } else {      // a second accumulator copy, slot records and batch marks
+      t.sum[1] = (unsigned long long*)dalloc(r, (size_t)N * nq * 8);
+      t.cnt[1] = (int*)dalloc(r, (size_t)N * 4);
+      t.touched[1] = (int*)dalloc(r, (size_t)4 * bs * 4);
+      t.pend[0] = (int*)dalloc(r, (size_t)N * 4);
+      t.pend[1] = (int*)dalloc(r, (size_t)N * 4);
+      ok = ok && t.sum[1] && t.cnt[1] && t.touched[1] && t.pend[0] && t.pend[1];
+    }
     RelTab& q = a.R;
     const int M = rel->rows;
     const bool ada = rel->opt == SKGE_ADAGRAD;
@@ -750,8 +1142,7 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
     q.A[0] = ada ? rel->state : nullptr;
     q.A[1] = ada ? (float*)dalloc(r, (size_t)M * d * 4) : nullptr;
     for (int k = 0; k < 3; ++k) q.acc[k] = (unsigned long long*)dalloc(r, (size_t)M * q.rw * 8);
-    if (!t.sum[1] || !t.cnt[1] || !t.touched[1] || !t.pend[0] || !t.pend[1] || !t.done ||
-        !q.P[1] || (ada && !q.A[1]) || !q.acc[0] || !q.acc[1] || !q.acc[2]) {
+    if (!ok || !q.P[1] || (ada && !q.A[1]) || !q.acc[0] || !q.acc[1] || !q.acc[2]) {
       set_error("pipelined runner: device allocation failed");
       pipe_free(r);
       return nullptr;
@@ -791,13 +1182,17 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
   a.trace = nullptr;
   a.err = r->err;
   a.E.err = r->err;
+  a.n_ent = ent->rows;
   int prev = 0;
   for (int b = 0; b <= nb1; ++b) {   // b == nb1: flush of the last batch (A role only)
     a.b = b;
     a.start = b < nb1 ? batches[b].first : 0;
     a.count = b < nb1 ? (int)batches[b].second : 0;
     a.prev_slots = 4 * prev;
-    const int a_items = 4 * prev + rel->rows;   // entity slots + every relation row
+    // A role: every relation row, then the previous batch's entity slots (lazy:
+    // no entity rows, except the flush's sweep over all rows in 64-row chunks)
+    const int a_items = rel->rows + (lazy ? (b == nb1 ? (ent->rows + 63) / 64 : 0)
+                                          : (4 * prev + ASLOTS - 1) / ASLOTS);
     constexpr int WPB = SKGE_PIPE_WG / 64;
     a.nA = std::max(1, std::min((a_items + WPB - 1) / WPB, 16384));
     const int nBb = std::max(1, std::min((a.count + WPB - 1) / WPB, 16384));
@@ -828,6 +1223,17 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
     return nullptr;
   }
   return r;
+}
+
+extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_table_t* ent,
+                                                       const skge_table_t* rel, int d,
+                                                       const int* trip, int64_t T, const void* set,
+                                                       int64_t set_capacity, int nbatches,
+                                                       uint64_t seed, uint64_t* epoch_key,
+                                                       float margin, int ntries,
+                                                       int* nviol_total) {
+  return skge_pipe_runner_create_ex(stream, ent, rel, d, trip, T, set, set_capacity, nbatches,
+                                    seed, epoch_key, margin, ntries, nviol_total, 0);
 }
 
 extern "C" int skge_pipe_runner_run(skge_pipe_runner_t* r, void* stream, int nepochs) {

@@ -19,6 +19,7 @@ SKGE_AF_LINEAR, SKGE_AF_SIGMOID, SKGE_AF_TANH, SKGE_AF_RELU = 0, 1, 2, 3
 SKGE_SGD, SKGE_ADAGRAD = 0, 1
 SKGE_POST_NONE, SKGE_POST_NORMALIZE, SKGE_POST_NORMLESS1 = 0, 1, 2
 SKGE_ACC_F32, SKGE_ACC_I16X4, SKGE_ACC_I32X2 = 0, 1, 2
+SKGE_PIPE_LAZY = 1
 
 c_p = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -77,6 +78,8 @@ SIGNATURES = {
     "skge_pair_runner_destroy": (None, [c_p]),
     "skge_pipe_runner_create": (c_p, [c_p, T_P, T_P, c_i, c_p, c_i64, c_p, c_i64, c_i, c_u64, c_p,
                                       c_f, c_i, c_p]),
+    "skge_pipe_runner_create_ex": (c_p, [c_p, T_P, T_P, c_i, c_p, c_i64, c_p, c_i64, c_i, c_u64,
+                                         c_p, c_f, c_i, c_p, c_i]),
     "skge_pipe_runner_run": (c_i, [c_p, c_p, c_i]),
     "skge_pipe_runner_error": (c_i, [c_p, c_p]),
     "skge_pipe_runner_profile": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_p, c_i64]),

@@ -39,6 +39,10 @@ class DeviceKG(object):
 
 
 PACKED_MAX = 32767   # a 16-bit packed field's bound (csrc/skge_pipeline.hip PACKED_MAX)
+import os as _os
+# the pipelined runner's entity apply: lazy (by the row's next reader, SKGE_PIPE_LAZY) or
+# by apply waves of the next launch
+LAZY_DEFAULT = _os.environ.get("SKGE_LAZY", "0") == "1"
 
 
 def _bincount_max(col, n):
@@ -63,14 +67,15 @@ def packed_count_bound(kg, n_ent, batch):
     return det + corr
 
 
-def relation_replicas(kg, n_rel, batch, max_reps=32):
+def relation_replicas(kg, n_rel, batch, max_reps=32, ranks=1):
     """Accumulator copies the two-launch runner's packed relation sums need:
     positive j adds into copy j mod reps, so a copy holds at most
-    ceil(batch / reps) positives, each adding <= 4 to its relation's count.
+    ceil(batch / reps) positives (per rank: the sharded runner all-reduces
+    each copy over `ranks` batches), each adding <= 4 to its relation's count.
     Returns 0 when even max_reps copies cannot keep the count <= PACKED_MAX."""
     top = int(_bincount_max(kg.trip[:, 2], n_rel).max().item())
     reps = 1
-    while 4 * min(top, -(-int(batch) // reps)) > PACKED_MAX:
+    while 4 * min(top, int(ranks) * -(-int(batch) // reps)) > PACKED_MAX:
         reps *= 2
         if reps > max_reps:
             return 0
@@ -94,7 +99,8 @@ class EpochRunner(object):
     """
 
     def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, stream=None,
-                 nviol_total=None, force_f32=False, replicas=1, pipelined=None, packed=None):
+                 nviol_total=None, force_f32=False, replicas=1, pipelined=None, packed=None,
+                 lazy=None):
         from .transe import TransE
         if not isinstance(model, TransE):
             raise NotImplementedError("device_loop supports TransE (the north-star path) only")
@@ -127,12 +133,16 @@ class EpochRunner(object):
         if pipelined and not can_pipe:
             raise ValueError("pipelined runner needs TransE-L1, d % 4 == 0, packed sums "
                              "and replicas == 1")
+        want_lazy = LAZY_DEFAULT if lazy is None else bool(lazy)
         if can_pipe and pipelined is None:
-            # the pipelined runner's scratch: a second entity accumulator copy,
-            # per-row marks and the epoch's records (auto mode: only if it fits)
+            # the pipelined runner's scratch: the epoch's records and per-row
+            # words, plus (not lazy) a second entity accumulator copy (auto
+            # mode: only if it fits)
             torch.cuda.synchronize(dev)
             torch.cuda.empty_cache()
-            extra = E.rows * E.width * 2 + E.rows * 12 + kg.T * 20 + (64 << 20)
+            acc = E.rows * (E.width * 2 + 4) + 4 * 4 * bs   # the entity accumulator itself
+            extra = acc + kg.T * 20 + (64 << 20) + (E.rows * 8 if want_lazy else
+                                                    E.rows * E.width * 2 + E.rows * 12)
             can_pipe = extra < torch.cuda.mem_get_info(dev)[0] * 0.9
         torch.cuda.current_stream().synchronize()
         lib = L.lib()
@@ -140,10 +150,12 @@ class EpochRunner(object):
             # relation sums in 16-bit fields while a relation's per-batch count
             # fits them (faster: half the atomics), else int32x2
             self._tables(model, updaters, packed, 1, rel_w32=rel_reps != 1)
-            h = lib.skge_pipe_runner_create(
+            self.lazy = want_lazy
+            h = lib.skge_pipe_runner_create_ex(
                 L.stream_ptr(self.stream), self.te, self.tr, model.d, L.ptr(kg.trip), kg.T,
                 L.ptr(kg.slots), kg.capacity, int(nbatches), int(seed) & (2 ** 64 - 1),
-                L.ptr(self.epoch_key), float(model.margin), int(ntries), L.ptr(self.nviol_total))
+                L.ptr(self.epoch_key), float(model.margin), int(ntries), L.ptr(self.nviol_total),
+                L.SKGE_PIPE_LAZY if self.lazy else 0)
             if h:
                 self.pipelined = True
                 self.handle = h
@@ -153,7 +165,10 @@ class EpochRunner(object):
             if not (self._auto and "allocation" in err):
                 raise L.SkgeError("skge_pipe_runner_create: %s" % err)
             # auto mode: out of device memory -> two-launch runner
+            self.accE = self.accR = self.te = self.tr = None
+            torch.cuda.empty_cache()
         self.pipelined = False
+        self.lazy = False
         if packed and rel_reps == 0:
             if not auto_packed:
                 raise ValueError("packed sums: a relation's per-batch count exceeds what 32 "

@@ -208,7 +208,16 @@ class ShardedRunner(object):
         self.batches = [(s0, max(0, min(bs, self.T - s0))) for s0 in range(0, T_max, bs)]
         self.accE = Accumulator(self.E.rows, self.d, dev, slots=4 * bs * self.G,
                                 mode=L.SKGE_ACC_I16X4)
-        self.accR = Accumulator(self.R.rows, self.d, dev, mode=L.SKGE_ACC_I16X4, dense=True)
+        # packed relation sums all-reduced over the ranks' batches: positive j
+        # adds into copy j mod reps, enough copies that no 16-bit field of the
+        # union batch can wrap (the apply folds them, device.relation_replicas)
+        from .device import relation_replicas
+        reps = relation_replicas(self.kg, self.R.rows, bs, ranks=self.G)
+        if reps == 0:
+            raise ValueError("sharded runner: a relation's count in the union batch exceeds "
+                             "what 32 packed accumulator copies hold; use more batches")
+        self.accR = Accumulator(self.R.rows, self.d, dev, mode=L.SKGE_ACC_I16X4, dense=True,
+                                replicas=reps)
         self.te = self.updE.table(self.accE, counters=False)
         self.tr = self.updR.table(self.accR, counters=False)
         self.cstride = int(L.lib().skge_shard_contrib_stride(self.d))

@@ -190,7 +190,7 @@ def test_runner_wn18_full_size_properties(l1):
         assert float(acc.sum.abs().sum().item()) == 0.0
 
 
-def _runner_result(n_ent, n_rel, T, d, nb, pipelined, epochs=2, seed=11, trip=None):
+def _runner_result(n_ent, n_rel, T, d, nb, pipelined, epochs=2, seed=11, trip=None, lazy=False):
     import skge_amd as S
     from skge_amd.device import DeviceKG, EpochRunner
     np.random.seed(seed)
@@ -200,8 +200,8 @@ def _runner_result(n_ent, n_rel, T, d, nb, pipelined, epochs=2, seed=11, trip=No
     if trip is None:
         trip, _ = make_kg(n_ent, n_rel, T)
     kg = DeviceKG(trip, m.device)
-    r = EpochRunner(m, upd, kg, nbatches=nb, seed=seed, pipelined=pipelined)
-    assert r.pipelined == pipelined
+    r = EpochRunner(m, upd, kg, nbatches=nb, seed=seed, pipelined=pipelined, lazy=lazy)
+    assert r.pipelined == pipelined and r.lazy == (lazy and pipelined)
     r.run(epochs)
     r.synchronize()
     for acc in (r.accE, r.accR):
@@ -226,11 +226,12 @@ def test_pipelined_runner_bitwise_equals_two_launch(n_ent, n_rel, T, d, nb):
     """The pipelined runner (one launch per batch, cross-workgroup hand-off of
     the previous batch's updates) must reproduce the two-launch loop exactly."""
     a, trip = _runner_result(n_ent, n_rel, T, d, nb, pipelined=False)
-    b, _ = _runner_result(n_ent, n_rel, T, d, nb, pipelined=True, trip=trip)
-    assert a["key"] == b["key"] == 2
-    assert a["nviol"] == b["nviol"] > 0
-    for k in ("E", "R", "pE", "pR"):
-        assert np.array_equal(a[k], b[k]), k
+    for lazy in (False, True):   # apply waves / lazy apply by the rows' next readers
+        b, _ = _runner_result(n_ent, n_rel, T, d, nb, pipelined=True, trip=trip, lazy=lazy)
+        assert a["key"] == b["key"] == 2
+        assert a["nviol"] == b["nviol"] > 0
+        for k in ("E", "R", "pE", "pR"):
+            assert np.array_equal(a[k], b[k]), (k, lazy)
 
 
 def test_trainer_device_loop_fit():

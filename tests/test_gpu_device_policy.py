@@ -68,11 +68,12 @@ def test_dominant_relation_large_batch_exact(pipelined):
     np.testing.assert_allclose(E1, E2, atol=1e-5, rtol=1e-5)
 
 
-def test_dominant_relation_pipelined_equals_two_launch_bitwise():
+@pytest.mark.parametrize("lazy", [False, True])
+def test_dominant_relation_pipelined_equals_two_launch_bitwise(lazy):
     trip = _dominant_kg(3000, 7, 24000, 0.5, seed=4)
-    a = _train(trip, 3000, 7, 200, 2, epochs=2, pipelined=True)
+    a = _train(trip, 3000, 7, 200, 2, epochs=2, pipelined=True, lazy=lazy)
     b = _train(trip, 3000, 7, 200, 2, epochs=2, pipelined=False)
-    assert a[3].packed and b[3].packed and b[3].accR.replicas >= 2
+    assert a[3].packed and b[3].packed and b[3].accR.replicas >= 2 and a[3].lazy == lazy
     assert a[2] == b[2] > 0
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
@@ -214,3 +215,24 @@ def test_pair_runner_holds_captured_buffers():
     r.run(1)
     r.synchronize()
     assert np.isfinite(np.asarray(m.E)).all()
+
+
+def test_sharded_dominant_relation_uses_copies_and_matches_runner():
+    """The row-sharded runner's packed relation sums are all-reduced over the
+    ranks' batches: a relation holding half the triples gets accumulator
+    copies, and G = 1 still equals the two-launch device runner bit for bit."""
+    import skge_amd as S
+    from skge_amd.shard import ShardedRunner
+    trip = _dominant_kg(3000, 7, 24000, 0.5, seed=4)
+    E1, R1, v1, r1 = _train(trip, 3000, 7, 64, 2, epochs=2, seed=11, pipelined=False)
+    assert r1.packed and r1.accR.replicas >= 2
+    np.random.seed(11)
+    m = S.TransE((3000, 3000, 7), 64)
+    sr = ShardedRunner(3000, m.E.data.clone(), m.R.data.clone(),
+                       torch.as_tensor(trip, device=m.device), 2, lr=0.1, margin=2.0, seed=3)
+    assert sr.accR.replicas >= 2
+    sr.run(2)
+    sr.synchronize()
+    assert int(sr.nviol_total.item()) == v1 > 0
+    assert np.array_equal(sr.E.data.cpu().numpy(), E1)
+    assert np.array_equal(sr.R.data.cpu().numpy(), R1)

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--d", type=int, default=200)
     ap.add_argument("--nb", type=int, default=100)
+    ap.add_argument("--lazy", type=int, default=0)
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -44,7 +45,7 @@ def main():
     m.add_hyperparam("margin", 2.0)
     upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
     kg = DeviceKG(trip, dev)
-    r = EpochRunner(m, upd, kg, nbatches=args.nb, seed=5)
+    r = EpochRunner(m, upd, kg, nbatches=args.nb, seed=5, lazy=bool(args.lazy))
     r.run(args.warmup)
     r.synchronize()
     for rep in range(2):
@@ -63,6 +64,21 @@ def main():
                   (np.array([bin(int(x)).count("1") for x in pend]) == 1).sum(),
                   (np.array([bin(int(x)).count("1") for x in pend]) >= 2).sum(), len(A),
                   stats[args.launch].tolist()))
+        if args.lazy:
+            cnz, wt, clm = B[:, 5] & 0xf, (B[:, 5] >> 4) & 0xf, (B[:, 5] >> 12) & 0xf
+            print("lazy: waves applying a row %d (rows %d), waiting %d, claiming %d" % (
+                (cnz != 0).sum(), sum(bin(int(x)).count("1") for x in cnz), (wt != 0).sum(),
+                (clm != 0).sum()))
+            print("percentiles (us)           p0     p10    p50    p90    p100")
+            print("B start                  ", pct(B[:, 0] - t0))
+            print("B record+claim+rows      ", pct(B[:, 1] - B[:, 0]))
+            print("B apply+drain (applying) ", pct((B[:, 2] - B[:, 1])[cnz != 0]))
+            print("B wait+score (waiting)   ", pct((B[:, 3] - B[:, 2])[wt != 0]))
+            print("B score (not waiting)    ", pct((B[:, 3] - B[:, 2])[wt == 0]))
+            print("B atomics issue (viol)   ", pct((B[:, 4] - B[:, 3])[viol == 1]))
+            print("B issue end              ", pct(B[:, 4] - t0))
+            print("last end %.2f us" % ((B[:, 4].max() - t0) / 100))
+            continue
         print("percentiles (us)           p0     p10    p50    p90    p100")
         print("B start                  ", pct(B[:, 0] - t0))
         print("B rows+marks (ballot)    ", pct(B[:, 1] - B[:, 0]))
