@@ -63,23 +63,39 @@ def packed_count_bound(kg, n_ent, batch):
     occ = _bincount_max(kg.trip[:, 0], n_ent) + _bincount_max(kg.trip[:, 1], n_ent)
     det = 3 * min(int(occ.max().item()), 2 * int(batch))
     lam = 2.0 * batch / max(n_ent, 1)
-    corr = min(2 * int(batch), int(math.ceil(lam + 12.0 * math.sqrt(lam) + 40)))
+    corr = min(2 * int(batch), int(math.ceil(_tail(lam))))
     return det + corr
 
 
+def _tail(mu):
+    """Poisson/binomial upper tail used for the random parts of the count
+    bounds: mu + 12 sqrt(mu) + 40 (never reached in practice; the applies
+    still check every count at run time)."""
+    return mu + 12.0 * math.sqrt(mu) + 40.0
+
+
 def relation_replicas(kg, n_rel, batch, max_reps=32, ranks=1):
-    """Accumulator copies the two-launch runner's packed relation sums need:
-    positive j adds into copy j mod reps, so a copy holds at most
-    ceil(batch / reps) positives (per rank: the sharded runner all-reduces
-    each copy over `ranks` batches), each adding <= 4 to its relation's count.
-    Returns 0 when even max_reps copies cannot keep the count <= PACKED_MAX."""
-    top = int(_bincount_max(kg.trip[:, 2], n_rel).max().item())
+    """Accumulator copies the packed relation sums need (the two-launch
+    runner; the pipelined runner switches to int32x2 sums when this is not 1).
+    Positive j adds into copy j mod reps, so a copy of a (union, over `ranks`)
+    batch holds per = ranks * ceil(batch / reps) positives; relation p's count
+    among them is at most min(per, count_p) and, the batch being a uniform
+    sample of the triples, below the binomial tail of mu = per * count_p / T.
+    Each positive adds <= 4 to its relation's count.  Returns 0 when even
+    max_reps copies cannot keep 4 * bound <= PACKED_MAX."""
+    cnt = _bincount_max(kg.trip[:, 2], n_rel).double()
+    T = float(max(int(kg.trip.shape[0]), 1))
     reps = 1
-    while 4 * min(top, int(ranks) * -(-int(batch) // reps)) > PACKED_MAX:
+    while True:
+        per = float(int(ranks) * -(-int(batch) // reps))
+        mu = cnt * (per / T)
+        tail = mu + 12.0 * torch.sqrt(mu) + 40.0
+        bound = torch.minimum(torch.minimum(cnt, torch.full_like(cnt, per)), tail)
+        if 4.0 * float(bound.max().item()) <= PACKED_MAX:
+            return reps
         reps *= 2
         if reps > max_reps:
             return 0
-    return reps
 
 
 class EpochRunner(object):

@@ -60,5 +60,17 @@ def test_relation_replicas_dominant_relation():
     kg = _kg(trip)
     assert relation_replicas(kg, 18, 1414) == 1          # 4 * 1414 fits
     r = relation_replicas(kg, 18, 70721)                   # ~35k positives of relation 0
-    assert r > 1 and 4 * -(-70721 // r) <= PACKED_MAX
+    mu = 70721 / r * 0.5                                   # relation 0's expected share of a copy
+    assert r == 8 and 4 * (mu + 12 * np.sqrt(mu) + 40) <= PACKED_MAX
     assert relation_replicas(kg, 18, 70721, max_reps=4) == 0
+
+
+def test_relation_replicas_config5_shape():
+    # |R| = 10k uniform, 10k triples each (T = 100M scaled by 1/100 here, the
+    # same per-relation share): ~13 positives of a relation per 131072-batch
+    rs = np.random.RandomState(3)
+    T = 1000000
+    trip = np.stack([rs.randint(500000, size=T), rs.randint(500000, size=T),
+                     rs.randint(10000, size=T)], axis=1)
+    assert relation_replicas(_kg(trip), 10000, 131072) == 1
+    assert relation_replicas(_kg(trip), 10000, 131072, ranks=8) == 1   # the sharded union batch

@@ -70,7 +70,7 @@ def test_dominant_relation_large_batch_exact(pipelined):
 
 @pytest.mark.parametrize("lazy", [False, True])
 def test_dominant_relation_pipelined_equals_two_launch_bitwise(lazy):
-    trip = _dominant_kg(3000, 7, 24000, 0.5, seed=4)
+    trip = _dominant_kg(3000, 7, 24000, 0.7, seed=4)
     a = _train(trip, 3000, 7, 200, 2, epochs=2, pipelined=True, lazy=lazy)
     b = _train(trip, 3000, 7, 200, 2, epochs=2, pipelined=False)
     assert a[3].packed and b[3].packed and b[3].accR.replicas >= 2 and a[3].lazy == lazy
@@ -223,7 +223,7 @@ def test_sharded_dominant_relation_uses_copies_and_matches_runner():
     copies, and G = 1 still equals the two-launch device runner bit for bit."""
     import skge_amd as S
     from skge_amd.shard import ShardedRunner
-    trip = _dominant_kg(3000, 7, 24000, 0.5, seed=4)
+    trip = _dominant_kg(3000, 7, 24000, 0.7, seed=4)
     E1, R1, v1, r1 = _train(trip, 3000, 7, 64, 2, epochs=2, seed=11, pipelined=False)
     assert r1.packed and r1.accR.replicas >= 2
     np.random.seed(11)
