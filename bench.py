@@ -167,6 +167,8 @@ def main():
                     help="config 5 only: scale |E| and T (quick rehearsals)")
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the measured gather roofline (skge_roofline_gather)")
+    ap.add_argument("--runner", default="auto", choices=["auto", "pairs", "hole_pipe"],
+                    help="configs 3/4: device runner (auto: HolE pipelined where it applies)")
     ap.add_argument("--shard", action="store_true",
                     help="config 5 only: row-shard E and its AdaGrad state over the ranks "
                          "(skge_amd.shard; RCCL all-to-all row fetch + contribution "
@@ -759,7 +761,7 @@ def run_config34(args):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     import skge_amd as S
-    from skge_amd.device import DeviceKG, PairLoopRunner, batch_sizes
+    from skge_amd.device import DeviceKG, batch_sizes, make_runner
     kind = "hole" if args.config == 3 else "rescal"
     d, nb, margin = args.d, args.nb, 0.2
     trip = make_wn18_kg(seed=rank)
@@ -768,7 +770,7 @@ def run_config34(args):
     model.add_hyperparam("margin", margin)
     upd = {pid: S.AdaGrad(p, 0.1) for pid, p in model.params.items()}
     kg = DeviceKG(trip, dev)
-    runner = PairLoopRunner(model, upd, kg, nb, seed=1234 + rank)
+    runner = make_runner(model, upd, kg, nb, seed=1234 + rank, runner=args.runner)
     init = {pid: p.data.clone() for pid, p in model.params.items()}
     runner.run(args.warmup)
     runner.synchronize()
@@ -817,6 +819,7 @@ def run_config34(args):
             "cpu_baseline": cpu,
             "detail": {"violations_per_pair": round(V / float(P), 4),
                        "graph_nodes_per_step": runner.nlaunches,
+                       "runner": type(runner).__name__,
                        "batches": len(batch_sizes(N_TRIPLES, nb))},
         }
         print(json.dumps(line))

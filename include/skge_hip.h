@@ -346,6 +346,22 @@ skge_pipe_runner_t *skge_pipe_runner_create_ex(void *stream, const skge_table_t 
                                                int nbatches, uint64_t seed, uint64_t *epoch_key,
                                                float margin, int ntries, int *nviol_total,
                                                int flags);
+/*
+ * Pipelined HolE pairwise runner (skge/hole.py:44-100, E post normless1):
+ * the same epoch structure as skge_pipe_runner_create -- launch g scores
+ * batch b (both pairs of a positive per wave: k_hole_pos's seven correlations
+ * and arithmetic) while other workgroups apply batch b-1's rows -- with fp32
+ * sums: ent F32 with slot records (capacity >= 4 * batch), rel F32 dense
+ * single copy, d % 4 == 0, 4 <= d <= 256, af an SKGE_AF_* code, no gates.
+ * Draws the same pairs as skge_pair_runner_create's HolE path; parameters
+ * equal its to fp32 rounding.  Driven by skge_pipe_runner_run / _profile /
+ * _error / _nlaunches / _destroy.  Replaces skge/base.py:1268-1284 for HolE.
+ */
+skge_pipe_runner_t *skge_hole_pipe_runner_create(void *stream, int af, const skge_table_t *ent,
+                                                 const skge_table_t *rel, int d, const int *trip,
+                                                 int64_t T, const void *set, int64_t set_capacity,
+                                                 int nbatches, uint64_t seed, uint64_t *epoch_key,
+                                                 float margin, int ntries, int *nviol_total);
 int skge_pipe_runner_run(skge_pipe_runner_t *r, void *stream, int nepochs);
 /* synchronizes the stream; returns 0, or a bit set (results then invalid):
  * 1 = a bounded cross-workgroup wait gave up, 2 = a row's per-batch count

@@ -31,8 +31,10 @@
 // Every row update depends only on that row's own (exact integer) sums, count,
 // parameters and AdaGrad state, computed by the same code (row_update), so the
 // result is bitwise identical to the two-launch loop (tested).
+#include <cstdlib>
 #include <vector>
 
+#include "skge_hole.h"
 #include "skge_host.h"
 #include "skge_sampler.h"
 
@@ -91,6 +93,8 @@ struct PipeArgs {
   const uint64_t* epoch_key;
   int d, nA;                   // nA: workgroups of the A role
   int n_ent;                   // entity rows (the lazy flush scans them all)
+  int af;                      // HolE: activation (skge/actfun.py)
+  int b_first;                 // HolE: scoring workgroups dispatched first
   float margin;
   int* nviol_total;            // the caller's counter: += the epoch's violations, at the flush
   int* nviol_shards;           // [NSHARD][SHARD_STRIDE]: this epoch's violations so far
@@ -919,6 +923,367 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_lazy_batch(PipeA
   }
 }
 
+// ======================== HolE pairwise, pipelined ========================
+//
+// The launch structure of k_pipe_batch for HolE (skge/hole.py:44-100, the
+// pairwise gradients, E post normless1): launch g scores batch b -- one wave
+// per positive, both of its pairs, k_hole_pos's seven correlations and exact
+// arithmetic -- while other workgroups apply batch b-1's rows (claim,
+// write-through publish, done word; a scoring wave reading a row batch b-1
+// touched applies it itself or waits).  Sums are fp32 (HolE contributions are
+// not small integers): entity sums [rows][d] double-buffered by batch parity,
+// relation sums [rows][rw words] (floats 0..d-1, count as an int at float d)
+// triple-buffered by launch id, one copy (every scoring wave recomputes
+// R_b[p] from R_{b-1}[p] and batch b-1's sums, as k_pipe_batch does).  Float
+// atomics add in any order, so the result equals the two-launch HolE loop to
+// fp32 rounding, not bit for bit.  Scoring workgroups are dispatched first
+// (their correlations are the launch's long pole): the apply waves then run
+// beside them.
+
+// One row's update from fp32 sums (zero past the row); row_update's arithmetic
+template <int KQ>
+__device__ __forceinline__ void row_update_f(const UpdParams& t, int c, int d,
+                                             const float4 (&sm)[KQ], float4 (&p)[KQ],
+                                             float4 (&a)[KQ]) {
+  const int l = lane_id(), nq = d >> 2;
+  const bool ada = t.opt == OPT_ADAGRAD;
+  const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
+  float ss = 0.0f;
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const bool in = 64 * m + l < nq;
+#define SKGE_UP(X)                                                      \
+  {                                                                     \
+    const float g = (sm[m].X + t.rin * p[m].X) / div + t.rout * p[m].X; \
+    float pv = p[m].X;                                                  \
+    if (ada) {                                                          \
+      a[m].X = a[m].X + g * g;                        /* param.py:147 */\
+      pv = pv - (t.lr * g) / fmaxf(sqrtf(a[m].X), 1e-7f); /* 152-155 */ \
+    } else {                                                            \
+      pv = pv - t.lr * g;                             /* param.py:130 */\
+    }                                                                   \
+    p[m].X = in ? pv : 0.0f;                                            \
+    ss += p[m].X * p[m].X;                                              \
+  }
+    SKGE_UP(x)
+    SKGE_UP(y)
+    SKGE_UP(z)
+    SKGE_UP(w)
+#undef SKGE_UP
+  }
+  if (t.post != POST_NONE) {
+    ss = wave_sum(ss);
+    const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss) : (ss < 1.0f ? 1.0f : ss);
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+      p[m].x = p[m].x / nrm;
+      p[m].y = p[m].y / nrm;
+      p[m].z = p[m].z / nrm;
+      p[m].w = p[m].w / nrm;
+    }
+  }
+}
+
+// P, A (P again when A is null: discarded) and fp32 sums of one quad-layout
+// row, unconditional 16-B loads; sums zero past the row
+template <int KQ>
+__device__ __forceinline__ void load_f32_row(const float* P, const float* A, const float* S,
+                                             int row, int d, float4 (&p)[KQ], float4 (&a)[KQ],
+                                             float4 (&sm)[KQ]) {
+  const int l = lane_id(), nq = d >> 2;
+  const float4* prow = reinterpret_cast<const float4*>(P + (size_t)row * d);
+  const float4* arow = reinterpret_cast<const float4*>((A ? A : P) + (size_t)row * d);
+  const float4* srow = reinterpret_cast<const float4*>(S + (size_t)row * d);
+  const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
+    const float4 sv = srow[qc];
+    p[m] = prow[qc];
+    a[m] = arow[qc];
+    sm[m] = q < nq ? sv : z;
+  }
+}
+
+template <int KQ>
+__device__ __forceinline__ void claim_and_apply_f(const PipeTab& t, int pp, int row, int d,
+                                                  int gp) {
+  const int l = lane_id(), nq = d >> 2;
+  int c = 0;
+  if (l == 0) c = atomicExch(t.cnt[pp] + row, 0);
+  float* S = reinterpret_cast<float*>(t.sum[pp]);
+  float4 sm[KQ], p[KQ], a[KQ];
+  load_f32_row<KQ>(t.P, t.A, S, row, d, p, a, sm);
+  c = __builtin_amdgcn_readfirstlane(c);
+  if (c == 0) return;   // another wave owns the row
+  row_update_f<KQ>(t.u, c, d, sm, p, a);
+  float4* srow = reinterpret_cast<float4*>(S + (size_t)row * d);
+#pragma unroll
+  for (int m = 0; m < KQ; ++m)
+    if (64 * m + l < nq) srow[64 * m + l] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  store_row4_sc1<KQ>(t.P, row, d, p);
+  if (t.A) store_row4_sc1<KQ>(t.A, row, d, a);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+  if (l == 0) __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
+}
+
+// The HolE launch's A role: its scoring waves hold ~180 VGPRs (2 waves per
+// SIMD), so the apply waves only get the residency the scoring waves leave
+// (~600 waves); each handles HGROUP slot-recorded rows at once -- the HGROUP
+// claims in one atomic instruction, every row's loads in flight together,
+// one drain, the done words in one store instruction.
+constexpr int HGROUP = 8;
+template <int KQ>
+__device__ __forceinline__ void claim_and_apply_group_f(const PipeTab& t, int pp, int s0, int ns,
+                                                        int d, int gp) {
+  const int l = lane_id(), nq = d >> 2;
+  int row = -1;
+  if (l < HGROUP && s0 + l < ns) row = t.touched[pp][s0 + l];
+  int c = 0;
+  if (row >= 0) c = atomicExch(t.cnt[pp] + row, 0);
+  float* S = reinterpret_cast<float*>(t.sum[pp]);
+  int rk[HGROUP];
+  float4 sm[HGROUP][KQ], p[HGROUP][KQ], a[HGROUP][KQ];
+#pragma unroll
+  for (int k = 0; k < HGROUP; ++k) {
+    rk[k] = __builtin_amdgcn_readlane(row, k);
+    load_f32_row<KQ>(t.P, t.A, S, rk[k] >= 0 ? rk[k] : 0, d, p[k], a[k], sm[k]);
+  }
+  const uint64_t won = __ballot(c != 0) & ((1ull << HGROUP) - 1);
+  if (!won) return;   // empty slots, or rows other waves own
+#pragma unroll
+  for (int k = 0; k < HGROUP; ++k) {
+    if (!((won >> k) & 1ull)) continue;
+    const int ck = __builtin_amdgcn_readlane(c, k);
+    row_update_f<KQ>(t.u, ck, d, sm[k], p[k], a[k]);
+    float4* srow = reinterpret_cast<float4*>(S + (size_t)rk[k] * d);
+#pragma unroll
+    for (int m = 0; m < KQ; ++m)
+      if (64 * m + l < nq) srow[64 * m + l] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    store_row4_sc1<KQ>(t.P, rk[k], d, p[k]);
+    if (t.A) store_row4_sc1<KQ>(t.A, rk[k], d, a[k]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+  if (c != 0) __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t.claims && l == 0) atomicAdd(shard_of(t.claims), (int)__builtin_popcountll(won));
+}
+
+template <int KQ>
+__device__ __forceinline__ void ensure_applied_f(const PipeTab& t, int pp, int row, int d, int gp,
+                                                 int* err) {
+  if (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gp) return;
+  claim_and_apply_f<KQ>(t, pp, row, d, gp);
+  unsigned spins = 0;
+  while (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gp) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > (1u << 22)) {   // ~0.5 s: never hang the GPU; report instead
+      if (lane_id() == 0) atomicOr(err, ERR_WAIT);
+      break;
+    }
+    if ((spins & 1023u) == 0 &&
+        __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      break;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the re-read below the poll
+}
+
+// relation row R_b[row] from R_{b-1} (buffer rd) and batch b-1's fp32 sums
+// (copy ra: floats [0, d), count at float d); zero past the row
+template <int KQ>
+__device__ __forceinline__ void rel_row_f(const RelTab& t, int row, int d, int rd, int ra,
+                                          float4 (&p)[KQ], float4 (&a)[KQ], int& c) {
+  const int l = lane_id(), nq = d >> 2;
+  const float* acc = reinterpret_cast<const float*>(t.acc[ra] + (size_t)row * t.rw);
+  float4 sm[KQ];
+  load_f32_row<KQ>(t.P[rd] + (size_t)row * d, t.A[rd] ? t.A[rd] + (size_t)row * d : nullptr,
+                   acc, 0, d, p, a, sm);
+  c = __builtin_amdgcn_readfirstlane(__float_as_int(acc[d]));
+  if (c) {
+    row_update_f<KQ>(t.u, c, d, sm, p, a);
+  } else {
+#pragma unroll
+    for (int m = 0; m < KQ; ++m)
+      if (64 * m + l >= nq) p[m] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+}
+
+template <int KQ>
+__device__ __forceinline__ void rel_publish_f(const PipeArgs& a, int w, int rd, int rw,
+                                              int ra_prev, int ra_old) {
+  const int l = lane_id(), d = a.d, nq = d >> 2;
+  float4 p[KQ], av[KQ];
+  int c;
+  rel_row_f<KQ>(a.R, w, d, rd, ra_prev, p, av, c);
+  float4* prow = reinterpret_cast<float4*>(a.R.P[rw] + (size_t)w * d);
+  float4* arow = a.R.A[rw] ? reinterpret_cast<float4*>(a.R.A[rw] + (size_t)w * d) : nullptr;
+  unsigned long long* old = a.R.acc[ra_old] + (size_t)w * a.R.rw;
+  unsigned long long* prev = a.R.acc[ra_prev] + (size_t)w * a.R.rw;
+  const bool flush = a.b == a.nb1;
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l;
+    if (q < nq) {
+      prow[q] = p[m];
+      if (arow) arow[q] = av[m];
+    }
+  }
+  for (int q = l; q < a.R.rw; q += 64) {   // rw 8-B words: the sums and the count
+    old[q] = 0ull;
+    if (flush) prev[q] = 0ull;
+  }
+  if (c && a.R.updated && l == 0) atomicAdd(shard_of(a.R.updated), 1);
+}
+
+template <int KM>
+__global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6;
+  const int l = lane_id();
+  const int d = a.d;
+  const int g = launch_id(a), gp = g - 1;
+  const int cp = a.b & 1, pp = cp ^ 1;
+  const int rd = a.b & 1;
+  const int rw = a.b < a.nb1 ? rd ^ 1 : 0;
+  const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
+  const int nB = gridDim.x - a.nA;
+  const int blk = (int)blockIdx.x;
+  const bool is_a = a.b_first ? blk >= nB : blk < a.nA;
+  if (is_a) {
+    // ---- A role: write R_b, then apply the previous batch's entity rows ----
+    const int blk_a = a.b_first ? blk - nB : blk;
+    const int nR = a.R.rows;
+    const int total = nR + (a.prev_slots + HGROUP - 1) / HGROUP;   // relation rows, slot groups
+    const int wa = blk_a * wpb + wave;
+    if (a.b == a.nb1 && wa == 0) fold_shards(a.nviol_shards, a.nviol_total);
+    for (int w = wa; w < total; w += a.nA * wpb) {
+      if (w < nR)
+        rel_publish_f<1>(a, w, rd, rw, ra_prev, ra_old);
+      else
+        claim_and_apply_group_f<1>(a.E, pp, HGROUP * (w - nR), a.prev_slots, d, gp);
+    }
+    return;
+  }
+  // ---- B role: score batch b (k_hole_pos's arithmetic), scatter into cp / ra_cur ----
+  const int blk_b = a.b_first ? blk : blk - a.nA;
+  float* sEs = smem + wave * hole_pos_lds_floats(d);   // a operands
+  float* sFs = sEs + d;
+  float* rEs = sEs + 2 * d;
+  float* rFs = sEs + 3 * d;
+  float* sR2 = sEs + 4 * d;                            // doubled b operands
+  float* sO2 = sR2 + 2 * d + 4;
+  float* sQ2 = sO2 + 2 * d + 4;
+  Accum aE;
+  aE.sum = reinterpret_cast<float*>(a.E.sum[cp]);
+  aE.width = d;
+  float* const racc = reinterpret_cast<float*>(a.R.acc[ra_cur]);
+  const int rstride = 2 * a.R.rw;   // floats per relation accumulator row
+  int nv = 0;
+  for (int w = blk_b * wpb + wave; w < a.count; w += nB * wpb) {
+    const long long j = a.start + w;
+    const int4 r4 = a.rec[j];
+    const int r1 = a.rec_n1[j];
+    __builtin_amdgcn_sched_barrier(0);
+    const int s = uni(r4.x), o = uni(r4.y), p = uni(r4.z), neg0 = uni(r4.w);
+    const int neg1 = uni(r1);
+    const int n0r = neg0 >= 0 ? neg0 : s, n1r = neg1 >= 0 ? neg1 : o;
+    float4 es[1], eo[1], rp[1], fs[1], fo[1];
+    load_row4<1>(a.E.P, s, d, es);
+    load_row4<1>(a.E.P, o, d, eo);
+    load_row4<1>(a.E.P, n0r, d, fs);
+    load_row4<1>(a.E.P, n1r, d, fo);
+    int mark = 0;
+    if (l < 4) mark = a.E.pend[pp][sel4(l, s, o, n0r, n1r)];
+    {
+      float4 ra[1];
+      int c;
+      rel_row_f<1>(a.R, p, d, rd, ra_prev, rp, ra, c);
+    }
+#ifndef SKGE_HPIPE_ABL_NO_PEND   // timing-only ablation: pending rows ignored
+    const uint64_t pend = __ballot(mark == gp) & 0xfull;
+#else
+    const uint64_t pend = 0ull * __ballot(mark == gp);
+#endif
+    if (pend) {
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) {
+        if (!((pend >> k) & 1ull)) continue;
+        ensure_applied_f<1>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err);
+      }
+      if (pend & 1ull) load_row4_sc1<1>(a.E.P, s, d, es);
+      if (pend & 2ull) load_row4_sc1<1>(a.E.P, o, d, eo);
+      if (pend & 4ull) load_row4_sc1<1>(a.E.P, n0r, d, fs);
+      if (pend & 8ull) load_row4_sc1<1>(a.E.P, n1r, d, fo);
+    }
+    q_lds(sEs, es[0], d);
+    q_lds(sFs, fs[0], d);
+    q_lds_rev(rEs, es[0], d);
+    q_lds_rev(rFs, fs[0], d);
+    q_lds_dbl(sR2, rp[0], d);
+    q_lds_dbl(sO2, eo[0], d);
+    q_lds_dbl(sQ2, fo[0], d);
+    __builtin_amdgcn_wave_barrier();
+    float4 c1[3], c2[2], c3[2];
+    {
+      const float* const a1[3] = {sEs, sFs, sR2};
+      corr_quad<3>(a1, sO2, d, c1);
+      const float* const a2[2] = {sEs, sR2};
+      corr_quad<2>(a2, sQ2, d, c2);
+      const float* const a3[2] = {rEs, rFs};
+      corr_quad<2>(a3, sR2, d, c3);
+    }
+    __builtin_amdgcn_wave_barrier();   // sEs is reused as the stage below
+    const float4 X = c1[0], Y = c1[1], A = c1[2], Z = c2[0], B = c2[1], C = c3[0], D = c3[1];
+    const float praw = score_q<KM>(X, sR2, d, sEs);
+    const float raw0 = score_q<KM>(Y, sR2, d, sEs), raw1 = score_q<KM>(Z, sR2, d, sEs);
+    const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
+    const int v0 = (neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0;   // hole.py:56
+    const int v1 = (neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0;
+    {
+      const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
+      const int rE = sel4(l, s, o, neg0, neg1);
+      if (l < 4) {
+        commit_slot(a.E.cnt[cp], a.E.touched[cp], rE, cE, 4 * w + l);
+        if (cE > 0) a.E.pend[cp][rE] = g;
+      } else if (l == 4 && v0 + v1 > 0) {
+        atomicAdd(reinterpret_cast<int*>(racc + (size_t)p * rstride + d), 2 * (v0 + v1));
+      }
+    }
+    if (v0 + v1 == 0) continue;
+    nv += v0 + v1;
+    const float gpf = -af_g_given_f(a.af, pf);   // hole.py:66
+    const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
+    const float fv0 = (float)v0, fv1 = (float)v1;
+    float4 cs, co, c0, cq, cr;
+#define SKGE_HC(M)                                                \
+  cs.M = fv0 * (gpf * A.M) + fv1 * (gpf * A.M + g1 * B.M);        \
+  co.M = fv0 * (gpf * C.M + g0 * D.M) + fv1 * (gpf * C.M);        \
+  c0.M = g0 * A.M;                                                \
+  cq.M = g1 * C.M;                                                \
+  cr.M = fv0 * (gpf * X.M + g0 * Y.M) + fv1 * (gpf * X.M + g1 * Z.M);
+    SKGE_HC(x)
+    SKGE_HC(y)
+    SKGE_HC(z)
+    SKGE_HC(w)
+#undef SKGE_HC
+    Accum aR;
+    aR.sum = racc + (size_t)p * rstride;
+    aR.width = d;
+#ifndef SKGE_HPIPE_ABL_NO_RATOM   // timing-only ablation: relation sums dropped
+    acc_q<KM>(aR, 0, cr, d, sEs);
+#endif
+    acc_q<KM>(aE, s, cs, d, sEs);
+    acc_q<KM>(aE, o, co, d, sEs);
+    if (v0) acc_q<KM>(aE, neg0, c0, d, sEs);
+    if (v1) acc_q<KM>(aE, neg1, cq, d, sEs);
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (l == 0 && nv) {
+    atomicAdd(shard_of(a.nviol_shards), nv);
+    if (a.stats_viol) atomicAdd(shard_of(a.stats_viol), nv);
+  }
+}
+
 __global__ void k_pipe_advance(uint64_t* ek) { *ek += 1; }
 
 // draw every negative of the epoch: one thread per positive, the same draws and
@@ -988,6 +1353,8 @@ struct skge_pipe_runner {
   std::vector<int> grid;
   bool w32 = false;                // int32x2 relation sums
   bool lazy = false;               // SKGE_PIPE_LAZY: entity rows applied by their next reader
+  bool hole = false;               // HolE pairwise (k_hole_pipe, fp32 sums)
+  size_t lds = 0;                  // HolE: dynamic LDS per workgroup
   int nlaunch() const { return (int)batch.size() + 2; }
 };
 
@@ -1044,7 +1411,15 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
       else hipLaunchKernelGGL((k_pipe_batch<K, false>), gr, bl, 0, st, a);                       \
     }                                                                                            \
   } while (0)
-    if (r->kq <= 1) SKGE_PB(1);
+    if (r->hole) {
+      const dim3 gr(r->grid[k]), bl(SKGE_PIPE_WG);
+      switch (km_for(a.d)) {
+        case 1: hipLaunchKernelGGL((k_hole_pipe<1>), gr, bl, r->lds, st, a); break;
+        case 2: hipLaunchKernelGGL((k_hole_pipe<2>), gr, bl, r->lds, st, a); break;
+        case 3: hipLaunchKernelGGL((k_hole_pipe<3>), gr, bl, r->lds, st, a); break;
+        default: hipLaunchKernelGGL((k_hole_pipe<4>), gr, bl, r->lds, st, a); break;
+      }
+    } else if (r->kq <= 1) SKGE_PB(1);
     else if (r->kq <= 2) SKGE_PB(2);
     else SKGE_PB(4);
 #undef SKGE_PB
@@ -1054,20 +1429,34 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
   if (ev) (void)hipEventRecord(ev[i + 1], st);
 }
 
-extern "C" skge_pipe_runner_t* skge_pipe_runner_create_ex(
-    void* stream, const skge_table_t* ent, const skge_table_t* rel, int d, const int* trip,
-    int64_t T, const void* set, int64_t set_capacity, int nbatches, uint64_t seed,
-    uint64_t* epoch_key, float margin, int ntries, int* nviol_total, int flags) {
+static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
+                                       const skge_table_t* rel, int d, const int* trip, int64_t T,
+                                       const void* set, int64_t set_capacity, int nbatches,
+                                       uint64_t seed, uint64_t* epoch_key, float margin,
+                                       int ntries, int* nviol_total, int flags, bool hole, int af) {
   const bool lazy = (flags & SKGE_PIPE_LAZY) != 0;
-  if (flags & ~SKGE_PIPE_LAZY) {
+  if ((flags & ~SKGE_PIPE_LAZY) || (hole && flags)) {
     set_error("pipelined runner: unknown flags %d", flags);
     return nullptr;
   }
-  // the pipelined loop is the packed TransE-L1 path
+  if (!ent || !rel) {
+    set_error("pipelined runner: NULL table");
+    return nullptr;
+  }
   skge_table_t relc = *rel;   // the relation encoding is the runner's own (checked below)
   if (relc.acc_mode == SKGE_ACC_I32X2) relc.acc_mode = SKGE_ACC_I16X4;
   if (check_table(ent, "ent", true) || check_table(&relc, "rel", true)) return nullptr;
-  if (ent->acc_mode != SKGE_ACC_I16X4 ||
+  if (hole) {   // HolE: fp32 sums, quad rows (d % 4 == 0, d <= 256)
+    if (ent->acc_mode != SKGE_ACC_F32 || rel->acc_mode != SKGE_ACC_F32 || d % 4 || d < 4 ||
+        d > 256 || ent->width != d || rel->width != d || ent->acc_touched == nullptr ||
+        rel->acc_touched != nullptr || rel->acc_replicas > 1 || ent->acc_replicas > 1 ||
+        ent->gate || rel->gate || af < 0 || af > 3) {
+      set_error("pipelined HolE runner: needs fp32 accumulators (entity table with slot "
+                "records, dense single-copy relation table), d %% 4 == 0, 4 <= d <= 256, no "
+                "gates");
+      return nullptr;
+    }
+  } else if (ent->acc_mode != SKGE_ACC_I16X4 ||
       (rel->acc_mode != SKGE_ACC_I16X4 && rel->acc_mode != SKGE_ACC_I32X2) || d % 4 || d > 1024 ||
       ent->width != d || rel->width != d || (ent->acc_touched == nullptr && !lazy) ||
       rel->acc_touched != nullptr || rel->acc_replicas > 1 || ent->acc_replicas > 1 ||
@@ -1093,6 +1482,7 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create_ex(
   const int nb1 = (int)batches.size();
   skge_pipe_runner* r = new skge_pipe_runner();
   r->lazy = lazy;
+  r->hole = hole;
   const int nq = d / 4;
   PipeArgs a = {};
   auto upd = [](const skge_table_t* s) {
@@ -1122,7 +1512,7 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create_ex(
       t.claim = (int*)dalloc(r, (size_t)N * 4);
       ok = ok && t.claim;
     } else {      // a second accumulator copy, slot records and batch marks
-      t.sum[1] = (unsigned long long*)dalloc(r, (size_t)N * nq * 8);
+      t.sum[1] = (unsigned long long*)dalloc(r, (size_t)N * nq * (hole ? 16 : 8));
       t.cnt[1] = (int*)dalloc(r, (size_t)N * 4);
       t.touched[1] = (int*)dalloc(r, (size_t)4 * bs * 4);
       t.pend[0] = (int*)dalloc(r, (size_t)N * 4);
@@ -1134,7 +1524,9 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create_ex(
     const bool ada = rel->opt == SKGE_ADAGRAD;
     q.rows = M;
     r->w32 = rel->acc_mode == SKGE_ACC_I32X2;
-    q.rw = ((r->w32 ? 2 * nq : nq) + 1 + 15) / 16 * 16;   // sums + count, whole 128-B lines
+    // 8-B words per relation row: sums + count, whole 128-B lines (HolE: d
+    // floats, then the count as an int)
+    q.rw = hole ? ((d + 2) / 2 + 15) / 16 * 16 : ((r->w32 ? 2 * nq : nq) + 1 + 15) / 16 * 16;
     q.u = upd(rel);
     q.updated = nullptr;
     q.P[0] = rel->param;
@@ -1183,6 +1575,12 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create_ex(
   a.err = r->err;
   a.E.err = r->err;
   a.n_ent = ent->rows;
+  a.af = af;
+  {
+    const char* af_env = getenv("SKGE_HPIPE_AFIRST");   // A/B switch: 0 = scoring WGs first
+    a.b_first = hole && af_env && atoi(af_env) == 0 ? 1 : 0;   // default: apply WGs first
+  }
+  r->lds = hole ? (size_t)(SKGE_PIPE_WG / 64) * hole_pos_lds_floats(d) * sizeof(float) : 0;
   int prev = 0;
   for (int b = 0; b <= nb1; ++b) {   // b == nb1: flush of the last batch (A role only)
     a.b = b;
@@ -1191,10 +1589,16 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create_ex(
     a.prev_slots = 4 * prev;
     // A role: every relation row, then the previous batch's entity slots (lazy:
     // no entity rows, except the flush's sweep over all rows in 64-row chunks)
-    const int a_items = rel->rows + (lazy ? (b == nb1 ? (ent->rows + 63) / 64 : 0)
-                                          : (4 * prev + ASLOTS - 1) / ASLOTS);
+    const int a_items =
+        rel->rows + (hole ? (4 * prev + HGROUP - 1) / HGROUP
+                          : lazy ? (b == nb1 ? (ent->rows + 63) / 64 : 0)
+                                 : (4 * prev + ASLOTS - 1) / ASLOTS);
     constexpr int WPB = SKGE_PIPE_WG / 64;
-    a.nA = std::max(1, std::min((a_items + WPB - 1) / WPB, 16384));
+    // HolE: the apply waves loop over their items within the residency the
+    // scoring waves leave (2 waves per SIMD at ~180 VGPRs; the flush has the
+    // chip to itself)
+    const int a_cap = hole && b < nb1 ? std::max(1, (2 * 4 * 256 - (int)((batches[b].second + WPB - 1) / WPB) * WPB) / WPB - 8) : 16384;
+    a.nA = std::max(1, std::min((a_items + WPB - 1) / WPB, std::min(a_cap, 16384)));
     const int nBb = std::max(1, std::min((a.count + WPB - 1) / WPB, 16384));
     r->batch.push_back(a);
     r->grid.push_back(a.nA + (a.count > 0 ? nBb : 0));
@@ -1223,6 +1627,22 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create_ex(
     return nullptr;
   }
   return r;
+}
+
+extern "C" skge_pipe_runner_t* skge_pipe_runner_create_ex(
+    void* stream, const skge_table_t* ent, const skge_table_t* rel, int d, const int* trip,
+    int64_t T, const void* set, int64_t set_capacity, int nbatches, uint64_t seed,
+    uint64_t* epoch_key, float margin, int ntries, int* nviol_total, int flags) {
+  return pipe_create(stream, ent, rel, d, trip, T, set, set_capacity, nbatches, seed, epoch_key,
+                     margin, ntries, nviol_total, flags, false, 0);
+}
+
+extern "C" skge_pipe_runner_t* skge_hole_pipe_runner_create(
+    void* stream, int af, const skge_table_t* ent, const skge_table_t* rel, int d,
+    const int* trip, int64_t T, const void* set, int64_t set_capacity, int nbatches,
+    uint64_t seed, uint64_t* epoch_key, float margin, int ntries, int* nviol_total) {
+  return pipe_create(stream, ent, rel, d, trip, T, set, set_capacity, nbatches, seed, epoch_key,
+                     margin, ntries, nviol_total, 0, true, af);
 }
 
 extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_table_t* ent,

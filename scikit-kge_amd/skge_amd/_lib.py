@@ -80,6 +80,8 @@ SIGNATURES = {
                                       c_f, c_i, c_p]),
     "skge_pipe_runner_create_ex": (c_p, [c_p, T_P, T_P, c_i, c_p, c_i64, c_p, c_i64, c_i, c_u64,
                                          c_p, c_f, c_i, c_p, c_i]),
+    "skge_hole_pipe_runner_create": (c_p, [c_p, c_i, T_P, T_P, c_i, c_p, c_i64, c_p, c_i64, c_i,
+                                           c_u64, c_p, c_f, c_i, c_p]),
     "skge_pipe_runner_run": (c_i, [c_p, c_p, c_i]),
     "skge_pipe_runner_error": (c_i, [c_p, c_p]),
     "skge_pipe_runner_profile": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_p, c_i64]),

@@ -38,11 +38,6 @@ _FILE_GRADIENTS = "gradients.txt"
 _FILE_EMBEDDINGS = "embeddings.txt"
 
 
-def _epoch_runner_type():
-    from .device import EpochRunner
-    return EpochRunner
-
-
 class Model(object):
     """Base class of all models (skge/base.py:1140-1192).
 
@@ -445,10 +440,10 @@ class PairwiseStochasticTrainer(StochasticTrainer):
         if self.file_gradients is not None:
             # E.violations / E.updateCounts: device counters of the per-batch
             # paths and the device pair loop; the TransE epoch runners keep none
-            if device and isinstance(self._runner, _epoch_runner_type()):
-                warnings.warn("device_loop (TransE epoch runner) keeps no per-row counters: "
-                              "the #(violations) and #(updates) columns of file_grad are zero; "
-                              "use device_runner='pairs' to count them")
+            if device and not getattr(self._runner, "counters", True):
+                warnings.warn("device_loop (%s) keeps no per-row counters: the #(violations) "
+                              "and #(updates) columns of file_grad are zero; use "
+                              "device_runner='pairs' to count them" % type(self._runner).__name__)
             viol = self.model.E.violations
             upd = self.model.E.updateCounts
             self.file_gradients.write("Entity,Degree,#(violations),#(updates)\n")

@@ -99,7 +99,8 @@ def relation_replicas(kg, n_rel, batch, max_reps=32, ranks=1):
 
 
 class EpochRunner(object):
-    """Native hipGraph epoch of the TransE device batch loop.
+    """Native hipGraph epoch of the TransE device batch loop (keeps no per-row
+    counters).
 
     pipelined: None (auto) uses the one-launch-per-batch pipelined runner
     (skge_pipe_runner_*) whenever it applies (TransE-L1, packed accumulators,
@@ -113,6 +114,8 @@ class EpochRunner(object):
     insists).  The pipelined runner keeps relation sums as int32x2; the
     two-launch runner spreads them over relation_replicas() copies.
     """
+
+    counters = False
 
     def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, stream=None,
                  nviol_total=None, force_f32=False, replicas=1, pipelined=None, packed=None,
@@ -275,6 +278,86 @@ class EpochRunner(object):
             self.handle = None
 
 
+class HolePipeRunner(object):
+    """Pipelined HolE device loop (skge_hole_pipe_runner_create,
+    csrc/skge_pipeline.hip k_hole_pipe): the TransE pipelined runner's launch
+    structure -- launch g scores batch b (both pairs of a positive per wave,
+    k_hole_pos's arithmetic) while batch b-1's rows are applied beside it --
+    with fp32 sums.  Same pairs as PairLoopRunner's HolE path (the same
+    device draws); parameters equal to fp32 rounding (float atomics add in
+    any order).  Needs d % 4 == 0, 4 <= d <= 256.  Keeps no per-row
+    counters."""
+
+    pipelined = True
+    counters = False   # keeps no per-row counters (updateCounts)
+
+    def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, stream=None,
+                 nviol_total=None):
+        from .hole import HolE
+        from .param import Accumulator
+        if not isinstance(model, HolE):
+            raise TypeError("HolePipeRunner trains HolE")
+        dev = model.device
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=dev)
+        self.kg = kg
+        self.model = model
+        self.nbatches = nbatches
+        self.lazy = False
+        self.epoch_key = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.nviol_total = nviol_total if nviol_total is not None else \
+            torch.zeros(1, dtype=torch.int32, device=dev)
+        E, R = model.params["E"], model.params["R"]
+        bs = kg.T // nbatches
+        self.accE = Accumulator(E.rows, E.width, dev, slots=4 * bs)
+        self.accR = Accumulator(R.rows, R.width, dev, dense=True)
+        reg = model._reg("pairwise")
+        self.te = updaters["E"].table(self.accE, counters=False, rin=reg["E"][0],
+                                      rout=reg["E"][1], fixed_div=reg["E"][2])
+        self.tr = updaters["R"].table(self.accR, counters=False, rin=reg["R"][0],
+                                      rout=reg["R"][1], fixed_div=reg["R"][2])
+        torch.cuda.current_stream().synchronize()
+        lib = L.lib()
+        h = lib.skge_hole_pipe_runner_create(
+            L.stream_ptr(self.stream), model._af_code(), self.te, self.tr, model.d,
+            L.ptr(kg.trip), kg.T, L.ptr(kg.slots), kg.capacity, int(nbatches),
+            int(seed) & (2 ** 64 - 1), L.ptr(self.epoch_key), float(model.margin), int(ntries),
+            L.ptr(self.nviol_total))
+        if not h:
+            raise L.SkgeError("skge_hole_pipe_runner_create: %s" % lib.skge_last_error().decode())
+        self.handle = h
+        self.nlaunches = lib.skge_pipe_runner_nlaunches(h)
+
+    @staticmethod
+    def eligible(model):
+        from .hole import HolE
+        d = model.d
+        return isinstance(model, HolE) and d % 4 == 0 and 4 <= d <= 256
+
+    def run(self, nepochs=1):
+        L.check(L.lib().skge_pipe_runner_run(self.handle, L.stream_ptr(self.stream),
+                                             int(nepochs)), "hole runner run")
+
+    profile = EpochRunner.profile
+
+    def synchronize(self):
+        self.stream.synchronize()
+        rc = L.lib().skge_pipe_runner_error(self.handle, L.stream_ptr(self.stream))
+        if rc < 0:
+            raise L.SkgeError("pipelined HolE runner: %s" % L.lib().skge_last_error().decode())
+        if rc & 1:
+            raise L.SkgeError("pipelined HolE runner: a cross-workgroup wait timed out")
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                self.stream.synchronize()
+                L.lib().skge_pipe_runner_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
 def batch_sizes(T, nbatches):
     """Batch sizes of StochasticTrainer._optim's np.split (skge/base.py:1246-1268)."""
     bs = T // nbatches
@@ -295,6 +378,7 @@ class PairLoopRunner(object):
     as on that path."""
 
     pipelined = False
+    counters = True    # updateCounts / TransE violations, as on the per-batch path
 
     def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, stream=None,
                  nviol_total=None):
@@ -360,10 +444,15 @@ def epoch_records(kg, n_ent, seed, epoch_key, ntries=100, stream=None):
 def make_runner(model, updaters, kg, nbatches, seed=0, ntries=100, nviol_total=None,
                 runner="auto"):
     """runner: 'auto' (TransE -> EpochRunner, the fused sampler/score runners;
-    HolE / RESCAL -> PairLoopRunner), 'epoch' or 'pairs'."""
+    HolE -> HolePipeRunner where it applies, RESCAL -> PairLoopRunner),
+    'epoch', 'hole_pipe' or 'pairs'."""
     from .transe import TransE
     if runner == "auto":
-        runner = "epoch" if isinstance(model, TransE) else "pairs"
+        runner = "epoch" if isinstance(model, TransE) else \
+            ("hole_pipe" if HolePipeRunner.eligible(model) else "pairs")
+    if runner == "hole_pipe":
+        return HolePipeRunner(model, updaters, kg, nbatches, seed=seed, ntries=ntries,
+                              nviol_total=nviol_total)
     if runner == "epoch":
         return EpochRunner(model, updaters, kg, nbatches, seed=seed, ntries=ntries,
                            nviol_total=nviol_total)

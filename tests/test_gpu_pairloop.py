@@ -174,8 +174,8 @@ def test_trainer_device_loop_any_model(kind):
     E0 = m.E.data.clone()
     seen = []
     tr = S.PairwiseStochasticTrainer(m, nbatches=10, max_epochs=3, learning_rate=0.1,
-                                     margin=0.2, device_loop=True, file_grad=None,
-                                     file_embed=None,
+                                     margin=0.2, device_loop=True, device_runner="pairs",
+                                     file_grad=None, file_embed=None,
                                      post_epoch=[lambda t: seen.append(t.nviolations) or True])
     tr.fit(xs, [1] * len(xs))
     assert len(seen) == 3 and all(v > 0 for v in seen)
@@ -266,3 +266,53 @@ def test_per_positive_paths_at_wn18_batch_geometry(kind, env, monkeypatch):
     for pid in out[0][1]:
         np.testing.assert_allclose(out[0][1][pid], out[1][1][pid], rtol=RTOL, atol=ATOL,
                                    err_msg="%s %s" % (kind, pid))
+
+
+def _hole_epochs(runner_cls, xs, n_ent, n_rel, d, nb, epochs, margin=0.2, seed=9, opt="sgd"):
+    import skge_amd as S
+    from skge_amd.device import DeviceKG
+    m = make_model("hole", (n_ent, n_ent, n_rel), d)
+    m.add_hyperparam("margin", margin)
+    U = S.SGD if opt == "sgd" else S.AdaGrad
+    upd = {pid: U(p, 0.1) for pid, p in m.params.items()}
+    r = runner_cls(m, upd, DeviceKG(xs, m.device), nb, seed=seed)
+    with torch.cuda.stream(r.stream):
+        r.run(epochs)
+    r.synchronize()
+    return (int(r.nviol_total.item()), int(r.epoch_key.item()),
+            {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()})
+
+
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb,epochs,opt", [
+    (300, 7, 2000, 32, 7, 2, "sgd"),        # ragged remainder batch
+    (40, 3, 1200, 200, 4, 2, "sgd"),        # tiny graph: most rows pending every batch
+    (500, 5, 3000, 64, 10, 3, "adagrad"),   # AdaGrad state through the hand-off
+    (40943, 18, 14140, 200, 10, 1, "sgd"),  # WN18 entity count, d, batch size
+])
+def test_hole_pipelined_runner_matches_pair_loop(n_ent, n_rel, T, d, nb, epochs, opt):
+    """The pipelined HolE runner (launch g scores batch b while batch b-1's
+    rows are applied beside it) against the two-launch device pair loop on
+    the same draws: the same pairs and scores up to fp32 summation order, so
+    violation totals agree (within a tie or two) and parameters within the
+    fp32 tolerance (rparam 0.05: the relation rows' rout term included)."""
+    from skge_amd.device import HolePipeRunner, PairLoopRunner
+    xs = make_kg(n_ent, n_rel, T, seed=3)
+    a = _hole_epochs(PairLoopRunner, xs, n_ent, n_rel, d, nb, epochs, opt=opt)
+    b = _hole_epochs(HolePipeRunner, xs, n_ent, n_rel, d, nb, epochs, opt=opt)
+    assert a[1] == b[1] == epochs
+    assert a[0] > 0 and abs(a[0] - b[0]) <= 2, (a[0], b[0])
+    for pid in a[2]:
+        np.testing.assert_allclose(b[2][pid], a[2][pid], rtol=RTOL, atol=ATOL,
+                                   err_msg="%s (%d, %d)" % (pid, a[0], b[0]))
+
+
+def test_hole_device_loop_auto_selects_pipelined_runner():
+    import skge_amd as S
+    from skge_amd.device import HolePipeRunner
+    xs = make_kg(200, 5, 1500)
+    m = make_model("hole", (200, 200, 5), 16)
+    tr = S.PairwiseStochasticTrainer(m, nbatches=10, max_epochs=2, margin=0.2, device_loop=True,
+                                     file_grad=None, file_embed=None)
+    tr.fit(xs, [1] * len(xs))
+    assert isinstance(tr._runner, HolePipeRunner)
+    assert np.isfinite(m.E.data.cpu().numpy()).all()

@@ -9,6 +9,6 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     SKGE_LIB_PATH=$lib timeout -k 10 300 python bench.py --no-cpu ${BENCH_ARGS:-} > gpurun_out/abn_$v.log 2>&1 || { tail -5 gpurun_out/abn_$v.log; exit 1; }
     python3 -c "
 import json; l=[x for x in open('gpurun_out/abn_$v.log') if x.startswith('{')][0]; j=json.loads(l)
-print('$v', round(j['value']/1e6,2), 'M', j['roofline']['avg_launch_us'], 'us', round(j['detail'].get('large_batch',{}).get('value',0)/1e6,1), 'M(nb2)')"
+print('$v', round(j['value']/1e6,2), 'M', j['roofline'].get('avg_launch_us'), 'us', round(j['detail'].get('large_batch',{}).get('value',0)/1e6,1), 'M(nb2)', j['ms_per_step'], 'ms/step')"
   done
 done
