@@ -1033,7 +1033,10 @@ __device__ __forceinline__ void claim_and_apply_f(const PipeTab& t, int pp, int 
 // (~600 waves); each handles HGROUP slot-recorded rows at once -- the HGROUP
 // claims in one atomic instruction, every row's loads in flight together,
 // one drain, the done words in one store instruction.
-constexpr int HGROUP = 8;
+#ifndef SKGE_HPIPE_GROUP
+#define SKGE_HPIPE_GROUP 1   // A/B on WN18 d=200: 1 row 51.7M, 2: 51.4M, 4: 49.6M, 8: 48.0M
+#endif
+constexpr int HGROUP = SKGE_HPIPE_GROUP;
 template <int KQ>
 __device__ __forceinline__ void claim_and_apply_group_f(const PipeTab& t, int pp, int s0, int ns,
                                                         int d, int gp) {
@@ -1597,7 +1600,10 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     // HolE: the apply waves loop over their items within the residency the
     // scoring waves leave (2 waves per SIMD at ~180 VGPRs; the flush has the
     // chip to itself)
-    const int a_cap = hole && b < nb1 ? std::max(1, (2 * 4 * 256 - (int)((batches[b].second + WPB - 1) / WPB) * WPB) / WPB - 8) : 16384;
+    int a_cap = hole && b < nb1 ? std::max(1, (2 * 4 * 256 - (int)((batches[b].second + WPB - 1) / WPB) * WPB) / WPB - 8) : 16384;
+    if (hole && b < nb1 && getenv("SKGE_HPIPE_ACAP")) a_cap = std::max(1, atoi(getenv("SKGE_HPIPE_ACAP")));
+    if (!hole && !lazy && b < nb1 && getenv("SKGE_PIPE_ACAP"))   // A/B switch (TransE)
+      a_cap = std::max(1, atoi(getenv("SKGE_PIPE_ACAP")));
     a.nA = std::max(1, std::min((a_items + WPB - 1) / WPB, std::min(a_cap, 16384)));
     const int nBb = std::max(1, std::min((a.count + WPB - 1) / WPB, 16384));
     r->batch.push_back(a);

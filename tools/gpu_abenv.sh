@@ -8,6 +8,6 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     env $e timeout -k 10 300 python bench.py --no-cpu ${BENCH_ARGS:-} > gpurun_out/abenv.log 2>&1 || { tail -5 gpurun_out/abenv.log; exit 1; }
     python3 -c "
 import json; l=[x for x in open('gpurun_out/abenv.log') if x.startswith('{')][0]; j=json.loads(l)
-print('$e', round(j['value']/1e6,2), 'M', j['roofline']['avg_launch_us'], 'us', j['roofline']['achieved'], 'GB/s', round(j['detail'].get('large_batch',{}).get('value',0)/1e6,1), 'M(nb2)')"
+print('$e', round(j['value']/1e6,2), 'M', j['roofline'].get('avg_launch_us'), 'us', j['roofline']['achieved'], j['roofline']['unit'], round(j['detail'].get('large_batch',{}).get('value',0)/1e6,1), 'M(nb2)', j['ms_per_step'], 'ms/step')"
   done
 done
