@@ -127,6 +127,15 @@ int launch_hole_pos(hipStream_t st, int af, const skge_table_t* ent, const skge_
 
 // skge_rescal.hip / skge_update.hip: the device pair loop's RESCAL batch
 bool rescal_pair_mfma_selected(int d, int M);
+// the device pair loop's RESCAL buckets for a whole epoch (skge_rescal.hip)
+bool rescal_epoch_ok(int M);
+size_t rescal_epoch_ws_bytes(int bs, int nb, int M, int d);
+int rescal_epoch_bucket(hipStream_t st, const int* pos, const int* neg, long long T, int bs, int nb,
+                        int M, int d, void* ws);
+int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent,
+                                 const skge_table_t* rel, int d, const int4* rec,
+                                 const int* rec_n1, long long T, int bs, int nb, int b,
+                                 float margin, void* ws, int* nviol);
 int skge_rescal_pos_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
                               const skge_table_t* rel, int d, const int* pos, const int* neg,
                               const int4* rec, const int* rec_n1, long long start, int count,

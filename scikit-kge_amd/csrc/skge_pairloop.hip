@@ -158,8 +158,14 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
   const bool rpos = model == SKGE_RESCAL && !(rp && atoi(rp)) &&
                     rescal_pair_mfma_selected(d, rel->rows);
   const int nb = (int)batches.size();
+  // RESCAL: every batch's relation buckets built once per epoch, up front (the
+  // items do not depend on the parameters); SKGE_RESCAL_EPOCH_BUCKETS=0 keeps
+  // the per-batch bucketing
+  const char* eb = getenv("SKGE_RESCAL_EPOCH_BUCKETS");
+  const bool rep = rpos && rescal_epoch_ok(rel->rows) && !(eb && atoi(eb) == 0);
   skge_pair_runner_t* r = new skge_pair_runner_t();
-  r->ws_bytes = skge_pair_step_workspace_bytes(model, Pmax, rel->rows, d);
+  r->ws_bytes = rep ? rescal_epoch_ws_bytes((int)bs, nb, rel->rows, d)
+                    : skge_pair_step_workspace_bytes(model, Pmax, rel->rows, d);
   if (hipMalloc(&r->rec, (size_t)T * sizeof(int4)) != hipSuccess ||
       hipMalloc(&r->rec_n1, (size_t)T * sizeof(int)) != hipSuccess ||
       (!hpos && hipMalloc(&r->pairs, (size_t)T * 12 * sizeof(int)) != hipSuccess) ||
@@ -187,6 +193,8 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
       set_error("pairs launch failed");
       rc = SKGE_EHIP;
     }
+    if (!rc && rep) rc = rescal_epoch_bucket(st, pos, neg, (long long)T, (int)bs, nb, rel->rows, d,
+                                             r->ws);
   }
   for (int k = 0; k < nb && !rc; ++k) {
     const long long start = batches[k].first;
@@ -203,9 +211,11 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
         rc = skge_accum_apply(stream, t, 2, ns);
       }
     } else if (rpos) {
-      rc = skge_rescal_pos_grad_mfma(st, af, ent, rel, d, pos + 3 * start, neg + 6 * start,
-                                     r->rec, r->rec_n1, start, count, margin, r->ws, r->ws_bytes,
-                                     gate);
+      rc = rep ? skge_rescal_pos_grad_mfma_ep(st, af, ent, rel, d, r->rec, r->rec_n1, (long long)T,
+                                              (int)bs, nb, k, margin, r->ws, gate)
+               : skge_rescal_pos_grad_mfma(st, af, ent, rel, d, pos + 3 * start, neg + 6 * start,
+                                           r->rec, r->rec_n1, start, count, margin, r->ws,
+                                           r->ws_bytes, gate);
       if (!rc) {   // the entity table's apply (W was updated by the dW kernel)
         skge_table_t te = *ent;
         te.gate = gate;

@@ -116,12 +116,10 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void k_rs_count(const int* __restrict__ pos,
-                                                  const int* __restrict__ neg, int P, int n,
-                                                  int M, RescalWs ws) {
-  const int nchunks = (n + 63) / 64, l = lane_id();
-  const int c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (c >= nchunks) return;
+__device__ __forceinline__ void rs_count_chunk(const int* __restrict__ pos,
+                                               const int* __restrict__ neg, int P, int n, int M,
+                                               const RescalWs& ws, int c) {
+  const int l = lane_id();
   const int k = c * 64 + l;
   const int b = k < n ? item_trip(pos, neg, P, k)[2] : -1;
   if (M <= 64) {   // lane p owns relation p: the whole row is written, no memset
@@ -143,9 +141,17 @@ __global__ __launch_bounds__(256) void k_rs_count(const int* __restrict__ pos,
   }
 }
 
-__global__ __launch_bounds__(1024) void k_rs_scan(int n, int M, RescalWs ws) {
-  extern __shared__ int lds[];   // cnt[M], tile_base[M+1]
-  int* cnt = lds;
+__global__ __launch_bounds__(256) void k_rs_count(const int* __restrict__ pos,
+                                                  const int* __restrict__ neg, int P, int n,
+                                                  int M, RescalWs ws) {
+  const int nchunks = (n + 63) / 64;
+  const int c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (c >= nchunks) return;
+  rs_count_chunk(pos, neg, P, n, M, ws, c);
+}
+
+__device__ __forceinline__ void rs_scan_body(int n, int M, const RescalWs& ws, int* lds) {
+  int* cnt = lds;   // cnt[M], tile_base[M+1]
   int* tbase = lds + M;
   const int nchunks = (n + 63) / 64;
   const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6, nw = blockDim.x >> 6;
@@ -197,12 +203,15 @@ __global__ __launch_bounds__(1024) void k_rs_scan(int n, int M, RescalWs ws) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_rs_scatter(const int* __restrict__ pos,
-                                                    const int* __restrict__ neg, int P, int n,
-                                                    int M, RescalWs ws) {
-  const int nchunks = (n + 63) / 64, l = lane_id();
-  const int c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (c >= nchunks) return;
+__global__ __launch_bounds__(1024) void k_rs_scan(int n, int M, RescalWs ws) {
+  extern __shared__ int lds[];
+  rs_scan_body(n, M, ws, lds);
+}
+
+__device__ __forceinline__ void rs_scatter_chunk(const int* __restrict__ pos,
+                                                 const int* __restrict__ neg, int P, int n, int M,
+                                                 const RescalWs& ws, int c) {
+  const int l = lane_id();
   const int k = c * 64 + l;
   const int* tr = item_trip(pos, neg, P, k < n ? k : 0);
   const int ts = tr[0], to = tr[1], b = k < n ? tr[2] : -1;
@@ -221,6 +230,79 @@ __global__ __launch_bounds__(256) void k_rs_scatter(const int* __restrict__ pos,
     }
     act &= ~m;
   }
+}
+
+__global__ __launch_bounds__(256) void k_rs_scatter(const int* __restrict__ pos,
+                                                    const int* __restrict__ neg, int P, int n,
+                                                    int M, RescalWs ws) {
+  const int nchunks = (n + 63) / 64;
+  const int c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (c >= nchunks) return;
+  rs_scatter_chunk(pos, neg, P, n, M, ws, c);
+}
+
+// ---- the whole epoch's buckets at once (device pair loop, M <= 64) ----
+// The epoch's items do not depend on the parameters (k_pairs_of_epoch), so
+// every batch's stable relation buckets are built by three launches per
+// EPOCH instead of three per batch.  Batch b (np.split geometry: bs positives,
+// the last batch the remainder) is items [0, 3 count_b) of its dedup lists;
+// its bucket arrays live in its own slice of the workspace (RescalEpoch).
+struct RescalEpoch {
+  RescalWs ws0;          // batch 0's view (the shared WE / EW / spart / coef included)
+  long long stride;      // bytes between consecutive batches' bucket slices
+  long long T;
+  int bs, nb, M, cpb;    // cpb: 64-item chunks of a full batch
+};
+
+__device__ __forceinline__ RescalWs rs_batch_view(const RescalEpoch& e, int b) {
+  RescalWs w = e.ws0;
+  const long long o = e.stride * b;
+  auto sh = [o](auto* p) { return reinterpret_cast<decltype(p)>(reinterpret_cast<char*>(p) + o); };
+  w.chunk = sh(w.chunk);
+  w.rel_off = sh(w.rel_off);
+  w.items = sh(w.items);
+  w.tile_rel = sh(w.tile_rel);
+  w.tile_start = sh(w.tile_start);
+  w.tile_cnt = sh(w.tile_cnt);
+  w.ntiles = sh(w.ntiles);
+  w.sorted_s = sh(w.sorted_s);
+  w.sorted_o = sh(w.sorted_o);
+  w.bpos = sh(w.bpos);
+  return w;
+}
+
+__device__ __forceinline__ int rs_batch_count(const RescalEpoch& e, int b) {
+  const long long s0 = (long long)b * e.bs;
+  return (int)(s0 + e.bs <= e.T ? e.bs : e.T - s0);
+}
+
+__global__ __launch_bounds__(256) void k_rs_count_ep(const int* __restrict__ pos,
+                                                     const int* __restrict__ neg, RescalEpoch e) {
+  const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int b = gw / e.cpb, c = gw - b * e.cpb;
+  if (b >= e.nb) return;
+  const int cnt = rs_batch_count(e, b), n = 3 * cnt;
+  if (c * 64 >= n) return;
+  const long long s0 = (long long)b * e.bs;
+  rs_count_chunk(pos + 3 * s0, neg + 6 * s0, cnt, n, e.M, rs_batch_view(e, b), c);
+}
+
+__global__ __launch_bounds__(1024) void k_rs_scan_ep(RescalEpoch e) {
+  extern __shared__ int lds[];
+  const int b = blockIdx.x;
+  rs_scan_body(3 * rs_batch_count(e, b), e.M, rs_batch_view(e, b), lds);
+}
+
+__global__ __launch_bounds__(256) void k_rs_scatter_ep(const int* __restrict__ pos,
+                                                       const int* __restrict__ neg,
+                                                       RescalEpoch e) {
+  const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int b = gw / e.cpb, c = gw - b * e.cpb;
+  if (b >= e.nb) return;
+  const int cnt = rs_batch_count(e, b), n = 3 * cnt;
+  if (c * 64 >= n) return;
+  const long long s0 = (long long)b * e.bs;
+  rs_scatter_chunk(pos + 3 * s0, neg + 6 * s0, cnt, n, e.M, rs_batch_view(e, b), c);
 }
 
 // Small batches (n <= SB_MAXN triples, M <= SB_MAXM relations): the same
@@ -876,9 +958,12 @@ bool skge_rescal_mfma_ok(int d, int M) {
 // bucket the n = na + nb triples (list a, then list b) by relation and run the
 // two GEMMs (WE^T, EW, partial scores)
 static int rescal_front(hipStream_t st, const skge_table_t* ent, const skge_table_t* rel, int d,
-                        const int* a, int na, const int* b, int n, const RescalWs& ws) {
+                        const int* a, int na, const int* b, int n, const RescalWs& ws,
+                        bool bucketed = false) {
   const int M = rel->rows;
-  if (M <= SB_MAXM && n <= SB_MAXN) {
+  if (bucketed) {
+    // the epoch's buckets were built up front (rescal_epoch_bucket)
+  } else if (M <= SB_MAXM && n <= SB_MAXN) {
     hipLaunchKernelGGL(k_rs_bucket_small, dim3(1), dim3(1024), 0, st, a, b, na, n, M, ws);
   } else {
     const int nchunks = (n + 63) / 64;
@@ -996,6 +1081,117 @@ int skge_rescal_pos_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
                  d, af, margin, ws, accum_of(ent), nviol)
   rescal_wgrad_launch(st, ent, rel, d, ws, true, nviol);
   SKGE_CHECK_LAUNCH("rescal positive grad");
+  return SKGE_OK;
+}
+
+// ---- epoch-level bucketing for the device pair loop ----
+// workspace: the shared part (spart, coef, WE, EW for one batch of n = 3 bs
+// items) once, then nb bucket slices of `stride` bytes (chunk counts,
+// offsets, items, tiles, sorted rows, positions), batch b at slice b
+static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, RescalWs* ws0,
+                                  long long* stride) {
+  const int n = 3 * bs, nchunks = (n + 63) / 64, tmax = rs_tmax(n, M);
+  size_t off = 0;
+  char* p = (char*)base;
+  auto take = [&](size_t bytes) {
+    char* q = p ? p + off : nullptr;
+    off += al256(bytes);
+    return q;
+  };
+  RescalWs w;
+  w.spart = (float*)take((size_t)n * ((d + GC - 1) / GC) * 4);
+  w.coef = (float*)take((size_t)n * 4);
+  w.WE = (float*)take((size_t)n * d * 4);
+  w.EW = (float*)take((size_t)n * d * 4);
+  const size_t s0 = off;
+  w.chunk = (int*)take((size_t)nchunks * M * 4);
+  w.rel_off = (int*)take((size_t)(M + 1) * 4);
+  w.items = (int*)take((size_t)n * 4);
+  w.tile_rel = (int*)take((size_t)tmax * 4);
+  w.tile_start = (int*)take((size_t)tmax * 4);
+  w.tile_cnt = (int*)take((size_t)tmax * 4);
+  w.ntiles = (int*)take(4);
+  w.sorted_s = (int*)take((size_t)n * 4);
+  w.sorted_o = (int*)take((size_t)n * 4);
+  w.bpos = (int*)take((size_t)n * 4);
+  const size_t slice = off - s0;
+  if (ws0) *ws0 = w;
+  if (stride) *stride = (long long)slice;
+  return s0 + (size_t)nb * slice;
+}
+
+bool rescal_epoch_ok(int M) { return M <= 64; }
+
+size_t rescal_epoch_ws_bytes(int bs, int nb, int M, int d) {
+  return rescal_epoch_layout(bs, nb, M, d, nullptr, nullptr, nullptr);
+}
+
+static RescalEpoch rescal_epoch_view(void* ws, long long T, int bs, int nb, int M, int d) {
+  RescalEpoch e;
+  rescal_epoch_layout(bs, nb, M, d, ws, &e.ws0, &e.stride);
+  e.T = T;
+  e.bs = bs;
+  e.nb = nb;
+  e.M = M;
+  e.cpb = (3 * bs + 63) / 64;
+  return e;
+}
+
+// every batch's buckets of the epoch, three launches (dedup lists: pos [T][3],
+// neg [T][2][3], k_pairs_of_epoch's RESCAL form)
+int rescal_epoch_bucket(hipStream_t st, const int* pos, const int* neg, long long T, int bs, int nb,
+                        int M, int d, void* ws) {
+  SKGE_CHECK_ARG(rescal_epoch_ok(M), "epoch bucketing needs M <= 64");
+  const RescalEpoch e = rescal_epoch_view(ws, T, bs, nb, M, d);
+  const long long waves = (long long)nb * e.cpb;
+  const unsigned blocks = (unsigned)((waves + 3) / 4);
+  hipLaunchKernelGGL(k_rs_count_ep, dim3(blocks), dim3(256), 0, st, pos, neg, e);
+  hipLaunchKernelGGL(k_rs_scan_ep, dim3((unsigned)nb), dim3(1024), (size_t)(2 * M + 1) * sizeof(int),
+                     st, e);
+  hipLaunchKernelGGL(k_rs_scatter_ep, dim3(blocks), dim3(256), 0, st, pos, neg, e);
+  SKGE_CHECK_LAUNCH("rescal epoch bucketing");
+  return SKGE_OK;
+}
+
+// the device pair loop's RESCAL batch b on pre-built buckets
+int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent,
+                                 const skge_table_t* rel, int d, const int4* rec,
+                                 const int* rec_n1, long long T, int bs, int nb, int b,
+                                 float margin, void* ws, int* nviol) {
+  int rc;
+  const long long start = (long long)b * bs;
+  const int count = (int)(start + bs <= T ? bs : T - start);
+  if ((rc = check_table(ent, "ent", true)) || (rc = check_table(rel, "rel", false)) ||
+      (rc = check_f32(ent, "ent")) || (rc = check_f32(rel, "rel")) ||
+      (rc = check_single(ent, "ent")) || (rc = check_single(rel, "rel")) ||
+      (rc = check_slots(ent, 4ll * count, "ent")) || (rc = check_slots(rel, rel->rows, "W")))
+    return rc;
+  SKGE_CHECK_ARG(ent->width == d && rel->width == d * d, "RESCAL table widths");
+  SKGE_CHECK_ARG(af >= 0 && af <= 3, "unknown activation %d", af);
+  SKGE_CHECK_ARG(rel->opt == SKGE_SGD || rel->state, "AdaGrad needs state");
+  SKGE_CHECK_ARG(nviol, "the fused W update is gated on nviol");
+  SKGE_CHECK_ARG(rescal_epoch_ok(rel->rows), "epoch bucketing needs M <= 64");
+  const RescalEpoch e = rescal_epoch_view(ws, T, bs, nb, rel->rows, d);
+  RescalWs w = e.ws0;   // host-side batch view (same arithmetic as rs_batch_view)
+  const long long o = e.stride * b;
+  auto sh = [o](auto* p) { return reinterpret_cast<decltype(p)>(reinterpret_cast<char*>(p) + o); };
+  w.chunk = sh(w.chunk);
+  w.rel_off = sh(w.rel_off);
+  w.items = sh(w.items);
+  w.tile_rel = sh(w.tile_rel);
+  w.tile_start = sh(w.tile_start);
+  w.tile_cnt = sh(w.tile_cnt);
+  w.ntiles = sh(w.ntiles);
+  w.sorted_s = sh(w.sorted_s);
+  w.sorted_o = sh(w.sorted_o);
+  w.bpos = sh(w.bpos);
+  rc = rescal_front(st, ent, rel, d, nullptr, count, nullptr, 3 * count, w, true);
+  if (rc) return rc;
+  const int blocks = std::max(1, std::min((count + 3) / 4, 16384));
+  SKGE_KM_SWITCH(k_rescal_pos_scatter, dim3(blocks), dim3(256), 0, st, rec, rec_n1, start, count,
+                 d, af, margin, w, accum_of(ent), nviol)
+  rescal_wgrad_launch(st, ent, rel, d, w, true, nviol);
+  SKGE_CHECK_LAUNCH("rescal positive grad (epoch buckets)");
   return SKGE_OK;
 }
 

@@ -316,3 +316,35 @@ def test_hole_device_loop_auto_selects_pipelined_runner():
     tr.fit(xs, [1] * len(xs))
     assert isinstance(tr._runner, HolePipeRunner)
     assert np.isfinite(m.E.data.cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb", [
+    (300, 7, 2000, 16, 7),          # ragged remainder batch
+    (40943, 18, 14140, 200, 10),    # WN18 entity / relation counts, d, batch size
+])
+def test_rescal_epoch_buckets_match_per_batch_buckets(n_ent, n_rel, T, d, nb, monkeypatch):
+    """The RESCAL pair loop with every batch's relation buckets built once per
+    epoch (three launches per epoch) against per-batch bucketing on the same
+    draws: the buckets are the same stable order, so violation totals are
+    equal and parameters agree to the entity sums' float-atomic rounding."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    xs = make_kg(n_ent, n_rel, T, seed=2)
+    out = []
+    for eb in ("0", "1"):
+        monkeypatch.setenv("SKGE_RESCAL_EPOCH_BUCKETS", eb)
+        m = make_model("rescal", (n_ent, n_ent, n_rel), d)
+        m.add_hyperparam("margin", 0.2)
+        # SGD keeps the comparison linear (AdaGrad turns rounding-level
+        # differences of a near-zero first gradient into +-lr steps)
+        upd = {pid: S.SGD(p, 0.1) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), nb, seed=4)
+        with torch.cuda.stream(r.stream):
+            r.run(2)
+        r.synchronize()
+        out.append((int(r.nviol_total.item()),
+                    {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}))
+    assert out[0][0] == out[1][0] > 0
+    for pid in out[0][1]:
+        np.testing.assert_allclose(out[1][1][pid], out[0][1][pid], rtol=RTOL, atol=ATOL,
+                                   err_msg=pid)
