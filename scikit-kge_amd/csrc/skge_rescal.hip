@@ -790,6 +790,10 @@ constexpr int WG_T = 64;    // rows / columns of a dW tile
 constexpr int WG_CH = 64;   // items staged per step
 constexpr int WG_TPI = 256 / WG_CH;       // threads per item
 constexpr int WG_FPT = WG_T / WG_TPI;     // row floats per thread and operand
+#ifndef SKGE_RS_WG_PF
+#define SKGE_RS_WG_PF 2   // A/B on WN18 d=200: 1 group of 4 chunks 20.5M, 2 chunks 24.2M, round 1 (1-deep pipeline) 23.3M
+#endif
+constexpr int WG_PF = SKGE_RS_WG_PF;      // chunks of items loaded together
 
 template <bool APPLY, bool VEC>
 __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restrict__ E, int d,
@@ -816,82 +820,14 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
   f32x4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  // thread -> item it of a chunk, WG_FPT columns from h of its
-  // E[s] segment (rows r0..) and E[o] segment (columns c0..).  Software
-  // pipeline: chunk b+1's rows are in flight during chunk b's MFMAs and chunk
-  // b+2's item ids behind them.
+  // thread -> item it of a chunk, WG_FPT columns from h of its E[s] segment
+  // (rows r0..) and E[o] segment (columns c0..).  The items are loaded WG_PF
+  // chunks at a time, every load of the group in flight together (one round
+  // trip for the ids, one for the rows, per group -- at the reference's batch
+  // size a relation's items fit one group), then staged chunk by chunk
+  // through the double-buffered LDS and contracted.
   const int it = tid / WG_TPI, h = (tid % WG_TPI) * WG_FPT;
-  int nxt_s = 0, nxt_o = 0;
-  float nxt_c = 0.0f;
-  auto load_idx = [&](int b0) {
-    const int i = b0 + it;
-    const int at = off + (i < cnt ? i : cnt - 1);
-    nxt_s = ws.sorted_s[at];
-    nxt_o = ws.sorted_o[at];
-    nxt_c = i < cnt ? ws.coef[at] : 0.0f;
-  };
-  float4 es[WG_FPT / 4], eo[WG_FPT / 4];
-  float cur_c = 0.0f;
-  auto load_rows = [&]() {   // raw loads from clamped in-range addresses
-    const float* srow = E + (size_t)nxt_s * d;
-    const float* orow = E + (size_t)nxt_o * d;
-#pragma unroll
-    for (int m = 0; m < WG_FPT / 4; ++m) {
-      const int cs = r0 + h + 4 * m, co = c0 + h + 4 * m;
-      if (VEC) {
-        es[m] = *reinterpret_cast<const float4*>(srow + (cs < d ? cs : 0));
-        eo[m] = *reinterpret_cast<const float4*>(orow + (co < d ? co : 0));
-      } else {
-        es[m] = make_float4(srow[cs < d ? cs : 0], srow[cs + 1 < d ? cs + 1 : 0],
-                            srow[cs + 2 < d ? cs + 2 : 0], srow[cs + 3 < d ? cs + 3 : 0]);
-        eo[m] = make_float4(orow[co < d ? co : 0], orow[co + 1 < d ? co + 1 : 0],
-                            orow[co + 2 < d ? co + 2 : 0], orow[co + 3 < d ? co + 3 : 0]);
-      }
-    }
-    cur_c = nxt_c;
-  };
-  const int nch = (cnt + WG_CH - 1) / WG_CH;
-  load_idx(0);
-  load_rows();
-  if (nch > 1) load_idx(WG_CH);
-  for (int b = 0; b < nch; ++b) {
-    const int buf = b & 1;
-#pragma unroll
-    for (int m = 0; m < WG_FPT / 4; ++m) {   // coef-scaled E[s], E[o]; zero past d
-      const int cs = r0 + h + 4 * m, co = c0 + h + 4 * m;
-      float4 a = es[m], o = eo[m];
-      a.x = cs + 0 < d ? cur_c * a.x : 0.0f;
-      a.y = cs + 1 < d ? cur_c * a.y : 0.0f;
-      a.z = cs + 2 < d ? cur_c * a.z : 0.0f;
-      a.w = cs + 3 < d ? cur_c * a.w : 0.0f;
-      o.x = co + 0 < d ? o.x : 0.0f;
-      o.y = co + 1 < d ? o.y : 0.0f;
-      o.z = co + 2 < d ? o.z : 0.0f;
-      o.w = co + 3 < d ? o.w : 0.0f;
-      *reinterpret_cast<float4*>(&sEs[buf][it][h + 4 * m]) = a;
-      *reinterpret_cast<float4*>(&sEo[buf][it][h + 4 * m]) = o;
-    }
-    __syncthreads();   // (also: every wave is done with buf's use two chunks ago)
-    if (b + 1 < nch) {
-      load_rows();                                        // chunk b+1
-      if (b + 2 < nch) load_idx((b + 2) * WG_CH);         // chunk b+2's ids
-    }
-    const int m = min(WG_CH, cnt - b * WG_CH);   // items past m are zero (coef 0)
-    // A[row i][k = item] = coef Es[item][i], B[k = item][col j] = Eo[item][j]
-#ifdef SKGE_ABL_WG_NOMFMA   // timing-only ablation (tools/ablate.sh): no contraction
-    if (m < 0)
-#endif
-    for (int k0 = 0; k0 < m; k0 += 4) {
-      const int ik = k0 + (l >> 4);
-      const float a = sEs[buf][ik][16 * wave + (l & 15)];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, sEo[buf][ik][16 * j + (l & 15)], acc[j],
-                                                      0, 0, 0);
-    }
-  }
-  // D[row 4g + reg][col] of accumulator j; out-of-range elements read a
-  // clamped in-range address and are not stored
+  // the W updater's operands do not depend on dW: in flight from the start
   size_t os[16];
   bool in[16];
 #pragma unroll
@@ -902,6 +838,85 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
       in[4 * j + reg] = r < d && cc < d;
       os[4 * j + reg] = (size_t)p * d * d + (size_t)(r < d ? r : 0) * d + (cc < d ? cc : 0);
     }
+  float pv[16], av[16];
+  if (APPLY) {
+    const bool ada = wa.opt == OPT_ADAGRAD;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      pv[e] = wa.W[os[e]];
+      av[e] = ada ? wa.A[os[e]] : 0.0f;
+    }
+  }
+  const int nch = (cnt + WG_CH - 1) / WG_CH;
+  for (int g0 = 0; g0 < nch; g0 += WG_PF) {
+    int ns[WG_PF], no[WG_PF];
+    float nc[WG_PF];
+#pragma unroll
+    for (int q = 0; q < WG_PF; ++q) {   // the group's item ids (clamped in-range addresses)
+      const int i = (g0 + q) * WG_CH + it;
+      const int at = off + (i < cnt ? i : cnt - 1);
+      ns[q] = ws.sorted_s[at];
+      no[q] = ws.sorted_o[at];
+      nc[q] = i < cnt ? ws.coef[at] : 0.0f;
+    }
+    float4 es[WG_PF][WG_FPT / 4], eo[WG_PF][WG_FPT / 4];
+#pragma unroll
+    for (int q = 0; q < WG_PF; ++q) {   // the group's row segments
+      const float* srow = E + (size_t)ns[q] * d;
+      const float* orow = E + (size_t)no[q] * d;
+#pragma unroll
+      for (int m = 0; m < WG_FPT / 4; ++m) {
+        const int cs = r0 + h + 4 * m, co = c0 + h + 4 * m;
+        if (VEC) {
+          es[q][m] = *reinterpret_cast<const float4*>(srow + (cs < d ? cs : 0));
+          eo[q][m] = *reinterpret_cast<const float4*>(orow + (co < d ? co : 0));
+        } else {
+          es[q][m] = make_float4(srow[cs < d ? cs : 0], srow[cs + 1 < d ? cs + 1 : 0],
+                                 srow[cs + 2 < d ? cs + 2 : 0], srow[cs + 3 < d ? cs + 3 : 0]);
+          eo[q][m] = make_float4(orow[co < d ? co : 0], orow[co + 1 < d ? co + 1 : 0],
+                                 orow[co + 2 < d ? co + 2 : 0], orow[co + 3 < d ? co + 3 : 0]);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < WG_PF; ++q) {
+      const int b = g0 + q;
+      if (b >= nch) break;
+      const int buf = b & 1;
+#pragma unroll
+      for (int m = 0; m < WG_FPT / 4; ++m) {   // coef-scaled E[s], E[o]; zero past d
+        const int cs = r0 + h + 4 * m, co = c0 + h + 4 * m;
+        float4 a = es[q][m], o = eo[q][m];
+        const float cur_c = nc[q];
+        a.x = cs + 0 < d ? cur_c * a.x : 0.0f;
+        a.y = cs + 1 < d ? cur_c * a.y : 0.0f;
+        a.z = cs + 2 < d ? cur_c * a.z : 0.0f;
+        a.w = cs + 3 < d ? cur_c * a.w : 0.0f;
+        o.x = co + 0 < d ? o.x : 0.0f;
+        o.y = co + 1 < d ? o.y : 0.0f;
+        o.z = co + 2 < d ? o.z : 0.0f;
+        o.w = co + 3 < d ? o.w : 0.0f;
+        *reinterpret_cast<float4*>(&sEs[buf][it][h + 4 * m]) = a;
+        *reinterpret_cast<float4*>(&sEo[buf][it][h + 4 * m]) = o;
+      }
+      __syncthreads();   // (also: every wave is done with buf's use two chunks ago)
+      const int mm = min(WG_CH, cnt - b * WG_CH);   // items past mm are zero (coef 0)
+      // A[row i][k = item] = coef Es[item][i], B[k = item][col j] = Eo[item][j]
+#ifdef SKGE_ABL_WG_NOMFMA   // timing-only ablation (tools/ablate.sh): no contraction
+      if (mm < 0)
+#endif
+      for (int k0 = 0; k0 < mm; k0 += 4) {
+        const int ik = k0 + (l >> 4);
+        const float av_ = sEs[buf][ik][16 * wave + (l & 15)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av_, sEo[buf][ik][16 * j + (l & 15)],
+                                                        acc[j], 0, 0, 0);
+      }
+    }
+  }
+  // D[row 4g + reg][col] of accumulator j (os / in above: out-of-range
+  // elements read a clamped in-range address and are not stored)
   if (!APPLY) {
 #pragma unroll
     for (int e = 0; e < 16; ++e)
@@ -920,12 +935,6 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
   // tile issued before any of it is used
   const float div = wa.fdiv > 0.0f ? wa.fdiv : (float)cnt;
   const bool ada = wa.opt == OPT_ADAGRAD;
-  float pv[16], av[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    pv[e] = wa.W[os[e]];
-    av[e] = ada ? wa.A[os[e]] : 0.0f;
-  }
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const float g = (acc[e >> 2][e & 3] + wa.rin * pv[e]) / div + wa.rout * pv[e];
