@@ -458,6 +458,21 @@ int skge_roofline_gather(void *stream, float *P, float *A, void *S, int rows, in
  * skge_rank_workspace_bytes(nq, d) bytes.
  */
 size_t skge_rank_workspace_bytes(int nq, int d);
+/*
+ * skge_rank with the filter given as each query's KNOWN ANSWERS instead of a
+ * triple set: tail_ent[tail_off[i] .. tail_off[i+1]) = every o' != o with
+ * (s, o', p) known, head_ent[head_off[i] .. head_off[i+1]) = every s' != s
+ * with (s', o, p) known (int32, offsets nq + 1).  rank_filtered = rank_raw -
+ * #{those answers scoring strictly above the true entity}: the same positions
+ * as skge_rank, with no triple-set lookups in the all-entity pass (which also
+ * spreads each query block over entity slices).  Workspace:
+ * skge_rank_known_workspace_bytes(nq, d).
+ */
+size_t skge_rank_known_workspace_bytes(int nq, int d);
+int skge_rank_known(void *stream, int model, const float *E, const float *R, int N, int d,
+                    const int *queries, int nq, const int *tail_off, const int *tail_ent,
+                    const int *head_off, const int *head_ent, void *workspace, size_t ws_bytes,
+                    int *ranks_out);
 int skge_rank(void *stream, int model, const float *E, const float *R, int N, int d,
               const int *queries, int nq, const void *set, int64_t set_capacity,
               void *workspace, size_t ws_bytes, int *ranks_out);

@@ -21,6 +21,8 @@
 // rank = 1 + #{entities scoring strictly higher}: ties go the true entity's
 // way (the reference's order among exact ties is that of numpy's unstable
 // argsort, reversed).
+#include <algorithm>
+
 #include "skge_host.h"
 
 namespace skge {
@@ -213,9 +215,243 @@ __global__ __launch_bounds__(256) void k_rank_count(RankArgs a) {
   }
 }
 
+// ---- round 2: raw counts over entity slices + filtered counts from the
+// queries' known answers ----
+// rank_filtered = rank_raw - #{known answers of the query, other than the
+// true entity, scoring strictly above it}: the counting pass needs no
+// triple-set lookups (at random parameters half the entities score above the
+// true one, so the lookups were most of the pass), and the known answers --
+// a handful per query -- are scored by their own small kernel with the
+// counting pass's arithmetic (sequential k).
+constexpr int QB2 = 64;    // query vectors per workgroup
+constexpr int EB2 = 128;   // entities per LDS tile
+constexpr int KC2 = 32;    // dims per LDS chunk
+constexpr int PADQ = QB2 + 4, PADE = EB2 + 4;   // rows stay 16-B aligned
+
+struct RankArgs2 {
+  const float* E;
+  int N, d, nv;        // nv = 2 nq query vectors
+  int eslice;          // entities per workgroup slice (multiple of EB2)
+  const float* Q;      // [nv][d]
+  const float* tgt;    // [nv]
+  int* raw;            // [nv] entities scoring strictly higher (atomics over the slices)
+};
+
+// one workgroup: QB2 query vectors x one entity slice; thread: 8 entities x 4
+// queries, every accumulator a sequential-k chain (the true score's arithmetic)
+template <bool L1>
+__global__ __launch_bounds__(256) void k_rank_count2(RankArgs2 a) {
+  __shared__ __attribute__((aligned(16))) float sQ[KC2][PADQ];
+  __shared__ __attribute__((aligned(16))) float sE[KC2][PADE];
+  __shared__ int s_raw[QB2];
+  __shared__ float s_tgt[QB2];
+  const int tid = threadIdx.x, d = a.d;
+  const int v0 = blockIdx.x * QB2;
+  const int ebeg = blockIdx.y * a.eslice, eend = min(a.N, ebeg + a.eslice);
+  if (tid < QB2) {
+    const int v = v0 + tid;
+    s_tgt[tid] = v < a.nv ? a.tgt[v] : INFINITY;
+    s_raw[tid] = 0;
+  }
+  const int te = (tid & 15) * 8, tq = (tid >> 4) * 4;
+  int raw[4] = {0, 0, 0, 0};
+  // staging maps: Q chunk = 64 vectors x 8 float4 (2 per thread), E chunk =
+  // 128 entities x 8 float4 (4 per thread); k fastest in global memory
+  const int sq_v = tid >> 2, sq_k = (tid & 3) * 4;          // + 16 for the second float4
+  const int se_e = tid >> 1, se_k = (tid & 1) * 4;          // + 8, 16, 24
+  for (int e0 = ebeg; e0 < eend; e0 += EB2) {
+    float acc[8][4];
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) acc[x][y] = 0.0f;
+    for (int k0 = 0; k0 < d; k0 += KC2) {
+      float4 qa[2], ea[4];
+      {
+        const int v = v0 + sq_v;
+        const float* qrow = a.Q + (size_t)(v < a.nv ? v : 0) * d;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int k = k0 + sq_k + 16 * u;
+          float4 x = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          if (v < a.nv) {
+            if ((d & 3) == 0 && k + 3 < d) {
+              x = *reinterpret_cast<const float4*>(qrow + k);
+            } else {
+              x.x = k < d ? qrow[k] : 0.0f;
+              x.y = k + 1 < d ? qrow[k + 1] : 0.0f;
+              x.z = k + 2 < d ? qrow[k + 2] : 0.0f;
+              x.w = k + 3 < d ? qrow[k + 3] : 0.0f;
+            }
+          }
+          qa[u] = x;
+        }
+        const int e = e0 + se_e;
+        const float* erow = a.E + (size_t)(e < eend ? e : ebeg) * d;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = k0 + se_k + 8 * u;
+          float4 x = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          if (e < eend) {
+            if ((d & 3) == 0 && k + 3 < d) {
+              x = *reinterpret_cast<const float4*>(erow + k);
+            } else {
+              x.x = k < d ? erow[k] : 0.0f;
+              x.y = k + 1 < d ? erow[k + 1] : 0.0f;
+              x.z = k + 2 < d ? erow[k + 2] : 0.0f;
+              x.w = k + 3 < d ? erow[k + 3] : 0.0f;
+            }
+          }
+          ea[u] = x;
+        }
+      }
+      __syncthreads();   // the previous chunk's reads are done
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k = sq_k + 16 * u;
+        sQ[k][sq_v] = qa[u].x;
+        sQ[k + 1][sq_v] = qa[u].y;
+        sQ[k + 2][sq_v] = qa[u].z;
+        sQ[k + 3][sq_v] = qa[u].w;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = se_k + 8 * u;
+        sE[k][se_e] = ea[u].x;
+        sE[k + 1][se_e] = ea[u].y;
+        sE[k + 2][se_e] = ea[u].z;
+        sE[k + 3][se_e] = ea[u].w;
+      }
+      __syncthreads();
+      const int kn = min(KC2, d - k0);
+      for (int k = 0; k < kn; ++k) {
+        const float4 e4a = *reinterpret_cast<const float4*>(&sE[k][te]);
+        const float4 e4b = *reinterpret_cast<const float4*>(&sE[k][te + 4]);
+        const float4 q4 = *reinterpret_cast<const float4*>(&sQ[k][tq]);
+        const float ev[8] = {e4a.x, e4a.y, e4a.z, e4a.w, e4b.x, e4b.y, e4b.z, e4b.w};
+        const float qv[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+        for (int x = 0; x < 8; ++x)
+#pragma unroll
+          for (int y = 0; y < 4; ++y)
+            acc[x][y] = L1 ? acc[x][y] - fabsf(qv[y] - ev[x]) : fmaf(ev[x], qv[y], acc[x][y]);
+      }
+    }
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const float t = s_tgt[tq + y];
+#pragma unroll
+      for (int x = 0; x < 8; ++x)
+        if (e0 + te + x < eend && acc[x][y] > t) ++raw[y];
+    }
+  }
+#pragma unroll
+  for (int y = 0; y < 4; ++y)
+    if (raw[y]) atomicAdd(&s_raw[tq + y], raw[y]);
+  __syncthreads();
+  if (tid < QB2) {
+    const int v = v0 + tid;
+    if (v < a.nv && s_raw[tid]) atomicAdd(a.raw + v, s_raw[tid]);
+  }
+}
+
+// filtered correction + the ranks: one thread per query vector, its known
+// answers (CSR, the true entity excluded by the caller) scored with the
+// counting pass's arithmetic (sequential k)
+template <bool L1>
+__global__ __launch_bounds__(256) void k_rank_known(const float* __restrict__ E, int d, int nq,
+                                                    const float* __restrict__ Q,
+                                                    const float* __restrict__ tgt,
+                                                    const int* __restrict__ raw,
+                                                    const int* __restrict__ tail_off,
+                                                    const int* __restrict__ tail_ent,
+                                                    const int* __restrict__ head_off,
+                                                    const int* __restrict__ head_ent,
+                                                    int* __restrict__ ranks) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= 2 * nq) return;
+  const int qi = v >> 1, dir = v & 1;   // 0: tail (vary o), 1: head (vary s)
+  const int* off = dir ? head_off : tail_off;
+  const int* ent = dir ? head_ent : tail_ent;
+  const float* q = Q + (size_t)v * d;
+  const float t = tgt[v];
+  int dec = 0;
+  for (int i = off[qi]; i < off[qi + 1]; ++i) {
+    const float* e = E + (size_t)ent[i] * d;
+    float acc = 0.0f;
+    for (int k = 0; k < d; ++k) acc = L1 ? acc - fabsf(q[k] - e[k]) : fmaf(e[k], q[k], acc);
+    if (acc > t) ++dec;
+  }
+  ranks[4 * qi + 2 * dir] = 1 + raw[v];
+  ranks[4 * qi + 2 * dir + 1] = 1 + raw[v] - dec;
+}
+
 }  // namespace skge
 
 using namespace skge;
+
+extern "C" size_t skge_rank_known_workspace_bytes(int nq, int d) {
+  return (size_t)2 * nq * d * sizeof(float) + (size_t)2 * nq * (sizeof(float) + sizeof(int)) + 512;
+}
+
+extern "C" int skge_rank_known(void* stream, int model, const float* E, const float* R, int N,
+                               int d, const int* queries, int nq, const int* tail_off,
+                               const int* tail_ent, const int* head_off, const int* head_ent,
+                               void* workspace, size_t ws_bytes, int* ranks_out) {
+  SKGE_CHECK_ARG(E && R && queries && ranks_out && tail_off && head_off, "NULL argument");
+  SKGE_CHECK_ARG(model >= 0 && model <= 3, "unknown model %d", model);
+  SKGE_CHECK_ARG(N > 0 && d > 0 && d <= 1024 && nq >= 0, "bad sizes (d <= 1024)");
+  if (nq == 0) return SKGE_OK;
+  SKGE_CHECK_ARG(workspace && ws_bytes >= skge_rank_known_workspace_bytes(nq, d),
+                 "rank workspace needs %zu bytes", skge_rank_known_workspace_bytes(nq, d));
+  RankArgs a = {};
+  a.E = E;
+  a.R = R;
+  a.N = N;
+  a.d = d;
+  a.model = model;
+  a.nq = nq;
+  a.queries = queries;
+  a.has_set = 0;
+  a.Q = (float*)workspace;
+  a.tgt = a.Q + (size_t)2 * nq * d;
+  int* raw = (int*)(a.tgt + 2 * (size_t)nq);
+  a.ranks = ranks_out;
+  hipStream_t st = as_stream(stream);
+  SKGE_CHECK_HIP(hipMemsetAsync(raw, 0, (size_t)2 * nq * sizeof(int), st));
+  const int qblocks = std::max(1, std::min((nq + 1) / 2, 16384));
+  hipLaunchKernelGGL(k_rank_query, dim3(qblocks), dim3(128), (size_t)2 * 5 * d * sizeof(float), st,
+                     a);
+  RankArgs2 b;
+  b.E = E;
+  b.N = N;
+  b.d = d;
+  b.nv = 2 * nq;
+  b.Q = a.Q;
+  b.tgt = a.tgt;
+  b.raw = raw;
+  // enough workgroups to fill the chip: query blocks x entity slices
+  const int qb = (2 * nq + QB2 - 1) / QB2;
+  const int tiles = (N + EB2 - 1) / EB2;
+  const int want = std::max(1, std::min(tiles, (2048 + qb - 1) / qb));
+  const int per = (tiles + want - 1) / want;
+  b.eslice = per * EB2;
+  const int ns = (tiles + per - 1) / per;
+  const bool l1 = model == SKGE_TRANSE_L1 || model == SKGE_TRANSE_L2;
+  if (l1)
+    hipLaunchKernelGGL((k_rank_count2<true>), dim3(qb, ns), dim3(256), 0, st, b);
+  else
+    hipLaunchKernelGGL((k_rank_count2<false>), dim3(qb, ns), dim3(256), 0, st, b);
+  const int kb = (2 * nq + 255) / 256;
+  if (l1)
+    hipLaunchKernelGGL((k_rank_known<true>), dim3(kb), dim3(256), 0, st, E, d, nq, a.Q, a.tgt, raw,
+                       tail_off, tail_ent, head_off, head_ent, ranks_out);
+  else
+    hipLaunchKernelGGL((k_rank_known<false>), dim3(kb), dim3(256), 0, st, E, d, nq, a.Q, a.tgt,
+                       raw, tail_off, tail_ent, head_off, head_ent, ranks_out);
+  SKGE_CHECK_LAUNCH("rank (known answers)");
+  return SKGE_OK;
+}
 
 extern "C" size_t skge_rank_workspace_bytes(int nq, int d) {
   return (size_t)2 * nq * d * sizeof(float) + (size_t)2 * nq * sizeof(float) + 256;

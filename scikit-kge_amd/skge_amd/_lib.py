@@ -56,6 +56,9 @@ SIGNATURES = {
     "skge_device_error": (c_i, [c_p, c_i]),
     "skge_rank_workspace_bytes": (c_sz, [c_i, c_i]),
     "skge_rank": (c_i, [c_p, c_i, c_p, c_p, c_i, c_i, c_p, c_i, c_p, c_i64, c_p, c_sz, c_p]),
+    "skge_rank_known_workspace_bytes": (c_sz, [c_i, c_i]),
+    "skge_rank_known": (c_i, [c_p, c_i, c_p, c_p, c_i, c_i, c_p, c_i, c_p, c_p, c_p, c_p, c_p,
+                              c_sz, c_p]),
     "skge_pair_step_workspace_bytes": (c_sz, [c_i, c_i, c_i, c_i]),
     "skge_triple_step_workspace_bytes": (c_sz, [c_i, c_i, c_i, c_i]),
     "skge_triple_step": (c_i, [c_p, c_i, T_P, T_P, c_i, c_p, c_p, c_i, c_p, c_sz, c_p]),

@@ -10,6 +10,7 @@ than the true one: the reference's descending-argsort position whenever no
 other entity ties the true score exactly (among exact ties the reference
 follows numpy's unstable argsort order).
 """
+import os
 from collections import defaultdict
 
 import numpy as np
@@ -47,12 +48,33 @@ class FilteredRankingEval(object):
         self.idx = dict(idx)
         self._true = triples_array(true_triples)
         self._kg = None
+        self._answers = None
         self.last_ranks = None
 
     def _known_set(self, device):
         if self._kg is None:
             self._kg = DeviceKG(self._true, device)
         return self._kg
+
+    def _known_answers(self, q, device):
+        """Per query (s, o, p) its other known tails {o' != o: (s, o', p) known}
+        and heads {s' != s: (s', o, p) known}, as int32 CSR on the device (the
+        filter of skge/base.py:913-1031 as lists: a handful per query)."""
+        if self._answers is None:
+            tails, heads = defaultdict(set), defaultdict(set)
+            for s, o, p in self._true.tolist():
+                tails[(s, p)].add(o)
+                heads[(o, p)].add(s)
+            toff, tent, hoff, hent = [0], [], [0], []
+            for s, o, p in q:
+                tent.extend(sorted(x for x in tails.get((s, p), ()) if x != o))
+                toff.append(len(tent))
+                hent.extend(sorted(x for x in heads.get((o, p), ()) if x != s))
+                hoff.append(len(hent))
+            as_dev = lambda v: torch.as_tensor(np.asarray(v if v else [0], dtype=np.int32),
+                                               device=device)
+            self._answers = (as_dev(toff), as_dev(tent), as_dev(hoff), as_dev(hent))
+        return self._answers
 
     def ranks(self, model):
         """[n, 4] int array: tail raw, tail filtered, head raw, head filtered,
@@ -64,15 +86,24 @@ class FilteredRankingEval(object):
         if not q:
             return np.zeros((0, 4), dtype=np.int64)
         queries = torch.as_tensor(np.asarray(q, dtype=np.int32), device=dev)
-        kg = self._known_set(dev)
         E = model.params["E"]
         lib = L.lib()
-        nbytes = lib.skge_rank_workspace_bytes(len(q), model.d)
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         out = torch.empty((len(q), 4), dtype=torch.int32, device=dev)
-        L.check(lib.skge_rank(L.stream_ptr(), code, L.ptr(E.data), L.ptr(rel.data), E.rows,
-                              model.d, L.ptr(queries), len(q), L.ptr(kg.slots), kg.capacity,
-                              L.ptr(ws), nbytes, L.ptr(out)), "rank")
+        if os.environ.get("SKGE_RANK_SET") == "1":   # A/B: the triple-set form (round 1)
+            kg = self._known_set(dev)
+            nbytes = lib.skge_rank_workspace_bytes(len(q), model.d)
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            L.check(lib.skge_rank(L.stream_ptr(), code, L.ptr(E.data), L.ptr(rel.data), E.rows,
+                                  model.d, L.ptr(queries), len(q), L.ptr(kg.slots), kg.capacity,
+                                  L.ptr(ws), nbytes, L.ptr(out)), "rank")
+        else:
+            toff, tent, hoff, hent = self._known_answers(q, dev)
+            nbytes = lib.skge_rank_known_workspace_bytes(len(q), model.d)
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            L.check(lib.skge_rank_known(L.stream_ptr(), code, L.ptr(E.data), L.ptr(rel.data),
+                                        E.rows, model.d, L.ptr(queries), len(q), L.ptr(toff),
+                                        L.ptr(tent), L.ptr(hoff), L.ptr(hent), L.ptr(ws), nbytes,
+                                        L.ptr(out)), "rank")
         self.last_ranks = out.cpu().numpy().astype(np.int64)
         return self.last_ranks
 

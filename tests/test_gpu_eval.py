@@ -84,3 +84,26 @@ def test_wn18_scale_ranking_runs():
     assert (r[:, 1] <= r[:, 0]).all() and (r[:, 3] <= r[:, 2]).all()   # filtering only removes
     (mrr, mean, hits), (fmrr, fmean, fhits) = S.ranking_scores(*ev.positions(m))
     assert 0 < mrr <= fmrr <= 1
+
+
+@pytest.mark.parametrize("name,d,n_ent", [("transe", 200, 3000), ("hole", 200, 3000),
+                                          ("rescal", 37, 1500), ("transe", 30, 5000)])
+def test_known_answer_ranks_equal_triple_set_ranks(name, d, n_ent, monkeypatch):
+    """The all-entity pass over entity slices with the filter applied from the
+    queries' known answers (skge_rank_known) against the triple-set form
+    (skge_rank): identical positions, raw and filtered, both directions --
+    incl. d % 4 != 0 and a KG dense enough that queries have many answers."""
+    import skge_amd as S
+    rs = np.random.RandomState(7)
+    n_rel = 4
+    known = np.unique(np.stack([rs.randint(n_ent // 10, size=20000), rs.randint(n_ent, size=20000),
+                                rs.randint(n_rel, size=20000)], axis=1), axis=0).astype(np.int32)
+    test = known[rs.choice(len(known), 700, replace=False)]
+    m = _model(name, n_ent, n_rel, d)
+    out = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("SKGE_RANK_SET", env)
+        ev = S.FilteredRankingEval(test.tolist(), known.tolist())
+        out.append(ev.ranks(m))
+    np.testing.assert_array_equal(out[0], out[1])
+    assert (out[1][:, 1] < out[1][:, 0]).any()   # the filter removed some known answers
