@@ -738,12 +738,15 @@ def hole_positive_path(d):
 def model_flops(kind, d, P, V):
     """Algorithmic FLOPs of one batch of P pairs with V violators:
     HolE: 2 scoring correlations per pair + 6 gradient correlations per
-    violating pair, 2d^2 each (direct form); RESCAL: W E_o for the 4 triples of
+    violating pair, 2d^2 each (direct form); on the per-positive path 2
+    correlations per positive (A = ccorr(R, E[o]), B = ccorr(R, E[o']) score
+    all three triples) + 2 per violating pair (3 for a positive whose second
+    pair alone violates: counted as 2, a lower bound); RESCAL: W E_o for the 4 triples of
     a positive's 2 pairs, E_s W for the violators' entity gradients (computed
     for all 4 by the GEMM) and the 4 dW outer products: 24 d^2 per positive."""
     if kind == "hole":
-        if hole_positive_path(d):   # k_hole_pos: 7 correlations per positive (P / 2)
-            return 2.0 * d * d * 7 * (P / 2.0)
+        if hole_positive_path(d):   # k_hole_pos / k_hole_pipe
+            return 2.0 * d * d * (2 * (P / 2.0) + 2 * V)
         return 2.0 * d * d * (2 * P + 6 * V)
     return 24.0 * d * d * (P / 2.0)
 

@@ -127,8 +127,9 @@ __device__ __forceinline__ void to_lds_rev(float* s, const float (&v)[KM], int d
 
 template <int KM>
 __device__ __forceinline__ void corr_fast(const float* sa, const float* sb2, float* sout, int d,
-                                          float (&out)[KM]) {
+                                          float (&out)[KM], float4* quad = nullptr) {
   const int l = lane_id(), base = 4 * l;
+  if (quad) *quad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (base < d) {
     f2 c01 = {0.0f, 0.0f}, c23 = {0.0f, 0.0f}, e01 = {0.0f, 0.0f}, e23 = {0.0f, 0.0f};
     float4 lo = *reinterpret_cast<const float4*>(sb2 + base);
@@ -152,6 +153,7 @@ __device__ __forceinline__ void corr_fast(const float* sa, const float* sb2, flo
     c01 += e01;
     c23 += e23;
     *reinterpret_cast<float4*>(sout + base) = make_float4(c01.x, c01.y, c23.x, c23.y);
+    if (quad) *quad = make_float4(c01.x, c01.y, c23.x, c23.y);
   }
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -323,8 +325,11 @@ __device__ __forceinline__ bool hole_pair(const PairArgs& a, int i, float* sw, c
   return true;
 }
 
-// HolE pair with the register-tiled correlations (hole_fast(d)); same
-// arithmetic steps as hole_pair, LDS per wave: hole_fast_lds_floats(d)
+// HolE pair with the register-tiled correlations (hole_fast(d)); the steps of
+// hole_pair with the scores taken as E[s] . ccorr(R[p], E[o]) (hole_score_q,
+// the same value as R[p] . ccorr(E[s], E[o]) in exact arithmetic), so the
+// sp / sn gradient rows come with the scores; LDS per wave:
+// hole_fast_lds_floats(d)
 template <int KM>
 __device__ __forceinline__ bool hole_pair_fast(const PairArgs& a, int i, float* sw,
                                                const int (&ix)[6]) {
@@ -355,16 +360,17 @@ __device__ __forceinline__ bool hole_pair_fast(const PairArgs& a, int i, float* 
   to_lds_dbl<KM>(sEo, eo, d);
   to_lds_dbl<KM>(sFo, fo, d);
   __builtin_amdgcn_wave_barrier();
-  float cp[KM], cn[KM];
-  corr_fast<KM>(sEs, sEo, sout, d, cp);  // ccorr(E[s], E[o])   (hole.py:20)
-  corr_fast<KM>(sFs, sFo, sout, d, cn);
-  float ps = 0.0f, ns = 0.0f;
-#pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    ps += rp[k] * cp[k];
-    ns += rn[k] * cn[k];
-  }
-  const float praw = wave_sum(ps), nraw = wave_sum(ns);
+  // scores R . ccorr(E[s], E[o]) (hole.py:20) as E[s] . ccorr(R[p], E[o])
+  // (hole_score_q): the correlations are the E[sp] / E[sn] gradient rows
+  float ap[KM], an[KM];
+  float4 qap, qan;
+  corr_fast<KM>(sRp, sEo, sout, d, ap, &qap);
+  corr_fast<KM>(sRn, sFo, sout, d, an, &qan);
+  const int base = 4 * lane_id();
+  const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  const float4 qes = base < d ? *reinterpret_cast<const float4*>(sEs + base) : z4;
+  const float4 qfs = base < d ? *reinterpret_cast<const float4*>(sFs + base) : z4;
+  const float praw = hole_score_q(qes, qap), nraw = hole_score_q(qfs, qan);
   if (lane_id() == 0) {
     if (a.pscore) a.pscore[i] = praw;
     if (a.nscore) a.nscore[i] = nraw;
@@ -378,19 +384,19 @@ __device__ __forceinline__ bool hole_pair_fast(const PairArgs& a, int i, float* 
   const float gp = -af_g_given_f(a.af, pf);  // hole.py:66
   const float gn = af_g_given_f(a.af, nf);   // hole.py:67
   float x[KM], y[KM], t[KM];
+#ifndef SKGE_ABL_HOLE_NO_GCORR
   // relation rows (pp, pn): (gp ccorr(E[sp],E[op]), gn ccorr(E[sn],E[on]))  hole.py:76-82
-  scale<KM>(x, cp, gp);
-  scale<KM>(y, cn, gn);
+  corr_fast<KM>(sEs, sEo, sout, d, t);
+  scale<KM>(x, t, gp);
+  corr_fast<KM>(sFs, sFo, sout, d, t);
+  scale<KM>(y, t, gn);
+#endif
 #ifndef SKGE_ABL_HOLE_NO_RATOM   // timing-only ablation builds (tools/ablate.sh)
   acc_two<KM>(replica(a.accR, i), pp, x, pn, y, d);
 #endif
-#ifndef SKGE_ABL_HOLE_NO_GCORR
   // entity rows (sp, sn): gp ccorr(R[pp],E[op]), gn ccorr(R[pn],E[on])   hole.py:93-94
-  corr_fast<KM>(sRp, sEo, sout, d, t);
-  scale<KM>(x, t, gp);
-  corr_fast<KM>(sRn, sFo, sout, d, t);
-  scale<KM>(y, t, gn);
-#endif
+  scale<KM>(x, ap, gp);
+  scale<KM>(y, an, gn);
 #ifndef SKGE_ABL_HOLE_NO_EATOM
   acc_two<KM>(a.accE, sp, x, sn, y, d);
 #endif
@@ -544,23 +550,23 @@ __global__ __launch_bounds__(256) void k_hole_pair_fast(PairArgs a) {
 // HolE pairwise, one positive and BOTH of its pairs per wave (device pair
 // loop).  Record j = (s, o, p, s'), o' gives pair 2j = ((s,o,p), (s',o,p)) and
 // pair 2j+1 = ((s,o,p), (s,o',p)) (skge/sample.py:41-46, base.py:1411-1416).
-// The two pairs share operands, so the 12 correlations of two
-// k_hole_pair_fast waves reduce to 7, in three loops that each slide ONE
-// window of their common second operand b (ccorr(a,b)_k = sum_j a_j b_{j+k}):
-//   b = E[o] : X = ccorr(E[s],E[o])   Y = ccorr(E[s'],E[o])   A = ccorr(R[p],E[o])
-//   b = E[o']: Z = ccorr(E[s],E[o'])  B = ccorr(R[p],E[o'])
-//   b = R[p] : C = cconv(E[s],R[p])   D = cconv(E[s'],R[p])
-// Scores R[p].X, R[p].Y, R[p].Z (hole.py:20) with k_hole_pair_fast's exact
-// arithmetic, so the margin decisions (hole.py:56) are the pair path's;
-// gp = -g(f(p)), gn = g(f(n)) (hole.py:66-67).  Per violating pair (v0, v1)
-// the contributions of hole.py:76-96, summed per row before the atomics:
-//   R[p] : v0 (gp X + g0 Y) + v1 (gp X + g1 Z)
-//   E[s] : v0 gp A + v1 (gp A + g1 B)          E[s']: v0 g0 A
-//   E[o] : v0 (gp C + g0 D) + v1 gp C          E[o']: v1 g1 C
+// Scores (hole.py:20) through the relation-side correlations (hole_score_q):
+//   A = ccorr(R[p], E[o]), B = ccorr(R[p], E[o'])   (one loop, a = R[p])
+//   f(s,o,p) = E[s] . A,  f(s',o,p) = E[s'] . A,  f(s,o',p) = E[s] . B
+// with k_hole_pair_fast's arithmetic, so the margin decisions (hole.py:56) are
+// the pair path's; gp = -g(f(p)), gn = g(f(n)) (hole.py:66-67).  A positive
+// with no violating pair is done after these 2 correlations.  Per violating
+// pair (v0, v1) the contributions of hole.py:76-96, summed per row, with the
+// correlations merged by linearity (u = (v0+v1) gp E[s] + v0 g0 E[s']):
+//   E[s] : (v0+v1) gp A + v1 g1 B                 E[s']: g0 A
+//   E[o] : cconv(u, R[p])                         E[o']: g1 cconv(E[s], R[p])
+//   R[p] : ccorr(u, E[o]) + v1 g1 ccorr(E[s], E[o'])
+// = 2 more correlations for v0 alone, 3 for v1 alone, 4 for both (was 7 per
+// positive whatever the outcome).  Entity slots 4j..4j+3 name (s, o, s', o')
 // with the occurrence counts grad_sum_matrix gives those lists (s: v0 + 2 v1,
-// o: 2 v0 + v1, s': v0, o': v1, p: 2 (v0 + v1)).  Entity slots 4j..4j+3 name
-// (s, o, s', o'), relation slot j names p.  Rows are held in the quad layout
-// (lane l: elements 4l..4l+3), so d % 4 == 0 and d <= 256.
+// o: 2 v0 + v1, s': v0, o': v1, p: 2 (v0 + v1)), relation slot j names p.
+// Rows are held in the quad layout (lane l: elements 4l..4l+3), so d % 4 == 0
+// and d <= 256.
 // ---------------------------------------------------------------------------
 struct HolePosArgs {
   const float* E;
@@ -585,13 +591,7 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
     if (a.total) *a.total += *a.fold;
     *a.fold = 0;
   }
-  float* sEs = smem + wave * hole_pos_lds_floats(d);   // a operands
-  float* sFs = sEs + d;
-  float* rEs = sEs + 2 * d;
-  float* rFs = sEs + 3 * d;
-  float* sR2 = sEs + 4 * d;                            // doubled b operands
-  float* sO2 = sR2 + 2 * d + 4;
-  float* sQ2 = sO2 + 2 * d + 4;
+  const HolePosLds L(smem + wave * hole_pos_lds_floats(d), d);
   int nv = 0;
   for (int j = blockIdx.x * wpb + wave; j < a.count; j += gridDim.x * wpb) {
     const int4 r4 = a.rec[a.start + j];
@@ -604,34 +604,25 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
     load_row4<1>(a.R, p, d, rp);
     load_row4<1>(a.E, n0r, d, fs);
     load_row4<1>(a.E, n1r, d, fo);
-    q_lds(sEs, es[0], d);
-    q_lds(sFs, fs[0], d);
-    q_lds_rev(rEs, es[0], d);
-    q_lds_rev(rFs, fs[0], d);
-    q_lds_dbl(sR2, rp[0], d);
-    q_lds_dbl(sO2, eo[0], d);
-    q_lds_dbl(sQ2, fo[0], d);
+    q_lds_dbl(L.R2, rp[0], d);
+    q_lds_dbl(L.O2, eo[0], d);
+    q_lds_dbl(L.Q2, fo[0], d);
     __builtin_amdgcn_wave_barrier();
-    float4 c1[3], c2[2], c3[2];
+    float4 AB[2];
 #ifndef SKGE_ABL_HPOS_NO_CORR   // timing-only ablation builds (tools/ablate.sh)
     {
-      const float* const a1[3] = {sEs, sFs, sR2};
-      corr_quad<3>(a1, sO2, d, c1);
-      const float* const a2[2] = {sEs, sR2};
-      corr_quad<2>(a2, sQ2, d, c2);
-      const float* const a3[2] = {rEs, rFs};
-      corr_quad<2>(a3, sR2, d, c3);
+      const float* const b2[2] = {L.O2, L.Q2};
+      corr_quad_b<2>(L.R2, b2, d, AB);
     }
 #else
-    c1[0] = c1[1] = c1[2] = c2[0] = c2[1] = c3[0] = c3[1] = eo[0];
+    AB[0] = AB[1] = eo[0];
 #endif
-    __builtin_amdgcn_wave_barrier();   // sEs is reused as the stage below
-    const float4 X = c1[0], Y = c1[1], A = c1[2], Z = c2[0], B = c2[1], C = c3[0], D = c3[1];
-    const float praw = score_q<KM>(X, sR2, d, sEs);
-    const float raw0 = score_q<KM>(Y, sR2, d, sEs), raw1 = score_q<KM>(Z, sR2, d, sEs);
+    const float4 A = AB[0], B = AB[1];
+    const float praw = hole_score_q(es[0], A);
+    const float raw0 = hole_score_q(fs[0], A), raw1 = hole_score_q(es[0], B);
     const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
-    const int v0 = (neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0;   // hole.py:56
-    const int v1 = (neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0;
+    const int v0 = uni((neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0);   // hole.py:56
+    const int v1 = uni((neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0);
     const Accum aR = replica(a.accR, j);
     if (l < 4)
       commit_slot(a.accE, sel4(l, s, o, neg0, neg1), sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1),
@@ -642,25 +633,13 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
     nv += v0 + v1;
     const float gp = -af_g_given_f(a.af, pf);   // hole.py:66
     const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
-    const float fv0 = (float)v0, fv1 = (float)v1;
-    float4 cs, co, c0, cq, cr;
-#define SKGE_HC(M)                                                \
-  cs.M = fv0 * (gp * A.M) + fv1 * (gp * A.M + g1 * B.M);          \
-  co.M = fv0 * (gp * C.M + g0 * D.M) + fv1 * (gp * C.M);          \
-  c0.M = g0 * A.M;                                                \
-  cq.M = g1 * C.M;                                                \
-  cr.M = fv0 * (gp * X.M + g0 * Y.M) + fv1 * (gp * X.M + g1 * Z.M);
-    SKGE_HC(x)
-    SKGE_HC(y)
-    SKGE_HC(z)
-    SKGE_HC(w)
-#undef SKGE_HC
+    const HoleRows h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gp, g0, g1);
 #ifndef SKGE_ABL_HPOS_NO_ATOM
-    acc_q<KM>(aR, p, cr, d, sEs);
-    acc_q<KM>(a.accE, s, cs, d, sEs);
-    acc_q<KM>(a.accE, o, co, d, sEs);
-    if (v0) acc_q<KM>(a.accE, neg0, c0, d, sEs);
-    if (v1) acc_q<KM>(a.accE, neg1, cq, d, sEs);
+    acc_q<KM>(aR, p, h.cr, d, L.U);
+    acc_q<KM>(a.accE, s, h.cs, d, L.U);
+    acc_q<KM>(a.accE, o, h.co, d, L.U);
+    if (v0) acc_q<KM>(a.accE, neg0, h.c0, d, L.U);
+    if (v1) acc_q<KM>(a.accE, neg1, h.cq, d, L.U);
 #endif
     __builtin_amdgcn_wave_barrier();
   }

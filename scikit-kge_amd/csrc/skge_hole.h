@@ -85,6 +85,118 @@ __device__ __forceinline__ void corr_quad(const float* const (&sa)[NA], const fl
   }
 }
 
+// NB correlations sharing the first operand: out[n] = ccorr(a, b_n), every b_n
+// doubled in sb2[n]; per output the FMA sequence of corr_quad / corr_fast
+template <int NB>
+__device__ __forceinline__ void corr_quad_b(const float* sa, const float* const (&sb2)[NB], int d,
+                                            float4 (&out)[NB]) {
+  const int base = 4 * lane_id();
+  f2 c01[NB], c23[NB], e01[NB], e23[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    c01[n] = f2{0.0f, 0.0f};
+    c23[n] = f2{0.0f, 0.0f};
+    e01[n] = f2{0.0f, 0.0f};
+    e23[n] = f2{0.0f, 0.0f};
+  }
+  if (base < d) {
+    float4 lo[NB], hi[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      lo[n] = *reinterpret_cast<const float4*>(sb2[n] + base);
+      hi[n] = *reinterpret_cast<const float4*>(sb2[n] + base + 4);
+    }
+    for (int j0 = 0; j0 < d; j0 += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(sa + j0);   // broadcast
+      const f2 ax = {a.x, a.x}, ay = {a.y, a.y}, az = {a.z, a.z}, aw = {a.w, a.w};
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const float4 nx = *reinterpret_cast<const float4*>(sb2[n] + j0 + 8 + base);
+        const f2 w01 = {lo[n].x, lo[n].y}, w12 = {lo[n].y, lo[n].z}, w23 = {lo[n].z, lo[n].w};
+        const f2 w34 = {lo[n].w, hi[n].x}, w45 = {hi[n].x, hi[n].y}, w56 = {hi[n].y, hi[n].z};
+        c01[n] = __builtin_elementwise_fma(ax, w01, c01[n]);
+        c23[n] = __builtin_elementwise_fma(ax, w23, c23[n]);
+        e01[n] = __builtin_elementwise_fma(ay, w12, e01[n]);
+        e23[n] = __builtin_elementwise_fma(ay, w34, e23[n]);
+        c01[n] = __builtin_elementwise_fma(az, w23, c01[n]);
+        c23[n] = __builtin_elementwise_fma(az, w45, c23[n]);
+        e01[n] = __builtin_elementwise_fma(aw, w34, e01[n]);
+        e23[n] = __builtin_elementwise_fma(aw, w56, e23[n]);
+        lo[n] = hi[n];
+        hi[n] = nx;
+      }
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const f2 u = c01[n] + e01[n], v = c23[n] + e23[n];
+    out[n] = make_float4(u.x, u.y, v.x, v.y);
+  }
+}
+
+// sum of NP correlations, out = sum_n ccorr(a_n, b_n) (b_n doubled): the
+// relation-row contribution of several pairs in one accumulator set
+template <int NP>
+__device__ __forceinline__ float4 corr_quad_sum(const float* const (&sa)[NP],
+                                                const float* const (&sb2)[NP], int d) {
+  const int base = 4 * lane_id();
+  f2 c01 = {0.0f, 0.0f}, c23 = {0.0f, 0.0f}, e01 = {0.0f, 0.0f}, e23 = {0.0f, 0.0f};
+  if (base < d) {
+    float4 lo[NP], hi[NP];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+      lo[n] = *reinterpret_cast<const float4*>(sb2[n] + base);
+      hi[n] = *reinterpret_cast<const float4*>(sb2[n] + base + 4);
+    }
+    for (int j0 = 0; j0 < d; j0 += 4) {
+#pragma unroll
+      for (int n = 0; n < NP; ++n) {
+        const float4 a = *reinterpret_cast<const float4*>(sa[n] + j0);   // broadcast
+        const float4 nx = *reinterpret_cast<const float4*>(sb2[n] + j0 + 8 + base);
+        const f2 ax = {a.x, a.x}, ay = {a.y, a.y}, az = {a.z, a.z}, aw = {a.w, a.w};
+        const f2 w01 = {lo[n].x, lo[n].y}, w12 = {lo[n].y, lo[n].z}, w23 = {lo[n].z, lo[n].w};
+        const f2 w34 = {lo[n].w, hi[n].x}, w45 = {hi[n].x, hi[n].y}, w56 = {hi[n].y, hi[n].z};
+        c01 = __builtin_elementwise_fma(ax, w01, c01);
+        c23 = __builtin_elementwise_fma(ax, w23, c23);
+        e01 = __builtin_elementwise_fma(ay, w12, e01);
+        e23 = __builtin_elementwise_fma(ay, w34, e23);
+        c01 = __builtin_elementwise_fma(az, w23, c01);
+        c23 = __builtin_elementwise_fma(az, w45, c23);
+        e01 = __builtin_elementwise_fma(aw, w34, e01);
+        e23 = __builtin_elementwise_fma(aw, w56, e23);
+        lo[n] = hi[n];
+        hi[n] = nx;
+      }
+    }
+  }
+  const f2 u = c01 + e01, v = c23 + e23;
+  return make_float4(u.x, u.y, v.x, v.y);
+}
+
+// lane partial of a quad-layout dot product (zeros past the row)
+__device__ __forceinline__ float dot_quad(const float4& x, const float4& y) {
+  return fmaf(x.w, y.w, fmaf(x.z, y.z, fmaf(x.y, y.y, x.x * y.x)));
+}
+
+__device__ __forceinline__ float4 axpby4(float a, const float4& x, float b, const float4& y) {
+  return make_float4(fmaf(a, x.x, b * y.x), fmaf(a, x.y, b * y.y), fmaf(a, x.z, b * y.z),
+                     fmaf(a, x.w, b * y.w));
+}
+__device__ __forceinline__ float4 scale4(float a, const float4& x) {
+  return make_float4(a * x.x, a * x.y, a * x.z, a * x.w);
+}
+
+// HolE score through the relation-side correlation:
+//   R . ccorr(a, b) = sum_k R_k sum_j a_j b_{j+k} = sum_j a_j ccorr(R, b)_j,
+// so a positive and its two negatives are scored from A = ccorr(R[p], E[o])
+// and B = ccorr(R[p], E[o']) -- the very rows the E[s] / E[s'] gradients use
+// (hole.py:93-94) -- instead of three ccorr(E, E) evaluations.  Every HolE
+// pairwise kernel with d % 4 == 0, d <= 256 scores this way, with this
+// arithmetic (quad partial, then the wave sum), so their margin decisions agree.
+__device__ __forceinline__ float hole_score_q(const float4& a, const float4& Acorr) {
+  return wave_sum(dot_quad(a, Acorr));
+}
+
 // score R . c with k_hole_pair_fast's arithmetic: lane-strided products
 // summed over k, then the wave sum (c staged through the wave's LDS)
 template <int KM>
@@ -120,6 +232,76 @@ __device__ __forceinline__ void acc_q(const Accum& acc, int row, const float4& v
   }
   __builtin_amdgcn_wave_barrier();
   acc_row<KM>(acc, row, x, d);
+}
+
+
+// wave-private LDS of the per-positive HolE kernels: three doubled b operands
+// (R[p], E[o], E[o']) and four a operands / stages
+struct HolePosLds {
+  float *R2, *O2, *Q2, *U, *Ur, *Er, *W;
+  __device__ HolePosLds(float* w, int d)
+      : R2(w), O2(w + 2 * d + 4), Q2(w + 4 * d + 8), U(w + 6 * d + 12), Ur(w + 7 * d + 12),
+        Er(w + 8 * d + 12), W(w + 9 * d + 12) {}
+};
+
+// The per-positive HolE step after the margin test (v0 + v1 > 0): the violating
+// pairs' contribution rows (see above).  The rows (quad layout) and A, B are
+// in registers, R[p] / E[o] / E[o'] doubled in L.
+struct HoleRows {
+  float4 cs, co, c0, cq, cr;
+};
+__device__ __forceinline__ HoleRows hole_pos_rows(const HolePosLds& L, int d, const float4& es,
+                                                  const float4& fs, const float4& A,
+                                                  const float4& B, int v0, int v1, float gp,
+                                                  float g0, float g1) {
+  HoleRows h;
+  const float cu = (float)(v0 + v1) * gp, cf = v0 ? g0 : 0.0f;
+  const float4 u = axpby4(cu, es, cf, fs);
+  q_lds(L.U, u, d);
+  q_lds_rev(L.Ur, u, d);
+  if (v1) {
+    q_lds_rev(L.Er, es, d);
+    q_lds(L.W, scale4(g1, es), d);
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (v1) {
+    if (v0) {
+      const float* const a2[2] = {L.Ur, L.Er};
+      float4 cc[2];
+      corr_quad<2>(a2, L.R2, d, cc);
+      h.co = cc[0];
+      h.cq = scale4(g1, cc[1]);
+    } else {   // u = gp E[s]: one cconv serves both rows
+      const float* const a1[1] = {L.Er};
+      float4 cc[1];
+      corr_quad<1>(a1, L.R2, d, cc);
+      h.co = scale4(gp, cc[0]);
+      h.cq = scale4(g1, cc[0]);
+    }
+    const float* const sa[2] = {L.U, L.W};
+    const float* const sb[2] = {L.O2, L.Q2};
+    h.cr = corr_quad_sum<2>(sa, sb, d);
+  } else {
+    const float* const a1[1] = {L.Ur};
+    float4 cc[1];
+    corr_quad<1>(a1, L.R2, d, cc);
+    h.co = cc[0];
+    h.cq = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const float* const sa[1] = {L.U};
+    const float* const sb[1] = {L.O2};
+    h.cr = corr_quad_sum<1>(sa, sb, d);
+  }
+  const float fv0 = (float)v0, fv1 = (float)v1;
+#define SKGE_HC(M)                                         \
+  h.cs.M = fv0 * (gp * A.M) + fv1 * (gp * A.M + g1 * B.M); \
+  h.c0.M = g0 * A.M;
+  SKGE_HC(x)
+  SKGE_HC(y)
+  SKGE_HC(z)
+  SKGE_HC(w)
+#undef SKGE_HC
+  __builtin_amdgcn_wave_barrier();   // L.U is the atomics' stage after this
+  return h;
 }
 
 

@@ -1169,13 +1169,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
   }
   // ---- B role: score batch b (k_hole_pos's arithmetic), scatter into cp / ra_cur ----
   const int blk_b = a.b_first ? blk : blk - a.nA;
-  float* sEs = smem + wave * hole_pos_lds_floats(d);   // a operands
-  float* sFs = sEs + d;
-  float* rEs = sEs + 2 * d;
-  float* rFs = sEs + 3 * d;
-  float* sR2 = sEs + 4 * d;                            // doubled b operands
-  float* sO2 = sR2 + 2 * d + 4;
-  float* sQ2 = sO2 + 2 * d + 4;
+  const HolePosLds L(smem + wave * hole_pos_lds_floats(d), d);
   Accum aE;
   aE.sum = reinterpret_cast<float*>(a.E.sum[cp]);
   aE.width = d;
@@ -1218,30 +1212,21 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
       if (pend & 4ull) load_row4_sc1<1>(a.E.P, n0r, d, fs);
       if (pend & 8ull) load_row4_sc1<1>(a.E.P, n1r, d, fo);
     }
-    q_lds(sEs, es[0], d);
-    q_lds(sFs, fs[0], d);
-    q_lds_rev(rEs, es[0], d);
-    q_lds_rev(rFs, fs[0], d);
-    q_lds_dbl(sR2, rp[0], d);
-    q_lds_dbl(sO2, eo[0], d);
-    q_lds_dbl(sQ2, fo[0], d);
+    q_lds_dbl(L.R2, rp[0], d);
+    q_lds_dbl(L.O2, eo[0], d);
+    q_lds_dbl(L.Q2, fo[0], d);
     __builtin_amdgcn_wave_barrier();
-    float4 c1[3], c2[2], c3[2];
+    float4 AB[2];
     {
-      const float* const a1[3] = {sEs, sFs, sR2};
-      corr_quad<3>(a1, sO2, d, c1);
-      const float* const a2[2] = {sEs, sR2};
-      corr_quad<2>(a2, sQ2, d, c2);
-      const float* const a3[2] = {rEs, rFs};
-      corr_quad<2>(a3, sR2, d, c3);
+      const float* const b2[2] = {L.O2, L.Q2};
+      corr_quad_b<2>(L.R2, b2, d, AB);
     }
-    __builtin_amdgcn_wave_barrier();   // sEs is reused as the stage below
-    const float4 X = c1[0], Y = c1[1], A = c1[2], Z = c2[0], B = c2[1], C = c3[0], D = c3[1];
-    const float praw = score_q<KM>(X, sR2, d, sEs);
-    const float raw0 = score_q<KM>(Y, sR2, d, sEs), raw1 = score_q<KM>(Z, sR2, d, sEs);
+    const float4 A = AB[0], B = AB[1];
+    const float praw = hole_score_q(es[0], A);
+    const float raw0 = hole_score_q(fs[0], A), raw1 = hole_score_q(es[0], B);
     const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
-    const int v0 = (neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0;   // hole.py:56
-    const int v1 = (neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0;
+    const int v0 = uni((neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0);   // hole.py:56
+    const int v1 = uni((neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0);
     {
       const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
       const int rE = sel4(l, s, o, neg0, neg1);
@@ -1256,29 +1241,17 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
     nv += v0 + v1;
     const float gpf = -af_g_given_f(a.af, pf);   // hole.py:66
     const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
-    const float fv0 = (float)v0, fv1 = (float)v1;
-    float4 cs, co, c0, cq, cr;
-#define SKGE_HC(M)                                                \
-  cs.M = fv0 * (gpf * A.M) + fv1 * (gpf * A.M + g1 * B.M);        \
-  co.M = fv0 * (gpf * C.M + g0 * D.M) + fv1 * (gpf * C.M);        \
-  c0.M = g0 * A.M;                                                \
-  cq.M = g1 * C.M;                                                \
-  cr.M = fv0 * (gpf * X.M + g0 * Y.M) + fv1 * (gpf * X.M + g1 * Z.M);
-    SKGE_HC(x)
-    SKGE_HC(y)
-    SKGE_HC(z)
-    SKGE_HC(w)
-#undef SKGE_HC
+    const HoleRows h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gpf, g0, g1);
     Accum aR;
     aR.sum = racc + (size_t)p * rstride;
     aR.width = d;
 #ifndef SKGE_HPIPE_ABL_NO_RATOM   // timing-only ablation: relation sums dropped
-    acc_q<KM>(aR, 0, cr, d, sEs);
+    acc_q<KM>(aR, 0, h.cr, d, L.U);
 #endif
-    acc_q<KM>(aE, s, cs, d, sEs);
-    acc_q<KM>(aE, o, co, d, sEs);
-    if (v0) acc_q<KM>(aE, neg0, c0, d, sEs);
-    if (v1) acc_q<KM>(aE, neg1, cq, d, sEs);
+    acc_q<KM>(aE, s, h.cs, d, L.U);
+    acc_q<KM>(aE, o, h.co, d, L.U);
+    if (v0) acc_q<KM>(aE, neg0, h.c0, d, L.U);
+    if (v1) acc_q<KM>(aE, neg1, h.cq, d, L.U);
     __builtin_amdgcn_wave_barrier();
   }
   if (l == 0 && nv) {
