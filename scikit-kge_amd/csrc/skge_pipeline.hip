@@ -1138,8 +1138,17 @@ __device__ __forceinline__ void rel_publish_f(const PipeArgs& a, int w, int rd, 
   if (c && a.R.updated && l == 0) atomicAdd(shard_of(a.R.updated), 1);
 }
 
+#ifndef SKGE_HPIPE_OCC
+#define SKGE_HPIPE_OCC 2   // scoring waves per SIMD the apply-workgroup cap assumes
+#endif
+#if SKGE_HPIPE_OCC > 2
+#define SKGE_HPIPE_ATTR __attribute__((amdgpu_waves_per_eu(SKGE_HPIPE_OCC)))
+#else
+#define SKGE_HPIPE_ATTR
+#endif
+
 template <int KM>
-__global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
+__global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(PipeArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6;
   const int l = lane_id();
@@ -1571,9 +1580,9 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
                                  : (4 * prev + ASLOTS - 1) / ASLOTS);
     constexpr int WPB = SKGE_PIPE_WG / 64;
     // HolE: the apply waves loop over their items within the residency the
-    // scoring waves leave (2 waves per SIMD at ~180 VGPRs; the flush has the
-    // chip to itself)
-    int a_cap = hole && b < nb1 ? std::max(1, (2 * 4 * 256 - (int)((batches[b].second + WPB - 1) / WPB) * WPB) / WPB - 8) : 16384;
+    // scoring waves leave (SKGE_HPIPE_OCC waves per SIMD: 2 at ~180 VGPRs; the
+    // flush has the chip to itself)
+    int a_cap = hole && b < nb1 ? std::max(1, (SKGE_HPIPE_OCC * 4 * 256 - (int)((batches[b].second + WPB - 1) / WPB) * WPB) / WPB - 8) : 16384;
     if (hole && b < nb1 && getenv("SKGE_HPIPE_ACAP")) a_cap = std::max(1, atoi(getenv("SKGE_HPIPE_ACAP")));
     // TransE, large batches: the A role's waves loop over their slots within ~768
     // workgroups instead of one wave per slot (the scoring waves then find the
