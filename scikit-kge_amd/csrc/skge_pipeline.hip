@@ -1037,6 +1037,9 @@ __device__ __forceinline__ void claim_and_apply_f(const PipeTab& t, int pp, int 
 #define SKGE_HPIPE_GROUP 1   // A/B on WN18 d=200: 1 row 51.7M, 2: 51.4M, 4: 49.6M, 8: 48.0M
 #endif
 constexpr int HGROUP = SKGE_HPIPE_GROUP;
+#ifndef SKGE_HPIPE_SLOTS_PREFETCH
+#define SKGE_HPIPE_SLOTS_PREFETCH 1   // apply_slots_f (0: one slot group per iteration)
+#endif
 template <int KQ>
 __device__ __forceinline__ void claim_and_apply_group_f(const PipeTab& t, int pp, int s0, int ns,
                                                         int d, int gp) {
@@ -1070,6 +1073,65 @@ __device__ __forceinline__ void claim_and_apply_group_f(const PipeTab& t, int pp
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
   if (c != 0) __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (t.claims && l == 0) atomicAdd(shard_of(t.claims), (int)__builtin_popcountll(won));
+}
+
+// The HolE launch's A role over its share of the slot records: slots k0,
+// k0 + ks, ... < ns.  The slot ids come in one vector load per 64 slots (empty
+// slots cost nothing more), and each touched row's claim and loads are issued
+// while the previous row is updated and published, so a wave's rows overlap
+// instead of paying a dependent slot load + claim round trip each.
+template <int KQ>
+__device__ __forceinline__ void apply_slots_f(const PipeTab& t, int pp, int k0, int ks, int ns,
+                                              int d, int gp) {
+  const int l = lane_id(), nq = d >> 2;
+  float* S = reinterpret_cast<float*>(t.sum[pp]);
+  for (int base = k0; base < ns; base += 64 * ks) {
+    const int k = base + l * ks;
+    const int rowl = k < ns ? t.touched[pp][k] : -1;
+    uint64_t m = __ballot(rowl >= 0);
+    if (!m) continue;
+    int i = __builtin_ctzll(m);
+    m &= m - 1;
+    int r = __builtin_amdgcn_readlane(rowl, i), c = 0;
+    float4 sm[KQ], p[KQ], a[KQ];
+    if (l == 0) c = atomicExch(t.cnt[pp] + r, 0);
+    load_f32_row<KQ>(t.P, t.A, S, r, d, p, a, sm);
+    int nclaim = 0;
+    while (true) {
+      int rn = -1, cn = 0;
+      float4 smn[KQ], pn[KQ], an[KQ];
+      if (m) {   // the next row's claim and loads in flight behind this row
+        i = __builtin_ctzll(m);
+        m &= m - 1;
+        rn = __builtin_amdgcn_readlane(rowl, i);
+        if (l == 0) cn = atomicExch(t.cnt[pp] + rn, 0);
+        load_f32_row<KQ>(t.P, t.A, S, rn, d, pn, an, smn);
+      }
+      c = __builtin_amdgcn_readfirstlane(c);
+      if (c != 0) {   // this wave owns the row
+        row_update_f<KQ>(t.u, c, d, sm, p, a);
+        float4* srow = reinterpret_cast<float4*>(S + (size_t)r * d);
+#pragma unroll
+        for (int q = 0; q < KQ; ++q)
+          if (64 * q + l < nq) srow[64 * q + l] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        store_row4_sc1<KQ>(t.P, r, d, p);
+        if (t.A) store_row4_sc1<KQ>(t.A, r, d, a);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+        if (l == 0) __hip_atomic_store(t.done + r, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ++nclaim;
+      }
+      if (rn < 0) break;
+      r = rn;
+      c = cn;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        sm[q] = smn[q];
+        p[q] = pn[q];
+        a[q] = an[q];
+      }
+    }
+    if (t.claims && l == 0 && nclaim) atomicAdd(shard_of(t.claims), nclaim);
+  }
 }
 
 template <int KQ>
@@ -1165,14 +1227,28 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     // ---- A role: write R_b, then apply the previous batch's entity rows ----
     const int blk_a = a.b_first ? blk - nB : blk;
     const int nR = a.R.rows;
-    const int total = nR + (a.prev_slots + HGROUP - 1) / HGROUP;   // relation rows, slot groups
     const int wa = blk_a * wpb + wave;
+    const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
     if (a.b == a.nb1 && wa == 0) fold_shards(a.nviol_shards, a.nviol_total);
+#if SKGE_HPIPE_SLOTS_PREFETCH
+    // items w = wa, wa + S, ...: relation rows w < nR, then entity slots w - nR
+    const int S = a.nA * wpb;
+    for (int w = wa; w < nR; w += S) rel_publish_f<1>(a, w, rd, rw, ra_prev, ra_old);
+    const int k0 = wa >= nR ? wa - nR : wa - nR + ((nR - wa + S - 1) / S) * S;
+    apply_slots_f<1>(a.E, pp, k0, S, a.prev_slots, d, gp);
+#else
+    const int total = nR + (a.prev_slots + HGROUP - 1) / HGROUP;   // relation rows, slot groups
     for (int w = wa; w < total; w += a.nA * wpb) {
       if (w < nR)
         rel_publish_f<1>(a, w, rd, rw, ra_prev, ra_old);
       else
         claim_and_apply_group_f<1>(a.E, pp, HGROUP * (w - nR), a.prev_slots, d, gp);
+    }
+#endif
+    if (a.trace && l == 0) {   // diagnostics (skge_pipe_runner_profile, tools/hole_trace.py)
+      unsigned long long* tr = a.trace + 2 + 6 * (size_t)a.count + 2 * (size_t)wa;
+      tr[0] = ta0;
+      tr[1] = now_10ns();
     }
     return;
   }
@@ -1186,6 +1262,8 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
   const int rstride = 2 * a.R.rw;   // floats per relation accumulator row
   int nv = 0;
   for (int w = blk_b * wpb + wave; w < a.count; w += nB * wpb) {
+    unsigned long long tt[4] = {0ull, 0ull, 0ull, 0ull};
+    if (a.trace) tt[0] = now_10ns();
     const long long j = a.start + w;
     const int4 r4 = a.rec[j];
     const int r1 = a.rec_n1[j];
@@ -1210,6 +1288,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
 #else
     const uint64_t pend = 0ull * __ballot(mark == gp);
 #endif
+    if (a.trace) tt[1] = now_10ns();
     if (pend) {
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) {
@@ -1221,6 +1300,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
       if (pend & 4ull) load_row4_sc1<1>(a.E.P, n0r, d, fs);
       if (pend & 8ull) load_row4_sc1<1>(a.E.P, n1r, d, fo);
     }
+    if (a.trace) tt[2] = now_10ns();
     q_lds_dbl(L.R2, rp[0], d);
     q_lds_dbl(L.O2, eo[0], d);
     q_lds_dbl(L.Q2, fo[0], d);
@@ -1236,6 +1316,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
     const int v0 = uni((neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0);   // hole.py:56
     const int v1 = uni((neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0);
+    if (a.trace) tt[3] = now_10ns();
     {
       const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
       const int rE = sel4(l, s, o, neg0, neg1);
@@ -1245,6 +1326,11 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
       } else if (l == 4 && v0 + v1 > 0) {
         atomicAdd(reinterpret_cast<int*>(racc + (size_t)p * rstride + d), 2 * (v0 + v1));
       }
+    }
+    if (a.trace && l == 0 && v0 + v1 == 0) {
+      unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
+      tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
+      tr[5] = pend;
     }
     if (v0 + v1 == 0) continue;
     nv += v0 + v1;
@@ -1262,6 +1348,11 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     if (v0) acc_q<KM>(aE, neg0, h.c0, d, L.U);
     if (v1) acc_q<KM>(aE, neg1, h.cq, d, L.U);
     __builtin_amdgcn_wave_barrier();
+    if (a.trace && l == 0) {   // stamp after issue (no drain)
+      unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
+      tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
+      tr[5] = pend | (1ull << 8) | ((unsigned long long)v0 << 9) | ((unsigned long long)v1 << 10);
+    }
   }
   if (l == 0 && nv) {
     atomicAdd(shard_of(a.nviol_shards), nv);

@@ -16,6 +16,24 @@ __device__ inline unsigned hsh(unsigned x) { x ^= x >> 16; x *= 0x85EBCA6Bu; x ^
 
 __global__ void k_empty(int n) {}
 
+// persistent grid: `iters` grid-wide barriers (one agent-scope counter, WG
+// leaders arrive then poll); bounded spins, err[0] set on timeout
+__global__ __launch_bounds__(256) void k_gridbar(unsigned* ctr, int iters, unsigned* err) {
+  const unsigned nwg = gridDim.x;
+  for (int it = 1; it <= iters; ++it) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned spins = 0;
+      while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < nwg * it) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 22)) { atomicOr(err, 1u); break; }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <int ROWS, bool ATOM, bool CHAIN, bool CNT>
 __global__ __launch_bounds__(256) void k_rows(const float* __restrict__ E, float* acc, int* cnt,
                                               const int* __restrict__ idx, float* out, int nw, unsigned salt) {
@@ -124,5 +142,20 @@ int main() {
   timeit("applylike 7070 waves", [&] { hipLaunchKernelGGL(k_applylike, dim3((nws + 3) / 4), dim3(256), 0, st, P, A, S, slots, nws); }, st);
   timeit("applylike 5656 waves", [&] { hipLaunchKernelGGL(k_applylike, dim3((5656 + 3) / 4), dim3(256), 0, st, P, A, S, slots, 5656); }, st);
   timeit("applylike 1414 waves", [&] { hipLaunchKernelGGL(k_applylike, dim3((1414 + 3) / 4), dim3(256), 0, st, P, A, S, slots, 1414); }, st);
+  unsigned *ctr, *err;
+  CK(hipMalloc(&ctr, 4)); CK(hipMalloc(&err, 4)); CK(hipMemset(err, 0, 4));
+  for (int nwg : {256, 512, 1024}) {
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    const int iters = 200;
+    for (int rep = 0; rep < 2; ++rep) {
+      CK(hipMemsetAsync(ctr, 0, 4, st));
+      CK(hipEventRecord(e0, st));
+      hipLaunchKernelGGL(k_gridbar, dim3(nwg), dim3(256), 0, st, ctr, iters, err);
+      CK(hipEventRecord(e1, st)); CK(hipStreamSynchronize(st));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      unsigned he; CK(hipMemcpy(&he, err, 4, hipMemcpyDeviceToHost));
+      if (rep) printf("grid barrier %4d WGs x256            %7.2f us/barrier%s\n", nwg, 1e3f * ms / iters, he ? " (TIMEOUT)" : "");
+    }
+  }
   return 0;
 }
