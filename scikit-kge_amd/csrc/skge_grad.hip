@@ -91,15 +91,15 @@ __device__ __forceinline__ void cconv_lds(const float* sa, const float* sb, int 
 }
 
 // ---- register-tiled circular correlation (HolE, d % 4 == 0, d <= 256) ----
-// c_k = sum_j a_j b_{(j+k) mod d}: lane l owns outputs 4l..4l+3 and slides an
-// 8-float window of b along j (b stored twice in LDS so j+k needs no mod):
-// per 4 j's one broadcast 16-B read of a, one 16-B read of b, 8 v_pk_fma_f32.
+// corr_quad_b (skge_hole.h): lane l owns outputs 4l..4l+3 and slides an
+// 8-float window of b along j (b stored twice in LDS so j+k needs no mod);
 // cconv(a, b) = ccorr(a', b) with a'_m = a_{(-m) mod d} (stored reversed).
 // The quad result goes through a wave-private LDS row back to the lane-
 // strided layout of the rest of the kernel.
 __device__ __forceinline__ bool hole_fast(int d) { return (d & 3) == 0 && d >= 4 && d <= 256; }
-// wave-private LDS floats of the fast HolE pair kernel
-__host__ __device__ __forceinline__ int hole_fast_lds_floats(int d) { return 13 * d + 16; }
+// wave-private LDS floats of the fast HolE pair kernel: four a operands
+// (d + 4), four doubled rows (2d + 4), the output row
+__host__ __device__ __forceinline__ int hole_fast_lds_floats(int d) { return 13 * d + 32; }
 
 template <int KM>
 __device__ __forceinline__ void to_lds_dbl(float* s2, const float (&v)[KM], int d) {
@@ -115,6 +115,18 @@ __device__ __forceinline__ void to_lds_dbl(float* s2, const float (&v)[KM], int 
   if (l < 4) s2[2 * d + l] = 0.0f;   // read (unused) by the last window refill
 }
 
+// a operand of corr_fast (d + 4 floats): a[d] = a[0]
+template <int KM>
+__device__ __forceinline__ void to_lds_a(float* s, const float (&v)[KM], int d) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k;
+    if (e < d) s[e] = v[k];
+  }
+  if (l == 0) s[d] = v[0];
+}
+
 template <int KM>
 __device__ __forceinline__ void to_lds_rev(float* s, const float (&v)[KM], int d) {
   const int l = lane_id();
@@ -123,38 +135,18 @@ __device__ __forceinline__ void to_lds_rev(float* s, const float (&v)[KM], int d
     const int e = l + 64 * k;
     if (e < d) s[e == 0 ? 0 : d - e] = v[k];
   }
+  if (l == 0) s[d] = v[0];
 }
 
 template <int KM>
 __device__ __forceinline__ void corr_fast(const float* sa, const float* sb2, float* sout, int d,
                                           float (&out)[KM], float4* quad = nullptr) {
   const int l = lane_id(), base = 4 * l;
-  if (quad) *quad = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  if (base < d) {
-    f2 c01 = {0.0f, 0.0f}, c23 = {0.0f, 0.0f}, e01 = {0.0f, 0.0f}, e23 = {0.0f, 0.0f};
-    float4 lo = *reinterpret_cast<const float4*>(sb2 + base);
-    float4 hi = *reinterpret_cast<const float4*>(sb2 + base + 4);
-    for (int j0 = 0; j0 < d; j0 += 4) {
-      const float4 a = *reinterpret_cast<const float4*>(sa + j0);   // broadcast
-      const f2 w01 = {lo.x, lo.y}, w12 = {lo.y, lo.z}, w23 = {lo.z, lo.w}, w34 = {lo.w, hi.x};
-      const f2 w45 = {hi.x, hi.y}, w56 = {hi.y, hi.z};
-      const f2 ax = {a.x, a.x}, ay = {a.y, a.y}, az = {a.z, a.z}, aw = {a.w, a.w};
-      c01 = __builtin_elementwise_fma(ax, w01, c01);   // c_r += a_{j0+s} b_{j0+s+base+r}
-      c23 = __builtin_elementwise_fma(ax, w23, c23);
-      e01 = __builtin_elementwise_fma(ay, w12, e01);
-      e23 = __builtin_elementwise_fma(ay, w34, e23);
-      c01 = __builtin_elementwise_fma(az, w23, c01);
-      c23 = __builtin_elementwise_fma(az, w45, c23);
-      e01 = __builtin_elementwise_fma(aw, w34, e01);
-      e23 = __builtin_elementwise_fma(aw, w56, e23);
-      lo = hi;
-      hi = *reinterpret_cast<const float4*>(sb2 + j0 + 8 + base);
-    }
-    c01 += e01;
-    c23 += e23;
-    *reinterpret_cast<float4*>(sout + base) = make_float4(c01.x, c01.y, c23.x, c23.y);
-    if (quad) *quad = make_float4(c01.x, c01.y, c23.x, c23.y);
-  }
+  const float* const b1[1] = {sb2};
+  float4 q[1];
+  corr_quad_b<1>(sa, b1, d, q);
+  if (quad) *quad = q[0];   // zeros past the row
+  if (base < d) *reinterpret_cast<float4*>(sout + base) = q[0];
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
@@ -335,11 +327,11 @@ __device__ __forceinline__ bool hole_pair_fast(const PairArgs& a, int i, float* 
                                                const int (&ix)[6]) {
   const int d = a.d;
   const int sp = ix[0], op = ix[1], pp = ix[2], sn = ix[3], on = ix[4], pn = ix[5];
-  float* sEs = sw;               // a operands: E[sp], E[sn], reversed copies
-  float* sFs = sw + d;
-  float* rEs = sw + 2 * d;
-  float* rFs = sw + 3 * d;
-  float* sRp = sw + 4 * d;       // doubled rows (2d + 4)
+  float* sEs = sw;               // a operands (d + 4): E[sp], E[sn], reversed copies
+  float* sFs = sw + d + 4;
+  float* rEs = sw + 2 * d + 8;
+  float* rFs = sw + 3 * d + 12;
+  float* sRp = sw + 4 * d + 16;  // doubled rows (2d + 4)
   float* sRn = sRp + 2 * d + 4;
   float* sEo = sRn + 2 * d + 4;
   float* sFo = sEo + 2 * d + 4;
@@ -351,8 +343,8 @@ __device__ __forceinline__ bool hole_pair_fast(const PairArgs& a, int i, float* 
   load_row<KM>(a.E, sn, d, fs);
   load_row<KM>(a.E, on, d, fo);
   load_row<KM>(a.R, pn, d, rn);
-  to_lds<KM>(sEs, es, d);
-  to_lds<KM>(sFs, fs, d);
+  to_lds_a<KM>(sEs, es, d);
+  to_lds_a<KM>(sFs, fs, d);
   to_lds_rev<KM>(rEs, es, d);
   to_lds_rev<KM>(rFs, fs, d);
   to_lds_dbl<KM>(sRp, rp, d);
@@ -710,10 +702,10 @@ __global__ __launch_bounds__(256) void k_triple_grad(PairArgs a) {
   float* sEs = smem + wave * (fast ? hole_fast_lds_floats(d) : 3 * stride);
   float* sEo = sEs + stride;
   float* sRp = sEs + 2 * stride;
-  // fast layout: E[s], E[s] reversed (d each), E[o], R[p] doubled, output row
+  // fast layout: E[s], E[s] reversed (d + 4 each), E[o], R[p] doubled, output row
   float* fEs = sEs;
-  float* fEsr = sEs + d;
-  float* fEo2 = sEs + 2 * d;
+  float* fEsr = sEs + d + 4;
+  float* fEo2 = sEs + 2 * d + 8;
   float* fRp2 = fEo2 + 2 * d + 4;
   float* fout = fRp2 + 2 * d + 4;
   float lsum = 0.0f;
@@ -727,7 +719,7 @@ __global__ __launch_bounds__(256) void k_triple_grad(PairArgs a) {
     if (MODEL == HOLE && KM <= 4 && fast) {
       float rp[KM], c[KM];
       load_row<KM>(a.R, p, d, rp);
-      to_lds<KM>(fEs, es, d);
+      to_lds_a<KM>(fEs, es, d);
       to_lds_rev<KM>(fEsr, es, d);
       to_lds_dbl<KM>(fEo2, eo, d);
       to_lds_dbl<KM>(fRp2, rp, d);

@@ -12,11 +12,14 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-__host__ __device__ __forceinline__ int hole_pos_lds_floats(int d) { return 10 * d + 12; }
+// three doubled rows (2d + 4) and four a operands (d + 4) per wave
+__host__ __device__ __forceinline__ int hole_pos_lds_floats(int d) { return 10 * d + 28; }
 
+// a operand (d + 4 floats): a[d..d+3] = a[0..3] for the correlation's last step
 __device__ __forceinline__ void q_lds(float* s, const float4& v, int d) {
   const int base = 4 * lane_id();
   if (base < d) *reinterpret_cast<float4*>(s + base) = v;
+  if (base == 0) *reinterpret_cast<float4*>(s + d) = v;
 }
 
 // doubled row (b operand): s2[e] = s2[e + d] = v_e, 4 zeros after
@@ -29,10 +32,11 @@ __device__ __forceinline__ void q_lds_dbl(float* s2, const float4& v, int d) {
   if (l < 4) s2[2 * d + l] = 0.0f;
 }
 
-// reversed row a'_m = a_{-m mod d}: cconv(a, b) = ccorr(a', b)
+// reversed row a'_m = a_{-m mod d}: cconv(a, b) = ccorr(a', b); a'[d] = a'[0]
 __device__ __forceinline__ void q_lds_rev(float* s, const float4& v, int d) {
   const int base = 4 * lane_id();
   if (base < d) {
+    if (base == 0) s[d] = v.x;
     s[base == 0 ? 0 : d - base] = v.x;
     s[d - base - 1] = v.y;
     s[d - base - 2] = v.z;
@@ -40,65 +44,87 @@ __device__ __forceinline__ void q_lds_rev(float* s, const float4& v, int d) {
   }
 }
 
-// NA correlations against one second operand: out[n] (quad layout) =
-// ccorr(sa[n], b) with b doubled in sb2; per output the FMA sequence of corr_fast
+// ---- direct circular correlation, quad layout (lane l: outputs 4l..4l+3) ----
+// c_k = sum_j a_j b_{(j+k) mod d} (skge/util.py:30-50), b doubled in LDS
+// (b2[e] = b2[e + d] = b_e, 4 zeros after), a with a[d] = a[0] (the staging
+// helpers below write it).  Each packed FMA pairs two consecutive j of ONE
+// output (the two halves are that output's even-j and odd-j partial sums), so
+// every b operand is an aligned register pair of the lane's 8-float window
+// w = b[4l+j0 .. 4l+j0+7] and no window pair needs a register move:
+//   out 4l+0 += {a_j0,a_j0+1}*w01   + {a_j0+2,a_j0+3}*w23
+//   out 4l+1 += {a_j0+1,a_j0+2}*w23 + {a_j0+3,a_j0+4}*w45
+//   out 4l+2 += {a_j0,a_j0+1}*w23   + {a_j0+2,a_j0+3}*w45
+//   out 4l+3 += {a_j0+1,a_j0+2}*w45 + {a_j0+3,a_j0+4}*w67
+// The two misaligned a pairs are built once per step and shared by every b.
+struct CorrA {
+  f2 xy, zw, yz, wx;
+};
+// A = a[j0 .. j0+3], An = a[j0+4 .. j0+7] (16-B broadcast reads; An is the
+// next step's A, and a[d] = a[0] at the last step)
+__device__ __forceinline__ CorrA corr_a(const float4& A, const float4& An) {
+  return {f2{A.x, A.y}, f2{A.z, A.w}, f2{A.y, A.z}, f2{A.w, An.x}};
+}
+__device__ __forceinline__ float4 lds4(const float* s) {
+  return *reinterpret_cast<const float4*>(s);
+}
+struct CorrAcc {
+  f2 c0, c1, c2, c3;
+};
+__device__ __forceinline__ void corr_zero(CorrAcc& c) {
+  c.c0 = c.c1 = c.c2 = c.c3 = f2{0.0f, 0.0f};
+}
+__device__ __forceinline__ void corr_step(CorrAcc& c, const CorrA& a, const float4& lo,
+                                          const float4& hi) {
+  const f2 w01 = {lo.x, lo.y}, w23 = {lo.z, lo.w}, w45 = {hi.x, hi.y}, w67 = {hi.z, hi.w};
+  c.c0 = __builtin_elementwise_fma(a.xy, w01, c.c0);
+  c.c1 = __builtin_elementwise_fma(a.yz, w23, c.c1);
+  c.c2 = __builtin_elementwise_fma(a.xy, w23, c.c2);
+  c.c3 = __builtin_elementwise_fma(a.yz, w45, c.c3);
+  c.c0 = __builtin_elementwise_fma(a.zw, w23, c.c0);
+  c.c1 = __builtin_elementwise_fma(a.wx, w45, c.c1);
+  c.c2 = __builtin_elementwise_fma(a.zw, w45, c.c2);
+  c.c3 = __builtin_elementwise_fma(a.wx, w67, c.c3);
+}
+__device__ __forceinline__ float4 corr_out(const CorrAcc& c) {
+  return make_float4(c.c0.x + c.c0.y, c.c1.x + c.c1.y, c.c2.x + c.c2.y, c.c3.x + c.c3.y);
+}
+
+// NA correlations against one second operand: out[n] = ccorr(sa[n], b)
 template <int NA>
 __device__ __forceinline__ void corr_quad(const float* const (&sa)[NA], const float* sb2, int d,
                                           float4 (&out)[NA]) {
   const int base = 4 * lane_id();
-  f2 c01[NA], c23[NA], e01[NA], e23[NA];
+  CorrAcc c[NA];
 #pragma unroll
-  for (int n = 0; n < NA; ++n) {
-    c01[n] = f2{0.0f, 0.0f};
-    c23[n] = f2{0.0f, 0.0f};
-    e01[n] = f2{0.0f, 0.0f};
-    e23[n] = f2{0.0f, 0.0f};
-  }
+  for (int n = 0; n < NA; ++n) corr_zero(c[n]);
   if (base < d) {
-    float4 lo = *reinterpret_cast<const float4*>(sb2 + base);
-    float4 hi = *reinterpret_cast<const float4*>(sb2 + base + 4);
+    float4 lo = lds4(sb2 + base), hi = lds4(sb2 + base + 4), A[NA];
+#pragma unroll
+    for (int n = 0; n < NA; ++n) A[n] = lds4(sa[n]);
     for (int j0 = 0; j0 < d; j0 += 4) {
-      const float4 nx = *reinterpret_cast<const float4*>(sb2 + j0 + 8 + base);
-      const f2 w01 = {lo.x, lo.y}, w12 = {lo.y, lo.z}, w23 = {lo.z, lo.w}, w34 = {lo.w, hi.x};
-      const f2 w45 = {hi.x, hi.y}, w56 = {hi.y, hi.z};
+      const float4 nx = lds4(sb2 + j0 + 8 + base);
 #pragma unroll
       for (int n = 0; n < NA; ++n) {
-        const float4 a = *reinterpret_cast<const float4*>(sa[n] + j0);   // broadcast
-        const f2 ax = {a.x, a.x}, ay = {a.y, a.y}, az = {a.z, a.z}, aw = {a.w, a.w};
-        c01[n] = __builtin_elementwise_fma(ax, w01, c01[n]);
-        c23[n] = __builtin_elementwise_fma(ax, w23, c23[n]);
-        e01[n] = __builtin_elementwise_fma(ay, w12, e01[n]);
-        e23[n] = __builtin_elementwise_fma(ay, w34, e23[n]);
-        c01[n] = __builtin_elementwise_fma(az, w23, c01[n]);
-        c23[n] = __builtin_elementwise_fma(az, w45, c23[n]);
-        e01[n] = __builtin_elementwise_fma(aw, w34, e01[n]);
-        e23[n] = __builtin_elementwise_fma(aw, w56, e23[n]);
+        const float4 An = lds4(sa[n] + j0 + 4);
+        corr_step(c[n], corr_a(A[n], An), lo, hi);
+        A[n] = An;
       }
       lo = hi;
       hi = nx;
     }
   }
 #pragma unroll
-  for (int n = 0; n < NA; ++n) {
-    const f2 u = c01[n] + e01[n], v = c23[n] + e23[n];
-    out[n] = make_float4(u.x, u.y, v.x, v.y);
-  }
+  for (int n = 0; n < NA; ++n) out[n] = corr_out(c[n]);
 }
 
-// NB correlations sharing the first operand: out[n] = ccorr(a, b_n), every b_n
-// doubled in sb2[n]; per output the FMA sequence of corr_quad / corr_fast
+// NB correlations sharing the first operand: out[n] = ccorr(a, b_n)
 template <int NB>
 __device__ __forceinline__ void corr_quad_b(const float* sa, const float* const (&sb2)[NB], int d,
                                             float4 (&out)[NB]) {
   const int base = 4 * lane_id();
-  f2 c01[NB], c23[NB], e01[NB], e23[NB];
+  CorrAcc c[NB];
 #pragma unroll
-  for (int n = 0; n < NB; ++n) {
-    c01[n] = f2{0.0f, 0.0f};
-    c23[n] = f2{0.0f, 0.0f};
-    e01[n] = f2{0.0f, 0.0f};
-    e23[n] = f2{0.0f, 0.0f};
-  }
+  for (int n = 0; n < NB; ++n) corr_zero(c[n]);
   if (base < d) {
     float4 lo[NB], hi[NB];
 #pragma unroll
@@ -106,41 +132,32 @@ __device__ __forceinline__ void corr_quad_b(const float* sa, const float* const 
       lo[n] = *reinterpret_cast<const float4*>(sb2[n] + base);
       hi[n] = *reinterpret_cast<const float4*>(sb2[n] + base + 4);
     }
+    float4 A = lds4(sa);
     for (int j0 = 0; j0 < d; j0 += 4) {
-      const float4 a = *reinterpret_cast<const float4*>(sa + j0);   // broadcast
-      const f2 ax = {a.x, a.x}, ay = {a.y, a.y}, az = {a.z, a.z}, aw = {a.w, a.w};
+      const float4 An = lds4(sa + j0 + 4);
+      const CorrA a = corr_a(A, An);
+      A = An;
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
         const float4 nx = *reinterpret_cast<const float4*>(sb2[n] + j0 + 8 + base);
-        const f2 w01 = {lo[n].x, lo[n].y}, w12 = {lo[n].y, lo[n].z}, w23 = {lo[n].z, lo[n].w};
-        const f2 w34 = {lo[n].w, hi[n].x}, w45 = {hi[n].x, hi[n].y}, w56 = {hi[n].y, hi[n].z};
-        c01[n] = __builtin_elementwise_fma(ax, w01, c01[n]);
-        c23[n] = __builtin_elementwise_fma(ax, w23, c23[n]);
-        e01[n] = __builtin_elementwise_fma(ay, w12, e01[n]);
-        e23[n] = __builtin_elementwise_fma(ay, w34, e23[n]);
-        c01[n] = __builtin_elementwise_fma(az, w23, c01[n]);
-        c23[n] = __builtin_elementwise_fma(az, w45, c23[n]);
-        e01[n] = __builtin_elementwise_fma(aw, w34, e01[n]);
-        e23[n] = __builtin_elementwise_fma(aw, w56, e23[n]);
+        corr_step(c[n], a, lo[n], hi[n]);
         lo[n] = hi[n];
         hi[n] = nx;
       }
     }
   }
 #pragma unroll
-  for (int n = 0; n < NB; ++n) {
-    const f2 u = c01[n] + e01[n], v = c23[n] + e23[n];
-    out[n] = make_float4(u.x, u.y, v.x, v.y);
-  }
+  for (int n = 0; n < NB; ++n) out[n] = corr_out(c[n]);
 }
 
-// sum of NP correlations, out = sum_n ccorr(a_n, b_n) (b_n doubled): the
-// relation-row contribution of several pairs in one accumulator set
+// sum of NP correlations, out = sum_n ccorr(a_n, b_n): the relation-row
+// contribution of several pairs in one accumulator set
 template <int NP>
 __device__ __forceinline__ float4 corr_quad_sum(const float* const (&sa)[NP],
                                                 const float* const (&sb2)[NP], int d) {
   const int base = 4 * lane_id();
-  f2 c01 = {0.0f, 0.0f}, c23 = {0.0f, 0.0f}, e01 = {0.0f, 0.0f}, e23 = {0.0f, 0.0f};
+  CorrAcc c;
+  corr_zero(c);
   if (base < d) {
     float4 lo[NP], hi[NP];
 #pragma unroll
@@ -148,29 +165,22 @@ __device__ __forceinline__ float4 corr_quad_sum(const float* const (&sa)[NP],
       lo[n] = *reinterpret_cast<const float4*>(sb2[n] + base);
       hi[n] = *reinterpret_cast<const float4*>(sb2[n] + base + 4);
     }
+    float4 A[NP];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) A[n] = lds4(sa[n]);
     for (int j0 = 0; j0 < d; j0 += 4) {
 #pragma unroll
       for (int n = 0; n < NP; ++n) {
-        const float4 a = *reinterpret_cast<const float4*>(sa[n] + j0);   // broadcast
-        const float4 nx = *reinterpret_cast<const float4*>(sb2[n] + j0 + 8 + base);
-        const f2 ax = {a.x, a.x}, ay = {a.y, a.y}, az = {a.z, a.z}, aw = {a.w, a.w};
-        const f2 w01 = {lo[n].x, lo[n].y}, w12 = {lo[n].y, lo[n].z}, w23 = {lo[n].z, lo[n].w};
-        const f2 w34 = {lo[n].w, hi[n].x}, w45 = {hi[n].x, hi[n].y}, w56 = {hi[n].y, hi[n].z};
-        c01 = __builtin_elementwise_fma(ax, w01, c01);
-        c23 = __builtin_elementwise_fma(ax, w23, c23);
-        e01 = __builtin_elementwise_fma(ay, w12, e01);
-        e23 = __builtin_elementwise_fma(ay, w34, e23);
-        c01 = __builtin_elementwise_fma(az, w23, c01);
-        c23 = __builtin_elementwise_fma(az, w45, c23);
-        e01 = __builtin_elementwise_fma(aw, w34, e01);
-        e23 = __builtin_elementwise_fma(aw, w56, e23);
+        const float4 nx = lds4(sb2[n] + j0 + 8 + base);
+        const float4 An = lds4(sa[n] + j0 + 4);
+        corr_step(c, corr_a(A[n], An), lo[n], hi[n]);
+        A[n] = An;
         lo[n] = hi[n];
         hi[n] = nx;
       }
     }
   }
-  const f2 u = c01 + e01, v = c23 + e23;
-  return make_float4(u.x, u.y, v.x, v.y);
+  return corr_out(c);
 }
 
 // lane partial of a quad-layout dot product (zeros past the row)
@@ -240,8 +250,8 @@ __device__ __forceinline__ void acc_q(const Accum& acc, int row, const float4& v
 struct HolePosLds {
   float *R2, *O2, *Q2, *U, *Ur, *Er, *W;
   __device__ HolePosLds(float* w, int d)
-      : R2(w), O2(w + 2 * d + 4), Q2(w + 4 * d + 8), U(w + 6 * d + 12), Ur(w + 7 * d + 12),
-        Er(w + 8 * d + 12), W(w + 9 * d + 12) {}
+      : R2(w), O2(w + 2 * d + 4), Q2(w + 4 * d + 8), U(w + 6 * d + 12), Ur(w + 7 * d + 16),
+        Er(w + 8 * d + 20), W(w + 9 * d + 24) {}
 };
 
 // The per-positive HolE step after the margin test (v0 + v1 > 0): the violating
