@@ -348,6 +348,11 @@ def main():
             "cpu_baseline": cpu,
             "detail": {
                 "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
+                # 2 pairs per positive (RandomModeSampler modes [0, 1]; on
+                # this sparse KG a negative is always found), the positive re-scored
+                # per pair (base.py:1411-1427): 4 scored triples per positive
+                "pairs_per_s": round(2.0 * value, 1),
+                "scored_triples_per_s": round(4.0 * value, 1),
                 "violations_per_pair": round(nviol / (2.0 * positives), 4),
                 "kernels": {n: {"avg_us": round(v["avg_us"], 3), "launches": v["launches"],
                                 "GB_s": round(v["achieved_gbs"], 1)}
