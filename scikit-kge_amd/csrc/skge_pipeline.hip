@@ -77,6 +77,8 @@ struct RelTab {                // relation table
   unsigned long long* acc[3];  // [rows][rw]: int16x4 sums in words [0, d/4), count in word d/4
                                // (w32: int32x2 sums in words [0, d/2), count in word d/2)
   int rows, rw;
+  int reps;                    // HolE: accumulator replicas per copy (row p of replica k at
+                               // k * rows + p); positive w adds into replica w % reps
   UpdParams u;
   int* updated;                // profile only: rows with a nonzero count (sharded)
 };
@@ -1164,6 +1166,23 @@ __device__ __forceinline__ void rel_row_f(const RelTab& t, int row, int d, int r
   load_f32_row<KQ>(t.P[rd] + (size_t)row * d, t.A[rd] ? t.A[rd] + (size_t)row * d : nullptr,
                    acc, 0, d, p, a, sm);
   c = __builtin_amdgcn_readfirstlane(__float_as_int(acc[d]));
+  for (int k = 1; k < t.reps; ++k) {   // large batches: the replicas, in a fixed order
+    const float* ak = reinterpret_cast<const float*>(t.acc[ra] +
+                                                     ((size_t)k * t.rows + row) * t.rw);
+    const float4* ak4 = reinterpret_cast<const float4*>(ak);
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+      const int q = 64 * m + l;
+      const float4 v = ak4[q < nq ? q : nq - 1];
+      if (q < nq) {
+        sm[m].x += v.x;
+        sm[m].y += v.y;
+        sm[m].z += v.z;
+        sm[m].w += v.w;
+      }
+    }
+    c += __builtin_amdgcn_readfirstlane(__float_as_int(ak[d]));
+  }
   if (c) {
     row_update_f<KQ>(t.u, c, d, sm, p, a);
   } else {
@@ -1193,9 +1212,12 @@ __device__ __forceinline__ void rel_publish_f(const PipeArgs& a, int w, int rd, 
       if (arow) arow[q] = av[m];
     }
   }
-  for (int q = l; q < a.R.rw; q += 64) {   // rw 8-B words: the sums and the count
-    old[q] = 0ull;
-    if (flush) prev[q] = 0ull;
+  for (int k = 0; k < a.R.reps; ++k) {   // rw 8-B words: the sums and the count
+    const size_t ko = (size_t)k * a.R.rows * a.R.rw;
+    for (int q = l; q < a.R.rw; q += 64) {
+      old[ko + q] = 0ull;
+      if (flush) prev[ko + q] = 0ull;
+    }
   }
   if (c && a.R.updated && l == 0) atomicAdd(shard_of(a.R.updated), 1);
 }
@@ -1258,10 +1280,11 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
   Accum aE;
   aE.sum = reinterpret_cast<float*>(a.E.sum[cp]);
   aE.width = d;
-  float* const racc = reinterpret_cast<float*>(a.R.acc[ra_cur]);
   const int rstride = 2 * a.R.rw;   // floats per relation accumulator row
   int nv = 0;
   for (int w = blk_b * wpb + wave; w < a.count; w += nB * wpb) {
+    float* const racc = reinterpret_cast<float*>(a.R.acc[ra_cur]) +
+                        (size_t)(w % a.R.reps) * a.R.rows * rstride;
     unsigned long long tt[4] = {0ull, 0ull, 0ull, 0ull};
     if (a.trace) tt[0] = now_10ns();
     const long long j = a.start + w;
@@ -1599,6 +1622,13 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     const int M = rel->rows;
     const bool ada = rel->opt == SKGE_ADAGRAD;
     q.rows = M;
+    // HolE (fp32 sums, float atomics): at large batches every relation row
+    // takes thousands of adds per launch, which serialise on its addresses;
+    // spread them over replicas (one per ~2k positives, <= 32; 1 at nb = 100)
+    q.reps = 1;
+    if (hole)
+      while (q.reps < 32 && (long long)q.reps * 2048 < bs) q.reps *= 2;
+    if (hole && getenv("SKGE_HPIPE_RREPS")) q.reps = std::max(1, atoi(getenv("SKGE_HPIPE_RREPS")));
     r->w32 = rel->acc_mode == SKGE_ACC_I32X2;
     // 8-B words per relation row: sums + count, whole 128-B lines (HolE: d
     // floats, then the count as an int)
@@ -1609,7 +1639,8 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     q.P[1] = (float*)dalloc(r, (size_t)M * d * 4);
     q.A[0] = ada ? rel->state : nullptr;
     q.A[1] = ada ? (float*)dalloc(r, (size_t)M * d * 4) : nullptr;
-    for (int k = 0; k < 3; ++k) q.acc[k] = (unsigned long long*)dalloc(r, (size_t)M * q.rw * 8);
+    for (int k = 0; k < 3; ++k)
+      q.acc[k] = (unsigned long long*)dalloc(r, (size_t)q.reps * M * q.rw * 8);
     if (!ok || !q.P[1] || (ada && !q.A[1]) || !q.acc[0] || !q.acc[1] || !q.acc[2]) {
       set_error("pipelined runner: device allocation failed");
       pipe_free(r);

@@ -288,6 +288,7 @@ def _hole_epochs(runner_cls, xs, n_ent, n_rel, d, nb, epochs, margin=0.2, seed=9
     (40, 3, 1200, 200, 4, 2, "sgd"),        # tiny graph: most rows pending every batch
     (500, 5, 3000, 64, 10, 3, "adagrad"),   # AdaGrad state through the hand-off
     (40943, 18, 14140, 200, 10, 1, "sgd"),  # WN18 entity count, d, batch size
+    (3000, 7, 14000, 32, 2, 2, "adagrad"),  # 7000 positives per batch: 4 relation replicas
 ])
 def test_hole_pipelined_runner_matches_pair_loop(n_ent, n_rel, T, d, nb, epochs, opt):
     """The pipelined HolE runner (launch g scores batch b while batch b-1's
@@ -304,6 +305,20 @@ def test_hole_pipelined_runner_matches_pair_loop(n_ent, n_rel, T, d, nb, epochs,
     for pid in a[2]:
         np.testing.assert_allclose(b[2][pid], a[2][pid], rtol=RTOL, atol=ATOL,
                                    err_msg="%s (%d, %d)" % (pid, a[0], b[0]))
+
+
+def test_hole_pipelined_runner_relation_replicas_forced(monkeypatch):
+    """Relation accumulator replicas (positive w adds into replica w % reps,
+    every reader sums them in a fixed order) forced to 3 at a small batch:
+    the same training as the pair loop up to fp32 summation order."""
+    from skge_amd.device import HolePipeRunner, PairLoopRunner
+    xs = make_kg(300, 7, 2000, seed=3)
+    a = _hole_epochs(PairLoopRunner, xs, 300, 7, 32, 7, 2, opt="adagrad")
+    monkeypatch.setenv("SKGE_HPIPE_RREPS", "3")
+    b = _hole_epochs(HolePipeRunner, xs, 300, 7, 32, 7, 2, opt="adagrad")
+    assert a[0] > 0 and abs(a[0] - b[0]) <= 2, (a[0], b[0])
+    for pid in a[2]:
+        np.testing.assert_allclose(b[2][pid], a[2][pid], rtol=RTOL, atol=ATOL, err_msg=pid)
 
 
 def test_hole_device_loop_auto_selects_pipelined_runner():
