@@ -58,9 +58,38 @@ struct RescalWs {
   float* coef;      // [n] dW coefficient of items[i] (bucket order)
   float* WE;        // [n][d]
   float* EW;        // [n][d]
+  float* wpart;     // [M][nt * nt][splits][64 * 64] split-K dW partial tiles (or null)
 };
 
 static int rs_tmax(int n, int M) { return n / RT_ITEMS + M + 1; }
+
+// dW split over K (a relation's items): at the reference's batch size a
+// relation holds ~235 items, which one workgroup per 64 x 64 dW tile walks in
+// two dependent rounds of gathers; `splits` workgroups per tile take every
+// splits-th group of 128 items each and write partial tiles, summed in split
+// order (deterministic) by the finishing kernel.  1 = the single fused kernel.
+#ifndef SKGE_RS_WG_SPLIT
+#define SKGE_RS_WG_SPLIT 8   // most splits per tile (1 disables)
+#endif
+constexpr int WS_TILE = 64;                 // == WG_T below
+constexpr int WS_GROUP = 128;               // items per group == WG_PF * WG_CH below
+static int rs_wsplit(int n, int M, int d) {
+  const long long nt = (d + WS_TILE - 1) / WS_TILE;
+  // (at the reference's batch, ~2 groups per relation, the extra launch costs
+  // more than the split saves: 22.5 M vs 24.1 M triples/s on WN18 d = 200;
+  // nb = 2, ~92 groups: 52.5 M vs 42.0 M)
+  const long long groups = ((long long)n / M + WS_GROUP - 1) / WS_GROUP;
+  int sp = groups < 4 ? 1 : (int)std::min<long long>(SKGE_RS_WG_SPLIT, groups);
+  const char* ns = getenv("SKGE_RS_NOSPLIT");   // A/B and test switch: the fused kernel only
+  if (ns && atoi(ns)) sp = 1;
+  while (sp > 1 && (long long)M * nt * nt * sp * WS_TILE * WS_TILE * 4 > (64ll << 20)) --sp;
+  return std::max(sp, 1);
+}
+static size_t rs_wpart_bytes(int n, int M, int d) {
+  const int sp = rs_wsplit(n, M, d);
+  const size_t nt = (d + WS_TILE - 1) / WS_TILE;
+  return sp > 1 ? (size_t)M * nt * nt * sp * WS_TILE * WS_TILE * 4 : 0;
+}
 
 // carve the workspace (base may be null: size only)
 // n: triples in the batch (2P for pairs: positives then negatives; T for
@@ -89,6 +118,8 @@ static size_t rescal_ws_layout(int n, int M, int d, void* base, RescalWs* ws) {
   w.coef = (float*)take((size_t)n * 4);
   w.WE = (float*)take((size_t)n * d * 4);
   w.EW = (float*)take((size_t)n * d * 4);
+  const size_t wpb = rs_wpart_bytes(n, M, d);
+  w.wpart = wpb ? (float*)take(wpb) : nullptr;
   if (ws) *ws = w;
   return off;
 }
@@ -952,6 +983,189 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
   }
 }
 
+// ---- split-K dW (rs_wsplit > 1) ----
+// k_rescal_wgrad_part: one workgroup per (relation, 64 x 64 tile, split s);
+// the tile's item groups g = s, s + splits, ... (WG_PF chunks of WG_CH items
+// each, every load of a group in flight together), contracted as in
+// k_rescal_wgrad_mfma but through one LDS buffer (a workgroup walks one group
+// at the reference's batch size, so double buffering buys nothing and halving
+// the LDS lets more workgroups be resident); the partial tile is stored whole.
+static_assert(WS_TILE == WG_T && WS_GROUP == WG_PF * WG_CH, "split-K group geometry");
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_rescal_wgrad_part(const float* __restrict__ E, int d,
+                                                           RescalWs ws, int splits) {
+  const int nt = (d + WG_T - 1) / WG_T;
+  const int blk = blockIdx.x / splits, sp = blockIdx.x - (blockIdx.x / splits) * splits;
+  const int p = blk / (nt * nt);
+  const int rem = blk - p * nt * nt;
+  const int rt = rem / nt, ct = rem - (rem / nt) * nt;
+  const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
+  const int off = ws.rel_off[p], cnt = ws.rel_off[p + 1] - off;
+  const int nch = (cnt + WG_CH - 1) / WG_CH, ngr = (nch + WG_PF - 1) / WG_PF;
+  if (sp >= ngr) return;   // no group for this split (the finishing kernel knows)
+  __shared__ float sEs[WG_CH][WG_T + 4];
+  __shared__ float sEo[WG_CH][WG_T + 4];
+  const int r0 = rt * WG_T, c0 = ct * WG_T;
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int it = tid / WG_TPI, h = (tid % WG_TPI) * WG_FPT;
+  for (int gr = sp; gr < ngr; gr += splits) {
+    const int g0 = gr * WG_PF;
+    int ns[WG_PF], no[WG_PF];
+    float nc[WG_PF];
+#pragma unroll
+    for (int q = 0; q < WG_PF; ++q) {
+      const int i = (g0 + q) * WG_CH + it;
+      const int at = off + (i < cnt ? i : cnt - 1);
+      ns[q] = ws.sorted_s[at];
+      no[q] = ws.sorted_o[at];
+      nc[q] = i < cnt ? ws.coef[at] : 0.0f;
+    }
+    float4 es[WG_PF][WG_FPT / 4], eo[WG_PF][WG_FPT / 4];
+#pragma unroll
+    for (int q = 0; q < WG_PF; ++q) {
+      const float* srow = E + (size_t)ns[q] * d;
+      const float* orow = E + (size_t)no[q] * d;
+#pragma unroll
+      for (int m = 0; m < WG_FPT / 4; ++m) {
+        const int cs = r0 + h + 4 * m, co = c0 + h + 4 * m;
+        if (VEC) {
+          es[q][m] = *reinterpret_cast<const float4*>(srow + (cs < d ? cs : 0));
+          eo[q][m] = *reinterpret_cast<const float4*>(orow + (co < d ? co : 0));
+        } else {
+          es[q][m] = make_float4(srow[cs < d ? cs : 0], srow[cs + 1 < d ? cs + 1 : 0],
+                                 srow[cs + 2 < d ? cs + 2 : 0], srow[cs + 3 < d ? cs + 3 : 0]);
+          eo[q][m] = make_float4(orow[co < d ? co : 0], orow[co + 1 < d ? co + 1 : 0],
+                                 orow[co + 2 < d ? co + 2 : 0], orow[co + 3 < d ? co + 3 : 0]);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < WG_PF; ++q) {
+      const int b = g0 + q;
+      if (b >= nch) break;
+      __syncthreads();   // every wave is done with the buffer's previous chunk
+#pragma unroll
+      for (int m = 0; m < WG_FPT / 4; ++m) {   // coef-scaled E[s], E[o]; zero past d
+        const int cs = r0 + h + 4 * m, co = c0 + h + 4 * m;
+        float4 a = es[q][m], o = eo[q][m];
+        const float cur_c = nc[q];
+        a.x = cs + 0 < d ? cur_c * a.x : 0.0f;
+        a.y = cs + 1 < d ? cur_c * a.y : 0.0f;
+        a.z = cs + 2 < d ? cur_c * a.z : 0.0f;
+        a.w = cs + 3 < d ? cur_c * a.w : 0.0f;
+        o.x = co + 0 < d ? o.x : 0.0f;
+        o.y = co + 1 < d ? o.y : 0.0f;
+        o.z = co + 2 < d ? o.z : 0.0f;
+        o.w = co + 3 < d ? o.w : 0.0f;
+        *reinterpret_cast<float4*>(&sEs[it][h + 4 * m]) = a;
+        *reinterpret_cast<float4*>(&sEo[it][h + 4 * m]) = o;
+      }
+      __syncthreads();
+      const int mm = min(WG_CH, cnt - b * WG_CH);
+      for (int k0 = 0; k0 < mm; k0 += 4) {
+        const int ik = k0 + (l >> 4);
+        const float av_ = sEs[ik][16 * wave + (l & 15)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av_, sEo[ik][16 * j + (l & 15)], acc[j], 0,
+                                                        0, 0);
+      }
+    }
+  }
+  // D[row 16 wave + 4 (l >> 4) + reg][col 16 j + (l & 15)] -> the partial tile
+  float* out = ws.wpart + ((size_t)blk * splits + sp) * (WG_T * WG_T);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg)
+      out[(16 * wave + 4 * (l >> 4) + reg) * WG_T + 16 * j + (l & 15)] = acc[j][reg];
+}
+
+// k_rescal_wgrad_fin: one workgroup per (relation, 64 x 64 tile): the tile's
+// partials summed in split order, then the accumulator write (slot map as
+// k_rescal_wgrad_mfma) or the W updater's step (the same arithmetic as its
+// APPLY epilogue)
+template <bool APPLY>
+__global__ __launch_bounds__(256) void k_rescal_wgrad_fin(int d, RescalWs ws, Accum accW,
+                                                          WApply wa, int splits) {
+  const int nt = (d + WG_T - 1) / WG_T;
+  const int blk = blockIdx.x;
+  const int p = blk / (nt * nt);
+  const int rem = blk - p * nt * nt;
+  const int rt = rem / nt, ct = rem - (rem / nt) * nt;
+  const int tid = threadIdx.x;
+  const int off = ws.rel_off[p], cnt = ws.rel_off[p + 1] - off;
+  if (!APPLY && rem == 0 && tid == 0) {   // slot p (skge_hip.h slot map)
+    if (accW.touched) accW.touched[p] = cnt > 0 ? p : -1;
+    accW.cnt[p] = cnt;
+  }
+  if (cnt == 0) return;
+  const bool upd = !APPLY || wa.gate == nullptr || *wa.gate != 0;
+  if (APPLY && !upd) return;   // the model returned None: no update
+  if (APPLY && rem == 0 && tid == 0 && wa.opt == OPT_ADAGRAD && wa.ucnt)
+    wa.ucnt[p] += 1;   // updateCounts, skge/param.py:149-150
+  const int nch = (cnt + WG_CH - 1) / WG_CH, ngr = (nch + WG_PF - 1) / WG_PF;
+  const int nsp = min(splits, ngr);
+  const float* part = ws.wpart + (size_t)blk * splits * (WG_T * WG_T);
+  const bool ada = wa.opt == OPT_ADAGRAD;
+  const float div = wa.fdiv > 0.0f ? wa.fdiv : (float)cnt;
+  constexpr int EPT = WG_T * WG_T / 256;   // 16 elements per thread, 4 float4
+  float sum[EPT], pw[EPT], aw[EPT];
+  size_t os[EPT];
+  bool in[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT / 4; ++k) {   // elements 4 (tid + 256 k) + m: row e / 64, col e % 64
+    const int e = 4 * (tid + 256 * k), r = rt * WG_T + e / WG_T, c = ct * WG_T + e % WG_T;
+    const float4 v = *reinterpret_cast<const float4*>(part + e);
+    sum[4 * k] = v.x;
+    sum[4 * k + 1] = v.y;
+    sum[4 * k + 2] = v.z;
+    sum[4 * k + 3] = v.w;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      in[4 * k + m] = r < d && c + m < d;
+      os[4 * k + m] = (size_t)p * d * d + (size_t)(r < d ? r : 0) * d + (c + m < d ? c + m : 0);
+    }
+  }
+  if (APPLY) {   // the W updater's operands, in flight with the partials
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      pw[e] = wa.W[os[e]];
+      aw[e] = ada ? wa.A[os[e]] : 0.0f;
+    }
+  }
+  for (int q = 1; q < nsp; ++q) {   // split order: deterministic sums
+#pragma unroll
+    for (int k = 0; k < EPT / 4; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)q * (WG_T * WG_T) +
+                                                        4 * (tid + 256 * k));
+      sum[4 * k] += v.x;
+      sum[4 * k + 1] += v.y;
+      sum[4 * k + 2] += v.z;
+      sum[4 * k + 3] += v.w;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    if (!in[e]) continue;
+    if (!APPLY) {
+      accW.sum[os[e]] = sum[e];
+      continue;
+    }
+    // same step as k_rescal_wgrad_mfma's APPLY epilogue (skge/param.py:115-155)
+    const float g = (sum[e] + wa.rin * pw[e]) / div + wa.rout * pw[e];
+    if (ada) {
+      const float a2 = aw[e] + g * g;
+      wa.W[os[e]] = pw[e] - (wa.lr * g) / fmaxf(sqrtf(a2), 1e-7f);
+      wa.A[os[e]] = a2;
+    } else {
+      wa.W[os[e]] = pw[e] - wa.lr * g;
+    }
+  }
+}
+
 }  // namespace skge
 
 using namespace skge;
@@ -1001,7 +1215,7 @@ static int rescal_front(hipStream_t st, const skge_table_t* ent, const skge_tabl
 // pass rel->gate semantics through `gate`)
 static void rescal_wgrad_launch(hipStream_t st, const skge_table_t* ent,
                                 const skge_table_t* rel, int d, const RescalWs& ws, bool apply,
-                                const int* gate) {
+                                const int* gate, int n) {
   const int nt = (d + WG_T - 1) / WG_T;
   const dim3 grid((unsigned)((long long)rel->rows * nt * nt));
   WApply wa = {};
@@ -1015,6 +1229,25 @@ static void rescal_wgrad_launch(hipStream_t st, const skge_table_t* ent,
     wa.fdiv = rel->fixed_div;
     wa.gate = gate;
     wa.ucnt = rel->upd_count;
+  }
+  const int splits = ws.wpart ? rs_wsplit(n, rel->rows, d) : 1;
+  if (splits > 1) {   // split-K: partial tiles, then the sum + accumulator write / W step
+    const dim3 pgrid(grid.x * (unsigned)splits);
+    if ((d & 3) == 0)
+      hipLaunchKernelGGL((k_rescal_wgrad_part<true>), pgrid, dim3(256), 0, st, ent->param, d, ws,
+                         splits);
+    else
+      hipLaunchKernelGGL((k_rescal_wgrad_part<false>), pgrid, dim3(256), 0, st, ent->param, d, ws,
+                         splits);
+    if (apply)
+      hipLaunchKernelGGL((k_rescal_wgrad_fin<true>), grid, dim3(256), 0, st, d, ws, accum_of(rel),
+                         wa, splits);
+    else
+      hipLaunchKernelGGL((k_rescal_wgrad_fin<false>), grid, dim3(256), 0, st, d, ws,
+                         accum_of(rel), wa, splits);
+    return;
+  }
+  if (apply) {
     if ((d & 3) == 0)
       hipLaunchKernelGGL((k_rescal_wgrad_mfma<true, true>), grid, dim3(256), 0, st, ent->param, d,
                          ws, accum_of(rel), wa);
@@ -1058,7 +1291,7 @@ int skge_rescal_pair_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
   const Accum aE = accum_of(ent);
   SKGE_KM_SWITCH(k_rescal_scatter, dim3(blocks), dim3(256), 0, st, pos, neg, P, d, af, margin, ws,
                  aE, pscore, nscore, nviol)
-  rescal_wgrad_launch(st, ent, rel, d, ws, apply_w, nviol);
+  rescal_wgrad_launch(st, ent, rel, d, ws, apply_w, nviol, 2 * P);
   SKGE_CHECK_LAUNCH("rescal mfma pair grad");
   return SKGE_OK;
 }
@@ -1088,7 +1321,7 @@ int skge_rescal_pos_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
   const int blocks = std::max(1, std::min((count + 3) / 4, 16384));
   SKGE_KM_SWITCH(k_rescal_pos_scatter, dim3(blocks), dim3(256), 0, st, rec, rec_n1, start, count,
                  d, af, margin, ws, accum_of(ent), nviol)
-  rescal_wgrad_launch(st, ent, rel, d, ws, true, nviol);
+  rescal_wgrad_launch(st, ent, rel, d, ws, true, nviol, 3 * count);
   SKGE_CHECK_LAUNCH("rescal positive grad");
   return SKGE_OK;
 }
@@ -1112,6 +1345,8 @@ static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, Resc
   w.coef = (float*)take((size_t)n * 4);
   w.WE = (float*)take((size_t)n * d * 4);
   w.EW = (float*)take((size_t)n * d * 4);
+  const size_t wpb = rs_wpart_bytes(n, M, d);   // batches of fewer items use fewer splits
+  w.wpart = wpb ? (float*)take(wpb) : nullptr;
   const size_t s0 = off;
   w.chunk = (int*)take((size_t)nchunks * M * 4);
   w.rel_off = (int*)take((size_t)(M + 1) * 4);
@@ -1199,7 +1434,7 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
   const int blocks = std::max(1, std::min((count + 3) / 4, 16384));
   SKGE_KM_SWITCH(k_rescal_pos_scatter, dim3(blocks), dim3(256), 0, st, rec, rec_n1, start, count,
                  d, af, margin, w, accum_of(ent), nviol)
-  rescal_wgrad_launch(st, ent, rel, d, w, true, nviol);
+  rescal_wgrad_launch(st, ent, rel, d, w, true, nviol, 3 * count);
   SKGE_CHECK_LAUNCH("rescal positive grad (epoch buckets)");
   return SKGE_OK;
 }
@@ -1219,7 +1454,7 @@ int skge_rescal_triple_grad_mfma(hipStream_t st, const skge_table_t* ent,
   const Accum aE = accum_of(ent);
   SKGE_KM_SWITCH(k_rescal_logistic, dim3(blocks), dim3(256), 0, st, trip, ys, T, d, ws, aE, score,
                  loss)
-  rescal_wgrad_launch(st, ent, rel, d, ws, apply_w, rel->gate);
+  rescal_wgrad_launch(st, ent, rel, d, ws, apply_w, rel->gate, T);
   SKGE_CHECK_LAUNCH("rescal mfma triple grad");
   return SKGE_OK;
 }

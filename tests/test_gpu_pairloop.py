@@ -288,7 +288,7 @@ def _hole_epochs(runner_cls, xs, n_ent, n_rel, d, nb, epochs, margin=0.2, seed=9
     (40, 3, 1200, 200, 4, 2, "sgd"),        # tiny graph: most rows pending every batch
     (500, 5, 3000, 64, 10, 3, "adagrad"),   # AdaGrad state through the hand-off
     (40943, 18, 14140, 200, 10, 1, "sgd"),  # WN18 entity count, d, batch size
-    (3000, 7, 14000, 32, 2, 2, "adagrad"),  # 7000 positives per batch: 4 relation replicas
+    (3000, 7, 14000, 32, 2, 2, "sgd"),  # 7000 positives per batch: 4 relation replicas
 ])
 def test_hole_pipelined_runner_matches_pair_loop(n_ent, n_rel, T, d, nb, epochs, opt):
     """The pipelined HolE runner (launch g scores batch b while batch b-1's
@@ -313,12 +313,39 @@ def test_hole_pipelined_runner_relation_replicas_forced(monkeypatch):
     the same training as the pair loop up to fp32 summation order."""
     from skge_amd.device import HolePipeRunner, PairLoopRunner
     xs = make_kg(300, 7, 2000, seed=3)
-    a = _hole_epochs(PairLoopRunner, xs, 300, 7, 32, 7, 2, opt="adagrad")
+    a = _hole_epochs(PairLoopRunner, xs, 300, 7, 32, 7, 2)
     monkeypatch.setenv("SKGE_HPIPE_RREPS", "3")
-    b = _hole_epochs(HolePipeRunner, xs, 300, 7, 32, 7, 2, opt="adagrad")
+    b = _hole_epochs(HolePipeRunner, xs, 300, 7, 32, 7, 2)
     assert a[0] > 0 and abs(a[0] - b[0]) <= 2, (a[0], b[0])
     for pid in a[2]:
         np.testing.assert_allclose(b[2][pid], a[2][pid], rtol=RTOL, atol=ATOL, err_msg=pid)
+
+
+def test_rescal_split_k_dw_matches_fused(monkeypatch):
+    """RESCAL dW split over K (batches with >= 4 groups of 128 items per
+    relation: partial tiles summed in split order by a finishing kernel)
+    against the single fused dW kernel (SKGE_RS_NOSPLIT=1) on the same draws:
+    equal violation totals, parameters within the fp32 tolerance (SGD)."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    n_ent, n_rel, T, nb, d = 3000, 3, 6000, 2, 40   # 3000 positives / batch: ~3000 items / relation
+    xs = make_kg(n_ent, n_rel, T, seed=4)
+    out = []
+    for nosplit in ("1", "0"):
+        monkeypatch.setenv("SKGE_RS_NOSPLIT", nosplit)
+        m = make_model("rescal", (n_ent, n_ent, n_rel), d)
+        m.add_hyperparam("margin", 0.5)
+        upd = {pid: S.SGD(p, 0.05) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), nb, seed=5)
+        with torch.cuda.stream(r.stream):
+            r.run(2)
+        r.synchronize()
+        out.append((int(r.nviol_total.item()),
+                    {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}))
+    assert out[0][0] == out[1][0] > 0
+    for pid in out[0][1]:
+        np.testing.assert_allclose(out[1][1][pid], out[0][1][pid], rtol=RTOL, atol=ATOL,
+                                   err_msg=pid)
 
 
 def test_hole_device_loop_auto_selects_pipelined_runner():
