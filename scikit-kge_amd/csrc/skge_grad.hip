@@ -10,6 +10,7 @@
 #include <stdarg.h>
 
 #include "skge_hole.h"
+#include "skge_hole_fft.h"
 #include "skge_host.h"
 
 namespace skge {
@@ -574,7 +575,7 @@ struct HolePosArgs {
   int* total;
 };
 
-template <int KM>
+template <int KM, bool FFT>
 __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int wave = threadIdx.x >> 6, wpb = blockDim.x >> 6, l = lane_id();
@@ -583,7 +584,14 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
     if (a.total) *a.total += *a.fold;
     *a.fold = 0;
   }
-  const HolePosLds L(smem + wave * hole_pos_lds_floats(d), d);
+  // FFT: the workgroup's twiddle table, then per wave two transform buffers
+  float2* const tw = reinterpret_cast<float2*>(smem);
+  if constexpr (FFT) {
+    fft_twiddles(tw, d);
+    __syncthreads();
+  }
+  float* const wb = FFT ? smem + 2 * d + wave * hole_fft_wave_floats(d) : nullptr;
+  const HolePosLds L(FFT ? smem : smem + wave * hole_pos_lds_floats(d), d);
   int nv = 0;
   for (int j = blockIdx.x * wpb + wave; j < a.count; j += gridDim.x * wpb) {
     const int4 r4 = a.rec[a.start + j];
@@ -596,22 +604,31 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
     load_row4<1>(a.R, p, d, rp);
     load_row4<1>(a.E, n0r, d, fs);
     load_row4<1>(a.E, n1r, d, fo);
-    q_lds_dbl(L.R2, rp[0], d);
-    q_lds_dbl(L.O2, eo[0], d);
-    q_lds_dbl(L.Q2, fo[0], d);
-    __builtin_amdgcn_wave_barrier();
-    float4 AB[2];
+    float praw, raw0, raw1;
+    float4 A = {}, B = {};
+    HoleSpec hs;
+    if constexpr (FFT) {
+      hs = hole_fft_forward(wb, tw, d, rp[0], es[0], fs[0], eo[0], fo[0], praw, raw0, raw1);
+    } else {
+      q_lds_dbl(L.R2, rp[0], d);
+      q_lds_dbl(L.O2, eo[0], d);
+      q_lds_dbl(L.Q2, fo[0], d);
+      __builtin_amdgcn_wave_barrier();
+      float4 AB[2];
 #ifndef SKGE_ABL_HPOS_NO_CORR   // timing-only ablation builds (tools/ablate.sh)
-    {
-      const float* const b2[2] = {L.O2, L.Q2};
-      corr_quad_b<2>(L.R2, b2, d, AB);
-    }
+      {
+        const float* const b2[2] = {L.O2, L.Q2};
+        corr_quad_b<2>(L.R2, b2, d, AB);
+      }
 #else
-    AB[0] = AB[1] = eo[0];
+      AB[0] = AB[1] = eo[0];
 #endif
-    const float4 A = AB[0], B = AB[1];
-    const float praw = hole_score_q(es[0], A);
-    const float raw0 = hole_score_q(fs[0], A), raw1 = hole_score_q(es[0], B);
+      A = AB[0];
+      B = AB[1];
+      praw = hole_score_q(es[0], A);
+      raw0 = hole_score_q(fs[0], A);
+      raw1 = hole_score_q(es[0], B);
+    }
     const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
     const int v0 = uni((neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0);   // hole.py:56
     const int v1 = uni((neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0);
@@ -625,18 +642,33 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
     nv += v0 + v1;
     const float gp = -af_g_given_f(a.af, pf);   // hole.py:66
     const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
-    const HoleRows h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gp, g0, g1);
+    HoleRows h;
+    float* stage;
+    if constexpr (FFT) {
+      h = hole_fft_rows(wb, tw, d, hs, v0, v1, gp, g0, g1);
+      stage = wb;
+    } else {
+      h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gp, g0, g1);
+      stage = L.U;
+    }
 #ifndef SKGE_ABL_HPOS_NO_ATOM
-    acc_q<KM>(aR, p, h.cr, d, L.U);
-    acc_q<KM>(a.accE, s, h.cs, d, L.U);
-    acc_q<KM>(a.accE, o, h.co, d, L.U);
-    if (v0) acc_q<KM>(a.accE, neg0, h.c0, d, L.U);
-    if (v1) acc_q<KM>(a.accE, neg1, h.cq, d, L.U);
+    acc_q<KM>(aR, p, h.cr, d, stage);
+    acc_q<KM>(a.accE, s, h.cs, d, stage);
+    acc_q<KM>(a.accE, o, h.co, d, stage);
+    if (v0) acc_q<KM>(a.accE, neg0, h.c0, d, stage);
+    if (v1) acc_q<KM>(a.accE, neg1, h.cq, d, stage);
 #endif
     __builtin_amdgcn_wave_barrier();
   }
   __shared__ int lds_nv;
   block_count_add(a.nviol, nv, &lds_nv);   // one atomic per workgroup
+}
+
+// the frequency-domain form of the per-positive HolE kernels (skge_hole_fft.h)
+// where it applies; SKGE_HOLE_DIRECT=1 selects the direct correlations
+bool hole_use_fft(int d) {
+  const char* e = getenv("SKGE_HOLE_DIRECT");
+  return hole_fft_ok(d) && !(e && atoi(e));
 }
 
 bool hole_pos_ok(int af, const skge_table_t* ent, const skge_table_t* rel, int d) {
@@ -671,13 +703,20 @@ int launch_hole_pos(hipStream_t st, int af, const skge_table_t* ent, const skge_
   a.fold = fold;
   a.total = total;
   const int blocks = std::max(1, std::min((count + 3) / 4, 8192));
-  const size_t lds = (size_t)4 * hole_pos_lds_floats(d) * sizeof(float);
+  const bool fft = hole_use_fft(d);
+  const size_t lds = fft ? hole_fft_lds_bytes(d, 4) : (size_t)4 * hole_pos_lds_floats(d) * sizeof(float);
+#define SKGE_HPOS(K)                                                                   \
+  if (fft)                                                                             \
+    hipLaunchKernelGGL((k_hole_pos<K, true>), dim3(blocks), dim3(256), lds, st, a);    \
+  else                                                                                 \
+    hipLaunchKernelGGL((k_hole_pos<K, false>), dim3(blocks), dim3(256), lds, st, a);
   switch (km_for(d)) {
-    case 1: hipLaunchKernelGGL((k_hole_pos<1>), dim3(blocks), dim3(256), lds, st, a); break;
-    case 2: hipLaunchKernelGGL((k_hole_pos<2>), dim3(blocks), dim3(256), lds, st, a); break;
-    case 3: hipLaunchKernelGGL((k_hole_pos<3>), dim3(blocks), dim3(256), lds, st, a); break;
-    default: hipLaunchKernelGGL((k_hole_pos<4>), dim3(blocks), dim3(256), lds, st, a); break;
+    case 1: SKGE_HPOS(1) break;
+    case 2: SKGE_HPOS(2) break;
+    case 3: SKGE_HPOS(3) break;
+    default: SKGE_HPOS(4) break;
   }
+#undef SKGE_HPOS
   SKGE_CHECK_LAUNCH("hole positive kernel");
   return SKGE_OK;
 }

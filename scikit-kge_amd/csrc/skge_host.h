@@ -119,6 +119,9 @@ int launch_epoch_sample(hipStream_t st, const int* trip, long long T, uint64_t s
 
 // skge_grad.hip: HolE pairwise, one positive (both of its pairs) per wave
 bool hole_pos_ok(int af, const skge_table_t* ent, const skge_table_t* rel, int d);
+// the per-positive HolE kernels run their correlations through the wave FFT
+// (skge_hole_fft.h) for this d (unless SKGE_HOLE_DIRECT=1)
+bool hole_use_fft(int d);
 int launch_hole_pos(hipStream_t st, int af, const skge_table_t* ent, const skge_table_t* rel,
                     int d, const int4* rec, const int* rec_n1, long long start, int count,
                     float margin, int* nviol, int* fold, int* total);

@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "skge_hole.h"
+#include "skge_hole_fft.h"
 #include "skge_host.h"
 #include "skge_sampler.h"
 
@@ -1231,7 +1232,7 @@ __device__ __forceinline__ void rel_publish_f(const PipeArgs& a, int w, int rd, 
 #define SKGE_HPIPE_ATTR
 #endif
 
-template <int KM>
+template <int KM, bool FFT>
 __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(PipeArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6;
@@ -1276,7 +1277,14 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
   }
   // ---- B role: score batch b (k_hole_pos's arithmetic), scatter into cp / ra_cur ----
   const int blk_b = a.b_first ? blk : blk - a.nA;
-  const HolePosLds L(smem + wave * hole_pos_lds_floats(d), d);
+  // FFT: the workgroup's twiddle table, then per wave two transform buffers
+  float2* const tw = reinterpret_cast<float2*>(smem);
+  if constexpr (FFT) {
+    fft_twiddles(tw, d);
+    __syncthreads();
+  }
+  float* const wb = FFT ? smem + 2 * d + wave * hole_fft_wave_floats(d) : nullptr;
+  const HolePosLds L(FFT ? smem : smem + wave * hole_pos_lds_floats(d), d);
   Accum aE;
   aE.sum = reinterpret_cast<float*>(a.E.sum[cp]);
   aE.width = d;
@@ -1324,18 +1332,27 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
       if (pend & 8ull) load_row4_sc1<1>(a.E.P, n1r, d, fo);
     }
     if (a.trace) tt[2] = now_10ns();
-    q_lds_dbl(L.R2, rp[0], d);
-    q_lds_dbl(L.O2, eo[0], d);
-    q_lds_dbl(L.Q2, fo[0], d);
-    __builtin_amdgcn_wave_barrier();
-    float4 AB[2];
-    {
-      const float* const b2[2] = {L.O2, L.Q2};
-      corr_quad_b<2>(L.R2, b2, d, AB);
+    float praw, raw0, raw1;
+    float4 A = {}, B = {};
+    HoleSpec hs;
+    if constexpr (FFT) {
+      hs = hole_fft_forward(wb, tw, d, rp[0], es[0], fs[0], eo[0], fo[0], praw, raw0, raw1);
+    } else {
+      q_lds_dbl(L.R2, rp[0], d);
+      q_lds_dbl(L.O2, eo[0], d);
+      q_lds_dbl(L.Q2, fo[0], d);
+      __builtin_amdgcn_wave_barrier();
+      float4 AB[2];
+      {
+        const float* const b2[2] = {L.O2, L.Q2};
+        corr_quad_b<2>(L.R2, b2, d, AB);
+      }
+      A = AB[0];
+      B = AB[1];
+      praw = hole_score_q(es[0], A);
+      raw0 = hole_score_q(fs[0], A);
+      raw1 = hole_score_q(es[0], B);
     }
-    const float4 A = AB[0], B = AB[1];
-    const float praw = hole_score_q(es[0], A);
-    const float raw0 = hole_score_q(fs[0], A), raw1 = hole_score_q(es[0], B);
     const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
     const int v0 = uni((neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0);   // hole.py:56
     const int v1 = uni((neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0);
@@ -1359,17 +1376,25 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     nv += v0 + v1;
     const float gpf = -af_g_given_f(a.af, pf);   // hole.py:66
     const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
-    const HoleRows h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gpf, g0, g1);
+    HoleRows h;
+    float* stage;
+    if constexpr (FFT) {
+      h = hole_fft_rows(wb, tw, d, hs, v0, v1, gpf, g0, g1);
+      stage = wb;
+    } else {
+      h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gpf, g0, g1);
+      stage = L.U;
+    }
     Accum aR;
     aR.sum = racc + (size_t)p * rstride;
     aR.width = d;
 #ifndef SKGE_HPIPE_ABL_NO_RATOM   // timing-only ablation: relation sums dropped
-    acc_q<KM>(aR, 0, h.cr, d, L.U);
+    acc_q<KM>(aR, 0, h.cr, d, stage);
 #endif
-    acc_q<KM>(aE, s, h.cs, d, L.U);
-    acc_q<KM>(aE, o, h.co, d, L.U);
-    if (v0) acc_q<KM>(aE, neg0, h.c0, d, L.U);
-    if (v1) acc_q<KM>(aE, neg1, h.cq, d, L.U);
+    acc_q<KM>(aE, s, h.cs, d, stage);
+    acc_q<KM>(aE, o, h.co, d, stage);
+    if (v0) acc_q<KM>(aE, neg0, h.c0, d, stage);
+    if (v1) acc_q<KM>(aE, neg1, h.cq, d, stage);
     __builtin_amdgcn_wave_barrier();
     if (a.trace && l == 0) {   // stamp after issue (no drain)
       unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
@@ -1453,6 +1478,7 @@ struct skge_pipe_runner {
   bool w32 = false;                // int32x2 relation sums
   bool lazy = false;               // SKGE_PIPE_LAZY: entity rows applied by their next reader
   bool hole = false;               // HolE pairwise (k_hole_pipe, fp32 sums)
+  bool fft = false;                // HolE: correlations in the frequency domain (skge_hole_fft.h)
   size_t lds = 0;                  // HolE: dynamic LDS per workgroup
   int nlaunch() const { return (int)batch.size() + 2; }
 };
@@ -1512,11 +1538,17 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
   } while (0)
     if (r->hole) {
       const dim3 gr(r->grid[k]), bl(SKGE_PIPE_WG);
+#define SKGE_HPIPE(K)                                                   \
+  if (r->fft)                                                           \
+    hipLaunchKernelGGL((k_hole_pipe<K, true>), gr, bl, r->lds, st, a);  \
+  else                                                                  \
+    hipLaunchKernelGGL((k_hole_pipe<K, false>), gr, bl, r->lds, st, a);
       switch (km_for(a.d)) {
-        case 1: hipLaunchKernelGGL((k_hole_pipe<1>), gr, bl, r->lds, st, a); break;
-        case 2: hipLaunchKernelGGL((k_hole_pipe<2>), gr, bl, r->lds, st, a); break;
-        case 3: hipLaunchKernelGGL((k_hole_pipe<3>), gr, bl, r->lds, st, a); break;
-        default: hipLaunchKernelGGL((k_hole_pipe<4>), gr, bl, r->lds, st, a); break;
+        case 1: SKGE_HPIPE(1) break;
+        case 2: SKGE_HPIPE(2) break;
+        case 3: SKGE_HPIPE(3) break;
+        default: SKGE_HPIPE(4) break;
+#undef SKGE_HPIPE
       }
     } else if (r->kq <= 1) SKGE_PB(1);
     else if (r->kq <= 2) SKGE_PB(2);
@@ -1687,7 +1719,10 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     const char* af_env = getenv("SKGE_HPIPE_AFIRST");   // A/B switch: 0 = scoring WGs first
     a.b_first = hole && af_env && atoi(af_env) == 0 ? 1 : 0;   // default: apply WGs first
   }
-  r->lds = hole ? (size_t)(SKGE_PIPE_WG / 64) * hole_pos_lds_floats(d) * sizeof(float) : 0;
+  r->fft = hole && hole_use_fft(d);
+  r->lds = !hole ? 0
+           : r->fft ? hole_fft_lds_bytes(d, SKGE_PIPE_WG / 64)
+                    : (size_t)(SKGE_PIPE_WG / 64) * hole_pos_lds_floats(d) * sizeof(float);
   int prev = 0;
   for (int b = 0; b <= nb1; ++b) {   // b == nb1: flush of the last batch (A role only)
     a.b = b;

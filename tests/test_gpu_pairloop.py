@@ -81,8 +81,12 @@ def replay(model, upd, kg, n_ent, nbatches, epochs, seed, ntries):
                                           ("hole", 16, True), ("rescal", 8, True),
                                           ("hole", 100, False), ("hole", 200, False),
                                           ("hole", 30, False)])
-def test_pair_loop_matches_host_replay(kind, d, dense):
+def test_pair_loop_matches_host_replay(kind, d, dense, monkeypatch):
     import skge_amd as S
+    # the per-positive HolE kernel with the explicit-pair kernel's direct
+    # correlations (same arithmetic -> same margin decisions); its FFT form is
+    # checked against this one in test_hole_fft_matches_direct
+    monkeypatch.setenv("SKGE_HOLE_DIRECT", "1")
     from skge_amd.device import DeviceKG, PairLoopRunner
     if dense:   # 70% of all triples: many negatives not found in 3 draws -> skipped pairs
         n_ent, n_rel, T, ntries = 12, 2, 200, 3
@@ -195,6 +199,7 @@ def test_hole_positive_kernel_matches_explicit_pairs(d, monkeypatch):
     n_ent, n_rel, T = 300, 7, 2000
     xs = make_kg(n_ent, n_rel, T)
     out = []
+    monkeypatch.setenv("SKGE_HOLE_DIRECT", "1")   # the explicit-pair kernel's arithmetic
     for pairs in ("0", "1"):
         monkeypatch.setenv("SKGE_HOLE_PAIRS", pairs)
         m = make_model("hole", (n_ent, n_ent, n_rel), d)
@@ -251,6 +256,7 @@ def test_per_positive_paths_at_wn18_batch_geometry(kind, env, monkeypatch):
     n_ent, n_rel, T, nb = 40943, 18, 14140, 10
     xs = make_kg(n_ent, n_rel, T, seed=3)
     out = []
+    monkeypatch.setenv("SKGE_HOLE_DIRECT", "1")   # the explicit-pair kernel's arithmetic
     for pairs in ("0", "1"):
         monkeypatch.setenv(env, pairs)
         m = make_model(kind, (n_ent, n_ent, n_rel), 200)
@@ -346,6 +352,46 @@ def test_rescal_split_k_dw_matches_fused(monkeypatch):
     for pid in out[0][1]:
         np.testing.assert_allclose(out[1][1][pid], out[0][1][pid], rtol=RTOL, atol=ATOL,
                                    err_msg=pid)
+
+
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb", [
+    (300, 7, 2000, 32, 7),          # M = 16 = 4 x 4
+    (300, 7, 2000, 24, 7),          # M = 12 = 4 x 3
+    (300, 7, 2000, 40, 7),          # M = 20 = 4 x 5
+    (300, 7, 2000, 60, 7),          # M = 30 = 2 x 3 x 5
+    (300, 7, 2000, 28, 7),          # M = 14 = 2 x 7: no FFT plan, direct sums
+    (40943, 18, 14140, 200, 10),    # WN18 entity count, d = 200 (M = 100 = 4 x 5 x 5)
+])
+def test_hole_fft_matches_direct(n_ent, n_rel, T, d, nb, monkeypatch):
+    """The per-positive HolE kernel with its correlations through the wave FFT
+    (skge_hole_fft.h: Stockham radix 4/2/3/5 over M = d/2, real rows packed as
+    complex, Hermitian sums for the scores) against the direct O(d^2) sums on
+    the same draws.  The scores differ by fp32 rounding only, so the margin
+    decisions agree but for a near-tie or two; parameters within the fp32
+    tolerance (SGD, rparam 0.05) wherever the decisions agree."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    xs = make_kg(n_ent, n_rel, T, seed=6)
+    out = []
+    for direct in ("1", "0"):
+        monkeypatch.setenv("SKGE_HOLE_DIRECT", direct)
+        m = make_model("hole", (n_ent, n_ent, n_rel), d)
+        m.add_hyperparam("margin", 0.2)
+        upd = {pid: S.SGD(p, 0.1) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), nb, seed=9)
+        with torch.cuda.stream(r.stream):
+            r.run(2 if n_ent < 1000 else 1)
+        r.synchronize()
+        out.append((int(r.nviol_total.item()),
+                    {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}))
+    (va, pa), (vb, pb) = out
+    assert va > 0 and abs(va - vb) <= 2, (va, vb)
+    for pid in pa:
+        close = np.abs(pb[pid] - pa[pid]) <= ATOL + RTOL * np.abs(pa[pid])
+        if va == vb:
+            assert close.all(), (pid, float(np.abs(pb[pid] - pa[pid]).max()))
+        else:   # a flipped near-tie moves the rows of that one pair
+            assert close.mean() > 0.999, (pid, close.mean())
 
 
 def test_hole_device_loop_auto_selects_pipelined_runner():
