@@ -1740,12 +1740,16 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     // scoring waves leave (SKGE_HPIPE_OCC waves per SIMD: 2 at ~180 VGPRs; the
     // flush has the chip to itself)
     auto nBwaves = [](long long cnt) { return (cnt + WPB - 1) / WPB * WPB; };
-    int a_cap = hole && b < nb1 ? std::max(1, (SKGE_HPIPE_OCC * 4 * 256 - (int)((batches[b].second + WPB - 1) / WPB) * WPB) / WPB - 8) : 16384;
+    // FFT variant (133 VGPRs, 3 waves per SIMD): the cap of a 4-wave residency,
+    // measured best on WN18 d = 200 (caps 150 / 250 / 400 / 600 / 800 / 1100:
+    // 74.7 / 77.6 / 80.5 / 81.7 / 75.4 / 70.5 M triples/s)
+    const int occ = r->fft ? 4 : SKGE_HPIPE_OCC;
+    int a_cap = hole && b < nb1 ? std::max(1, (occ * 4 * 256 - (int)((batches[b].second + WPB - 1) / WPB) * WPB) / WPB - 8) : 16384;
     // (large batches: more scoring waves than the chip holds -- they run in
     // rounds anyway -- so the apply waves get a fixed share instead of the
     // residency left over, which would be none: nb = 2 on WN18 had 4 apply
     // waves for 283k slot records, 42 ms per epoch)
-    if (hole && b < nb1 && (long long)nBwaves(batches[b].second) > SKGE_HPIPE_OCC * 4 * 256)
+    if (hole && b < nb1 && (long long)nBwaves(batches[b].second) > occ * 4 * 256)
       a_cap = std::max(a_cap, 256);
     if (hole && b < nb1 && getenv("SKGE_HPIPE_ACAP")) a_cap = std::max(1, atoi(getenv("SKGE_HPIPE_ACAP")));
     // TransE, large batches: the A role's waves loop over their slots within ~768
