@@ -642,22 +642,23 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
     nv += v0 + v1;
     const float gp = -af_g_given_f(a.af, pf);   // hole.py:66
     const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
-    HoleRows h;
-    float* stage;
     if constexpr (FFT) {
-      h = hole_fft_rows(wb, tw, d, hs, v0, v1, gp, g0, g1);
-      stage = wb;
+      const float* z = hole_fft_rows(wb, tw, d, hs, v0, v1, gp, g0, g1);
+      acc_fft_row<KM>(aR, p, z, 2, d);
+      acc_fft_row<KM>(a.accE, s, z, 0, d);
+      acc_fft_row<KM>(a.accE, o, z, 1, d);
+      if (v0) acc_fft_row<KM>(a.accE, neg0, z, 3, d);
+      if (v1) acc_fft_row<KM>(a.accE, neg1, z, 3 + v0, d);
     } else {
-      h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gp, g0, g1);
-      stage = L.U;
-    }
+      const HoleRows h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gp, g0, g1);
 #ifndef SKGE_ABL_HPOS_NO_ATOM
-    acc_q<KM>(aR, p, h.cr, d, stage);
-    acc_q<KM>(a.accE, s, h.cs, d, stage);
-    acc_q<KM>(a.accE, o, h.co, d, stage);
-    if (v0) acc_q<KM>(a.accE, neg0, h.c0, d, stage);
-    if (v1) acc_q<KM>(a.accE, neg1, h.cq, d, stage);
+      acc_q<KM>(aR, p, h.cr, d, L.U);
+      acc_q<KM>(a.accE, s, h.cs, d, L.U);
+      acc_q<KM>(a.accE, o, h.co, d, L.U);
+      if (v0) acc_q<KM>(a.accE, neg0, h.c0, d, L.U);
+      if (v1) acc_q<KM>(a.accE, neg1, h.cq, d, L.U);
 #endif
+    }
     __builtin_amdgcn_wave_barrier();
   }
   __shared__ int lds_nv;

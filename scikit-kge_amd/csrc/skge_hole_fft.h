@@ -273,12 +273,14 @@ __device__ __forceinline__ HoleSpec hole_fft_forward(float* wbuf, const float2* 
   return h;
 }
 
-// Inverse phase of a violating positive: the contribution rows (quad layout)
-// of hole_pos_rows, from the spectra.  Rows: cs, co, cr always, c0 when v0, cq
-// when v1 (zero otherwise).
-__device__ __forceinline__ HoleRows hole_fft_rows(float* wbuf, const float2* tw, int d,
-                                                  const HoleSpec& h, int v0, int v1, float gp,
-                                                  float g0, float g1) {
+// Inverse phase of a violating positive: the contribution rows of
+// hole_pos_rows as real rows in LDS -- the inverse transforms' output, whose
+// complex interleave (z_m = x_{2m} + i x_{2m+1}) is the real row in natural
+// order -- times 1/M.  Rows: 0 E[s], 1 E[o], 2 R[p], then E[s'] when v0, then
+// E[o'] when v1.  Returns the buffer (float view, row t at t * d).
+__device__ __forceinline__ const float* hole_fft_rows(float* wbuf, const float2* tw, int d,
+                                                      const HoleSpec& h, int v0, int v1,
+                                                      float gp, float g0, float g1) {
   const int M = d / 2;
   float2* b0 = reinterpret_cast<float2*>(wbuf);
   float2* b1 = b0 + 5 * M;
@@ -306,17 +308,24 @@ __device__ __forceinline__ HoleRows hole_fft_rows(float* wbuf, const float2* tw,
     if (v0) fft_real_inv_pair(b0 + (t++) * M, M, k, tw, H[3][0], H[3][1]);
     if (v1) fft_real_inv_pair(b0 + t * M, M, k, tw, H[4][0], H[4][1]);
   }
-  const float2* z = fft_run<true>(b0, b1, M, nt, tw, d);
-  const float s = 1.0f / (float)M;
-  HoleRows out;
-  out.cs = fft_get_row(z, M, 0, s, d);
-  out.co = fft_get_row(z, M, 1, s, d);
-  out.cr = fft_get_row(z, M, 2, s, d);
-  int t = 3;
-  out.c0 = v0 ? fft_get_row(z, M, t++, s, d) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  out.cq = v1 ? fft_get_row(z, M, t, s, d) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  __builtin_amdgcn_wave_barrier();   // the buffers are the atomics' stage after this
-  return out;
+  return reinterpret_cast<const float*>(fft_run<true>(b0, b1, M, nt, tw, d));
+}
+
+// row t of hole_fft_rows' output, scaled by 1/M, added into accumulator row
+// `row`: lane l takes elements l + 64 k, so each float-atomic instruction
+// covers contiguous bytes (MI355X_MICROARCH.md "Global float atomics")
+template <int KM>
+__device__ __forceinline__ void acc_fft_row(const Accum& acc, int row, const float* z, int t,
+                                            int d) {
+  const float s = 2.0f / (float)d;   // 1/M
+  float x[KM];
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k;
+    x[k] = e < d ? s * z[t * d + e] : 0.0f;
+  }
+  acc_row<KM>(acc, row, x, d);
 }
 
 }  // namespace skge

@@ -1376,25 +1376,26 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     nv += v0 + v1;
     const float gpf = -af_g_given_f(a.af, pf);   // hole.py:66
     const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
-    HoleRows h;
-    float* stage;
-    if constexpr (FFT) {
-      h = hole_fft_rows(wb, tw, d, hs, v0, v1, gpf, g0, g1);
-      stage = wb;
-    } else {
-      h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gpf, g0, g1);
-      stage = L.U;
-    }
     Accum aR;
     aR.sum = racc + (size_t)p * rstride;
     aR.width = d;
+    if constexpr (FFT) {
+      const float* z = hole_fft_rows(wb, tw, d, hs, v0, v1, gpf, g0, g1);
+      acc_fft_row<KM>(aR, 0, z, 2, d);
+      acc_fft_row<KM>(aE, s, z, 0, d);
+      acc_fft_row<KM>(aE, o, z, 1, d);
+      if (v0) acc_fft_row<KM>(aE, neg0, z, 3, d);
+      if (v1) acc_fft_row<KM>(aE, neg1, z, 3 + v0, d);
+    } else {
+      const HoleRows h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gpf, g0, g1);
 #ifndef SKGE_HPIPE_ABL_NO_RATOM   // timing-only ablation: relation sums dropped
-    acc_q<KM>(aR, 0, h.cr, d, stage);
+      acc_q<KM>(aR, 0, h.cr, d, L.U);
 #endif
-    acc_q<KM>(aE, s, h.cs, d, stage);
-    acc_q<KM>(aE, o, h.co, d, stage);
-    if (v0) acc_q<KM>(aE, neg0, h.c0, d, stage);
-    if (v1) acc_q<KM>(aE, neg1, h.cq, d, stage);
+      acc_q<KM>(aE, s, h.cs, d, L.U);
+      acc_q<KM>(aE, o, h.co, d, L.U);
+      if (v0) acc_q<KM>(aE, neg0, h.c0, d, L.U);
+      if (v1) acc_q<KM>(aE, neg1, h.cq, d, L.U);
+    }
     __builtin_amdgcn_wave_barrier();
     if (a.trace && l == 0) {   // stamp after issue (no drain)
       unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
