@@ -9,6 +9,11 @@
 // happens later, in skge_accum_apply / skge_accum_collect.
 #include <stdarg.h>
 
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <vector>
+
 #include "skge_hole.h"
 #include "skge_hole_fft.h"
 #include "skge_host.h"
@@ -573,6 +578,7 @@ struct HolePosArgs {
   int* nviol;        // this batch's gate word: += violating pairs
   int* fold;         // the previous batch's gate word: added to *total, then cleared
   int* total;
+  const float2* tw;  // FFT form: the twiddle table (hole_fft_table)
 };
 
 template <int KM, bool FFT>
@@ -587,7 +593,7 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
   // FFT: the workgroup's twiddle table, then per wave two transform buffers
   float2* const tw = reinterpret_cast<float2*>(smem);
   if constexpr (FFT) {
-    fft_twiddles(tw, d);
+    fft_twiddles(tw, a.tw, d);
     __syncthreads();
   }
   float* const wb = FFT ? smem + 2 * d + wave * hole_fft_wave_floats(d) : nullptr;
@@ -665,6 +671,27 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
   block_count_add(a.nviol, nv, &lds_nv);   // one atomic per workgroup
 }
 
+const float2* hole_fft_table(int d) {
+  static std::mutex mu;
+  static std::map<int, float2*> tabs;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = tabs.find(d);
+  if (it != tabs.end()) return it->second;
+  std::vector<float2> h(d);
+  for (int t = 0; t < d; ++t) {
+    const double a = -2.0 * M_PI * (double)t / (double)d;
+    h[t] = make_float2((float)std::cos(a), (float)std::sin(a));
+  }
+  float2* p = nullptr;
+  if (hipMalloc(&p, d * sizeof(float2)) != hipSuccess ||
+      hipMemcpy(p, h.data(), d * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  tabs[d] = p;
+  return p;
+}
+
 // the frequency-domain form of the per-positive HolE kernels (skge_hole_fft.h)
 // where it applies; SKGE_HOLE_DIRECT=1 selects the direct correlations
 bool hole_use_fft(int d) {
@@ -705,6 +732,10 @@ int launch_hole_pos(hipStream_t st, int af, const skge_table_t* ent, const skge_
   a.total = total;
   const int blocks = std::max(1, std::min((count + 3) / 4, 8192));
   const bool fft = hole_use_fft(d);
+  if (fft) {
+    a.tw = hole_fft_table(d);
+    SKGE_CHECK_ARG(a.tw != nullptr, "HolE FFT twiddle table allocation failed");
+  }
   const size_t lds = fft ? hole_fft_lds_bytes(d, 4) : (size_t)4 * hole_pos_lds_floats(d) * sizeof(float);
 #define SKGE_HPOS(K)                                                                   \
   if (fft)                                                                             \

@@ -21,8 +21,9 @@
 // become 3-5 inverse transforms.  Per positive: 5 forward + 3-5 inverse
 // transforms of length M (~(4+5+5) M complex multiply-adds each at d = 200)
 // instead of 2-6 direct correlations of d^2 multiply-adds.
-// Twiddles W^t = exp(-2 pi i t / d), t < d, are computed once per workgroup
-// in double precision into LDS; every twiddle of every stage is a power of W.
+// Twiddles W^t = exp(-2 pi i t / d), t < d, come from a table computed on the
+// host in double precision, copied into each wave's LDS; every twiddle of
+// every stage is a power of W.
 #pragma once
 #include "skge_hole.h"
 
@@ -39,10 +40,14 @@ __host__ __device__ __forceinline__ bool hole_fft_ok(int d) {
 }
 // wave-private floats: two ping-pong buffers of 5 complex rows of length M
 __host__ __device__ __forceinline__ int hole_fft_wave_floats(int d) { return 10 * d; }
-// workgroup LDS: the twiddle table, then the waves' regions
+// workgroup LDS: the twiddle table (d complex), then the waves' regions
 __host__ __device__ __forceinline__ size_t hole_fft_lds_bytes(int d, int waves) {
   return (size_t)(2 * d + waves * hole_fft_wave_floats(d)) * sizeof(float);
 }
+// the device twiddle table W^t = exp(-2 pi i t / d), t < d, computed on the
+// host in double precision; allocated once per d (call outside stream capture:
+// the runners call it at creation)
+const float2* hole_fft_table(int d);
 
 __device__ __forceinline__ float2 cmul(const float2& a, const float2& b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
@@ -61,13 +66,9 @@ __device__ __forceinline__ float2 cscale(float s, const float2& a) {
 }
 __device__ __forceinline__ float2 cconj(const float2& a) { return make_float2(a.x, -a.y); }
 
-// the workgroup's twiddle table (call by every thread, then a barrier)
-__device__ __forceinline__ void fft_twiddles(float2* tw, int d) {
-  for (int t = threadIdx.x; t < d; t += blockDim.x) {
-    double s, c;
-    sincospi(-2.0 * t / d, &s, &c);
-    tw[t] = make_float2((float)c, (float)s);
-  }
+// the workgroup's copy of the twiddle table (every thread, then a barrier)
+__device__ __forceinline__ void fft_twiddles(float2* tw, const float2* __restrict__ g, int d) {
+  for (int t = threadIdx.x; t < d; t += blockDim.x) tw[t] = g[t];
 }
 
 // DFT of R points, forward (exp(-2 pi i qt / R)) or inverse (conjugate):

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "skge_host.h"
+#include "skge_hole_fft.h"
 #include "skge_sampler.h"
 
 namespace skge {
@@ -178,6 +179,10 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
   int* pos = r->pairs;
   int* neg = r->pairs ? r->pairs + (size_t)T * 6 : nullptr;
   const TripleSet ts = triple_set_view(set, set_capacity);
+  if (hpos && hole_use_fft(d) && !hole_fft_table(d)) {   // allocated before the capture
+    pair_runner_free(r);
+    return fail("%s", "pair runner: HolE FFT twiddle table allocation failed");
+  }
   if (hipStreamSynchronize(st) != hipSuccess ||
       hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
     pair_runner_free(r);

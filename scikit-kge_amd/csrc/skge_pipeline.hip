@@ -103,6 +103,7 @@ struct PipeArgs {
   int* nviol_shards;           // [NSHARD][SHARD_STRIDE]: this epoch's violations so far
   int* stats_viol;             // profile only: violating pairs of this launch (sharded)
   unsigned long long* trace;   // diagnostics only: per-wave timestamps of one launch
+  const float2* tw;            // HolE FFT form: the twiddle table (hole_fft_table)
   int* err;                    // set when a bounded wait gives up
 };
 
@@ -1280,7 +1281,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
   // FFT: the workgroup's twiddle table, then per wave two transform buffers
   float2* const tw = reinterpret_cast<float2*>(smem);
   if constexpr (FFT) {
-    fft_twiddles(tw, d);
+    fft_twiddles(tw, a.tw, d);
     __syncthreads();
   }
   float* const wb = FFT ? smem + 2 * d + wave * hole_fft_wave_floats(d) : nullptr;
@@ -1721,6 +1722,12 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     a.b_first = hole && af_env && atoi(af_env) == 0 ? 1 : 0;   // default: apply WGs first
   }
   r->fft = hole && hole_use_fft(d);
+  a.tw = r->fft ? hole_fft_table(d) : nullptr;
+  if (r->fft && !a.tw) {
+    set_error("pipelined runner: HolE FFT twiddle table allocation failed");
+    pipe_free(r);
+    return nullptr;
+  }
   r->lds = !hole ? 0
            : r->fft ? hole_fft_lds_bytes(d, SKGE_PIPE_WG / 64)
                     : (size_t)(SKGE_PIPE_WG / 64) * hole_pos_lds_floats(d) * sizeof(float);
