@@ -894,22 +894,17 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
     }
   }
   const int nch = (cnt + WG_CH - 1) / WG_CH;
-  // the item ids of a group (clamped in-range addresses); the next group's
-  // are loaded while this group's rows are in flight
-  int ns[WG_PF], no[WG_PF];
-  float nc[WG_PF];
-  auto load_ids = [&](int g0, int (&s_)[WG_PF], int (&o_)[WG_PF], float (&c_)[WG_PF]) {
+  for (int g0 = 0; g0 < nch; g0 += WG_PF) {
+    int ns[WG_PF], no[WG_PF];
+    float nc[WG_PF];
 #pragma unroll
-    for (int q = 0; q < WG_PF; ++q) {
+    for (int q = 0; q < WG_PF; ++q) {   // the group's item ids (clamped in-range addresses)
       const int i = (g0 + q) * WG_CH + it;
       const int at = off + (i < cnt ? i : cnt - 1);
-      s_[q] = ws.sorted_s[at];
-      o_[q] = ws.sorted_o[at];
-      c_[q] = i < cnt ? ws.coef[at] : 0.0f;
+      ns[q] = ws.sorted_s[at];
+      no[q] = ws.sorted_o[at];
+      nc[q] = i < cnt ? ws.coef[at] : 0.0f;
     }
-  };
-  load_ids(0, ns, no, nc);
-  for (int g0 = 0; g0 < nch; g0 += WG_PF) {
     float4 es[WG_PF][WG_FPT / 4], eo[WG_PF][WG_FPT / 4];
 #pragma unroll
     for (int q = 0; q < WG_PF; ++q) {   // the group's row segments
@@ -929,9 +924,6 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
         }
       }
     }
-    int ns2[WG_PF], no2[WG_PF];
-    float nc2[WG_PF];
-    if (g0 + WG_PF < nch) load_ids(g0 + WG_PF, ns2, no2, nc2);
 #pragma unroll
     for (int q = 0; q < WG_PF; ++q) {
       const int b = g0 + q;
@@ -967,12 +959,6 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
           acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av_, sEo[buf][ik][16 * j + (l & 15)],
                                                         acc[j], 0, 0, 0);
       }
-    }
-#pragma unroll
-    for (int q = 0; q < WG_PF; ++q) {
-      ns[q] = ns2[q];
-      no[q] = no2[q];
-      nc[q] = nc2[q];
     }
   }
   // D[row 4g + reg][col] of accumulator j (os / in above: out-of-range
