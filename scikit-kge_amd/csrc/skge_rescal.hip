@@ -38,10 +38,6 @@ constexpr int GC = 64;          // output columns per GEMM tile
 #define SKGE_RS_KS 32
 #endif
 constexpr int KS = SKGE_RS_KS;  // k per staged step
-#ifndef SKGE_RS_GEMM_PF
-#define SKGE_RS_GEMM_PF 3       // k-steps of loads in flight in k_rescal_gemm (round 1: 2)
-#endif
-constexpr int GEMM_PF = SKGE_RS_GEMM_PF;
 constexpr int RS_MAX_D = 1024;  // d of the MFMA path
 constexpr int RS_MAX_M = 8192;  // relations (k_rs_scan keeps 2M+1 ints in LDS)
 
@@ -497,13 +493,10 @@ __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E
   // k + bq, columns c0 + bk.. (256 / KS threads share a row of 64 columns)
   const int bq = prod == 0 ? tid >> 2 : tid / (256 / KS);
   const int bk = prod == 0 ? (tid & 3) * SPT : (tid % (256 / KS)) * SPT;
-  // a ring of GEMM_PF k-steps of raw loads in flight (GEMM_PF - 1 ahead of
-  // the step being staged); the k loop is unrolled by GEMM_PF so every ring
-  // index is static
-  float ra_[GEMM_PF][SPT], rb_[GEMM_PF][SPT];
+  float ra[SPT], rb[SPT];
   // raw loads from clamped in-range addresses; masks are applied when the
   // values are staged (a select right after a load would wait for it)
-  auto load_step = [&](float (&ra)[SPT], float (&rb)[SPT], int ks) {
+  auto load_step = [&](int ks) {
     const int k = ks * KS;
     const float* brow;
     int boff;
@@ -532,7 +525,7 @@ __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E
       }
     }
   };
-  auto store_step = [&](const float (&ra)[SPT], const float (&rb)[SPT], int buf, int ks) {
+  auto store_step = [&](int buf, int ks) {
     const int k = ks * KS;
 #pragma unroll
     for (int m = 0; m < SPT / 4; ++m) {
@@ -564,27 +557,19 @@ __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
   const int row = wave * 16 + (l & 15), kq = l >> 4;
+  load_step(0);
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    store_step(buf, ks);
+    __syncthreads();   // (also: every wave is done with buf's previous use, step ks - 2)
+    if (ks + 1 < nk) load_step(ks + 1);   // in flight during this step's MFMAs
 #pragma unroll
-  for (int u = 0; u < GEMM_PF - 1; ++u)
-    if (u < nk) load_step(ra_[u], rb_[u], u);
-  for (int k0 = 0; k0 < nk; k0 += GEMM_PF) {
+    for (int k4 = 0; k4 < KS; k4 += 4) {
+      const float a = sA[buf][row][k4 + kq];
 #pragma unroll
-    for (int u = 0; u < GEMM_PF; ++u) {
-      const int ks = k0 + u;
-      if (ks >= nk) break;
-      const int buf = ks & 1;
-      store_step(ra_[u], rb_[u], buf, ks);
-      __syncthreads();   // (also: every wave is done with buf's previous use, step ks - 2)
-      const int un = (u + GEMM_PF - 1) % GEMM_PF;   // ring slot of step ks + GEMM_PF - 1
-      if (ks + GEMM_PF - 1 < nk) load_step(ra_[un], rb_[un], ks + GEMM_PF - 1);   // in flight
-#pragma unroll
-      for (int k4 = 0; k4 < KS; k4 += 4) {
-        const float a = sA[buf][row][k4 + kq];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, sB[buf][k4 + kq][q * 16 + (l & 15)],
-                                                        acc[q], 0, 0, 0);
-      }
+      for (int q = 0; q < 4; ++q)
+        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, sB[buf][k4 + kq][q * 16 + (l & 15)],
+                                                      acc[q], 0, 0, 0);
     }
   }
   // epilogue: D[row 4g + reg][col] of accumulator q -> triple 16w + 4g + reg, column c0 + 16q + c
