@@ -45,6 +45,7 @@ struct PairArgs {
   float* loss;
   int record;  // 0: score only (no contribution scatter, no slot writes)
   int* eviol;  // optional per-entity violation counter (TransE pairs)
+  const float2* tw;   // HolE FFT form: the twiddle table (hole_fft_table)
 };
 
 
@@ -544,6 +545,113 @@ __global__ __launch_bounds__(256) void k_hole_pair_fast(PairArgs a) {
   if (a.nviol) block_count_add(a.nviol, nv, &lds_nv);   // one atomic per workgroup
 }
 
+// HolE pair in the frequency domain (skge_hole_fft.h): the six rows E[sp],
+// E[op], R[pp], E[sn], E[on], R[pn] are transformed together; the scores are
+// Hermitian sums (1/d) sum_k conj(E^s_k R^_k) E^o_k, and a violating pair's six
+// contribution rows of hole.py:76-96 -- relation gp conj(E^s) E^o, subject
+// gp conj(R^) E^o, object gp E^s R^ (and the negative's with gn) -- come from
+// six inverse transforms.  LDS per wave: hole_pair_fft_wave_floats(d).
+__host__ __device__ __forceinline__ int hole_pair_fft_wave_floats(int d) { return 12 * d; }
+
+template <int KM>
+__device__ __forceinline__ bool hole_pair_fft(const PairArgs& a, int i, float* wb,
+                                              const float2* tw, const int (&ix)[6]) {
+  const int d = a.d, M = d / 2, l = lane_id();
+  const int sp = ix[0], op = ix[1], pp = ix[2], sn = ix[3], on = ix[4], pn = ix[5];
+  float4 es[1], eo[1], rp[1], fs[1], fo[1], rn[1];
+  load_row4<1>(a.E, sp, d, es);
+  load_row4<1>(a.E, op, d, eo);
+  load_row4<1>(a.R, pp, d, rp);
+  load_row4<1>(a.E, sn, d, fs);
+  load_row4<1>(a.E, on, d, fo);
+  load_row4<1>(a.R, pn, d, rn);
+  float2* b0 = reinterpret_cast<float2*>(wb);
+  float2* b1 = b0 + 6 * M;
+  __builtin_amdgcn_wave_barrier();   // the previous pair's reads of the buffers are done
+  fft_put_row(b0, M, 0, rp[0], d);
+  fft_put_row(b0, M, 1, es[0], d);
+  fft_put_row(b0, M, 2, eo[0], d);
+  fft_put_row(b0, M, 3, rn[0], d);
+  fft_put_row(b0, M, 4, fs[0], d);
+  fft_put_row(b0, M, 5, fo[0], d);
+  const float2* Z = fft_run<false>(b0, b1, M, 6, tw, d);
+  const int k = l;
+  const bool on_ = k <= M / 2;
+  float2 X[6][2];
+  float ps = 0.0f, ns = 0.0f;
+  if (on_) {
+#pragma unroll
+    for (int t = 0; t < 6; ++t) fft_real_pair(Z + t * M, M, k, tw, X[t][0], X[t][1]);
+    const float wk = k == 0 ? 1.0f : 2.0f, wm = k == 0 ? 1.0f : (M - k == k ? 0.0f : 2.0f);
+    ps = wk * fft_score_term(X[1][0], X[0][0], X[2][0]) + wm * fft_score_term(X[1][1], X[0][1], X[2][1]);
+    ns = wk * fft_score_term(X[4][0], X[3][0], X[5][0]) + wm * fft_score_term(X[4][1], X[3][1], X[5][1]);
+  }
+  const float inv_d = 1.0f / (float)d;
+  const float praw = wave_sum(ps) * inv_d, nraw = wave_sum(ns) * inv_d;
+  if (l == 0) {
+    if (a.pscore) a.pscore[i] = praw;
+    if (a.nscore) a.nscore[i] = nraw;
+  }
+  const float pf = af_f(a.af, praw), nf = af_f(a.af, nraw);
+  if (!(nf + a.margin > pf)) return false;   // hole.py:56
+  const float gp = -af_g_given_f(a.af, pf);   // hole.py:66
+  const float gn = af_g_given_f(a.af, nf);    // hole.py:67
+  __builtin_amdgcn_wave_barrier();   // every lane is done reading the forward buffers
+  if (on_) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float2 r = X[0][j], e_s = X[1][j], e_o = X[2][j], q = X[3][j], f_s = X[4][j], f_o = X[5][j];
+      X[0][j] = cscale(gp, cmulc(e_s, e_o));   // R[pp]: gp ccorr(E[sp], E[op])  hole.py:76-82
+      X[1][j] = cscale(gn, cmulc(f_s, f_o));   // R[pn]
+      X[2][j] = cscale(gp, cmulc(r, e_o));     // E[sp]: gp ccorr(R[pp], E[op])  hole.py:93-94
+      X[3][j] = cscale(gn, cmulc(q, f_o));     // E[sn]
+      X[4][j] = cscale(gp, cmul(e_s, r));      // E[op]: gp cconv(E[sp], R[pp]) hole.py:95-96
+      X[5][j] = cscale(gn, cmul(f_s, q));      // E[on]
+    }
+#pragma unroll
+    for (int t = 0; t < 6; ++t) fft_real_inv_pair(b0 + t * M, M, k, tw, X[t][0], X[t][1]);
+  }
+  const float* z = reinterpret_cast<const float*>(fft_run<true>(b0, b1, M, 6, tw, d));
+  const float sc = 2.0f / (float)d;   // 1/M
+  float x[KM], y[KM];
+  auto rows = [&](int t0) {
+#pragma unroll
+    for (int kk = 0; kk < KM; ++kk) {
+      const int e = l + 64 * kk;
+      x[kk] = e < d ? sc * z[t0 * d + e] : 0.0f;
+      y[kk] = e < d ? sc * z[(t0 + 1) * d + e] : 0.0f;
+    }
+  };
+  rows(0);
+  acc_two<KM>(replica(a.accR, i), pp, x, pn, y, d);
+  rows(2);
+  acc_two<KM>(a.accE, sp, x, sn, y, d);
+  rows(4);
+  acc_two<KM>(a.accE, op, x, on, y, d);
+  return true;
+}
+
+template <int KM>
+__global__ __launch_bounds__(256) void k_hole_pair_fft(PairArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wave = threadIdx.x >> 6, wpb = blockDim.x >> 6, d = a.d;
+  float2* const tw = reinterpret_cast<float2*>(smem);
+  fft_twiddles(tw, a.tw, d);
+  __syncthreads();
+  float* const wb = smem + 2 * d + wave * hole_pair_fft_wave_floats(d);
+  int nv = 0;
+  for (int i = blockIdx.x * wpb + wave; i < a.P; i += gridDim.x * wpb) {
+    const int ix[6] = {uni(a.pos[3 * i]), uni(a.pos[3 * i + 1]), uni(a.pos[3 * i + 2]),
+                       uni(a.neg[3 * i]), uni(a.neg[3 * i + 1]), uni(a.neg[3 * i + 2])};
+    const bool v = ix[2] >= 0 && hole_pair_fft<KM>(a, i, wb, tw, ix);   // p < 0: skipped pair
+    const Accum aR = replica(a.accR, i);
+    if (a.record) commit_pair(a.accE, &aR, v, ix, i);
+    nv += v ? 1 : 0;
+  }
+  __shared__ int lds_nv;
+  if (a.nviol) block_count_add(a.nviol, nv, &lds_nv);   // one atomic per workgroup
+}
+
 // ---------------------------------------------------------------------------
 // HolE pairwise, one positive and BOTH of its pairs per wave (device pair
 // loop).  Record j = (s, o, p, s'), o' gives pair 2j = ((s,o,p), (s',o,p)) and
@@ -965,6 +1073,20 @@ static int launch_pair(const PairArgs& a, int km, hipStream_t st, bool logistic_
   size_t lds = (MODEL == TRANSE_L1 || MODEL == TRANSE_L2) ? 0 : (size_t)4 * 6 * 64 * km * 4;
   const bool hfast = MODEL == HOLE && km <= 4 && (a.d & 3) == 0 && a.d >= 4 && a.d <= 256;
   if (hfast) lds = std::max(lds, (size_t)4 * hole_fast_lds_floats(a.d) * 4);
+  if (hfast && !logistic_mode && hole_use_fft(a.d) && a.record) {
+    PairArgs af = a;
+    af.tw = hole_fft_table(a.d);
+    SKGE_CHECK_ARG(af.tw != nullptr, "HolE FFT twiddle table allocation failed");
+    const size_t flds = (size_t)(2 * a.d + 4 * hole_pair_fft_wave_floats(a.d)) * sizeof(float);
+    switch (km) {
+      case 1: hipLaunchKernelGGL((k_hole_pair_fft<1>), dim3(blocks), dim3(threads), flds, st, af); break;
+      case 2: hipLaunchKernelGGL((k_hole_pair_fft<2>), dim3(blocks), dim3(threads), flds, st, af); break;
+      case 3: hipLaunchKernelGGL((k_hole_pair_fft<3>), dim3(blocks), dim3(threads), flds, st, af); break;
+      default: hipLaunchKernelGGL((k_hole_pair_fft<4>), dim3(blocks), dim3(threads), flds, st, af); break;
+    }
+    SKGE_CHECK_LAUNCH("hole fft pair launch");
+    return SKGE_OK;
+  }
   if (hfast && !logistic_mode) {
     switch (km) {
       case 1: hipLaunchKernelGGL((k_hole_pair_fast<1>), dim3(blocks), dim3(threads), lds, st, a); break;

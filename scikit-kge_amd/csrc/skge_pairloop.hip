@@ -179,7 +179,7 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
   int* pos = r->pairs;
   int* neg = r->pairs ? r->pairs + (size_t)T * 6 : nullptr;
   const TripleSet ts = triple_set_view(set, set_capacity);
-  if (hpos && hole_use_fft(d) && !hole_fft_table(d)) {   // allocated before the capture
+  if (model == SKGE_HOLE && hole_use_fft(d) && !hole_fft_table(d)) {   // before the capture
     pair_runner_free(r);
     return fail("%s", "pair runner: HolE FFT twiddle table allocation failed");
   }

@@ -394,6 +394,38 @@ def test_hole_fft_matches_direct(n_ent, n_rel, T, d, nb, monkeypatch):
             assert close.mean() > 0.999, (pid, close.mean())
 
 
+@pytest.mark.parametrize("d", [32, 200])
+def test_hole_explicit_pair_fft_matches_direct(d, monkeypatch):
+    """The explicit-pair HolE kernel (the reference-protocol / per-batch path)
+    in the frequency domain against its direct sums, through the pair loop's
+    explicit-pair form (SKGE_HOLE_PAIRS=1) on the same draws."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    n_ent, n_rel, T = 300, 7, 2000
+    xs = make_kg(n_ent, n_rel, T, seed=8)
+    monkeypatch.setenv("SKGE_HOLE_PAIRS", "1")
+    out = []
+    for direct in ("1", "0"):
+        monkeypatch.setenv("SKGE_HOLE_DIRECT", direct)
+        m = make_model("hole", (n_ent, n_ent, n_rel), d)
+        m.add_hyperparam("margin", 0.2)
+        upd = {pid: S.SGD(p, 0.1) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), 7, seed=2)
+        with torch.cuda.stream(r.stream):
+            r.run(2)
+        r.synchronize()
+        out.append((int(r.nviol_total.item()),
+                    {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}))
+    (va, pa), (vb, pb) = out
+    assert va > 0 and abs(va - vb) <= 2, (va, vb)
+    for pid in pa:
+        close = np.abs(pb[pid] - pa[pid]) <= ATOL + RTOL * np.abs(pa[pid])
+        if va == vb:
+            assert close.all(), (pid, float(np.abs(pb[pid] - pa[pid]).max()))
+        else:
+            assert close.mean() > 0.999, (pid, close.mean())
+
+
 def test_hole_device_loop_auto_selects_pipelined_runner():
     import skge_amd as S
     from skge_amd.device import HolePipeRunner
