@@ -188,9 +188,6 @@ __device__ __forceinline__ void apply_row(const TableDev& t, int row, bool upd) 
 // state in the same memory round trip; i16_finish applies the update if the
 // claim was won.  Rows in the quad layout (see load_row4): one 16-byte load /
 // store per lane per 1 KB of row.
-#ifndef SKGE_APPLY_NT
-#define SKGE_APPLY_NT 0
-#endif
 template <int KQ>
 __device__ __forceinline__ void i16_load(const TableDev& t, int row, int& c,
                                          unsigned long long (&sv)[KQ], float4 (&p)[KQ],
@@ -271,23 +268,11 @@ __device__ __forceinline__ void i16_finish(const TableDev& t, int row, bool upd,
   for (int m = 0; m < KQ; ++m) {
     const int q = 64 * m + l;
     if (q < nq) {
-#if SKGE_APPLY_NT   // A/B switch: nontemporal stores (rows not re-read soon at |E| = 50M)
-      typedef float nt4 __attribute__((ext_vector_type(4)));
-      __builtin_nontemporal_store(0ull, srow + q);
-      if (upd) {
-        __builtin_nontemporal_store(*reinterpret_cast<const nt4*>(&p[m]),
-                                    reinterpret_cast<nt4*>(prow + q));
-        if (ada)
-          __builtin_nontemporal_store(*reinterpret_cast<const nt4*>(&a[m]),
-                                      reinterpret_cast<nt4*>(arow + q));
-      }
-#else
       srow[q] = 0ull;
       if (upd) {
         prow[q] = p[m];
         if (ada) arow[q] = a[m];
       }
-#endif
     }
   }
 }
