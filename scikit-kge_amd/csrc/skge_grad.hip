@@ -971,6 +971,83 @@ __global__ __launch_bounds__(256) void k_triple_grad(PairArgs a) {
   if (a.loss) block_sum_add(a.loss, lsum, &lds_loss);   // one atomic per workgroup
 }
 
+// HolE logistic triples in the frequency domain (skge/hole.py:22-42): the
+// rows R[p], E[s], E[o] transformed together; score (1/d) sum_k conj(E^s_k
+// R^_k) E^o_k; fs from the logistic loss; the rows R[p] fs conj(E^s) E^o,
+// E[s] fs conj(R^) E^o, E[o] fs E^s R^ from three inverse transforms.
+// LDS per wave: 6d floats (two buffers of three length-d/2 complex rows).
+template <int KM>
+__global__ __launch_bounds__(256) void k_hole_triple_fft(PairArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wave = threadIdx.x >> 6, wpb = blockDim.x >> 6, d = a.d, M = d / 2, l = lane_id();
+  float2* const tw = reinterpret_cast<float2*>(smem);
+  fft_twiddles(tw, a.tw, d);
+  __syncthreads();
+  float2* const b0 = reinterpret_cast<float2*>(smem + 2 * d + wave * 6 * d);
+  float2* const b1 = b0 + 3 * M;
+  float lsum = 0.0f;
+  for (int i = blockIdx.x * wpb + wave; i < a.P; i += gridDim.x * wpb) {
+    const int s = uni(a.pos[3 * i]), o = uni(a.pos[3 * i + 1]), p = uni(a.pos[3 * i + 2]);
+    const float y = a.ys[i];
+    float4 es[1], eo[1], rp[1];
+    load_row4<1>(a.E, s, d, es);
+    load_row4<1>(a.E, o, d, eo);
+    load_row4<1>(a.R, p, d, rp);
+    __builtin_amdgcn_wave_barrier();   // the previous triple's reads of the buffers are done
+    fft_put_row(b0, M, 0, rp[0], d);
+    fft_put_row(b0, M, 1, es[0], d);
+    fft_put_row(b0, M, 2, eo[0], d);
+    const float2* Z = fft_run<false>(b0, b1, M, 3, tw, d);
+    const int k = l;
+    const bool on = k <= M / 2;
+    float2 X[3][2];
+    float ps = 0.0f;
+    if (on) {
+#pragma unroll
+      for (int t = 0; t < 3; ++t) fft_real_pair(Z + t * M, M, k, tw, X[t][0], X[t][1]);
+      const float wk = k == 0 ? 1.0f : 2.0f, wm = k == 0 ? 1.0f : (M - k == k ? 0.0f : 2.0f);
+      ps = wk * fft_score_term(X[1][0], X[0][0], X[2][0]) + wm * fft_score_term(X[1][1], X[0][1], X[2][1]);
+    }
+    const float score = wave_sum(ps) * (1.0f / (float)d);   // hole.py:20
+    float li, fs;
+    logistic(y, score, &li, &fs);
+    __builtin_amdgcn_wave_barrier();   // every lane is done reading the forward buffers
+    if (on) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float2 r = X[0][j], e_s = X[1][j], e_o = X[2][j];
+        X[0][j] = cscale(fs, cmulc(e_s, e_o));   // R[p]: fs ccorr(E[s], E[o])   hole.py:32
+        X[1][j] = cscale(fs, cmulc(r, e_o));     // E[s]: fs ccorr(R[p], E[o])   hole.py:37
+        X[2][j] = cscale(fs, cmul(e_s, r));      // E[o]: fs cconv(E[s], R[p])   hole.py:38
+      }
+#pragma unroll
+      for (int t = 0; t < 3; ++t) fft_real_inv_pair(b0 + t * M, M, k, tw, X[t][0], X[t][1]);
+    }
+    const float* z = reinterpret_cast<const float*>(fft_run<true>(b0, b1, M, 3, tw, d));
+    const float sc = 2.0f / (float)d;   // 1/M
+    float x[KM], yv[KM];
+#pragma unroll
+    for (int kk = 0; kk < KM; ++kk) {
+      const int e = l + 64 * kk;
+      x[kk] = e < d ? sc * z[e] : 0.0f;
+    }
+    acc_row<KM>(replica(a.accR, i), p, x, d);
+    if (l == 2) commit_slot(replica(a.accR, i), p, 1, i);
+#pragma unroll
+    for (int kk = 0; kk < KM; ++kk) {
+      const int e = l + 64 * kk;
+      x[kk] = e < d ? sc * z[d + e] : 0.0f;
+      yv[kk] = e < d ? sc * z[2 * d + e] : 0.0f;
+    }
+    acc_two<KM>(a.accE, s, x, o, yv, d);
+    if (l < 2) commit_slot(a.accE, l == 0 ? s : o, s == o ? (l == 0 ? 2 : 0) : 1, 2 * i + l);
+    if (l == 0 && a.pscore) a.pscore[i] = score;
+    lsum += li;
+  }
+  __shared__ float lds_loss;
+  if (a.loss) block_sum_add(a.loss, lsum, &lds_loss);   // one atomic per workgroup
+}
+
 // ---------------------------------------------------------------------------
 // RESCAL dW: acc[p] = sum_i coef_i outer(E[s_i], E[o_i]) over the items with
 // relation p (skge/rescal.py:61-70, 113-125).  One 256-thread workgroup owns
@@ -1073,6 +1150,20 @@ static int launch_pair(const PairArgs& a, int km, hipStream_t st, bool logistic_
   size_t lds = (MODEL == TRANSE_L1 || MODEL == TRANSE_L2) ? 0 : (size_t)4 * 6 * 64 * km * 4;
   const bool hfast = MODEL == HOLE && km <= 4 && (a.d & 3) == 0 && a.d >= 4 && a.d <= 256;
   if (hfast) lds = std::max(lds, (size_t)4 * hole_fast_lds_floats(a.d) * 4);
+  if (hfast && logistic_mode && hole_use_fft(a.d)) {
+    PairArgs af = a;
+    af.tw = hole_fft_table(a.d);
+    SKGE_CHECK_ARG(af.tw != nullptr, "HolE FFT twiddle table allocation failed");
+    const size_t flds = (size_t)(2 * a.d + 4 * 6 * a.d) * sizeof(float);
+    switch (km) {
+      case 1: hipLaunchKernelGGL((k_hole_triple_fft<1>), dim3(blocks), dim3(threads), flds, st, af); break;
+      case 2: hipLaunchKernelGGL((k_hole_triple_fft<2>), dim3(blocks), dim3(threads), flds, st, af); break;
+      case 3: hipLaunchKernelGGL((k_hole_triple_fft<3>), dim3(blocks), dim3(threads), flds, st, af); break;
+      default: hipLaunchKernelGGL((k_hole_triple_fft<4>), dim3(blocks), dim3(threads), flds, st, af); break;
+    }
+    SKGE_CHECK_LAUNCH("hole fft triple launch");
+    return SKGE_OK;
+  }
   if (hfast && !logistic_mode && hole_use_fft(a.d) && a.record) {
     PairArgs af = a;
     af.tw = hole_fft_table(a.d);
