@@ -781,9 +781,11 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
 
 const float2* hole_fft_table(int d) {
   static std::mutex mu;
-  static std::map<int, float2*> tabs;
+  static std::map<std::pair<int, int>, float2*> tabs;   // (device, d)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> lock(mu);
-  auto it = tabs.find(d);
+  auto it = tabs.find({dev, d});
   if (it != tabs.end()) return it->second;
   std::vector<float2> h(d);
   for (int t = 0; t < d; ++t) {
@@ -796,7 +798,7 @@ const float2* hole_fft_table(int d) {
     (void)hipGetLastError();
     return nullptr;
   }
-  tabs[d] = p;
+  tabs[{dev, d}] = p;
   return p;
 }
 
