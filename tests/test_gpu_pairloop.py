@@ -360,6 +360,9 @@ def test_rescal_split_k_dw_matches_fused(monkeypatch):
     (300, 7, 2000, 40, 7),          # M = 20 = 4 x 5
     (300, 7, 2000, 60, 7),          # M = 30 = 2 x 3 x 5
     (300, 7, 2000, 28, 7),          # M = 14 = 2 x 7: no FFT plan, direct sums
+    (300, 7, 2000, 4, 7),           # M = 2: one radix-2 stage, the middle pair only
+    (300, 7, 2000, 8, 7),           # M = 4
+    (300, 7, 2000, 240, 7),         # M = 120 = 4 x 2 x 3 x 5, 61 lanes of pairs
     (40943, 18, 14140, 200, 10),    # WN18 entity count, d = 200 (M = 100 = 4 x 5 x 5)
 ])
 def test_hole_fft_matches_direct(n_ent, n_rel, T, d, nb, monkeypatch):
