@@ -136,3 +136,22 @@ def test_rescal_logistic_rparam():
 @pytest.mark.parametrize("n_ent,n_rel,d,B", [(300, 7, 40, 300), (400, 18, 200, 250)])
 def test_hole_logistic_vs_oracle(n_ent, n_rel, d, B):
     _run_logistic("hole", n_ent, n_rel, d, B, nb=2)
+
+
+@pytest.mark.parametrize("name", ["transe", "hole", "rescal"])
+def test_empty_batch_is_a_no_op(name):
+    """A batch with no pairs (every negative draw rejected) or no triples: the
+    reference would fail unpacking empty lists (unzip_triples of []); here
+    _pairwise_gradients returns None with no violations, the fused steps
+    launch nothing harmful, and the parameters do not move."""
+    m, upd = _model(name, 50, 3, 16)
+    before = {pid: p.data.clone() for pid, p in m.params.items()}
+    assert m._pairwise_gradients([], []) is None
+    assert m.nviolations == 0
+    nviol = torch.zeros(1, dtype=torch.int32, device=m.device)
+    empty = torch.zeros((0, 3), dtype=torch.int32, device=m.device)
+    m._pairwise_step(empty, empty, upd, nviol)
+    torch.cuda.synchronize()
+    assert int(nviol.item()) == 0
+    for pid, p in m.params.items():
+        assert torch.equal(p.data, before[pid]), pid
