@@ -369,13 +369,16 @@ def main():
         dist.destroy_process_group()
 
 
-def _score_bytes(d, cnt, V, packed=True):
+def _score_bytes(d, cnt, V, packed=True, hole=False):
     """Scoring part of a batch: gathers of s, o, p + 2
     corrupted rows, 20 B of index/hash traffic per positive, and the atomic row
     adds of the violating positives (<= 5 rows each; 2 B per element with the
-    exact int16x4 sums, 4 B with fp32)."""
+    exact int16x4 sums, 4 B with fp32).  HolE (fp32): a violating positive adds
+    3 + (its violating pairs) rows, at least 2.5 V rows for V violating pairs
+    (the lower bound is used)."""
     ab = 2 * d if packed else 4 * d
-    return 4 * d * (3 * cnt + 2 * cnt) + 20 * cnt + ab * min(5 * cnt, 2 * V + 3 * cnt)
+    rows = 2.5 * V if hole else min(5 * cnt, 2 * V + 3 * cnt)
+    return 4 * d * (3 * cnt + 2 * cnt) + 20 * cnt + ab * rows
 
 
 def _apply_bytes(d, rows, packed=True):
@@ -384,7 +387,7 @@ def _apply_bytes(d, rows, packed=True):
     return (16 * d + (4 * d if packed else 8 * d)) * rows
 
 
-def pipe_profile(runner, kg, nb, d, epochs=1, gpu_ms_per_epoch=None):
+def pipe_profile(runner, kg, nb, d, epochs=1, gpu_ms_per_epoch=None, hole=False):
     """Pipelined runner: `epochs` eager epochs with HIP events around every
     launch and the kernel's own per-launch counters (skge_pipe_runner_profile,
     on the runner's stream), started from the same state as the timed region.
@@ -410,19 +413,22 @@ def pipe_profile(runner, kg, nb, d, epochs=1, gpu_ms_per_epoch=None):
         t_other += float(us[0]) + float(us[n + 1])
         for i, cnt in enumerate(counts, start=1):
             UE, UR, V = (int(x) for x in stats[i])
-            b = _score_bytes(d, cnt, V) + _apply_bytes(d, UE + UR)
+            b = _score_bytes(d, cnt, V, packed=not hole, hole=hole) + \
+                _apply_bytes(d, UE + UR, packed=not hole)
             b_pipe += b
             t_pipe += float(us[i])
             if cnt:
                 total += algorithmic_bytes(d, cnt, 2 * cnt, 0, 0)
             total += 12 * d * (UE + UR)
-            geo += (cnt, min(5 * cnt, 2 * V + 3 * cnt), UE + UR, 1)
+            geo += (cnt, 2.5 * V if hole else min(5 * cnt, 2 * V + 3 * cnt), UE + UR, 1)
     eager_us = t_pipe / (n * epochs)
     avg_us = eager_us
     if gpu_ms_per_epoch is not None:
         avg_us = (1000.0 * gpu_ms_per_epoch - t_other / epochs) / n
     bpl = b_pipe / (n * epochs)
-    kern = {"pipe_batch": {"name": "pipe_batch", "avg_us": avg_us, "launches": n,
+    kern = {("hole_pipe" if hole else "pipe_batch"): {
+                           "name": "hole_pipe" if hole else "pipe_batch", "avg_us": avg_us,
+                           "launches": n,
                            "eager_avg_us": eager_us, "bytes_per_launch": bpl,
                            "achieved_gbs": bpl / (avg_us * 1e-6) / 1e9},
             # per positive: triple 12 B, two filter words 8 B, record 20 B
@@ -430,7 +436,8 @@ def pipe_profile(runner, kg, nb, d, epochs=1, gpu_ms_per_epoch=None):
                              "bytes_per_launch": 40.0 * T,
                              "achieved_gbs": 40.0 * T / (us0 / epochs * 1e-6) / 1e9}}
     g = geo / geo[3]
-    return {"kernels": kern, "dominant": kern["pipe_batch"], "epoch_bytes": total / epochs,
+    return {"kernels": kern, "dominant": kern["hole_pipe" if hole else "pipe_batch"],
+            "epoch_bytes": total / epochs,
             "geometry": {"positives": g[0], "atomic_rows": g[1], "applied_rows": g[2]}}
 
 
@@ -805,6 +812,12 @@ def run_config34(args):
     tfs = flops / elapsed / 1e12 * world
     nl = runner.nlaunches
     rname = type(runner).__name__
+    prof = None
+    if kind == "hole" and getattr(runner, "pipelined", False):
+        # the pipelined HolE runner's own counters over one more (eager) epoch;
+        # the batch launches' time from the timed region's wall clock per epoch
+        prof = pipe_profile(runner, kg, nb, d, gpu_ms_per_epoch=1000.0 * elapsed / args.steps,
+                            hole=True)
     del runner
     large = None
     if args.large_nb > 0:
@@ -849,11 +862,23 @@ def run_config34(args):
                                    % (name, d, "Sigmoid" if kind == "hole" else "Linear",
                                       margin, nb, N_TRIPLES // nb),
                        "global_batch": N_TRIPLES // nb, "parallelism": "replicas%d" % world},
-            "roofline": {"bound": "valu" if kind == "hole" else "mfma", "kernel": "whole step",
-                         "achieved": round(tfs, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": round(tfs / FP32_PEAK_TFS, 4), "traffic": None},
+            "roofline": ({"bound": "hbm", "kernel": "k_hole_pipe",
+                          "achieved": round(prof["dominant"]["achieved_gbs"], 1),
+                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(prof["dominant"]["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                          "traffic": None,
+                          "bytes_per_launch": round(prof["dominant"]["bytes_per_launch"]),
+                          "avg_launch_us": round(prof["dominant"]["avg_us"], 3),
+                          "note": "row gathers, fp32 atomic rows (2.5 V lower bound) and "
+                                  "applies, as config 2; the correlations run through the "
+                                  "wave FFT (skge_hole_fft.h)"}
+                         if prof is not None else
+                         {"bound": "valu" if kind == "hole" else "mfma", "kernel": "whole step",
+                          "achieved": round(tfs, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
+                          "frac": round(tfs / FP32_PEAK_TFS, 4), "traffic": None}),
             "cpu_baseline": cpu,
             "detail": {"violations_per_pair": round(V / float(P), 4),
+                       "direct_form_TFLOP_s": round(tfs, 2),   # model_flops at the timed rate
                        "graph_nodes_per_step": nl,
                        "runner": rname,
                        "batches": len(batch_sizes(N_TRIPLES, nb)),
