@@ -462,14 +462,20 @@ __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E
                                                      RescalWs ws) {
   const int ncb = (d + GC - 1) / GC;
   const int t = blockIdx.x / (2 * ncb);
-  if (t >= *ws.ntiles) return;
+  // the tile's fields and the tile count in one round trip (t < rs_tmax: the
+  // fields are in bounds, read before the check, used after it)
+  const int nti = *ws.ntiles;
+  const int p = ws.tile_rel[t], s0 = ws.tile_start[t], cnt = ws.tile_cnt[t];
+  if (t >= nti) return;
   const int rem = blockIdx.x - t * 2 * ncb;
   const int prod = rem / ncb, cb = rem - (rem / ncb) * ncb;
   const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
-  const int p = ws.tile_rel[t], s0 = ws.tile_start[t], cnt = ws.tile_cnt[t];
   const int c0 = cb * GC;
   __shared__ float sA[2][RT_ITEMS][KS + 4];
-  __shared__ float sB[2][KS][GC + 4];
+  // B: product 0 as [GC][KS + 4] (W rows as loaded, column-major B), product 1
+  // as [KS][GC + 4]; both read conflict-free by the MFMA loop
+  constexpr int SB0 = GC * (KS + 4), SB1 = KS * (GC + 4);
+  __shared__ float sB[2][SB0 > SB1 ? SB0 : SB1];
   __shared__ int s_row[RT_ITEMS], s_gid[RT_ITEMS], s_es[RT_ITEMS];
   if (tid < RT_ITEMS) {
     const bool ok = tid < cnt;
@@ -498,6 +504,11 @@ __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E
   // values are staged (a select right after a load would wait for it)
   auto load_step = [&](int ks) {
     const int k = ks * KS;
+#ifdef SKGE_ABL_GEMM_NOLOAD   // timing-only ablation (tools/ablate.sh): no operand loads
+#pragma unroll
+    for (int e = 0; e < SPT; ++e) ra[e] = rb[e] = (float)(k + e);
+    return;
+#endif
     const float* brow;
     int boff;
     if (prod == 0) {
@@ -536,10 +547,17 @@ __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E
       v.w = (a_ok && k + ak + 4 * m + 3 < d) ? ra[4 * m + 3] : 0.0f;
       *reinterpret_cast<float4*>(&sA[buf][ai][ak + 4 * m]) = v;
     }
-    if (prod == 0) {   // B[k][r] = W[r][k]
+    if (prod == 0) {   // B[k][r] = W[r][k], kept as W's rows: sB[r][k]
       const bool rok = c0 + bq < d;
 #pragma unroll
-      for (int e = 0; e < SPT; ++e) sB[buf][bk + e][bq] = (rok && k + bk + e < d) ? rb[e] : 0.0f;
+      for (int m = 0; m < SPT / 4; ++m) {
+        float4 v;
+        v.x = (rok && k + bk + 4 * m + 0 < d) ? rb[4 * m + 0] : 0.0f;
+        v.y = (rok && k + bk + 4 * m + 1 < d) ? rb[4 * m + 1] : 0.0f;
+        v.z = (rok && k + bk + 4 * m + 2 < d) ? rb[4 * m + 2] : 0.0f;
+        v.w = (rok && k + bk + 4 * m + 3 < d) ? rb[4 * m + 3] : 0.0f;
+        *reinterpret_cast<float4*>(&sB[buf][bq * (KS + 4) + bk + 4 * m]) = v;
+      }
     } else {
       const bool kok = k + bq < d;
 #pragma unroll
@@ -549,7 +567,7 @@ __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E
         v.y = (kok && c0 + bk + 4 * m + 1 < d) ? rb[4 * m + 1] : 0.0f;
         v.z = (kok && c0 + bk + 4 * m + 2 < d) ? rb[4 * m + 2] : 0.0f;
         v.w = (kok && c0 + bk + 4 * m + 3 < d) ? rb[4 * m + 3] : 0.0f;
-        *reinterpret_cast<float4*>(&sB[buf][bq][bk + 4 * m]) = v;
+        *reinterpret_cast<float4*>(&sB[buf][bq * (GC + 4) + bk + 4 * m]) = v;
       }
     }
   };
@@ -563,14 +581,33 @@ __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E
     store_step(buf, ks);
     __syncthreads();   // (also: every wave is done with buf's previous use, step ks - 2)
     if (ks + 1 < nk) load_step(ks + 1);   // in flight during this step's MFMAs
+#ifdef SKGE_ABL_GEMM_NOMFMA   // timing-only ablation: no contraction
+    acc[0][0] += sA[buf][row][kq] + sB[buf][kq * (GC + 4) + (l & 15)];
+#else
+    // B[k4 + kq][16 q + c]: product 0 at sB[(16 q + c)(KS + 4) + k4 + kq]
+    // (banks 36 c + kq: distinct), product 1 at sB[(k4 + kq)(GC + 4) + 16 q + c]
+    if (prod == 0) {
+      const float* b0 = &sB[buf][(l & 15) * (KS + 4) + kq];
 #pragma unroll
-    for (int k4 = 0; k4 < KS; k4 += 4) {
-      const float a = sA[buf][row][k4 + kq];
+      for (int k4 = 0; k4 < KS; k4 += 4) {
+        const float a = sA[buf][row][k4 + kq];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, sB[buf][k4 + kq][q * 16 + (l & 15)],
-                                                      acc[q], 0, 0, 0);
+        for (int q = 0; q < 4; ++q)
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b0[q * 16 * (KS + 4) + k4], acc[q], 0,
+                                                        0, 0);
+      }
+    } else {
+      const float* b1 = &sB[buf][kq * (GC + 4) + (l & 15)];
+#pragma unroll
+      for (int k4 = 0; k4 < KS; k4 += 4) {
+        const float a = sA[buf][row][k4 + kq];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b1[k4 * (GC + 4) + q * 16], acc[q], 0,
+                                                        0, 0);
+      }
     }
+#endif
   }
   // epilogue: D[row 4g + reg][col] of accumulator q -> triple 16w + 4g + reg, column c0 + 16q + c
   float* out = prod == 0 ? ws.WE : ws.EW;
@@ -836,12 +873,13 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
   const int rt = rem / nt, ct = rem - (rem / nt) * nt;
   const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
   const int off = ws.rel_off[p], cnt = ws.rel_off[p + 1] - off;
+  const int gv = APPLY && wa.gate != nullptr ? *wa.gate : 1;   // (loaded with rel_off)
   if (!APPLY && rem == 0 && tid == 0) {   // slot p (skge_hip.h slot map)
     if (accW.touched) accW.touched[p] = cnt > 0 ? p : -1;
     accW.cnt[p] = cnt;
   }
   if (cnt == 0) return;
-  const bool upd = !APPLY || wa.gate == nullptr || *wa.gate != 0;
+  const bool upd = gv != 0;
   if (APPLY && !upd) return;   // the model returned None: no update
   if (APPLY && rem == 0 && tid == 0 && wa.opt == OPT_ADAGRAD && wa.ucnt)
     wa.ucnt[p] += 1;   // updateCounts, skge/param.py:149-150
@@ -1097,12 +1135,13 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_fin(int d, RescalWs ws, Ac
   const int rt = rem / nt, ct = rem - (rem / nt) * nt;
   const int tid = threadIdx.x;
   const int off = ws.rel_off[p], cnt = ws.rel_off[p + 1] - off;
+  const int gv = APPLY && wa.gate != nullptr ? *wa.gate : 1;   // (loaded with rel_off)
   if (!APPLY && rem == 0 && tid == 0) {   // slot p (skge_hip.h slot map)
     if (accW.touched) accW.touched[p] = cnt > 0 ? p : -1;
     accW.cnt[p] = cnt;
   }
   if (cnt == 0) return;
-  const bool upd = !APPLY || wa.gate == nullptr || *wa.gate != 0;
+  const bool upd = gv != 0;
   if (APPLY && !upd) return;   // the model returned None: no update
   if (APPLY && rem == 0 && tid == 0 && wa.opt == OPT_ADAGRAD && wa.ucnt)
     wa.ucnt[p] += 1;   // updateCounts, skge/param.py:149-150
