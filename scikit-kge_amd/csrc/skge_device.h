@@ -21,19 +21,42 @@ enum Post : int { POST_NONE = 0, POST_NORMALIZE = 1, POST_NORMLESS1 = 2 };
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-// xor-butterfly all-reduce: every lane ends with the bitwise-identical sum
-// (each level adds the same two operands, commutatively), so decisions taken
-// on the reduced value (the margin test) are wave-uniform.
+// DPP lane moves within 16-lane rows (VALU, no LDS round trip): quad_perm
+// [1,0,3,2] (lane ^ 1), [2,3,0,1] (lane ^ 2), row_half_mirror (lane i of an
+// 8-lane half takes lane 7 - i), row_mirror (lane i takes 15 - i)
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, true);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, dpp_i<CTRL>(__builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ float lane_f(float v, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
+
+// All-reduce over the wave (every lane active): four DPP adds give every lane
+// its 16-lane row's sum -- after the quad steps the lanes of a quad hold the
+// same value, so the mirrors add the other quad / half exactly like an xor --
+// then the four row sums, read with v_readlane, are added as (r0 + r1) +
+// (r2 + r3).  Every lane ends with the bitwise-identical sum, so decisions
+// taken on it (the margin test) are wave-uniform.
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-  return v;
+  v += dpp_f<0xb1>(v);
+  v += dpp_f<0x4e>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
 }
 
 __device__ __forceinline__ int wave_sum_int(int v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-  return v;
+  v += dpp_i<0xb1>(v);
+  v += dpp_i<0x4e>(v);
+  v += dpp_i<0x141>(v);
+  v += dpp_i<0x140>(v);
+  return (__builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16)) +
+         (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
 }
 
 // activation functions, skge/actfun.py:13-57
