@@ -126,6 +126,22 @@ int launch_hole_pos(hipStream_t st, int af, const skge_table_t* ent, const skge_
                     int d, const int4* rec, const int* rec_n1, long long start, int count,
                     float margin, int* nviol, int* fold, int* total);
 
+// The RESCAL W updater's step after the fused front (skge_rescal.hip
+// k_rescal_front_fused): W[p] from relation p's split-K dW partial tiles,
+// gated on the batch's violations; run by the entity apply's launch
+// (skge_update.hip k_apply_wstep).  part == nullptr: no W step pending.
+struct WStep {
+  const float* part;      // [M][nt * nt][splits][64 * 64]
+  const int* rel_off;     // [M + 1] the batch's relation bucket offsets
+  float* W;
+  float* A;               // AdaGrad state or nullptr
+  int* ucnt;              // optional updateCounts
+  const int* gate;        // the batch's violation count
+  int M, d, splits, opt;
+  float lr, rin, rout, fdiv;
+};
+int apply_with_wstep(hipStream_t st, const skge_table_t* ent, int nslots, const WStep& w);
+
 }  // namespace skge
 
 // skge_rescal.hip / skge_update.hip: the device pair loop's RESCAL batch
@@ -138,7 +154,8 @@ int rescal_epoch_bucket(hipStream_t st, const int* pos, const int* neg, long lon
 int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent,
                                  const skge_table_t* rel, int d, const int4* rec,
                                  const int* rec_n1, long long T, int bs, int nb, int b,
-                                 float margin, void* ws, int* nviol);
+                                 float margin, void* ws, int* nviol,
+                                 skge::WStep* wstep = nullptr);
 int skge_rescal_pos_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
                               const skge_table_t* rel, int d, const int* pos, const int* neg,
                               const int4* rec, const int* rec_n1, long long start, int count,

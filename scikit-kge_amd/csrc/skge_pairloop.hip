@@ -216,16 +216,17 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
         rc = skge_accum_apply(stream, t, 2, ns);
       }
     } else if (rpos) {
+      WStep wst{};   // set by the fused front (Linear): the W step rides the entity apply
       rc = rep ? skge_rescal_pos_grad_mfma_ep(st, af, ent, rel, d, r->rec, r->rec_n1, (long long)T,
-                                              (int)bs, nb, k, margin, r->ws, gate)
+                                              (int)bs, nb, k, margin, r->ws, gate, &wst)
                : skge_rescal_pos_grad_mfma(st, af, ent, rel, d, pos + 3 * start, neg + 6 * start,
                                            r->rec, r->rec_n1, start, count, margin, r->ws,
                                            r->ws_bytes, gate);
-      if (!rc) {   // the entity table's apply (W was updated by the dW kernel)
+      if (!rc) {   // the entity table's apply (and W's, unless the dW kernel updated it)
         skge_table_t te = *ent;
         te.gate = gate;
         const int ns = 4 * count;
-        rc = skge_accum_apply(stream, &te, 1, &ns);
+        rc = wst.part ? apply_with_wstep(st, &te, ns, wst) : skge_accum_apply(stream, &te, 1, &ns);
       }
     } else {
       rc = skge_pair_step(stream, model, af, ent, rel, d, pos + 6 * start, neg + 6 * start,

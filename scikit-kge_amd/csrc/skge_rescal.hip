@@ -59,6 +59,8 @@ struct RescalWs {
   float* WE;        // [n][d]
   float* EW;        // [n][d]
   float* wpart;     // [M][nt * nt][splits][64 * 64] split-K dW partial tiles (or null)
+  float* ecoef;     // [n] Linear dW coefficients in bucket order, written with the
+                    // epoch's buckets (device pair loop only, else null)
 };
 
 static int rs_tmax(int n, int M) { return n / RT_ITEMS + M + 1; }
@@ -90,6 +92,28 @@ static size_t rs_wpart_bytes(int n, int M, int d) {
   const size_t nt = (d + WS_TILE - 1) / WS_TILE;
   return sp > 1 ? (size_t)M * nt * nt * sp * WS_TILE * WS_TILE * 4 : 0;
 }
+// the fused front (k_rescal_front_fused): splits of its dW grid -- the split-K
+// count where that applies, else SKGE_RS_FSPLIT (default 1; each split adds a
+// workgroup per tile beside the GEMM's); 0 = no fused front (SKGE_RESCAL_FUSED=0,
+// or the partial tiles would pass 64 MB)
+static int rs_front_splits(int n, int M, int d) {
+  const char* fe = getenv("SKGE_RESCAL_FUSED");
+  if (fe && atoi(fe) == 0) return 0;
+  const long long nt = (d + WS_TILE - 1) / WS_TILE;
+  int sp = rs_wsplit(n, M, d);
+  if (sp == 1) {
+    const char* fs = getenv("SKGE_RS_FSPLIT");
+    sp = fs ? std::max(1, atoi(fs)) : 1;
+    const long long groups = ((long long)n / M + WS_GROUP - 1) / WS_GROUP;
+    sp = (int)std::max(1ll, std::min<long long>(sp, groups));
+  }
+  if ((long long)M * nt * nt * sp * WS_TILE * WS_TILE * 4 > (64ll << 20)) return 0;
+  return sp;
+}
+static size_t rs_front_wpart_bytes(int n, int M, int d) {
+  const size_t nt = (d + WS_TILE - 1) / WS_TILE;
+  return (size_t)M * nt * nt * rs_front_splits(n, M, d) * WS_TILE * WS_TILE * 4;
+}
 
 // carve the workspace (base may be null: size only)
 // n: triples in the batch (2P for pairs: positives then negatives; T for
@@ -120,6 +144,7 @@ static size_t rescal_ws_layout(int n, int M, int d, void* base, RescalWs* ws) {
   w.EW = (float*)take((size_t)n * d * 4);
   const size_t wpb = rs_wpart_bytes(n, M, d);
   w.wpart = wpb ? (float*)take(wpb) : nullptr;
+  w.ecoef = nullptr;
   if (ws) *ws = w;
   return off;
 }
@@ -246,6 +271,12 @@ __device__ __forceinline__ void rs_scatter_chunk(const int* __restrict__ pos,
   const int k = c * 64 + l;
   const int* tr = item_trip(pos, neg, P, k < n ? k : 0);
   const int ts = tr[0], to = tr[1], b = k < n ? tr[2] : -1;
+  // epoch buckets (dedup lists: positive j's negatives at neg[6j .. 6j + 5]):
+  // the Linear dW coefficient, gp (k0 + k1) = -(k0 + k1) for a positive and
+  // gn = +1 for a negative, as k_rescal_pos_scatter computes it
+  float ec = 1.0f;
+  if (ws.ecoef && k < P)
+    ec = -(float)((neg[6 * (size_t)k + 2] >= 0 ? 1 : 0) + (neg[6 * (size_t)k + 5] >= 0 ? 1 : 0));
   uint64_t act = __ballot(b >= 0);
   while (act) {
     const int leader = __ffsll((unsigned long long)act) - 1;
@@ -258,6 +289,7 @@ __device__ __forceinline__ void rs_scatter_chunk(const int* __restrict__ pos,
       ws.sorted_s[at] = ts;
       ws.sorted_o[at] = to;
       ws.bpos[k] = at;
+      if (ws.ecoef) ws.ecoef[at] = ec;
     }
     act &= ~m;
   }
@@ -299,6 +331,7 @@ __device__ __forceinline__ RescalWs rs_batch_view(const RescalEpoch& e, int b) {
   w.sorted_s = sh(w.sorted_s);
   w.sorted_o = sh(w.sorted_o);
   w.bpos = sh(w.bpos);
+  w.ecoef = sh(w.ecoef);
   return w;
 }
 
@@ -456,27 +489,31 @@ __global__ __launch_bounds__(1024) void k_rs_bucket_small(const int* __restrict_
 // accumulators (independent chains hide the MFMA latency).  Product-0 blocks
 // also write each triple's partial score E[s_i] . WE_i over their 64 columns.
 // ---------------------------------------------------------------------------
+// B: product 0 as [GC][KS + 4] (W rows as loaded, column-major B), product 1
+// as [KS][GC + 4]; both read conflict-free by the MFMA loop
+constexpr int SB0 = GC * (KS + 4), SB1 = KS * (GC + 4);
+constexpr int SBN = SB0 > SB1 ? SB0 : SB1;
+// one GEMM workgroup's LDS: sA [2][RT_ITEMS][KS + 4], sB [2][SBN], 3 x RT_ITEMS ints
+constexpr int GEMM_LDS_FLOATS = 2 * RT_ITEMS * (KS + 4) + 2 * SBN + 3 * RT_ITEMS;
+
+// workgroup `bid` of the GEMM grid (k_rescal_gemm, k_rescal_front_fused)
 template <bool VEC>
-__global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E,
-                                                     const float* __restrict__ W, int d,
-                                                     RescalWs ws) {
+__device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
+                                                 const float* __restrict__ W, int d,
+                                                 const RescalWs& ws, int bid,
+                                                 float (*sA)[RT_ITEMS][KS + 4], float (*sB)[SBN],
+                                                 int* s_row, int* s_gid, int* s_es) {
   const int ncb = (d + GC - 1) / GC;
-  const int t = blockIdx.x / (2 * ncb);
+  const int t = bid / (2 * ncb);
   // the tile's fields and the tile count in one round trip (t < rs_tmax: the
   // fields are in bounds, read before the check, used after it)
   const int nti = *ws.ntiles;
   const int p = ws.tile_rel[t], s0 = ws.tile_start[t], cnt = ws.tile_cnt[t];
   if (t >= nti) return;
-  const int rem = blockIdx.x - t * 2 * ncb;
+  const int rem = bid - t * 2 * ncb;
   const int prod = rem / ncb, cb = rem - (rem / ncb) * ncb;
   const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
   const int c0 = cb * GC;
-  __shared__ float sA[2][RT_ITEMS][KS + 4];
-  // B: product 0 as [GC][KS + 4] (W rows as loaded, column-major B), product 1
-  // as [KS][GC + 4]; both read conflict-free by the MFMA loop
-  constexpr int SB0 = GC * (KS + 4), SB1 = KS * (GC + 4);
-  __shared__ float sB[2][SB0 > SB1 ? SB0 : SB1];
-  __shared__ int s_row[RT_ITEMS], s_gid[RT_ITEMS], s_es[RT_ITEMS];
   if (tid < RT_ITEMS) {
     const bool ok = tid < cnt;
     const int at = s0 + (ok ? tid : 0);
@@ -645,6 +682,16 @@ __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E
       if (c == 0 && it < cnt) ws.spart[(size_t)s_gid[it] * ncb + cb] = v;
     }
   }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E,
+                                                     const float* __restrict__ W, int d,
+                                                     RescalWs ws) {
+  __shared__ float sA[2][RT_ITEMS][KS + 4];
+  __shared__ float sB[2][SBN];
+  __shared__ int s_row[RT_ITEMS], s_gid[RT_ITEMS], s_es[RT_ITEMS];
+  rescal_gemm_body<VEC>(E, W, d, ws, (int)blockIdx.x, sA, sB, s_row, s_gid, s_es);
 }
 
 // ---------------------------------------------------------------------------
@@ -1029,11 +1076,17 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
 // at the reference's batch size, so double buffering buys nothing and halving
 // the LDS lets more workgroups be resident); the partial tile is stored whole.
 static_assert(WS_TILE == WG_T && WS_GROUP == WG_PF * WG_CH, "split-K group geometry");
+// workgroup `bid` of the split-K dW grid (k_rescal_wgrad_part,
+// k_rescal_front_fused); coef: the items' dW coefficients in bucket order
+constexpr int WPART_LDS_FLOATS = 2 * WG_CH * (WG_T + 4);
 template <bool VEC>
-__global__ __launch_bounds__(256) void k_rescal_wgrad_part(const float* __restrict__ E, int d,
-                                                           RescalWs ws, int splits) {
+__device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__ E, int d,
+                                                       const RescalWs& ws,
+                                                       const float* __restrict__ coef, int splits,
+                                                       int bid, float (*sEs)[WG_T + 4],
+                                                       float (*sEo)[WG_T + 4]) {
   const int nt = (d + WG_T - 1) / WG_T;
-  const int blk = blockIdx.x / splits, sp = blockIdx.x - (blockIdx.x / splits) * splits;
+  const int blk = bid / splits, sp = bid - (bid / splits) * splits;
   const int p = blk / (nt * nt);
   const int rem = blk - p * nt * nt;
   const int rt = rem / nt, ct = rem - (rem / nt) * nt;
@@ -1041,8 +1094,6 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_part(const float* __restri
   const int off = ws.rel_off[p], cnt = ws.rel_off[p + 1] - off;
   const int nch = (cnt + WG_CH - 1) / WG_CH, ngr = (nch + WG_PF - 1) / WG_PF;
   if (sp >= ngr) return;   // no group for this split (the finishing kernel knows)
-  __shared__ float sEs[WG_CH][WG_T + 4];
-  __shared__ float sEo[WG_CH][WG_T + 4];
   const int r0 = rt * WG_T, c0 = ct * WG_T;
   f32x4 acc[4];
 #pragma unroll
@@ -1058,7 +1109,7 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_part(const float* __restri
       const int at = off + (i < cnt ? i : cnt - 1);
       ns[q] = ws.sorted_s[at];
       no[q] = ws.sorted_o[at];
-      nc[q] = i < cnt ? ws.coef[at] : 0.0f;
+      nc[q] = i < cnt ? coef[at] : 0.0f;
     }
     float4 es[WG_PF][WG_FPT / 4], eo[WG_PF][WG_FPT / 4];
 #pragma unroll
@@ -1119,6 +1170,47 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_part(const float* __restri
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg)
       out[(16 * wave + 4 * (l >> 4) + reg) * WG_T + 16 * j + (l & 15)] = acc[j][reg];
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_rescal_wgrad_part(const float* __restrict__ E, int d,
+                                                           RescalWs ws, int splits) {
+  __shared__ float sEs[WG_CH][WG_T + 4];
+  __shared__ float sEo[WG_CH][WG_T + 4];
+  rescal_wgrad_part_body<VEC>(E, d, ws, ws.coef, splits, (int)blockIdx.x, sEs, sEo);
+}
+
+// ---------------------------------------------------------------------------
+// The device pair loop's fused front (Linear activation): with g = 1 the dW
+// coefficients do not depend on the scores (gp = -1 per pair the positive is
+// in, gn = +1; rescal.py:113-125, 275), so they are written when the epoch's
+// buckets are built (ws.ecoef) and batch b's dW contraction needs only E --
+// the same operand the GEMMs read.  ONE launch runs both: the first nwg
+// workgroups are the split-K dW grid (partial tiles into ws.wpart), the rest
+// the GEMM grid; the W step (k_rescal_wgrad_fin, gated on the batch's
+// violations) follows the scatter.  The LDS is one buffer carved per role.
+// Same arithmetic, same k order as the unfused kernels: bitwise the same W.
+// ---------------------------------------------------------------------------
+constexpr int FRONT_LDS_FLOATS =
+    GEMM_LDS_FLOATS > WPART_LDS_FLOATS ? GEMM_LDS_FLOATS : WPART_LDS_FLOATS;
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_rescal_front_fused(const float* __restrict__ E,
+                                                            const float* __restrict__ W, int d,
+                                                            RescalWs ws, int splits, int nwg) {
+  __shared__ __attribute__((aligned(16))) float lds[FRONT_LDS_FLOATS];
+  const int bid = (int)blockIdx.x;
+  if (bid < nwg) {
+    rescal_wgrad_part_body<VEC>(E, d, ws, ws.ecoef, splits, bid,
+                                reinterpret_cast<float(*)[WG_T + 4]>(lds),
+                                reinterpret_cast<float(*)[WG_T + 4]>(lds + WG_CH * (WG_T + 4)));
+  } else {
+    float* sb = lds + 2 * RT_ITEMS * (KS + 4);
+    int* si = reinterpret_cast<int*>(sb + 2 * SBN);
+    rescal_gemm_body<VEC>(E, W, d, ws, bid - nwg,
+                          reinterpret_cast<float(*)[RT_ITEMS][KS + 4]>(lds),
+                          reinterpret_cast<float(*)[SBN]>(sb), si, si + RT_ITEMS,
+                          si + 2 * RT_ITEMS);
+  }
 }
 
 // k_rescal_wgrad_fin: one workgroup per (relation, 64 x 64 tile): the tile's
@@ -1384,7 +1476,9 @@ static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, Resc
   w.coef = (float*)take((size_t)n * 4);
   w.WE = (float*)take((size_t)n * d * 4);
   w.EW = (float*)take((size_t)n * d * 4);
-  const size_t wpb = rs_wpart_bytes(n, M, d);   // batches of fewer items use fewer splits
+  // batches of fewer items use fewer splits; the fused front (Linear) needs
+  // partial tiles even at one split
+  const size_t wpb = std::max(rs_wpart_bytes(n, M, d), rs_front_wpart_bytes(n, M, d));
   w.wpart = wpb ? (float*)take(wpb) : nullptr;
   const size_t s0 = off;
   w.chunk = (int*)take((size_t)nchunks * M * 4);
@@ -1397,6 +1491,7 @@ static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, Resc
   w.sorted_s = (int*)take((size_t)n * 4);
   w.sorted_o = (int*)take((size_t)n * 4);
   w.bpos = (int*)take((size_t)n * 4);
+  w.ecoef = (float*)take((size_t)n * 4);
   const size_t slice = off - s0;
   if (ws0) *ws0 = w;
   if (stride) *stride = (long long)slice;
@@ -1440,8 +1535,9 @@ int rescal_epoch_bucket(hipStream_t st, const int* pos, const int* neg, long lon
 int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent,
                                  const skge_table_t* rel, int d, const int4* rec,
                                  const int* rec_n1, long long T, int bs, int nb, int b,
-                                 float margin, void* ws, int* nviol) {
+                                 float margin, void* ws, int* nviol, WStep* wstep) {
   int rc;
+  if (wstep) wstep->part = nullptr;
   const long long start = (long long)b * bs;
   const int count = (int)(start + bs <= T ? bs : T - start);
   if ((rc = check_table(ent, "ent", true)) || (rc = check_table(rel, "rel", false)) ||
@@ -1468,9 +1564,37 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
   w.sorted_s = sh(w.sorted_s);
   w.sorted_o = sh(w.sorted_o);
   w.bpos = sh(w.bpos);
+  w.ecoef = sh(w.ecoef);
+  const int n = 3 * count, M = rel->rows;
+  const int fsplits = af == AF_LINEAR ? rs_front_splits(n, M, d) : 0;
+  const int blocks = std::max(1, std::min((count + 3) / 4, 16384));
+  if (fsplits > 0) {   // k_rescal_front_fused: dW contraction and GEMMs in one launch
+    const int nt = (d + WG_T - 1) / WG_T, ncb = (d + GC - 1) / GC;
+    const int nwg = M * nt * nt * fsplits;
+    const dim3 grid((unsigned)(nwg + rs_tmax(n, M) * 2 * ncb));
+    if ((d & 3) == 0)
+      hipLaunchKernelGGL((k_rescal_front_fused<true>), grid, dim3(256), 0, st, ent->param,
+                         rel->param, d, w, fsplits, nwg);
+    else
+      hipLaunchKernelGGL((k_rescal_front_fused<false>), grid, dim3(256), 0, st, ent->param,
+                         rel->param, d, w, fsplits, nwg);
+    SKGE_KM_SWITCH(k_rescal_pos_scatter, dim3(blocks), dim3(256), 0, st, rec, rec_n1, start,
+                   count, d, af, margin, w, accum_of(ent), nviol)
+    const char* sep = getenv("SKGE_RS_WSTEP_SEP");   // A/B: the W step in its own launch
+    if (wstep && !(sep && atoi(sep))) {   // the caller's entity apply runs the W step
+      *wstep = WStep{w.wpart, w.rel_off, rel->param, rel->state, rel->upd_count, nviol, M, d,
+                     fsplits, rel->opt, rel->lr, rel->rin, rel->rout, rel->fixed_div};
+    } else {
+      WApply wa = {rel->param, rel->state, rel->opt, rel->lr, rel->rin, rel->rout,
+                   rel->fixed_div, nviol, rel->upd_count};
+      hipLaunchKernelGGL((k_rescal_wgrad_fin<true>), dim3((unsigned)(M * nt * nt)), dim3(256), 0,
+                         st, d, w, accum_of(rel), wa, fsplits);
+    }
+    SKGE_CHECK_LAUNCH("rescal positive grad (fused front)");
+    return SKGE_OK;
+  }
   rc = rescal_front(st, ent, rel, d, nullptr, count, nullptr, 3 * count, w, true);
   if (rc) return rc;
-  const int blocks = std::max(1, std::min((count + 3) / 4, 16384));
   SKGE_KM_SWITCH(k_rescal_pos_scatter, dim3(blocks), dim3(256), 0, st, rec, rec_n1, start, count,
                  d, af, margin, w, accum_of(ent), nviol)
   rescal_wgrad_launch(st, ent, rel, d, w, true, nviol, 3 * count);

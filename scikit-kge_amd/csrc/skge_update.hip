@@ -734,6 +734,104 @@ static int grid_for_elems(long long elems) {
   return (int)b;
 }
 
+// The RESCAL W step (WStep, after k_rescal_front_fused) beside the entity
+// apply, one launch: the first nwb workgroups take four consecutive elements
+// of a 64 x 64 dW tile per thread -- the split partials summed in split order,
+// then the W updater's step (skge/param.py:115-155; the arithmetic of
+// k_rescal_wgrad_fin, bitwise) -- the rest apply the entity slots as k_apply.
+constexpr int WS_T = 64;   // dW tile edge (skge_rescal.hip WG_T)
+__device__ __forceinline__ void wstep_quad(const WStep& w, long long q) {
+  const int nt = (w.d + WS_T - 1) / WS_T;
+  const long long per_rel = (long long)nt * nt * (WS_T * WS_T / 4);
+  const int p = (int)(q / per_rel);
+  const int rem = (int)(q - (long long)p * per_rel);
+  const int tile = rem / (WS_T * WS_T / 4), e = 4 * (rem - tile * (WS_T * WS_T / 4));
+  const int off = w.rel_off[p], cnt = w.rel_off[p + 1] - off;
+  const int gv = *w.gate;
+  if (cnt == 0 || gv == 0) return;   // relation not in the batch / the model returned None
+  const int rt = tile / nt, ct = tile - rt * nt;
+  const int r = rt * WS_T + e / WS_T, c = ct * WS_T + e % WS_T;
+  if (r >= w.d || c >= w.d) return;
+  if (tile == 0 && e == 0 && w.opt == OPT_ADAGRAD && w.ucnt) w.ucnt[p] += 1;   // param.py:149-150
+  // split-K groups of 128 items (skge_rescal.hip WS_GROUP): splits past the
+  // relation's groups wrote nothing
+  const int ngr = (cnt + 127) / 128, nsp = min(w.splits, ngr);
+  const float* part = w.part + ((size_t)(p * nt * nt + tile) * w.splits) * (WS_T * WS_T) + e;
+  float4 s = *reinterpret_cast<const float4*>(part);
+  const size_t o = (size_t)p * w.d * w.d + (size_t)r * w.d + c;
+  const bool ada = w.opt == OPT_ADAGRAD;
+  float pv[4], av[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const bool in = c + m < w.d;
+    pv[m] = in ? w.W[o + m] : 0.0f;
+    av[m] = in && ada ? w.A[o + m] : 0.0f;
+  }
+  for (int k = 1; k < nsp; ++k) {   // split order: deterministic sums
+    const float4 v = *reinterpret_cast<const float4*>(part + (size_t)k * (WS_T * WS_T));
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  const float sv[4] = {s.x, s.y, s.z, s.w};
+  const float div = w.fdiv > 0.0f ? w.fdiv : (float)cnt;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    if (c + m >= w.d) continue;
+    const float g = (sv[m] + w.rin * pv[m]) / div + w.rout * pv[m];
+    if (ada) {
+      const float a2 = av[m] + g * g;
+      w.W[o + m] = pv[m] - (w.lr * g) / fmaxf(sqrtf(a2), 1e-7f);
+      w.A[o + m] = a2;
+    } else {
+      w.W[o + m] = pv[m] - w.lr * g;
+    }
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_apply_wstep(TableDev t0, int n0, WStep w, int nwb) {
+  if ((int)blockIdx.x < nwb) {
+    const long long nq = (long long)w.M * ((w.d + WS_T - 1) / WS_T) * ((w.d + WS_T - 1) / WS_T) *
+                         (WS_T * WS_T / 4);
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
+         q += (long long)nwb * blockDim.x)
+      wstep_quad(w, q);
+    return;
+  }
+  const int wpb = blockDim.x >> 6;
+  const int nw = ((int)gridDim.x - nwb) * wpb;
+  for (int s = ((int)blockIdx.x - nwb) * wpb + (threadIdx.x >> 6); s < n0; s += nw)
+    apply_slot<K, ACC_F32>(t0, s);
+}
+
+int apply_with_wstep(hipStream_t st, const skge_table_t* ent, int nslots, const WStep& w) {
+  int rc = check_table(ent, "ent", true);
+  if (rc) return rc;
+  if ((rc = check_slots(ent, nslots, "ent"))) return rc;
+  SKGE_CHECK_ARG(ent->acc_mode == SKGE_ACC_F32 && ent->acc_replicas <= 1,
+                 "W step beside the apply: single fp32 entity accumulator");
+  SKGE_CHECK_ARG(ent->opt == SKGE_SGD || ent->state, "AdaGrad needs state");
+  SKGE_CHECK_ARG(w.opt == SKGE_SGD || w.A, "AdaGrad needs state");
+  const int nt = (w.d + WS_T - 1) / WS_T;
+  const long long nq = (long long)w.M * nt * nt * (WS_T * WS_T / 4);
+  const int nwb = grid_for_elems(nq);
+  const int grid = nwb + grid_for_waves(nslots);
+  const TableDev td = table_dev(ent);
+  switch (km_for(ent->width)) {
+    case 1: hipLaunchKernelGGL((k_apply_wstep<1>), dim3(grid), dim3(256), 0, st, td, nslots, w, nwb); break;
+    case 2: hipLaunchKernelGGL((k_apply_wstep<2>), dim3(grid), dim3(256), 0, st, td, nslots, w, nwb); break;
+    case 3: hipLaunchKernelGGL((k_apply_wstep<3>), dim3(grid), dim3(256), 0, st, td, nslots, w, nwb); break;
+    case 4: hipLaunchKernelGGL((k_apply_wstep<4>), dim3(grid), dim3(256), 0, st, td, nslots, w, nwb); break;
+    case 8: hipLaunchKernelGGL((k_apply_wstep<8>), dim3(grid), dim3(256), 0, st, td, nslots, w, nwb); break;
+    case 16: hipLaunchKernelGGL((k_apply_wstep<16>), dim3(grid), dim3(256), 0, st, td, nslots, w, nwb); break;
+    default: set_error("entity width %d unsupported", ent->width); return SKGE_ENOTSUP;
+  }
+  SKGE_CHECK_LAUNCH("apply + W step");
+  return SKGE_OK;
+}
+
 }  // namespace skge
 
 using namespace skge;

@@ -471,3 +471,37 @@ def test_rescal_epoch_buckets_match_per_batch_buckets(n_ent, n_rel, T, d, nb, mo
     for pid in out[0][1]:
         np.testing.assert_allclose(out[1][1][pid], out[0][1][pid], rtol=RTOL, atol=ATOL,
                                    err_msg=pid)
+
+
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb,fsplit", [
+    (300, 7, 2000, 16, 7, "1"),          # ragged remainder batch
+    (300, 7, 2000, 36, 3, "2"),          # d % 4 == 0, two dW splits beside the GEMMs
+    (300, 5, 2000, 30, 3, "1"),          # d % 4 != 0 (scalar operand loads)
+    (40943, 18, 14140, 200, 10, "1"),    # WN18 entity / relation counts, d, batch size
+])
+def test_rescal_fused_front_matches_unfused(n_ent, n_rel, T, d, nb, fsplit, monkeypatch):
+    """The RESCAL pair loop's fused front (Linear: dW contraction and GEMMs in
+    one launch, dW coefficients written with the epoch's buckets, the W step
+    after the scatter) against the unfused kernels (SKGE_RESCAL_FUSED=0) on the
+    same draws: equal violation totals, parameters within the fp32 tolerance
+    (the entity sums are float atomics in both)."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    xs = make_kg(n_ent, n_rel, T, seed=3)
+    monkeypatch.setenv("SKGE_RS_FSPLIT", fsplit)
+    out = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("SKGE_RESCAL_FUSED", fused)
+        m = make_model("rescal", (n_ent, n_ent, n_rel), d)
+        m.add_hyperparam("margin", 0.2)
+        upd = {pid: S.SGD(p, 0.1) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), nb, seed=6)
+        with torch.cuda.stream(r.stream):
+            r.run(2)
+        r.synchronize()
+        out.append((int(r.nviol_total.item()),
+                    {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}))
+    assert out[0][0] == out[1][0] > 0
+    for pid in out[0][1]:
+        np.testing.assert_allclose(out[1][1][pid], out[0][1][pid], rtol=RTOL, atol=ATOL,
+                                   err_msg=pid)
