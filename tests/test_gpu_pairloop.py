@@ -473,13 +473,14 @@ def test_rescal_epoch_buckets_match_per_batch_buckets(n_ent, n_rel, T, d, nb, mo
                                    err_msg=pid)
 
 
-@pytest.mark.parametrize("n_ent,n_rel,T,d,nb,fsplit", [
-    (300, 7, 2000, 16, 7, "1"),          # ragged remainder batch
-    (300, 7, 2000, 36, 3, "2"),          # d % 4 == 0, two dW splits beside the GEMMs
-    (300, 5, 2000, 30, 3, "1"),          # d % 4 != 0 (scalar operand loads)
-    (40943, 18, 14140, 200, 10, "1"),    # WN18 entity / relation counts, d, batch size
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb,fsplit,order", [
+    (300, 7, 2000, 16, 7, "1", "1"),          # ragged remainder batch
+    (300, 7, 2000, 36, 3, "2", "0"),          # d % 4 == 0, two dW splits, dW grid first
+    (300, 5, 2000, 30, 3, "1", "3"),          # d % 4 != 0, interleaved roles
+    (40943, 18, 14140, 200, 10, "1", "1"),    # WN18 entity / relation counts, d, batch size
+    (40943, 18, 14140, 200, 10, "1", "9"),    # interleave clamped to the grid
 ])
-def test_rescal_fused_front_matches_unfused(n_ent, n_rel, T, d, nb, fsplit, monkeypatch):
+def test_rescal_fused_front_matches_unfused(n_ent, n_rel, T, d, nb, fsplit, order, monkeypatch):
     """The RESCAL pair loop's fused front (Linear: dW contraction and GEMMs in
     one launch, dW coefficients written with the epoch's buckets, the W step
     after the scatter) against the unfused kernels (SKGE_RESCAL_FUSED=0) on the
@@ -489,6 +490,7 @@ def test_rescal_fused_front_matches_unfused(n_ent, n_rel, T, d, nb, fsplit, monk
     from skge_amd.device import DeviceKG, PairLoopRunner
     xs = make_kg(n_ent, n_rel, T, seed=3)
     monkeypatch.setenv("SKGE_RS_FSPLIT", fsplit)
+    monkeypatch.setenv("SKGE_RS_FRONT_ORDER", order)
     out = []
     for fused in ("0", "1"):
         monkeypatch.setenv("SKGE_RESCAL_FUSED", fused)
