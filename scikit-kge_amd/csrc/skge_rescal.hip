@@ -61,9 +61,26 @@ struct RescalWs {
   float* wpart;     // [M][nt * nt][splits][64 * 64] split-K dW partial tiles (or null)
   float* ecoef;     // [n] Linear dW coefficients in bucket order, written with the
                     // epoch's buckets (device pair loop only, else null)
+  // deduplicated GEMM rows (epoch buckets; npos = the batch's positives, 0 =
+  // off): a positive j and its s-corrupted negative share W E_o, j and its
+  // o-corrupted negative share E_s W, so product 0 (WE) runs over the
+  // positives and the o-corrupted negatives, product 1 (EW) over the
+  // positives and the s-corrupted negatives -- 2 rows per positive each
+  // instead of 3 -- and a positive's WE row also gives its s-corrupted
+  // negative's partial scores (s2: that negative's s' row, bucket order)
+  int* s2;
+  int npos;
 };
 
 static int rs_tmax(int n, int M) { return n / RT_ITEMS + M + 1; }
+// deduplicated GEMM rows (RescalWs::npos): 2M segments of 2P rows in all
+static int rs_tmax_dedup(int P, int M) { return 4 * P / RT_ITEMS + 2 * M + 1; }
+// the device pair loop's epoch buckets deduplicate the GEMM rows
+// (SKGE_RS_DEDUP=0: three rows per positive, A/B)
+static bool rs_dedup_on() {
+  const char* e = getenv("SKGE_RS_DEDUP");
+  return !(e && atoi(e) == 0);
+}
 
 // dW split over K (a relation's items): at the reference's batch size a
 // relation holds ~235 items, which one workgroup per 64 x 64 dW tile walks in
@@ -145,6 +162,8 @@ static size_t rescal_ws_layout(int n, int M, int d, void* base, RescalWs* ws) {
   const size_t wpb = rs_wpart_bytes(n, M, d);
   w.wpart = wpb ? (float*)take(wpb) : nullptr;
   w.ecoef = nullptr;
+  w.s2 = nullptr;
+  w.npos = 0;
   if (ws) *ws = w;
   return off;
 }
@@ -172,12 +191,30 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
+// item of enumeration position u (-1: none).  Plain: u itself.  Deduplicated
+// epoch buckets (ws.npos == P > 0): three blocks of cpad = P rounded up to 64
+// -- the s-corrupted negatives (item P + 2j), the positives (j), the
+// o-corrupted negatives (P + 2j + 1) -- so every relation's stable bucket is
+// [s-corrupted | positives | o-corrupted]: product 1's rows (the first two
+// parts) and product 0's (the last two) are contiguous, and the blocks start
+// on chunk boundaries (their per-relation offsets are chunk prefixes)
+__device__ __forceinline__ int rs_item(int u, int P, int n, bool dedup) {
+  if (!dedup) return u < n ? u : -1;
+  const int cpad = (P + 63) & ~63;
+  const int blk = u >= 2 * cpad ? 2 : (u >= cpad ? 1 : 0), j = u - blk * cpad;
+  if (j >= P) return -1;
+  return blk == 1 ? j : P + 2 * j + (blk == 2 ? 1 : 0);
+}
+__device__ __forceinline__ int rs_nchunks(int P, int n, bool dedup) {
+  return dedup ? 3 * (((P + 63) & ~63) >> 6) : (n + 63) / 64;
+}
+
 __device__ __forceinline__ void rs_count_chunk(const int* __restrict__ pos,
                                                const int* __restrict__ neg, int P, int n, int M,
                                                const RescalWs& ws, int c) {
   const int l = lane_id();
-  const int k = c * 64 + l;
-  const int b = k < n ? item_trip(pos, neg, P, k)[2] : -1;
+  const int k = rs_item(c * 64 + l, P, n, ws.npos > 0);
+  const int b = k >= 0 ? item_trip(pos, neg, P, k)[2] : -1;
   if (M <= 64) {   // lane p owns relation p: the whole row is written, no memset
     int mine = 0;
     for (int p = 0; p < M; ++p) {
@@ -207,9 +244,10 @@ __global__ __launch_bounds__(256) void k_rs_count(const int* __restrict__ pos,
 }
 
 __device__ __forceinline__ void rs_scan_body(int n, int M, const RescalWs& ws, int* lds) {
-  int* cnt = lds;   // cnt[M], tile_base[M+1]
-  int* tbase = lds + M;
-  const int nchunks = (n + 63) / 64;
+  int* cnt = lds;   // cnt[M], tile_base[M+1] (deduplicated: then 2M segment starts, 2M
+  int* tbase = lds + M;   // lengths, 2M + 1 segment tile bases)
+  const bool dedup = ws.npos > 0;
+  const int nchunks = rs_nchunks(ws.npos, n, dedup);
   const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6, nw = blockDim.x >> 6;
   for (int p = wave; p < M; p += nw) {   // exclusive scan of relation p over the chunks
     int carry = 0;
@@ -243,6 +281,51 @@ __device__ __forceinline__ void rs_scan_body(int n, int M, const RescalWs& ws, i
     }
   }
   __syncthreads();
+  if (dedup) {   // 2M GEMM segments: product 0 of relation g, then product 1 of g - M
+    int* sst = lds + 2 * M + 1;
+    int* sln = sst + 2 * M;
+    int* sb = sln + 2 * M;
+    const int cpc = ((ws.npos + 63) & ~63) >> 6;   // chunks per enumeration block
+    for (int p = tid; p < M; p += blockDim.x) {
+      const int r0 = ws.rel_off[p];
+      const int n0 = ws.chunk[(size_t)cpc * M + p];       // s-corrupted negatives of p
+      const int n01 = ws.chunk[(size_t)2 * cpc * M + p];  // ... and its positives
+      sst[p] = r0 + n0;           // product 0: positives, o-corrupted negatives
+      sln[p] = cnt[p] - n0;
+      sst[M + p] = r0;            // product 1: s-corrupted negatives, positives
+      sln[M + p] = n01;
+    }
+    __syncthreads();
+    if (wave == 0) {
+      int toff = 0;
+      for (int g0 = 0; g0 < 2 * M; g0 += 64) {
+        const int g = g0 + l;
+        const int tv = g < 2 * M ? (sln[g] + RT_ITEMS - 1) / RT_ITEMS : 0;
+        const int tinc = wave_incl_scan(tv);
+        if (g < 2 * M) sb[g] = toff + tinc - tv;
+        toff += __shfl(tinc, 63, 64);
+      }
+      if (l == 0) {
+        sb[2 * M] = toff;
+        ws.ntiles[0] = toff;
+        ws.ntiles[1] = sb[M];   // product-0 tiles come first
+      }
+    }
+    __syncthreads();
+    const int nt2 = sb[2 * M];
+    for (int t = tid; t < nt2; t += blockDim.x) {
+      int lo = 0, hi = 2 * M - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (sb[mid] <= t) lo = mid; else hi = mid - 1;
+      }
+      const int g = lo, s = (t - sb[g]) * RT_ITEMS;
+      ws.tile_rel[t] = g < M ? g : g - M;
+      ws.tile_start[t] = sst[g] + s;
+      ws.tile_cnt[t] = min(RT_ITEMS, sln[g] - s);
+    }
+    return;
+  }
   const int nt = tbase[M];
   for (int t = tid; t < nt; t += blockDim.x) {   // tile t: relation p with tbase[p] <= t
     int lo = 0, hi = M - 1;
@@ -268,14 +351,17 @@ __device__ __forceinline__ void rs_scatter_chunk(const int* __restrict__ pos,
                                                  const int* __restrict__ neg, int P, int n, int M,
                                                  const RescalWs& ws, int c) {
   const int l = lane_id();
-  const int k = c * 64 + l;
-  const int* tr = item_trip(pos, neg, P, k < n ? k : 0);
-  const int ts = tr[0], to = tr[1], b = k < n ? tr[2] : -1;
+  const int k = rs_item(c * 64 + l, P, n, ws.npos > 0);
+  const int* tr = item_trip(pos, neg, P, k >= 0 ? k : 0);
+  const int ts = tr[0], to = tr[1], b = k >= 0 ? tr[2] : -1;
+  // deduplicated: a positive's s-corrupted negative's s' row (or -1)
+  const int ts2 = (ws.npos > 0 && k >= 0 && k < P && neg[6 * (size_t)k + 2] >= 0)
+                      ? neg[6 * (size_t)k] : -1;
   // epoch buckets (dedup lists: positive j's negatives at neg[6j .. 6j + 5]):
   // the Linear dW coefficient, gp (k0 + k1) = -(k0 + k1) for a positive and
   // gn = +1 for a negative, as k_rescal_pos_scatter computes it
   float ec = 1.0f;
-  if (ws.ecoef && k < P)
+  if (ws.ecoef && k >= 0 && k < P)
     ec = -(float)((neg[6 * (size_t)k + 2] >= 0 ? 1 : 0) + (neg[6 * (size_t)k + 5] >= 0 ? 1 : 0));
   uint64_t act = __ballot(b >= 0);
   while (act) {
@@ -290,6 +376,7 @@ __device__ __forceinline__ void rs_scatter_chunk(const int* __restrict__ pos,
       ws.sorted_o[at] = to;
       ws.bpos[k] = at;
       if (ws.ecoef) ws.ecoef[at] = ec;
+      if (ws.npos > 0) ws.s2[at] = ts2;
     }
     act &= ~m;
   }
@@ -315,7 +402,13 @@ struct RescalEpoch {
   long long stride;      // bytes between consecutive batches' bucket slices
   long long T;
   int bs, nb, M, cpb;    // cpb: 64-item chunks of a full batch
+  int dedup;             // deduplicated GEMM rows (RescalWs::npos)
 };
+
+__device__ __forceinline__ int rs_batch_count(const RescalEpoch& e, int b) {
+  const long long s0 = (long long)b * e.bs;
+  return (int)(s0 + e.bs <= e.T ? e.bs : e.T - s0);
+}
 
 __device__ __forceinline__ RescalWs rs_batch_view(const RescalEpoch& e, int b) {
   RescalWs w = e.ws0;
@@ -332,12 +425,9 @@ __device__ __forceinline__ RescalWs rs_batch_view(const RescalEpoch& e, int b) {
   w.sorted_o = sh(w.sorted_o);
   w.bpos = sh(w.bpos);
   w.ecoef = sh(w.ecoef);
+  w.s2 = sh(w.s2);
+  w.npos = e.dedup ? rs_batch_count(e, b) : 0;
   return w;
-}
-
-__device__ __forceinline__ int rs_batch_count(const RescalEpoch& e, int b) {
-  const long long s0 = (long long)b * e.bs;
-  return (int)(s0 + e.bs <= e.T ? e.bs : e.T - s0);
 }
 
 __global__ __launch_bounds__(256) void k_rs_count_ep(const int* __restrict__ pos,
@@ -346,7 +436,7 @@ __global__ __launch_bounds__(256) void k_rs_count_ep(const int* __restrict__ pos
   const int b = gw / e.cpb, c = gw - b * e.cpb;
   if (b >= e.nb) return;
   const int cnt = rs_batch_count(e, b), n = 3 * cnt;
-  if (c * 64 >= n) return;
+  if (c >= rs_nchunks(cnt, n, e.dedup != 0)) return;
   const long long s0 = (long long)b * e.bs;
   rs_count_chunk(pos + 3 * s0, neg + 6 * s0, cnt, n, e.M, rs_batch_view(e, b), c);
 }
@@ -364,7 +454,7 @@ __global__ __launch_bounds__(256) void k_rs_scatter_ep(const int* __restrict__ p
   const int b = gw / e.cpb, c = gw - b * e.cpb;
   if (b >= e.nb) return;
   const int cnt = rs_batch_count(e, b), n = 3 * cnt;
-  if (c * 64 >= n) return;
+  if (c >= rs_nchunks(cnt, n, e.dedup != 0)) return;
   const long long s0 = (long long)b * e.bs;
   rs_scatter_chunk(pos + 3 * s0, neg + 6 * s0, cnt, n, e.M, rs_batch_view(e, b), c);
 }
@@ -493,8 +583,8 @@ __global__ __launch_bounds__(1024) void k_rs_bucket_small(const int* __restrict_
 // as [KS][GC + 4]; both read conflict-free by the MFMA loop
 constexpr int SB0 = GC * (KS + 4), SB1 = KS * (GC + 4);
 constexpr int SBN = SB0 > SB1 ? SB0 : SB1;
-// one GEMM workgroup's LDS: sA [2][RT_ITEMS][KS + 4], sB [2][SBN], 3 x RT_ITEMS ints
-constexpr int GEMM_LDS_FLOATS = 2 * RT_ITEMS * (KS + 4) + 2 * SBN + 3 * RT_ITEMS;
+// one GEMM workgroup's LDS: sA [2][RT_ITEMS][KS + 4], sB [2][SBN], 4 x RT_ITEMS ints
+constexpr int GEMM_LDS_FLOATS = 2 * RT_ITEMS * (KS + 4) + 2 * SBN + 4 * RT_ITEMS;
 
 // workgroup `bid` of the GEMM grid (k_rescal_gemm, k_rescal_front_fused)
 template <bool VEC>
@@ -502,16 +592,20 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
                                                  const float* __restrict__ W, int d,
                                                  const RescalWs& ws, int bid,
                                                  float (*sA)[RT_ITEMS][KS + 4], float (*sB)[SBN],
-                                                 int* s_row, int* s_gid, int* s_es) {
+                                                 int* s_row, int* s_gid, int* s_es, int* s_es2) {
   const int ncb = (d + GC - 1) / GC;
-  const int t = bid / (2 * ncb);
+  // plain: (tile, product, column block); deduplicated (ws.npos > 0): (tile,
+  // column block), the product-0 tiles first
+  const bool dedup = ws.npos > 0;
+  const int t = dedup ? bid / ncb : bid / (2 * ncb);
   // the tile's fields and the tile count in one round trip (t < rs_tmax: the
   // fields are in bounds, read before the check, used after it)
-  const int nti = *ws.ntiles;
+  const int nti = ws.ntiles[0], nt0 = dedup ? ws.ntiles[1] : 0;
   const int p = ws.tile_rel[t], s0 = ws.tile_start[t], cnt = ws.tile_cnt[t];
   if (t >= nti) return;
-  const int rem = bid - t * 2 * ncb;
-  const int prod = rem / ncb, cb = rem - (rem / ncb) * ncb;
+  const int rem = dedup ? bid - t * ncb : bid - t * 2 * ncb;
+  const int prod = dedup ? (t < nt0 ? 0 : 1) : rem / ncb;
+  const int cb = dedup ? rem : rem - (rem / ncb) * ncb;
   const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
   const int c0 = cb * GC;
   if (tid < RT_ITEMS) {
@@ -520,6 +614,7 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
     s_row[tid] = prod == 0 ? ws.sorted_o[at] : ws.sorted_s[at];   // A rows: E[o] or E[s]
     s_es[tid] = ws.sorted_s[at];
     s_gid[tid] = ok ? ws.items[at] : -1;
+    s_es2[tid] = (dedup && prod == 0 && ok) ? ws.s2[at] : -1;
   }
   __syncthreads();
   const float* Wp = W + (size_t)p * d * d;
@@ -649,17 +744,27 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
   // epilogue: D[row 4g + reg][col] of accumulator q -> triple 16w + 4g + reg, column c0 + 16q + c
   float* out = prod == 0 ? ws.WE : ws.EW;
   const int g = l >> 4, c = l & 15;
-  float ev[4][4];
+  float ev[4][4], ev2[4][4];
+  // a row with a second subject (deduplicated: a positive's WE row also
+  // scores its s-corrupted negative); wave-uniform test, any row of the wave
+  bool two = false;
   if (prod == 0) {   // E[s_i] over the block's columns, all loads issued together
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) two = two || s_es2[wave * 16 + 4 * g + reg] >= 0;
+    two = __ballot(two) != 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) {
         const int col = c0 + q * 16 + c;
         ev[q][reg] = E[(size_t)s_es[wave * 16 + 4 * g + reg] * d + (col < d ? col : 0)];
+        if (two) {
+          const int r2 = s_es2[wave * 16 + 4 * g + reg];
+          ev2[q][reg] = E[(size_t)(r2 >= 0 ? r2 : 0) * d + (col < d ? col : 0)];
+        }
       }
   }
-  float ps[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  float ps[4] = {0.0f, 0.0f, 0.0f, 0.0f}, ps2[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int col = c0 + q * 16 + c;
@@ -668,6 +773,7 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
       const int it = wave * 16 + 4 * g + reg;
       if (it < cnt && col < d) out[(size_t)s_gid[it] * d + col] = acc[q][reg];
       if (prod == 0) ps[reg] += (col < d) ? acc[q][reg] * ev[q][reg] : 0.0f;
+      if (prod == 0 && two) ps2[reg] += (col < d) ? acc[q][reg] * ev2[q][reg] : 0.0f;
     }
   }
   if (prod == 0) {
@@ -680,6 +786,15 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
       v += __shfl_xor(v, 1, 64);
       const int it = wave * 16 + 4 * g + reg;
       if (c == 0 && it < cnt) ws.spart[(size_t)s_gid[it] * ncb + cb] = v;
+      if (two) {   // the s-corrupted negative (item npos + 2j) of positive j = s_gid
+        float v2 = ps2[reg];
+        v2 += __shfl_xor(v2, 8, 64);
+        v2 += __shfl_xor(v2, 4, 64);
+        v2 += __shfl_xor(v2, 2, 64);
+        v2 += __shfl_xor(v2, 1, 64);
+        if (c == 0 && it < cnt && s_es2[it] >= 0)
+          ws.spart[(size_t)(ws.npos + 2 * s_gid[it]) * ncb + cb] = v2;
+      }
     }
   }
 }
@@ -690,8 +805,8 @@ __global__ __launch_bounds__(256) void k_rescal_gemm(const float* __restrict__ E
                                                      RescalWs ws) {
   __shared__ float sA[2][RT_ITEMS][KS + 4];
   __shared__ float sB[2][SBN];
-  __shared__ int s_row[RT_ITEMS], s_gid[RT_ITEMS], s_es[RT_ITEMS];
-  rescal_gemm_body<VEC>(E, W, d, ws, (int)blockIdx.x, sA, sB, s_row, s_gid, s_es);
+  __shared__ int s_row[RT_ITEMS], s_gid[RT_ITEMS], s_es[RT_ITEMS], s_es2[RT_ITEMS];
+  rescal_gemm_body<VEC>(E, W, d, ws, (int)blockIdx.x, sA, sB, s_row, s_gid, s_es, s_es2);
 }
 
 // ---------------------------------------------------------------------------
@@ -809,12 +924,15 @@ __global__ __launch_bounds__(256) void k_rescal_pos_scatter(const int4* __restri
     nv += v0 + v1;
     // every row loaded (stale rows of absent negatives are not used)
     float wep[KM], ewp[KM], we0[KM], ew0[KM], we1[KM], ew1[KM], x[KM];
+    // (deduplicated GEMM rows: W E_o of (s', o, p) is positive j's row, E_s W
+    // of (s, o', p) likewise -- bitwise the same values)
+    const bool dd = ws.npos > 0;
     load_row<KM>(ws.WE, j, d, wep);
     load_row<KM>(ws.EW, j, d, ewp);
-    load_row<KM>(ws.WE, i0, d, we0);
+    load_row<KM>(ws.WE, dd ? j : i0, d, we0);
     load_row<KM>(ws.EW, i0, d, ew0);
     load_row<KM>(ws.WE, i1, d, we1);
-    load_row<KM>(ws.EW, i1, d, ew1);
+    load_row<KM>(ws.EW, dd ? j : i1, d, ew1);
     const float fv0 = (float)v0, fv1 = (float)v1;
 #pragma unroll
     for (int k = 0; k < KM; ++k) x[k] = fv0 * (gp * wep[k]) + fv1 * (gp * wep[k] + g1 * we1[k]);
@@ -1224,7 +1342,7 @@ __global__ __launch_bounds__(256) void k_rescal_front_fused(const float* __restr
     rescal_gemm_body<VEC>(E, W, d, ws, gid,
                           reinterpret_cast<float(*)[RT_ITEMS][KS + 4]>(lds),
                           reinterpret_cast<float(*)[SBN]>(sb), si, si + RT_ITEMS,
-                          si + 2 * RT_ITEMS);
+                          si + 2 * RT_ITEMS, si + 3 * RT_ITEMS);
   }
 }
 
@@ -1345,7 +1463,8 @@ static int rescal_front(hipStream_t st, const skge_table_t* ent, const skge_tabl
     hipLaunchKernelGGL(k_rs_scatter, dim3(cblocks), dim3(256), 0, st, a, b, na, n, M, ws);
   }
   const int ncb = (d + GC - 1) / GC;
-  const dim3 ggrid((unsigned)(rs_tmax(n, M) * 2 * ncb));
+  const dim3 ggrid((unsigned)(ws.npos > 0 ? rs_tmax_dedup(ws.npos, M) * ncb
+                                          : rs_tmax(n, M) * 2 * ncb));
   if ((d & 3) == 0)
     hipLaunchKernelGGL((k_rescal_gemm<true>), ggrid, dim3(256), 0, st, ent->param, rel->param, d,
                        ws);
@@ -1478,7 +1597,9 @@ int skge_rescal_pos_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
 // offsets, items, tiles, sorted rows, positions), batch b at slice b
 static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, RescalWs* ws0,
                                   long long* stride) {
-  const int n = 3 * bs, nchunks = (n + 63) / 64, tmax = rs_tmax(n, M);
+  // (sized for both enumerations: deduplicated blocks start on chunk boundaries)
+  const int n = 3 * bs, nchunks = 3 * ((bs + 63) / 64);
+  const int tmax = std::max(rs_tmax(n, M), rs_tmax_dedup(bs, M));
   size_t off = 0;
   char* p = (char*)base;
   auto take = [&](size_t bytes) {
@@ -1502,11 +1623,13 @@ static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, Resc
   w.tile_rel = (int*)take((size_t)tmax * 4);
   w.tile_start = (int*)take((size_t)tmax * 4);
   w.tile_cnt = (int*)take((size_t)tmax * 4);
-  w.ntiles = (int*)take(4);
+  w.ntiles = (int*)take(8);   // tiles; deduplicated: also the product-0 tiles
   w.sorted_s = (int*)take((size_t)n * 4);
   w.sorted_o = (int*)take((size_t)n * 4);
   w.bpos = (int*)take((size_t)n * 4);
   w.ecoef = (float*)take((size_t)n * 4);
+  w.s2 = (int*)take((size_t)n * 4);
+  w.npos = 0;   // (set per batch: rs_batch_view)
   const size_t slice = off - s0;
   if (ws0) *ws0 = w;
   if (stride) *stride = (long long)slice;
@@ -1526,7 +1649,8 @@ static RescalEpoch rescal_epoch_view(void* ws, long long T, int bs, int nb, int 
   e.bs = bs;
   e.nb = nb;
   e.M = M;
-  e.cpb = (3 * bs + 63) / 64;
+  e.dedup = rs_dedup_on() ? 1 : 0;
+  e.cpb = e.dedup ? 3 * ((bs + 63) / 64) : (3 * bs + 63) / 64;
   return e;
 }
 
@@ -1539,8 +1663,8 @@ int rescal_epoch_bucket(hipStream_t st, const int* pos, const int* neg, long lon
   const long long waves = (long long)nb * e.cpb;
   const unsigned blocks = (unsigned)((waves + 3) / 4);
   hipLaunchKernelGGL(k_rs_count_ep, dim3(blocks), dim3(256), 0, st, pos, neg, e);
-  hipLaunchKernelGGL(k_rs_scan_ep, dim3((unsigned)nb), dim3(1024), (size_t)(2 * M + 1) * sizeof(int),
-                     st, e);
+  hipLaunchKernelGGL(k_rs_scan_ep, dim3((unsigned)nb), dim3(1024),
+                     (size_t)(e.dedup ? 8 * M + 2 : 2 * M + 1) * sizeof(int), st, e);
   hipLaunchKernelGGL(k_rs_scatter_ep, dim3(blocks), dim3(256), 0, st, pos, neg, e);
   SKGE_CHECK_LAUNCH("rescal epoch bucketing");
   return SKGE_OK;
@@ -1580,13 +1704,16 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
   w.sorted_o = sh(w.sorted_o);
   w.bpos = sh(w.bpos);
   w.ecoef = sh(w.ecoef);
+  w.s2 = sh(w.s2);
+  w.npos = e.dedup ? count : 0;
   const int n = 3 * count, M = rel->rows;
   const int fsplits = af == AF_LINEAR ? rs_front_splits(n, M, d) : 0;
   const int blocks = std::max(1, std::min((count + 3) / 4, 16384));
   if (fsplits > 0) {   // k_rescal_front_fused: dW contraction and GEMMs in one launch
     const int nt = (d + WG_T - 1) / WG_T, ncb = (d + GC - 1) / GC;
     const int nwg = M * nt * nt * fsplits;
-    const dim3 grid((unsigned)(nwg + rs_tmax(n, M) * 2 * ncb));
+    const dim3 grid((unsigned)(nwg + (w.npos > 0 ? rs_tmax_dedup(count, M) * ncb
+                                                  : rs_tmax(n, M) * 2 * ncb)));
     // workgroup order of the two roles (k_rescal_front_fused): the GEMM grid
     // first (A/B on WN18 d = 200: 29.25 M vs 29.0 M triples/s with the dW
     // grid first, 29.2 M interleaving one dW workgroup in three)

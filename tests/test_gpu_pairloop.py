@@ -507,3 +507,39 @@ def test_rescal_fused_front_matches_unfused(n_ent, n_rel, T, d, nb, fsplit, orde
     for pid in out[0][1]:
         np.testing.assert_allclose(out[1][1][pid], out[0][1][pid], rtol=RTOL, atol=ATOL,
                                    err_msg=pid)
+
+
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb,af", [
+    (300, 7, 2000, 16, 7, "linear"),          # ragged remainder batch, fused front
+    (300, 7, 2000, 30, 3, "sigmoid"),         # d % 4 != 0, unfused kernels (scores drive dW)
+    (200, 3, 130, 24, 2, "linear"),           # batches of < 64 positives (padded blocks)
+    (40943, 18, 14140, 200, 10, "linear"),    # WN18 entity / relation counts, d, batch size
+    (40943, 18, 14140, 200, 10, "sigmoid"),
+])
+def test_rescal_dedup_gemm_rows_match_three_rows(n_ent, n_rel, T, d, nb, af, monkeypatch):
+    """The RESCAL pair loop's deduplicated GEMM rows (W E_o once per (o, p) of a
+    positive and its s-corrupted negative, E_s W once per (s, p) of a positive
+    and its o-corrupted negative: 2 rows per positive and product instead of
+    3) against three rows per positive (SKGE_RS_DEDUP=0) on the same draws:
+    the scores are the same values, so violation totals are equal; dW sums
+    its items in another bucket order, so parameters agree to fp32 rounding."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    xs = make_kg(n_ent, n_rel, T, seed=5)
+    out = []
+    for dedup in ("0", "1"):
+        monkeypatch.setenv("SKGE_RS_DEDUP", dedup)
+        np.random.seed(42)
+        m = S.RESCAL((n_ent, n_ent, n_rel), d, rparam=0.05, af=af)
+        m.add_hyperparam("margin", 0.2)
+        upd = {pid: S.SGD(p, 0.1) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), nb, seed=7)
+        with torch.cuda.stream(r.stream):
+            r.run(2)
+        r.synchronize()
+        out.append((int(r.nviol_total.item()),
+                    {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}))
+    assert out[0][0] == out[1][0] > 0
+    for pid in out[0][1]:
+        np.testing.assert_allclose(out[1][1][pid], out[0][1][pid], rtol=RTOL, atol=ATOL,
+                                   err_msg=pid)
