@@ -1332,6 +1332,12 @@ __global__ __launch_bounds__(256) void k_rescal_front_fused(const float* __restr
     if (bid - k * order == 0 && k < nwg) wid = k;
     gid = bid - min((bid + order - 1) / order, nwg);
   }
+#ifdef SKGE_ABL_FRONT_NODW   // timing-only ablations (tools/ablate.sh): one role only
+  if (wid >= 0) return;
+#endif
+#ifdef SKGE_ABL_FRONT_NOGEMM
+  if (wid < 0) return;
+#endif
   if (wid >= 0) {
     rescal_wgrad_part_body<VEC>(E, d, ws, ws.ecoef, splits, wid,
                                 reinterpret_cast<float(*)[WG_T + 4]>(lds),
