@@ -133,6 +133,7 @@ int launch_hole_pos(hipStream_t st, int af, const skge_table_t* ent, const skge_
 struct WStep {
   const float* part;      // [M][nt * nt][splits][64 * 64]
   const int* rel_off;     // [M + 1] the batch's relation bucket offsets
+  const int* dwcnt;       // [M] dW items per relation (combined dW), or nullptr: the buckets
   float* W;
   float* A;               // AdaGrad state or nullptr
   int* ucnt;              // optional updateCounts

@@ -70,6 +70,12 @@ struct RescalWs {
   // negative's partial scores (s2: that negative's s' row, bucket order)
   int* s2;
   int npos;
+  // deduplicated buckets, combined dW (fused front): a positive's items enter
+  // dW as ONE outer product E_s (x) (ecoef E_o + E_o') -- its o-corrupted
+  // negative folded in (o2: that negative's o' row, or -1) -- so dW runs over
+  // product 1's rows, n01[p] items of relation p from rel_off[p]
+  int* o2;
+  int* n01;
 };
 
 static int rs_tmax(int n, int M) { return n / RT_ITEMS + M + 1; }
@@ -164,6 +170,8 @@ static size_t rescal_ws_layout(int n, int M, int d, void* base, RescalWs* ws) {
   w.ecoef = nullptr;
   w.s2 = nullptr;
   w.npos = 0;
+  w.o2 = nullptr;
+  w.n01 = nullptr;
   if (ws) *ws = w;
   return off;
 }
@@ -294,6 +302,7 @@ __device__ __forceinline__ void rs_scan_body(int n, int M, const RescalWs& ws, i
       sln[p] = cnt[p] - n0;
       sst[M + p] = r0;            // product 1: s-corrupted negatives, positives
       sln[M + p] = n01;
+      ws.n01[p] = n01;            // (the combined dW's items)
     }
     __syncthreads();
     if (wave == 0) {
@@ -357,6 +366,9 @@ __device__ __forceinline__ void rs_scatter_chunk(const int* __restrict__ pos,
   // deduplicated: a positive's s-corrupted negative's s' row (or -1)
   const int ts2 = (ws.npos > 0 && k >= 0 && k < P && neg[6 * (size_t)k + 2] >= 0)
                       ? neg[6 * (size_t)k] : -1;
+  // ... and its o-corrupted negative's o' row (or -1)
+  const int to2 = (ws.npos > 0 && k >= 0 && k < P && neg[6 * (size_t)k + 5] >= 0)
+                      ? neg[6 * (size_t)k + 4] : -1;
   // epoch buckets (dedup lists: positive j's negatives at neg[6j .. 6j + 5]):
   // the Linear dW coefficient, gp (k0 + k1) = -(k0 + k1) for a positive and
   // gn = +1 for a negative, as k_rescal_pos_scatter computes it
@@ -376,7 +388,10 @@ __device__ __forceinline__ void rs_scatter_chunk(const int* __restrict__ pos,
       ws.sorted_o[at] = to;
       ws.bpos[k] = at;
       if (ws.ecoef) ws.ecoef[at] = ec;
-      if (ws.npos > 0) ws.s2[at] = ts2;
+      if (ws.npos > 0) {
+        ws.s2[at] = ts2;
+        ws.o2[at] = to2;
+      }
     }
     act &= ~m;
   }
@@ -426,6 +441,8 @@ __device__ __forceinline__ RescalWs rs_batch_view(const RescalEpoch& e, int b) {
   w.bpos = sh(w.bpos);
   w.ecoef = sh(w.ecoef);
   w.s2 = sh(w.s2);
+  w.o2 = sh(w.o2);
+  w.n01 = sh(w.n01);
   w.npos = e.dedup ? rs_batch_count(e, b) : 0;
   return w;
 }
@@ -1197,7 +1214,9 @@ static_assert(WS_TILE == WG_T && WS_GROUP == WG_PF * WG_CH, "split-K group geome
 // workgroup `bid` of the split-K dW grid (k_rescal_wgrad_part,
 // k_rescal_front_fused); coef: the items' dW coefficients in bucket order
 constexpr int WPART_LDS_FLOATS = 2 * WG_CH * (WG_T + 4);
-template <bool VEC>
+// COMB: the combined dW of deduplicated buckets (RescalWs::o2): items are
+// product 1's rows, A = E_s unscaled, B = coef E_o + E_o2
+template <bool VEC, bool COMB = false>
 __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__ E, int d,
                                                        const RescalWs& ws,
                                                        const float* __restrict__ coef, int splits,
@@ -1209,7 +1228,7 @@ __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__
   const int rem = blk - p * nt * nt;
   const int rt = rem / nt, ct = rem - (rem / nt) * nt;
   const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
-  const int off = ws.rel_off[p], cnt = ws.rel_off[p + 1] - off;
+  const int off = ws.rel_off[p], cnt = COMB ? ws.n01[p] : ws.rel_off[p + 1] - off;
   const int nch = (cnt + WG_CH - 1) / WG_CH, ngr = (nch + WG_PF - 1) / WG_PF;
   if (sp >= ngr) return;   // no group for this split (the finishing kernel knows)
   const int r0 = rt * WG_T, c0 = ct * WG_T;
@@ -1219,7 +1238,7 @@ __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__
   const int it = tid / WG_TPI, h = (tid % WG_TPI) * WG_FPT;
   for (int gr = sp; gr < ngr; gr += splits) {
     const int g0 = gr * WG_PF;
-    int ns[WG_PF], no[WG_PF];
+    int ns[WG_PF], no[WG_PF], no2[WG_PF];
     float nc[WG_PF];
 #pragma unroll
     for (int q = 0; q < WG_PF; ++q) {
@@ -1228,23 +1247,29 @@ __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__
       ns[q] = ws.sorted_s[at];
       no[q] = ws.sorted_o[at];
       nc[q] = i < cnt ? coef[at] : 0.0f;
+      if (COMB) no2[q] = i < cnt ? ws.o2[at] : -1;
     }
-    float4 es[WG_PF][WG_FPT / 4], eo[WG_PF][WG_FPT / 4];
+    float4 es[WG_PF][WG_FPT / 4], eo[WG_PF][WG_FPT / 4], eo2[WG_PF][WG_FPT / 4];
 #pragma unroll
     for (int q = 0; q < WG_PF; ++q) {
       const float* srow = E + (size_t)ns[q] * d;
       const float* orow = E + (size_t)no[q] * d;
+      const float* o2row = E + (size_t)(COMB && no2[q] >= 0 ? no2[q] : 0) * d;
 #pragma unroll
       for (int m = 0; m < WG_FPT / 4; ++m) {
         const int cs = r0 + h + 4 * m, co = c0 + h + 4 * m;
         if (VEC) {
           es[q][m] = *reinterpret_cast<const float4*>(srow + (cs < d ? cs : 0));
           eo[q][m] = *reinterpret_cast<const float4*>(orow + (co < d ? co : 0));
+          if (COMB) eo2[q][m] = *reinterpret_cast<const float4*>(o2row + (co < d ? co : 0));
         } else {
           es[q][m] = make_float4(srow[cs < d ? cs : 0], srow[cs + 1 < d ? cs + 1 : 0],
                                  srow[cs + 2 < d ? cs + 2 : 0], srow[cs + 3 < d ? cs + 3 : 0]);
           eo[q][m] = make_float4(orow[co < d ? co : 0], orow[co + 1 < d ? co + 1 : 0],
                                  orow[co + 2 < d ? co + 2 : 0], orow[co + 3 < d ? co + 3 : 0]);
+          if (COMB)
+            eo2[q][m] = make_float4(o2row[co < d ? co : 0], o2row[co + 1 < d ? co + 1 : 0],
+                                    o2row[co + 2 < d ? co + 2 : 0], o2row[co + 3 < d ? co + 3 : 0]);
         }
       }
     }
@@ -1258,14 +1283,27 @@ __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__
         const int cs = r0 + h + 4 * m, co = c0 + h + 4 * m;
         float4 a = es[q][m], o = eo[q][m];
         const float cur_c = nc[q];
-        a.x = cs + 0 < d ? cur_c * a.x : 0.0f;
-        a.y = cs + 1 < d ? cur_c * a.y : 0.0f;
-        a.z = cs + 2 < d ? cur_c * a.z : 0.0f;
-        a.w = cs + 3 < d ? cur_c * a.w : 0.0f;
-        o.x = co + 0 < d ? o.x : 0.0f;
-        o.y = co + 1 < d ? o.y : 0.0f;
-        o.z = co + 2 < d ? o.z : 0.0f;
-        o.w = co + 3 < d ? o.w : 0.0f;
+        if (COMB) {   // A = E_s, B = coef E_o + E_o2
+          const bool two = no2[q] >= 0;
+          const float4 o2 = eo2[q][m];
+          a.x = cs + 0 < d ? a.x : 0.0f;
+          a.y = cs + 1 < d ? a.y : 0.0f;
+          a.z = cs + 2 < d ? a.z : 0.0f;
+          a.w = cs + 3 < d ? a.w : 0.0f;
+          o.x = co + 0 < d ? cur_c * o.x + (two ? o2.x : 0.0f) : 0.0f;
+          o.y = co + 1 < d ? cur_c * o.y + (two ? o2.y : 0.0f) : 0.0f;
+          o.z = co + 2 < d ? cur_c * o.z + (two ? o2.z : 0.0f) : 0.0f;
+          o.w = co + 3 < d ? cur_c * o.w + (two ? o2.w : 0.0f) : 0.0f;
+        } else {
+          a.x = cs + 0 < d ? cur_c * a.x : 0.0f;
+          a.y = cs + 1 < d ? cur_c * a.y : 0.0f;
+          a.z = cs + 2 < d ? cur_c * a.z : 0.0f;
+          a.w = cs + 3 < d ? cur_c * a.w : 0.0f;
+          o.x = co + 0 < d ? o.x : 0.0f;
+          o.y = co + 1 < d ? o.y : 0.0f;
+          o.z = co + 2 < d ? o.z : 0.0f;
+          o.w = co + 3 < d ? o.w : 0.0f;
+        }
         *reinterpret_cast<float4*>(&sEs[it][h + 4 * m]) = a;
         *reinterpret_cast<float4*>(&sEo[it][h + 4 * m]) = o;
       }
@@ -1311,7 +1349,7 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_part(const float* __restri
 // ---------------------------------------------------------------------------
 constexpr int FRONT_LDS_FLOATS =
     GEMM_LDS_FLOATS > WPART_LDS_FLOATS ? GEMM_LDS_FLOATS : WPART_LDS_FLOATS;
-template <bool VEC>
+template <bool VEC, bool COMB>
 __global__ __launch_bounds__(256) void k_rescal_front_fused(const float* __restrict__ E,
                                                             const float* __restrict__ W, int d,
                                                             RescalWs ws, int splits, int nwg,
@@ -1339,7 +1377,7 @@ __global__ __launch_bounds__(256) void k_rescal_front_fused(const float* __restr
   if (wid < 0) return;
 #endif
   if (wid >= 0) {
-    rescal_wgrad_part_body<VEC>(E, d, ws, ws.ecoef, splits, wid,
+    rescal_wgrad_part_body<VEC, COMB>(E, d, ws, ws.ecoef, splits, wid,
                                 reinterpret_cast<float(*)[WG_T + 4]>(lds),
                                 reinterpret_cast<float(*)[WG_T + 4]>(lds + WG_CH * (WG_T + 4)));
   } else {
@@ -1635,6 +1673,8 @@ static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, Resc
   w.bpos = (int*)take((size_t)n * 4);
   w.ecoef = (float*)take((size_t)n * 4);
   w.s2 = (int*)take((size_t)n * 4);
+  w.o2 = (int*)take((size_t)n * 4);
+  w.n01 = (int*)take((size_t)M * 4);
   w.npos = 0;   // (set per batch: rs_batch_view)
   const size_t slice = off - s0;
   if (ws0) *ws0 = w;
@@ -1711,6 +1751,8 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
   w.bpos = sh(w.bpos);
   w.ecoef = sh(w.ecoef);
   w.s2 = sh(w.s2);
+  w.o2 = sh(w.o2);
+  w.n01 = sh(w.n01);
   w.npos = e.dedup ? count : 0;
   const int n = 3 * count, M = rel->rows;
   const int fsplits = af == AF_LINEAR ? rs_front_splits(n, M, d) : 0;
@@ -1729,18 +1771,27 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
       order = std::min<long long>(order, (long long)grid.x / nwg);
       if (order < 2) order = 0;
     }
-    if ((d & 3) == 0)
-      hipLaunchKernelGGL((k_rescal_front_fused<true>), grid, dim3(256), 0, st, ent->param,
-                         rel->param, d, w, fsplits, nwg, order);
-    else
-      hipLaunchKernelGGL((k_rescal_front_fused<false>), grid, dim3(256), 0, st, ent->param,
-                         rel->param, d, w, fsplits, nwg, order);
+    // combined dW: a positive's two outer products over E_s as one (SKGE_RS_DW2=0: three items)
+    // (the separate finishing kernel counts a relation's items by its bucket)
+    const char* c2 = getenv("SKGE_RS_DW2");
+    const char* sep = getenv("SKGE_RS_WSTEP_SEP");   // A/B: the W step in its own launch
+    const bool wstep_in_apply = wstep && !(sep && atoi(sep));
+    const bool comb = w.npos > 0 && wstep_in_apply && !(c2 && atoi(c2) == 0);
+#define SKGE_FRONT(V, C)                                                                          \
+  hipLaunchKernelGGL((k_rescal_front_fused<V, C>), grid, dim3(256), 0, st, ent->param, rel->param, \
+                     d, w, fsplits, nwg, order)
+    if ((d & 3) == 0) {
+      if (comb) SKGE_FRONT(true, true); else SKGE_FRONT(true, false);
+    } else {
+      if (comb) SKGE_FRONT(false, true); else SKGE_FRONT(false, false);
+    }
+#undef SKGE_FRONT
     SKGE_KM_SWITCH(k_rescal_pos_scatter, dim3(blocks), dim3(256), 0, st, rec, rec_n1, start,
                    count, d, af, margin, w, accum_of(ent), nviol)
-    const char* sep = getenv("SKGE_RS_WSTEP_SEP");   // A/B: the W step in its own launch
-    if (wstep && !(sep && atoi(sep))) {   // the caller's entity apply runs the W step
-      *wstep = WStep{w.wpart, w.rel_off, rel->param, rel->state, rel->upd_count, nviol, M, d,
-                     fsplits, rel->opt, rel->lr, rel->rin, rel->rout, rel->fixed_div};
+    if (wstep_in_apply) {   // the caller's entity apply runs the W step
+      *wstep = WStep{w.wpart, w.rel_off, comb ? w.n01 : nullptr, rel->param, rel->state,
+                     rel->upd_count, nviol, M, d, fsplits, rel->opt, rel->lr, rel->rin, rel->rout,
+                     rel->fixed_div};
     } else {
       WApply wa = {rel->param, rel->state, rel->opt, rel->lr, rel->rin, rel->rout,
                    rel->fixed_div, nviol, rel->upd_count};

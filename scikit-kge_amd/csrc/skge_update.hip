@@ -753,9 +753,10 @@ __device__ __forceinline__ void wstep_quad(const WStep& w, long long q) {
   const int r = rt * WS_T + e / WS_T, c = ct * WS_T + e % WS_T;
   if (r >= w.d || c >= w.d) return;
   if (tile == 0 && e == 0 && w.opt == OPT_ADAGRAD && w.ucnt) w.ucnt[p] += 1;   // param.py:149-150
-  // split-K groups of 128 items (skge_rescal.hip WS_GROUP): splits past the
-  // relation's groups wrote nothing
-  const int ngr = (cnt + 127) / 128, nsp = min(w.splits, ngr);
+  // split-K groups of 128 of the relation's dW items (skge_rescal.hip
+  // WS_GROUP): splits past its groups wrote nothing
+  const int nit = w.dwcnt ? w.dwcnt[p] : cnt;
+  const int ngr = (nit + 127) / 128, nsp = min(w.splits, ngr);
   const float* part = w.part + ((size_t)(p * nt * nt + tile) * w.splits) * (WS_T * WS_T) + e;
   float4 s = *reinterpret_cast<const float4*>(part);
   const size_t o = (size_t)p * w.d * w.d + (size_t)r * w.d + c;

@@ -543,3 +543,36 @@ def test_rescal_dedup_gemm_rows_match_three_rows(n_ent, n_rel, T, d, nb, af, mon
     for pid in out[0][1]:
         np.testing.assert_allclose(out[1][1][pid], out[0][1][pid], rtol=RTOL, atol=ATOL,
                                    err_msg=pid)
+
+
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb", [
+    (300, 7, 2000, 16, 7),          # ragged remainder batch
+    (300, 5, 2000, 30, 3),          # d % 4 != 0
+    (3000, 3, 6000, 40, 2),         # >= 4 item groups per relation: split-K partial tiles
+    (40943, 18, 14140, 200, 10),    # WN18 entity / relation counts, d, batch size
+])
+def test_rescal_combined_dw_matches_three_items(n_ent, n_rel, T, d, nb, monkeypatch):
+    """The fused front's combined dW (a positive and its o-corrupted negative
+    as ONE outer product E_s (x) (-(k0 + k1) E_o + E_o'), its s-corrupted
+    negative as E_s' (x) E_o: two outer products per positive instead of
+    three) against three items per positive (SKGE_RS_DW2=0) on the same
+    draws: equal violation totals, parameters within the fp32 tolerance."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    xs = make_kg(n_ent, n_rel, T, seed=9)
+    out = []
+    for dw2 in ("0", "1"):
+        monkeypatch.setenv("SKGE_RS_DW2", dw2)
+        m = make_model("rescal", (n_ent, n_ent, n_rel), d)
+        m.add_hyperparam("margin", 0.2)
+        upd = {pid: S.SGD(p, 0.1) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), nb, seed=8)
+        with torch.cuda.stream(r.stream):
+            r.run(2)
+        r.synchronize()
+        out.append((int(r.nviol_total.item()),
+                    {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}))
+    assert out[0][0] == out[1][0] > 0
+    for pid in out[0][1]:
+        np.testing.assert_allclose(out[1][1][pid], out[0][1][pid], rtol=RTOL, atol=ATOL,
+                                   err_msg=pid)
