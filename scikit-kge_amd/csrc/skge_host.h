@@ -140,8 +140,17 @@ struct WStep {
   const int* gate;        // the batch's violation count
   int M, d, splits, opt;
   float lr, rin, rout, fdiv;
+  // the W step done inside the fused front, speculatively into the other
+  // buffer (one dW split per tile): the apply only makes it current when the
+  // batch has violations (*cur ^= 1); cur == nullptr: the step above
+  int* cur;               // 0: W_b in W / A (the caller's), 1: in W1 / A1
+  float* W1;
+  float* A1;
 };
 int apply_with_wstep(hipStream_t st, const skge_table_t* ent, int nslots, const WStep& w);
+// end of an epoch with the in-front W step: the current buffer back into the
+// caller's W / state, cur = 0 (skge_rescal.hip)
+int rescal_w_sync(hipStream_t st, const WStep& w);
 
 }  // namespace skge
 

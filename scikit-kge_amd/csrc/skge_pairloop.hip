@@ -201,6 +201,7 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
     if (!rc && rep) rc = rescal_epoch_bucket(st, pos, neg, (long long)T, (int)bs, nb, rel->rows, d,
                                              r->ws);
   }
+  WStep wsync{};   // RESCAL with the in-front W step: synced back at the epoch's end
   for (int k = 0; k < nb && !rc; ++k) {
     const long long start = batches[k].first;
     const int count = (int)batches[k].second;
@@ -227,12 +228,14 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
         te.gate = gate;
         const int ns = 4 * count;
         rc = wst.part ? apply_with_wstep(st, &te, ns, wst) : skge_accum_apply(stream, &te, 1, &ns);
+        if (wst.cur) wsync = wst;
       }
     } else {
       rc = skge_pair_step(stream, model, af, ent, rel, d, pos + 6 * start, neg + 6 * start,
                           2 * count, margin, r->ws, r->ws_bytes, gate);
     }
   }
+  if (!rc && wsync.cur) rc = rescal_w_sync(st, wsync);
   if (!rc) {
     hipLaunchKernelGGL(k_pairs_epoch_end, dim3(1), dim3(256), 0, st, r->nviol, nb, nviol_total,
                        epoch_key);

@@ -76,6 +76,23 @@ struct RescalWs {
   // product 1's rows, n01[p] items of relation p from rel_off[p]
   int* o2;
   int* n01;
+  // the in-front W step's second W / state buffer and the current-buffer
+  // word (WStep::cur; epoch buckets, or null)
+  float* W1;
+  float* A1;
+  int* wcur;
+};
+
+// the fused front's in-front W step (WStep::cur): W_b is in buffer *cur
+// (0: W0 / A0 = the caller's); the dW workgroups write W_{b+1} into the other
+struct WFront {
+  const int* cur;   // nullptr: off
+  float* W0;
+  float* A0;
+  float* W1;
+  float* A1;
+  int opt;
+  float lr, rin, rout, fdiv;
 };
 
 static int rs_tmax(int n, int M) { return n / RT_ITEMS + M + 1; }
@@ -172,6 +189,8 @@ static size_t rescal_ws_layout(int n, int M, int d, void* base, RescalWs* ws) {
   w.npos = 0;
   w.o2 = nullptr;
   w.n01 = nullptr;
+  w.W1 = w.A1 = nullptr;
+  w.wcur = nullptr;
   if (ws) *ws = w;
   return off;
 }
@@ -461,6 +480,8 @@ __global__ __launch_bounds__(256) void k_rs_count_ep(const int* __restrict__ pos
 __global__ __launch_bounds__(1024) void k_rs_scan_ep(RescalEpoch e) {
   extern __shared__ int lds[];
   const int b = blockIdx.x;
+  // the epoch starts with W in the caller's buffer (the in-front W step's word)
+  if (e.ws0.wcur && b == 0 && threadIdx.x == 0) *e.ws0.wcur = 0;
   rs_scan_body(3 * rs_batch_count(e, b), e.M, rs_batch_view(e, b), lds);
 }
 
@@ -1216,22 +1237,53 @@ static_assert(WS_TILE == WG_T && WS_GROUP == WG_PF * WG_CH, "split-K group geome
 constexpr int WPART_LDS_FLOATS = 2 * WG_CH * (WG_T + 4);
 // COMB: the combined dW of deduplicated buckets (RescalWs::o2): items are
 // product 1's rows, A = E_s unscaled, B = coef E_o + E_o2
-template <bool VEC, bool COMB = false>
+// IF: one split, and the tile's W step written into the other buffer (WFront)
+// instead of the partial tile; a relation without items copies its tile over
+template <bool VEC, bool COMB = false, bool IF = false>
 __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__ E, int d,
                                                        const RescalWs& ws,
                                                        const float* __restrict__ coef, int splits,
                                                        int bid, float (*sEs)[WG_T + 4],
-                                                       float (*sEo)[WG_T + 4]) {
+                                                       float (*sEo)[WG_T + 4],
+                                                       const WFront& wf = WFront{}) {
   const int nt = (d + WG_T - 1) / WG_T;
   const int blk = bid / splits, sp = bid - (bid / splits) * splits;
   const int p = blk / (nt * nt);
   const int rem = blk - p * nt * nt;
   const int rt = rem / nt, ct = rem - (rem / nt) * nt;
   const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
-  const int off = ws.rel_off[p], cnt = COMB ? ws.n01[p] : ws.rel_off[p + 1] - off;
+  const int off = ws.rel_off[p], cntb = ws.rel_off[p + 1] - off;
+  const int cnt = COMB ? ws.n01[p] : cntb;
   const int nch = (cnt + WG_CH - 1) / WG_CH, ngr = (nch + WG_PF - 1) / WG_PF;
-  if (sp >= ngr) return;   // no group for this split (the finishing kernel knows)
   const int r0 = rt * WG_T, c0 = ct * WG_T;
+  // IF: the W updater's operands, element e = 4 j + reg of the tile: row r0 +
+  // 16 wave + 4 (l >> 4) + reg, column c0 + 16 j + (l & 15) (as
+  // k_rescal_wgrad_mfma); loaded after the contraction (held across it they
+  // would cost the launch a wave per SIMD)
+  const bool ada = wf.opt == OPT_ADAGRAD;
+  auto w_elem = [&](int e, size_t& o) {
+    const int r = r0 + 16 * wave + 4 * (l >> 4) + (e & 3), cc = c0 + 16 * (e >> 2) + (l & 15);
+    o = (size_t)p * d * d + (size_t)(r < d ? r : 0) * d + (cc < d ? cc : 0);
+    return r < d && cc < d;
+  };
+  if (sp >= ngr) {   // no group for this split (the finishing kernel knows)
+    if (IF && cnt == 0) {   // relation not in the batch: W_{b+1}[p] = W_b[p]
+      const int cur = *wf.cur;
+      const float* Wr = cur ? wf.W1 : wf.W0;
+      const float* Ar = cur ? wf.A1 : wf.A0;
+      float* Ww = cur ? wf.W0 : wf.W1;
+      float* Aw = cur ? wf.A0 : wf.A1;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        size_t o;
+        if (w_elem(e, o)) {
+          Ww[o] = Wr[o];
+          if (ada) Aw[o] = Ar[o];
+        }
+      }
+    }
+    return;
+  }
   f32x4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -1319,6 +1371,39 @@ __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__
       }
     }
   }
+  if (IF) {   // the W updater's step (skge/param.py:115-155) into the other buffer
+    const int cur = *wf.cur;
+    const float* Wr = cur ? wf.W1 : wf.W0;
+    const float* Ar = cur ? wf.A1 : wf.A0;
+    float* Ww = cur ? wf.W0 : wf.W1;
+    float* Aw = cur ? wf.A0 : wf.A1;
+    float pv[16], av[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {   // every load of the tile issued before any use
+      size_t o;
+      w_elem(e, o);
+      pv[e] = Wr[o];
+      av[e] = ada ? Ar[o] : 0.0f;
+    }
+    const float div = wf.fdiv > 0.0f ? wf.fdiv : (float)cntb;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float g = (acc[e >> 2][e & 3] + wf.rin * pv[e]) / div + wf.rout * pv[e];
+      float w, a2 = av[e];
+      if (ada) {
+        a2 = av[e] + g * g;
+        w = pv[e] - (wf.lr * g) / fmaxf(sqrtf(a2), 1e-7f);
+      } else {
+        w = pv[e] - wf.lr * g;
+      }
+      size_t o;
+      if (w_elem(e, o)) {
+        Ww[o] = w;
+        if (ada) Aw[o] = a2;
+      }
+    }
+    return;
+  }
   // D[row 16 wave + 4 (l >> 4) + reg][col 16 j + (l & 15)] -> the partial tile
   float* out = ws.wpart + ((size_t)blk * splits + sp) * (WG_T * WG_T);
 #pragma unroll
@@ -1349,11 +1434,11 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_part(const float* __restri
 // ---------------------------------------------------------------------------
 constexpr int FRONT_LDS_FLOATS =
     GEMM_LDS_FLOATS > WPART_LDS_FLOATS ? GEMM_LDS_FLOATS : WPART_LDS_FLOATS;
-template <bool VEC, bool COMB>
+template <bool VEC, bool COMB, bool IF>
 __global__ __launch_bounds__(256) void k_rescal_front_fused(const float* __restrict__ E,
                                                             const float* __restrict__ W, int d,
                                                             RescalWs ws, int splits, int nwg,
-                                                            int order) {
+                                                            int order, WFront wf) {
   __shared__ __attribute__((aligned(16))) float lds[FRONT_LDS_FLOATS];
   const int bid = (int)blockIdx.x, ng = (int)gridDim.x - nwg;
   // role of workgroup bid: order 0 = the dW grid first, 1 = the GEMM grid
@@ -1377,13 +1462,14 @@ __global__ __launch_bounds__(256) void k_rescal_front_fused(const float* __restr
   if (wid < 0) return;
 #endif
   if (wid >= 0) {
-    rescal_wgrad_part_body<VEC, COMB>(E, d, ws, ws.ecoef, splits, wid,
+    rescal_wgrad_part_body<VEC, COMB, IF>(E, d, ws, ws.ecoef, splits, wid,
                                 reinterpret_cast<float(*)[WG_T + 4]>(lds),
-                                reinterpret_cast<float(*)[WG_T + 4]>(lds + WG_CH * (WG_T + 4)));
+                                reinterpret_cast<float(*)[WG_T + 4]>(lds + WG_CH * (WG_T + 4)), wf);
   } else {
     float* sb = lds + 2 * RT_ITEMS * (KS + 4);
     int* si = reinterpret_cast<int*>(sb + 2 * SBN);
-    rescal_gemm_body<VEC>(E, W, d, ws, gid,
+    const float* Wb = IF && *wf.cur ? wf.W1 : W;   // W_b's buffer
+    rescal_gemm_body<VEC>(E, Wb, d, ws, gid,
                           reinterpret_cast<float(*)[RT_ITEMS][KS + 4]>(lds),
                           reinterpret_cast<float(*)[SBN]>(sb), si, si + RT_ITEMS,
                           si + 2 * RT_ITEMS, si + 3 * RT_ITEMS);
@@ -1660,6 +1746,11 @@ static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, Resc
   // partial tiles even at one split
   const size_t wpb = std::max(rs_wpart_bytes(n, M, d), rs_front_wpart_bytes(n, M, d));
   w.wpart = wpb ? (float*)take(wpb) : nullptr;
+  // the in-front W step's second buffers (up to 256 MB)
+  const bool wb = (size_t)M * d * d * 8 <= (256u << 20);
+  w.W1 = wb ? (float*)take((size_t)M * d * d * 4) : nullptr;
+  w.A1 = wb ? (float*)take((size_t)M * d * d * 4) : nullptr;
+  w.wcur = wb ? (int*)take(4) : nullptr;
   const size_t s0 = off;
   w.chunk = (int*)take((size_t)nchunks * M * 4);
   w.rel_off = (int*)take((size_t)(M + 1) * 4);
@@ -1777,13 +1868,28 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
     const char* sep = getenv("SKGE_RS_WSTEP_SEP");   // A/B: the W step in its own launch
     const bool wstep_in_apply = wstep && !(sep && atoi(sep));
     const bool comb = w.npos > 0 && wstep_in_apply && !(c2 && atoi(c2) == 0);
-#define SKGE_FRONT(V, C)                                                                          \
-  hipLaunchKernelGGL((k_rescal_front_fused<V, C>), grid, dim3(256), 0, st, ent->param, rel->param, \
-                     d, w, fsplits, nwg, order)
+    // the W step inside the front when every batch of the epoch has one dW
+    // split (SKGE_RS_WFRONT=0: in the apply, from partial tiles)
+    const char* wfe = getenv("SKGE_RS_WFRONT");
+    const long long last = T - (long long)(nb - 1) * bs;
+    const bool infront = comb && w.wcur && !(wfe && atoi(wfe) == 0) &&
+                         rs_front_splits(3 * bs, M, d) == 1 &&
+                         rs_front_splits((int)(3 * last), M, d) == 1;
+    WFront wf = {};
+    if (infront)
+      wf = WFront{w.wcur, rel->param, rel->state, w.W1, w.A1, rel->opt, rel->lr, rel->rin,
+                  rel->rout, rel->fixed_div};
+#define SKGE_FRONT(V, C, I)                                                                 \
+  hipLaunchKernelGGL((k_rescal_front_fused<V, C, I>), grid, dim3(256), 0, st, ent->param,    \
+                     rel->param, d, w, fsplits, nwg, order, wf)
     if ((d & 3) == 0) {
-      if (comb) SKGE_FRONT(true, true); else SKGE_FRONT(true, false);
+      if (infront) SKGE_FRONT(true, true, true);
+      else if (comb) SKGE_FRONT(true, true, false);
+      else SKGE_FRONT(true, false, false);
     } else {
-      if (comb) SKGE_FRONT(false, true); else SKGE_FRONT(false, false);
+      if (infront) SKGE_FRONT(false, true, true);
+      else if (comb) SKGE_FRONT(false, true, false);
+      else SKGE_FRONT(false, false, false);
     }
 #undef SKGE_FRONT
     SKGE_KM_SWITCH(k_rescal_pos_scatter, dim3(blocks), dim3(256), 0, st, rec, rec_n1, start,
@@ -1791,7 +1897,7 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
     if (wstep_in_apply) {   // the caller's entity apply runs the W step
       *wstep = WStep{w.wpart, w.rel_off, comb ? w.n01 : nullptr, rel->param, rel->state,
                      rel->upd_count, nviol, M, d, fsplits, rel->opt, rel->lr, rel->rin, rel->rout,
-                     rel->fixed_div};
+                     rel->fixed_div, infront ? w.wcur : nullptr, w.W1, w.A1};
     } else {
       WApply wa = {rel->param, rel->state, rel->opt, rel->lr, rel->rin, rel->rout,
                    rel->fixed_div, nviol, rel->upd_count};
@@ -1807,6 +1913,32 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
                  d, af, margin, w, accum_of(ent), nviol)
   rescal_wgrad_launch(st, ent, rel, d, w, true, nviol, 3 * count);
   SKGE_CHECK_LAUNCH("rescal positive grad (epoch buckets)");
+  return SKGE_OK;
+}
+
+// the in-front W step's epoch end: W / state back into the caller's buffers
+// when the other buffer is current (k_rescal_w_sync), then cur = 0
+__global__ __launch_bounds__(256) void k_rescal_w_sync(const int* __restrict__ cur, float* W0,
+                                                       float* A0, const float* __restrict__ W1,
+                                                       const float* __restrict__ A1, long long n4) {
+  if (*cur == 0) return;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    reinterpret_cast<float4*>(W0)[i] = reinterpret_cast<const float4*>(W1)[i];
+    if (A0) reinterpret_cast<float4*>(A0)[i] = reinterpret_cast<const float4*>(A1)[i];
+  }
+}
+__global__ void k_rescal_w_reset(int* cur) { *cur = 0; }
+
+int skge::rescal_w_sync(hipStream_t st, const WStep& w) {
+  if (!w.cur) return SKGE_OK;
+  const long long n = (long long)w.M * w.d * w.d;
+  SKGE_CHECK_ARG(n % 4 == 0, "W sync: M d^2 %% 4 != 0");
+  const long long blocks = std::min<long long>((n / 4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_rescal_w_sync, dim3((unsigned)blocks), dim3(256), 0, st, w.cur, w.W,
+                     w.A, w.W1, w.A1, n / 4);
+  hipLaunchKernelGGL(k_rescal_w_reset, dim3(1), dim3(1), 0, st, w.cur);
+  SKGE_CHECK_LAUNCH("rescal W sync");
   return SKGE_OK;
 }
 

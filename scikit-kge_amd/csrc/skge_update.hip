@@ -793,7 +793,17 @@ __device__ __forceinline__ void wstep_quad(const WStep& w, long long q) {
 
 template <int K>
 __global__ __launch_bounds__(256) void k_apply_wstep(TableDev t0, int n0, WStep w, int nwb) {
-  if ((int)blockIdx.x < nwb) {
+  if (w.cur) {   // the W step was done in the front: make it current if the batch updates
+    if ((int)blockIdx.x < nwb) {
+      if (blockIdx.x == 0 && threadIdx.x == 0 && *w.gate != 0) {
+        *w.cur ^= 1;
+        if (w.opt == OPT_ADAGRAD && w.ucnt)   // updateCounts, skge/param.py:149-150
+          for (int p = 0; p < w.M; ++p)
+            if (w.rel_off[p + 1] > w.rel_off[p]) w.ucnt[p] += 1;
+      }
+      return;
+    }
+  } else if ((int)blockIdx.x < nwb) {
     const long long nq = (long long)w.M * ((w.d + WS_T - 1) / WS_T) * ((w.d + WS_T - 1) / WS_T) *
                          (WS_T * WS_T / 4);
     for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
@@ -817,7 +827,7 @@ int apply_with_wstep(hipStream_t st, const skge_table_t* ent, int nslots, const 
   SKGE_CHECK_ARG(w.opt == SKGE_SGD || w.A, "AdaGrad needs state");
   const int nt = (w.d + WS_T - 1) / WS_T;
   const long long nq = (long long)w.M * nt * nt * (WS_T * WS_T / 4);
-  const int nwb = grid_for_elems(nq);
+  const int nwb = w.cur ? 1 : grid_for_elems(nq);
   const int grid = nwb + grid_for_waves(nslots);
   const TableDev td = table_dev(ent);
   switch (km_for(ent->width)) {

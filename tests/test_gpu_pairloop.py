@@ -576,3 +576,42 @@ def test_rescal_combined_dw_matches_three_items(n_ent, n_rel, T, d, nb, monkeypa
     for pid in out[0][1]:
         np.testing.assert_allclose(out[1][1][pid], out[0][1][pid], rtol=RTOL, atol=ATOL,
                                    err_msg=pid)
+
+
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb,opt", [
+    (300, 7, 2000, 16, 7, "sgd"),            # ragged remainder batch
+    (300, 40, 2000, 24, 50, "adagrad"),      # ~40 positives / batch: most relations absent
+    (300, 5, 2000, 30, 3, "adagrad"),        # d % 4 != 0
+    (40943, 18, 14140, 200, 10, "sgd"),      # WN18 entity / relation counts, d, batch size
+    (40943, 18, 14140, 200, 9, "sgd"),       # odd number of batches: W ends in the 2nd buffer
+])
+def test_rescal_in_front_w_step_matches_apply_side(n_ent, n_rel, T, d, nb, opt, monkeypatch):
+    """The W step inside the fused front (written speculatively into a second
+    W / state buffer, made current by the apply when the batch has violations,
+    copied back into the model's W at the epoch's end) against the W step in
+    the entity apply's launch (SKGE_RS_WFRONT=0) on the same draws: equal
+    violation totals, parameters and W's AdaGrad state within the fp32
+    tolerance after 2 epochs.  (AdaGrad only at small sizes: at WN18's, the
+    entity sums' float-atomic order turns rounding-level differences of a
+    near-zero first gradient into +-lr steps, as in the tests above.)"""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    xs = make_kg(n_ent, n_rel, T, seed=10)
+    out = []
+    for wf in ("0", "1"):
+        monkeypatch.setenv("SKGE_RS_WFRONT", wf)
+        m = make_model("rescal", (n_ent, n_ent, n_rel), d)
+        m.add_hyperparam("margin", 0.2)
+        cls = S.SGD if opt == "sgd" else S.AdaGrad
+        upd = {pid: cls(p, 0.1) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), nb, seed=11)
+        with torch.cuda.stream(r.stream):
+            r.run(2)
+        r.synchronize()
+        state = {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}
+        if opt == "adagrad":
+            state["W_p2"] = upd["W"].p2.cpu().numpy().copy()
+        out.append((int(r.nviol_total.item()), state))
+    assert out[0][0] == out[1][0] > 0
+    for k in out[0][1]:
+        np.testing.assert_allclose(out[1][1][k], out[0][1][k], rtol=RTOL, atol=ATOL, err_msg=k)
