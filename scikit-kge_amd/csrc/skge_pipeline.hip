@@ -70,6 +70,9 @@ struct PipeTab {               // entity table
   UpdParams u;
   int* claims;                 // profile only: rows applied in this launch (sharded)
   int* err;                    // ERR_* bits
+  unsigned long long* refs[2]; // owner mode, [rows] by batch parity: the batch's references to
+                               // the row, total (high word, fixed within the launch) and not
+                               // yet retired (low word) (k_own_batch)
 };
 
 struct RelTab {                // relation table
@@ -91,6 +94,7 @@ struct PipeArgs {
   const int* rec_n1;           // [T]: o'
   long long start;             // B role: this batch's positives [start, start + count)
   int count;
+  int count_next;              // owner mode: the next batch's positives (from start + count)
   int prev_slots;              // A role: entity slots of the previous batch
   int b, nb1;                  // batch index in the epoch (nb1: the flush), batches per epoch
   const uint64_t* epoch_key;
@@ -927,6 +931,299 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_lazy_batch(PipeA
   }
 }
 
+// ---- owner apply (SKGE_PIPE_OWNER): every entity row is updated inside the
+// launch that scores its batch, by the batch's LAST wave to reference it ----
+//
+// The batch's records are known before the launch, so the number of its
+// references to each entity row is counted ahead (refs[b & 1]: the previous
+// launch's scoring waves count the next batch's records; the epoch's first
+// batch, k_own_count) into one 64-bit word per row: the total in the high half,
+// which no wave of the launch changes until the row's last reference is
+// retired -- waves need not be resident together -- and the references not yet
+// retired in the low half.  A scoring wave loads its rows, their AdaGrad state
+// and their reference words with the record's rows (one round trip) and scores.
+//   * A row only this wave references (total 1; ~87% of references at
+//     WN18's batch) is updated from the wave's own contribution and count
+//     straight from registers -- the row's whole batch sum -- and stored; no
+//     atomics, no hand-off.
+//   * A shared row: the wave adds its exact packed contribution and count
+//     (memory-side atomics), waits for them to complete, then retires its
+//     reference (atomicSub with return).  The wave that retires the last one
+//     takes the row's sums and count with atomic exchanges (which also clear
+//     them: memory-side, so every wave's adds are seen) and updates the row
+//     from its registers: the row's parameters and state cannot have changed
+//     since the batch's waves loaded them, as each referencing wave had loaded
+//     them before retiring its reference.
+// After the launch every update of batch b has landed, so the next launch's
+// waves read plain rows: no pending marks, claims, waits or apply waves.
+// Relation rows keep the pipelined runner's scheme (double-buffered,
+// recomputed by every scoring wave, published by the A role's waves).  Every
+// row's update is row_update on its exact integer sums: bitwise the two-launch
+// runner's result.
+__global__ __launch_bounds__(256) void k_own_count(const int4* __restrict__ rec,
+                                                   const int* __restrict__ rec_n1, int count,
+                                                   unsigned long long* __restrict__ refs) {
+  constexpr unsigned long long ONE = 0x100000001ull;   // total + 1, live + 1
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
+    const int4 r = rec[j];
+    const int n1 = rec_n1[j];
+    atomicAdd(refs + r.x, ONE);
+    atomicAdd(refs + r.y, ONE);
+    if (r.w >= 0) atomicAdd(refs + r.w, ONE);
+    if (n1 >= 0) atomicAdd(refs + n1, ONE);
+  }
+}
+
+template <int KQ, bool W32>
+__global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_own_batch(PipeArgs a) {
+  const int wpb = blockDim.x >> 6;
+  const int l = lane_id();
+  const int d = a.d, nq = d >> 2;
+  const int rcw = W32 ? 2 * nq : nq;
+  const int g = launch_id(a);
+  const int cp = a.b & 1;
+  const int rd = a.b & 1;
+  const int rw = a.b < a.nb1 ? rd ^ 1 : 0;
+  const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
+  const int nB = gridDim.x - a.nA;
+  if ((int)blockIdx.x < a.nA) {   // A role: the relation rows (R_b for the next launch)
+    const int wa = (int)blockIdx.x * wpb + (threadIdx.x >> 6);
+    const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
+    if (a.b == a.nb1 && wa == 0) fold_shards(a.nviol_shards, a.nviol_total);
+    for (int w = wa; w < a.R.rows; w += a.nA * wpb) rel_publish<KQ, W32>(a, w, rd, rw, ra_prev, ra_old);
+    if (a.trace && l == 0) {
+      unsigned long long* tr = a.trace + 2 + 6 * (size_t)a.count + 2 * (size_t)wa;
+      tr[0] = ta0;
+      tr[1] = now_10ns();
+    }
+    return;
+  }
+  unsigned long long* const refs = opaque_ptr(a.E.refs[cp]);
+  unsigned long long* const refs_next = opaque_ptr(a.E.refs[cp ^ 1]);
+  int* const cnt = opaque_ptr(a.E.cnt[0]);
+  unsigned long long* const esum = opaque_ptr(a.E.sum[0]);
+  unsigned long long* const racc = opaque_ptr(a.R.acc[ra_cur]);
+  float* const EP = opaque_ptr(a.E.P);
+  float* const EA = a.E.A ? opaque_ptr(a.E.A) : nullptr;
+  const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int4*>(a.rec + a.start), 0, a.count * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rec1_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int*>(a.rec_n1 + a.start), 0, a.count * 4, 0x00020000);
+  // the next batch's records (counted here for the next launch)
+  const __amdgpu_buffer_rsrc_t nrec_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int4*>(a.rec + a.start + a.count), 0, a.count_next * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t nrec1_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int*>(a.rec_n1 + a.start + a.count), 0, a.count_next * 4, 0x00020000);
+  int nv = 0;
+  for (int w = (int)(blockIdx.x - a.nA) * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
+    unsigned long long tt[4];
+    if (a.trace) tt[0] = now_10ns();
+    const u32x4 rx = __builtin_amdgcn_raw_buffer_load_b128(rec_rs, w * 16, 0, 0);
+    const int r1 = (int)__builtin_amdgcn_raw_buffer_load_b32(rec1_rs, w * 4, 0, 0);
+    // (lanes past the next batch read 0 through the descriptor: unused)
+    const u32x4 nx = __builtin_amdgcn_raw_buffer_load_b128(nrec_rs, w * 16, 0, 0);
+    const int nn1 = (int)__builtin_amdgcn_raw_buffer_load_b32(nrec1_rs, w * 4, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    const int s = __builtin_amdgcn_readfirstlane((int)rx.x);
+    const int o = __builtin_amdgcn_readfirstlane((int)rx.y);
+    const int p = __builtin_amdgcn_readfirstlane((int)rx.z);
+    const int neg0 = __builtin_amdgcn_readfirstlane((int)rx.w);
+    const int neg1 = __builtin_amdgcn_readfirstlane(r1);
+    const int n0r = neg0 >= 0 ? neg0 : s, n1r = neg1 >= 0 ? neg1 : o;
+    // this wave's references: lane k < 4 holds row k (s, o, s', o'; -1 if absent)
+    const int myrow = l < 4 ? sel4(l, s, o, neg0, neg1) : -1;
+    float4 es[KQ], eo[KQ], rp[KQ], fs[KQ], fo[KQ];
+    float4 as_[KQ], ao[KQ], af0[KQ], af1[KQ];
+    load_row4<KQ>(EP, s, d, es);
+    load_row4<KQ>(EP, o, d, eo);
+    load_row4<KQ>(EP, n0r, d, fs);
+    load_row4<KQ>(EP, n1r, d, fo);
+#ifdef SKGE_OWN_ABL_NOA   // timing-only ablations (tools/ablate.sh)
+    if (false) {
+#else
+    if (EA) {
+#endif
+      load_row4<KQ>(EA, s, d, as_);
+      load_row4<KQ>(EA, o, d, ao);
+      load_row4<KQ>(EA, n0r, d, af0);
+      load_row4<KQ>(EA, n1r, d, af1);
+    } else {
+#pragma unroll
+      for (int m = 0; m < KQ; ++m)
+        as_[m] = ao[m] = af0[m] = af1[m] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    const int rc = myrow >= 0 ? (int)(refs[myrow] >> 32) : 0;   // the batch's references
+    {
+      float4 ra[KQ];
+      int c;
+      rel_row<KQ, W32>(a.R, p, d, rd, ra_prev, rp, ra, c);
+    }
+    float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
+    float4 gp4[KQ], g0[KQ], g1[KQ];
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+#define SKGE_EL(X)                                                                    \
+  {                                                                                   \
+    const float vp = (es[m].X + rp[m].X) - eo[m].X;   /* transe.py:32 */              \
+    const float v0 = (fs[m].X + rp[m].X) - eo[m].X;                                   \
+    const float v1 = (es[m].X + rp[m].X) - fo[m].X;                                   \
+    ps += fabsf(vp);                                                                  \
+    n0 += fabsf(v0);                                                                  \
+    n1 += fabsf(v1);                                                                  \
+    gp4[m].X = signf_np(-((eo[m].X - rp[m].X) - es[m].X)); /* transe.py:103,115 */    \
+    g0[m].X = signf_np((eo[m].X - rp[m].X) - fs[m].X);     /* transe.py:104,117 */    \
+    g1[m].X = signf_np((fo[m].X - rp[m].X) - es[m].X);                                \
+  }
+      SKGE_EL(x)
+      SKGE_EL(y)
+      SKGE_EL(z)
+      SKGE_EL(w)
+#undef SKGE_EL
+    }
+    const float pscore = -wave_sum(ps);
+    const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
+    const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // strict >, transe.py:73
+    const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
+    nv += v0 + v1;
+    if (a.trace) tt[1] = now_10ns();
+    // per reference: its count, and whether this wave holds the row's only
+    // reference (refs == 1 and no other reference of this wave to the row)
+    const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
+    bool dup = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int rk = __builtin_amdgcn_readlane(myrow, k);
+      dup = dup || (k != l && rk == myrow);
+    }
+#ifdef SKGE_OWN_ABL_ALLSOLE
+    const bool sole = myrow >= 0 && rc >= 0;
+#else
+    const bool sole = myrow >= 0 && rc == 1 && !dup;
+#endif
+    const uint64_t sole_m = __ballot(sole) & 0xfull;
+    const uint64_t upd_m = __ballot(myrow >= 0 && cE > 0) & 0xfull;   // rows with contributions
+    const uint64_t shared_m = __ballot(myrow >= 0 && !sole) & 0xfull;
+    // the four rows' contributions (transe.py:122-160: s +gp, o -gp, s' +gn, o' -gn)
+    const float fv0 = (float)v0, fv1 = (float)v1;
+    // k: 0 = s, 1 = o, 2 = s', 3 = o'
+#define SKGE_CONTRIB(K, M, X)                                                            \
+  ((K) == 0 ? fv0 * gp4[M].X + fv1 * (gp4[M].X + g1[M].X)                               \
+   : (K) == 1 ? -(fv0 * (gp4[M].X + g0[M].X) + fv1 * gp4[M].X)                          \
+   : (K) == 2 ? g0[M].X : -g1[M].X)
+    Accum aE;
+    aE.sum = reinterpret_cast<float*>(esum);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {   // shared rows with contributions: memory-side adds
+      if (!((shared_m >> k) & (upd_m >> k) & 1ull)) continue;
+      float4 c[KQ];
+#pragma unroll
+      for (int m = 0; m < KQ; ++m)
+        c[m] = make_float4(SKGE_CONTRIB(k, m, x), SKGE_CONTRIB(k, m, y), SKGE_CONTRIB(k, m, z),
+                           SKGE_CONTRIB(k, m, w));
+      acc_row4_i16<KQ>(aE, __builtin_amdgcn_readlane(myrow, k), c, d);
+    }
+    if (l < 4 && !sole && myrow >= 0 && cE > 0) atomicAdd(cnt + myrow, cE);
+    uint64_t last_m = 0;
+    if (shared_m) {   // retire the shared references once this wave's adds are done
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      unsigned long long old = 0;
+      if (l < 4 && !sole && myrow >= 0) old = atomicAdd(refs + myrow, ~0ull);   // live - 1
+      const bool lst = l < 4 && !sole && myrow >= 0 && (old & 0xffffffffull) == 1ull;
+      if (lst) refs[myrow] = 0ull;   // every other reference has read the total already
+      last_m = __ballot(lst) & 0xfull;
+    }
+    if (a.trace) tt[2] = now_10ns();
+    // update: sole rows with contributions, and the shared rows this wave retired last
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool own = (sole_m >> k) & (upd_m >> k) & 1ull;
+      const bool last = (last_m >> k) & 1ull;
+      if (!own && !last) continue;
+      const int row = __builtin_amdgcn_readlane(myrow, k);
+      unsigned long long sv[KQ];
+      int c;
+      if (own) {
+        c = __builtin_amdgcn_readlane(cE, k);
+#pragma unroll
+        for (int m = 0; m < KQ; ++m)
+          sv[m] = pack_i16x4(make_float4(SKGE_CONTRIB(k, m, x), SKGE_CONTRIB(k, m, y),
+                                         SKGE_CONTRIB(k, m, z), SKGE_CONTRIB(k, m, w)));
+      } else {   // the batch's sums and count, cleared in the same memory-side operation
+        int cx = 0;
+        if (l == 0) cx = atomicExch(cnt + row, 0);
+        unsigned long long* srow = esum + (size_t)row * nq;
+#pragma unroll
+        for (int m = 0; m < KQ; ++m) {
+          const int q = 64 * m + l;
+          sv[m] = q < nq ? atomicExch(srow + q, 0ull) : 0ull;
+        }
+        c = __builtin_amdgcn_readfirstlane(cx);
+        if (c == 0) continue;   // referenced, never violated
+        if (c > PACKED_MAX && l == 0) atomicOr(a.err, ERR_PACKED);
+      }
+      float4 pr[KQ], ar[KQ];
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) {
+        pr[m] = k == 0 ? es[m] : k == 1 ? eo[m] : k == 2 ? fs[m] : fo[m];
+        ar[m] = k == 0 ? as_[m] : k == 1 ? ao[m] : k == 2 ? af0[m] : af1[m];
+      }
+      row_update<KQ, false>(a.E.u, c, d, sv, sv, pr, ar);
+      if (a.E.claims && l == 0) atomicAdd(shard_of(a.E.claims), 1);   // profile: rows updated
+      float4* prow = reinterpret_cast<float4*>(EP + (size_t)row * d);
+      float4* arow = EA ? reinterpret_cast<float4*>(EA + (size_t)row * d) : nullptr;
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) {
+        const int q = 64 * m + l;
+        if (q < nq) {
+          prow[q] = pr[m];
+          if (arow) arow[q] = ar[m];
+        }
+      }
+    }
+    if (a.trace) tt[3] = now_10ns();
+    // no-return adds last: a wait for a later load or for the shared rows'
+    // adds would wait for them too (vmcnt counts in issue order)
+    if (l < 4 && sole) refs[myrow] = 0ull;   // retired (shared rows: by their last reference)
+    if (v0 + v1 > 0) {   // relation sums (int16x4 / int32x2), count word
+      const float fv0 = (float)v0, fv1 = (float)v1;
+      unsigned long long* rrow = racc + (size_t)p * a.R.rw;
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) {
+        const int q = 64 * m + l;
+        float4 cr;
+        cr.x = fv0 * (gp4[m].x + g0[m].x) + fv1 * (gp4[m].x + g1[m].x);
+        cr.y = fv0 * (gp4[m].y + g0[m].y) + fv1 * (gp4[m].y + g1[m].y);
+        cr.z = fv0 * (gp4[m].z + g0[m].z) + fv1 * (gp4[m].z + g1[m].z);
+        cr.w = fv0 * (gp4[m].w + g0[m].w) + fv1 * (gp4[m].w + g1[m].w);
+        if (q < nq) {
+          if (W32) {
+            atomicAdd(rrow + 2 * q, pack_i32x2(cr.x, cr.y));
+            atomicAdd(rrow + 2 * q + 1, pack_i32x2(cr.z, cr.w));
+          } else {
+            atomicAdd(rrow + q, pack_i16x4(cr));
+          }
+        }
+      }
+      if (l == 0) atomicAdd(racc + (size_t)p * a.R.rw + rcw, (unsigned long long)(2 * (v0 + v1)));
+    }
+    if (w < a.count_next && l < 4) {   // the next batch's references
+      const int nr = sel4(l, (int)nx.x, (int)nx.y, (int)nx.w, nn1);
+      if (nr >= 0) atomicAdd(refs_next + nr, 0x100000001ull);
+    }
+    if (a.trace && l == 0) {
+      unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
+      tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
+      tr[5] = sole_m | (shared_m << 4) | ((unsigned long long)(v0 + v1 > 0) << 8) | (last_m << 12) |
+              (upd_m << 16);
+    }
+#undef SKGE_CONTRIB
+  }
+  if (l == 0 && nv) {
+    atomicAdd(shard_of(a.nviol_shards), nv);
+    if (a.stats_viol) atomicAdd(shard_of(a.stats_viol), nv);
+  }
+}
+
 // ======================== HolE pairwise, pipelined ========================
 //
 // The launch structure of k_pipe_batch for HolE (skge/hole.py:44-100, the
@@ -1479,6 +1776,7 @@ struct skge_pipe_runner {
   std::vector<int> grid;
   bool w32 = false;                // int32x2 relation sums
   bool lazy = false;               // SKGE_PIPE_LAZY: entity rows applied by their next reader
+  bool owner = false;              // SKGE_PIPE_OWNER: rows updated by their batch's last reference
   bool hole = false;               // HolE pairwise (k_hole_pipe, fp32 sums)
   bool fft = false;                // HolE: correlations in the frequency domain (skge_hole_fft.h)
   size_t lds = 0;                  // HolE: dynamic LDS per workgroup
@@ -1515,6 +1813,9 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
     hipLaunchKernelGGL(k_epoch_sample, dim3((unsigned)blocks), dim3(256), 0, st, r->trip, r->T,
                        r->half, r->seed, (const uint64_t*)r->epoch_key, r->set, r->n_ent,
                        r->ntries, r->rec, r->rec_n1);
+    if (r->owner)   // the epoch's first batch's references (k_own_batch counts the rest)
+      hipLaunchKernelGGL(k_own_count, dim3(std::max(1, std::min((r->batch[0].count + 255) / 256, 4096))),
+                         dim3(256), 0, st, r->rec, r->rec_n1, r->batch[0].count, r->batch[0].E.refs[0]);
   }
   ++i;
   if (ev) (void)hipEventRecord(ev[i], st);
@@ -1533,6 +1834,9 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
     if (r->lazy) {                                                                               \
       if (r->w32) hipLaunchKernelGGL((k_lazy_batch<K, true>), gr, bl, 0, st, a);                 \
       else hipLaunchKernelGGL((k_lazy_batch<K, false>), gr, bl, 0, st, a);                       \
+    } else if (r->owner) {                                                                       \
+      if (r->w32) hipLaunchKernelGGL((k_own_batch<K, true>), gr, bl, 0, st, a);                  \
+      else hipLaunchKernelGGL((k_own_batch<K, false>), gr, bl, 0, st, a);                        \
     } else {                                                                                     \
       if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true>), gr, bl, 0, st, a);                 \
       else hipLaunchKernelGGL((k_pipe_batch<K, false>), gr, bl, 0, st, a);                       \
@@ -1616,6 +1920,10 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   skge_pipe_runner* r = new skge_pipe_runner();
   r->lazy = lazy;
   r->hole = hole;
+  {
+    const char* ow = getenv("SKGE_PIPE_OWNER");   // A/B: entity rows by their last reference
+    r->owner = !hole && !lazy && ow && atoi(ow) != 0;
+  }
   const int nq = d / 4;
   PipeArgs a = {};
   auto upd = [](const skge_table_t* s) {
@@ -1651,6 +1959,11 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
       t.pend[0] = (int*)dalloc(r, (size_t)N * 4);
       t.pend[1] = (int*)dalloc(r, (size_t)N * 4);
       ok = ok && t.sum[1] && t.cnt[1] && t.touched[1] && t.pend[0] && t.pend[1];
+    }
+    if (r->owner) {   // reference words by batch parity
+      t.refs[0] = (unsigned long long*)dalloc(r, (size_t)N * 8);
+      t.refs[1] = (unsigned long long*)dalloc(r, (size_t)N * 8);
+      ok = ok && t.refs[0] && t.refs[1];
     }
     RelTab& q = a.R;
     const int M = rel->rows;
@@ -1736,13 +2049,14 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     a.b = b;
     a.start = b < nb1 ? batches[b].first : 0;
     a.count = b < nb1 ? (int)batches[b].second : 0;
+    a.count_next = b + 1 < nb1 ? (int)batches[b + 1].second : 0;
     a.prev_slots = 4 * prev;
     // A role: every relation row, then the previous batch's entity slots (lazy:
     // no entity rows, except the flush's sweep over all rows in 64-row chunks)
     const int a_items =
         rel->rows + (hole ? (4 * prev + HGROUP - 1) / HGROUP
                           : lazy ? (b == nb1 ? (ent->rows + 63) / 64 : 0)
-                                 : (4 * prev + ASLOTS - 1) / ASLOTS);
+                                 : r->owner ? 0 : (4 * prev + ASLOTS - 1) / ASLOTS);
     constexpr int WPB = SKGE_PIPE_WG / 64;
     // HolE: the apply waves loop over their items within the residency the
     // scoring waves leave (SKGE_HPIPE_OCC waves per SIMD: 2 at ~180 VGPRs; the

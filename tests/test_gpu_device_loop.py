@@ -223,16 +223,20 @@ def _runner_result(n_ent, n_rel, T, d, nb, pipelined, epochs=2, seed=11, trip=No
     (40943, 18, 141442, 200, 100),  # WN18 geometry
     (20000, 11, 40000, 64, 2),    # large batch: the apply waves loop over their slots
 ])
-def test_pipelined_runner_bitwise_equals_two_launch(n_ent, n_rel, T, d, nb):
+def test_pipelined_runner_bitwise_equals_two_launch(n_ent, n_rel, T, d, nb, monkeypatch):
     """The pipelined runner (one launch per batch, cross-workgroup hand-off of
-    the previous batch's updates) must reproduce the two-launch loop exactly."""
+    the previous batch's updates) must reproduce the two-launch loop exactly --
+    with apply waves, with the lazy apply by the rows' next readers, and with
+    every row updated by its batch's last reference (SKGE_PIPE_OWNER)."""
     a, trip = _runner_result(n_ent, n_rel, T, d, nb, pipelined=False)
-    for lazy in (False, True):   # apply waves / lazy apply by the rows' next readers
-        b, _ = _runner_result(n_ent, n_rel, T, d, nb, pipelined=True, trip=trip, lazy=lazy)
+    for mode in ("apply", "lazy", "owner"):
+        monkeypatch.setenv("SKGE_PIPE_OWNER", "1" if mode == "owner" else "0")
+        b, _ = _runner_result(n_ent, n_rel, T, d, nb, pipelined=True, trip=trip,
+                              lazy=mode == "lazy")
         assert a["key"] == b["key"] == 2
-        assert a["nviol"] == b["nviol"] > 0
+        assert a["nviol"] == b["nviol"] > 0, mode
         for k in ("E", "R", "pE", "pR"):
-            assert np.array_equal(a[k], b[k]), (k, lazy)
+            assert np.array_equal(a[k], b[k]), (k, mode)
 
 
 def test_trainer_device_loop_fit():

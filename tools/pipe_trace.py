@@ -64,6 +64,22 @@ def main():
                   (np.array([bin(int(x)).count("1") for x in pend]) == 1).sum(),
                   (np.array([bin(int(x)).count("1") for x in pend]) >= 2).sum(), len(A),
                   stats[args.launch].tolist()))
+        if os.environ.get("SKGE_PIPE_OWNER", "0") != "0":   # owner-apply runner
+            sole, shared, lastm, updm = B[:, 5] & 0xf, (B[:, 5] >> 4) & 0xf, (B[:, 5] >> 12) & 0xf, (B[:, 5] >> 16) & 0xf
+            print("owner: waves with shared rows %d, retiring a row last %d, sole updates %d" % (
+                (shared != 0).sum(), (lastm != 0).sum(),
+                sum(bin(int(x & y)).count("1") for x, y in zip(sole, updm))))
+            print("percentiles (us)           p0     p10    p50    p90    p100")
+            print("B start                  ", pct(B[:, 0] - t0))
+            print("B record+rows+score      ", pct(B[:, 1] - B[:, 0]))
+            print("B shared adds+retire     ", pct((B[:, 2] - B[:, 1])[shared != 0]))
+            print("B update+stores          ", pct(B[:, 3] - B[:, 2]))
+            print("B tail adds              ", pct(B[:, 4] - B[:, 3]))
+            print("B end                    ", pct(B[:, 4] - t0))
+            if len(A):
+                print("A start / end            ", pct(A[:, 0] - t0), "/", pct(A[:, 1] - t0))
+            print("last end %.2f us" % ((max(B[:, 4].max(), A[:, 1].max() if len(A) else 0) - t0) / 100))
+            continue
         if args.lazy:
             cnz, wt, clm = B[:, 5] & 0xf, (B[:, 5] >> 4) & 0xf, (B[:, 5] >> 12) & 0xf
             print("lazy: waves applying a row %d (rows %d), waiting %d, claiming %d" % (
