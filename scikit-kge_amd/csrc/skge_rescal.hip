@@ -939,6 +939,14 @@ __global__ __launch_bounds__(256) void k_rescal_pos_scatter(const int4* __restri
     const int neg1 = __builtin_amdgcn_readfirstlane(rec_n1[start + j]);
     const int k0 = neg0 >= 0 ? 1 : 0, k1 = neg1 >= 0 ? 1 : 0;
     const int i0 = count + 2 * j, i1 = i0 + 1;   // the negatives' items
+    // the contribution rows, loaded with the partial scores (one round trip; a
+    // positive without a violation discards them): W E_o and E_s W of the
+    // positive, E_s' W of (s', o, p), W E_o' of (s, o', p)
+    float wep[KM], ewp[KM], ew0[KM], we1[KM];
+    load_row<KM>(ws.WE, j, d, wep);
+    load_row<KM>(ws.EW, j, d, ewp);
+    load_row<KM>(ws.EW, i0, d, ew0);
+    load_row<KM>(ws.WE, i1, d, we1);
     float praw = 0.0f, raw0 = 0.0f, raw1 = 0.0f;
     for (int q = 0; q < ncb; ++q) {   // fixed order: deterministic
       praw += ws.spart[(size_t)j * ncb + q];
@@ -948,7 +956,7 @@ __global__ __launch_bounds__(256) void k_rescal_pos_scatter(const int4* __restri
     const float pf = af_f(af, praw), f0 = af_f(af, raw0), f1 = af_f(af, raw1);
     const float gp = -af_g_given_f(af, pf);   // rescal.py:275 (all pairs)
     const float g0 = af_g_given_f(af, f0), g1 = af_g_given_f(af, f1);
-    if (l == 0 && k0 + k1 > 0) {
+    if (l == 0 && k0 + k1 > 0 && ws.coef) {   // (null: dW was formed from ecoef already)
       ws.coef[ws.bpos[j]] = gp * (float)(k0 + k1);
       if (k0) ws.coef[ws.bpos[i0]] = g0;
       if (k1) ws.coef[ws.bpos[i1]] = g1;
@@ -960,17 +968,20 @@ __global__ __launch_bounds__(256) void k_rescal_pos_scatter(const int4* __restri
                   4 * j + l);
     if (v0 + v1 == 0) continue;
     nv += v0 + v1;
-    // every row loaded (stale rows of absent negatives are not used)
-    float wep[KM], ewp[KM], we0[KM], ew0[KM], we1[KM], ew1[KM], x[KM];
-    // (deduplicated GEMM rows: W E_o of (s', o, p) is positive j's row, E_s W
-    // of (s, o', p) likewise -- bitwise the same values)
-    const bool dd = ws.npos > 0;
-    load_row<KM>(ws.WE, j, d, wep);
-    load_row<KM>(ws.EW, j, d, ewp);
-    load_row<KM>(ws.WE, dd ? j : i0, d, we0);
-    load_row<KM>(ws.EW, i0, d, ew0);
-    load_row<KM>(ws.WE, i1, d, we1);
-    load_row<KM>(ws.EW, dd ? j : i1, d, ew1);
+    // (stale rows of absent negatives are not used; deduplicated GEMM rows: W
+    // E_o of (s', o, p) is positive j's row, E_s W of (s, o', p) likewise --
+    // bitwise the same values)
+    float we0[KM], ew1[KM], x[KM];
+    if (ws.npos > 0) {
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        we0[k] = wep[k];
+        ew1[k] = ewp[k];
+      }
+    } else {
+      load_row<KM>(ws.WE, i0, d, we0);
+      load_row<KM>(ws.EW, i1, d, ew1);
+    }
     const float fv0 = (float)v0, fv1 = (float)v1;
 #pragma unroll
     for (int k = 0; k < KM; ++k) x[k] = fv0 * (gp * wep[k]) + fv1 * (gp * wep[k] + g1 * we1[k]);
@@ -1892,8 +1903,10 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
       else SKGE_FRONT(false, false, false);
     }
 #undef SKGE_FRONT
+    RescalWs wsc = w;
+    wsc.coef = nullptr;   // dW was formed from the bucketing's coefficients
     SKGE_KM_SWITCH(k_rescal_pos_scatter, dim3(blocks), dim3(256), 0, st, rec, rec_n1, start,
-                   count, d, af, margin, w, accum_of(ent), nviol)
+                   count, d, af, margin, wsc, accum_of(ent), nviol)
     if (wstep_in_apply) {   // the caller's entity apply runs the W step
       *wstep = WStep{w.wpart, w.rel_off, comb ? w.n01 : nullptr, rel->param, rel->state,
                      rel->upd_count, nviol, M, d, fsplits, rel->opt, rel->lr, rel->rin, rel->rout,

@@ -8,7 +8,7 @@ for v in "$@"; do
   name=${v%%=*}; flag=${v#*=}
   mkdir -p build_abl/$name
   for f in csrc/*.hip; do
-    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-hip-fp32-correctly-rounded-divide-sqrt -D$flag -c $f -o build_abl/$name/$(basename $f .hip).o &
+    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -D$flag -c $f -o build_abl/$name/$(basename $f .hip).o &
   done
   wait
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_abl/$name/libskgehip.so build_abl/$name/*.o
