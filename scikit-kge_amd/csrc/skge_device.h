@@ -77,6 +77,20 @@ __device__ __forceinline__ float af_g_given_f(int af, float fx) {
   }
 }
 
+// The packed (TransE-L1) row updates' AdaGrad step and projection scale in
+// the hardware's fast forms (v_sqrt_f32, v_rcp_f32: ~1 ulp instead of the
+// correctly rounded sequences).  Their gradients are exact small-integer sums
+// over the count (the mean itself stays correctly rounded), so H >= 1/32767
+// and the step's relative error stays ~1e-7: far inside the 1e-5 parity bar.
+// Shared by every packed apply (row_update, i16_finish): bitwise the same.
+__device__ __forceinline__ float adagrad_step_fast(float lr, float g, float a) {
+  return (lr * g) * __builtin_amdgcn_rcpf(fmaxf(__builtin_amdgcn_sqrtf(a), 1e-7f));
+}
+__device__ __forceinline__ float proj_scale_fast(int post, float ss) {
+  return __builtin_amdgcn_rcpf(post == POST_NORMALIZE ? __builtin_amdgcn_sqrtf(ss)
+                                                      : (ss < 1.0f ? 1.0f : ss));
+}
+
 __device__ __forceinline__ float signf_np(float x) {  // numpy.sign
   return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f);
 }

@@ -199,7 +199,7 @@ __device__ __forceinline__ void row_update(const UpdParams& t, int c, int d,
     float pv = p[m].X;                                                  \
     if (ada) {                                                          \
       a[m].X = a[m].X + g * g;                        /* param.py:147 */\
-      pv = pv - (t.lr * g) / fmaxf(sqrtf(a[m].X), 1e-7f); /* 152-155 */ \
+      pv = pv - adagrad_step_fast(t.lr, g, a[m].X);   /* 152-155 */     \
     } else {                                                            \
       pv = pv - t.lr * g;                             /* param.py:130 */\
     }                                                                   \
@@ -214,13 +214,13 @@ __device__ __forceinline__ void row_update(const UpdParams& t, int c, int d,
   }
   if (t.post != POST_NONE) {
     ss = wave_sum(ss);
-    const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss) : (ss < 1.0f ? 1.0f : ss);
+    const float inv = proj_scale_fast(t.post, ss);   // param.py:165-166 / 171-173
 #pragma unroll
     for (int m = 0; m < KQ; ++m) {
-      p[m].x = p[m].x / nrm;
-      p[m].y = p[m].y / nrm;
-      p[m].z = p[m].z / nrm;
-      p[m].w = p[m].w / nrm;
+      p[m].x = p[m].x * inv;
+      p[m].y = p[m].y * inv;
+      p[m].z = p[m].z * inv;
+      p[m].w = p[m].w * inv;
     }
   }
 }

@@ -240,7 +240,7 @@ __device__ __forceinline__ void i16_finish(const TableDev& t, int row, bool upd,
     float pv = p[m].X;                                                  \
     if (ada) {                                                          \
       a[m].X = a[m].X + g * g;                        /* param.py:147 */\
-      pv = pv - (t.lr * g) / fmaxf(sqrtf(a[m].X), 1e-7f); /* 152-155 */ \
+      pv = pv - adagrad_step_fast(t.lr, g, a[m].X);   /* 152-155 */     \
     } else {                                                            \
       pv = pv - t.lr * g;                             /* param.py:130 */\
     }                                                                   \
@@ -255,13 +255,13 @@ __device__ __forceinline__ void i16_finish(const TableDev& t, int row, bool upd,
   }
   if (t.post != POST_NONE && upd) {
     ss = wave_sum(ss);
-    const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss) : (ss < 1.0f ? 1.0f : ss);
+    const float inv = proj_scale_fast(t.post, ss);   // param.py:165-166 / 171-173
 #pragma unroll
     for (int m = 0; m < KQ; ++m) {
-      p[m].x = p[m].x / nrm;
-      p[m].y = p[m].y / nrm;
-      p[m].z = p[m].z / nrm;
-      p[m].w = p[m].w / nrm;
+      p[m].x = p[m].x * inv;
+      p[m].y = p[m].y * inv;
+      p[m].z = p[m].z * inv;
+      p[m].w = p[m].w * inv;
     }
   }
 #pragma unroll
@@ -412,7 +412,9 @@ __device__ __forceinline__ void apply_row_rep_block(const TableDev& t, int row, 
         float np = pv, na = av;
         if (ada) {
           na = av + g * g;
-          np = pv - (t.lr * g) / fmaxf(sqrtf(na), 1e-7f);
+          // packed (exact integer) sums: the fast step of every packed apply
+          np = MODE == ACC_I16X4 ? pv - adagrad_step_fast(t.lr, g, na)
+                                 : pv - (t.lr * g) / fmaxf(sqrtf(na), 1e-7f);
         } else {
           np = pv - t.lr * g;
         }
@@ -423,9 +425,15 @@ __device__ __forceinline__ void apply_row_rep_block(const TableDev& t, int row, 
     }
     if (t.post != POST_NONE && upd) {
       ss = wave_sum(ss);
-      const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss) : (ss < 1.0f ? 1.0f : ss);
+      if (MODE == ACC_I16X4) {
+        const float inv = proj_scale_fast(t.post, ss);
 #pragma unroll
-      for (int k = 0; k < KR; ++k) p[k] = p[k] / nrm;
+        for (int k = 0; k < KR; ++k) p[k] = p[k] * inv;
+      } else {
+        const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss) : (ss < 1.0f ? 1.0f : ss);
+#pragma unroll
+        for (int k = 0; k < KR; ++k) p[k] = p[k] / nrm;
+      }
     }
     if (upd && ada && t.ucnt && l == 0) t.ucnt[row] += 1;   // param.py:149-150
     if (upd) {
