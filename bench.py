@@ -95,7 +95,7 @@ def algorithmic_bytes(d, B, P, U_E, U_R, opt_k=12):
     return 4 * d * (3 * B + P) + opt_k * d * (U_E + U_R) + 20 * B
 
 
-def cpu_baseline(trip, d, nb, seconds=12.0, model="transe", margin=2.0):
+def cpu_baseline(trip, d, nb, seconds=12.0, model="transe", margin=2.0, opt="adagrad"):
     """The oracle (fp64 NumPy restatement, oracle/skge_oracle.py) on a bounded
     sample of the same workload: consecutive nb=100 batches of epoch 1,
     negatives from the reference-semantics host sampler (not timed)."""
@@ -128,7 +128,7 @@ def cpu_baseline(trip, d, nb, seconds=12.0, model="transe", margin=2.0):
         pos = np.array([p for p, _ in pairs])
         neg = np.array([n for _, n in pairs])
         t1 = time.perf_counter()
-        O.pairwise_step(model, params, state, pos, neg, 0.1, margin, "adagrad", l1=True)
+        O.pairwise_step(model, params, state, pos, neg, 0.1, margin, opt, l1=True)
         t2 = time.perf_counter()
         t_step += t2 - t1
         t_all += t2 - t0
@@ -137,11 +137,12 @@ def cpu_baseline(trip, d, nb, seconds=12.0, model="transe", margin=2.0):
         if t_all > seconds:
             break
     return {"value": npos / t_step, "unit": "triples/s", "cores": 1, "kind": "port",
-            "sample": "%d nb=100 batches (%d positives) of epoch 1, WN18-shaped KG, %s "
-                      "d=%d AdaGrad margin %g; oracle/skge_oracle.py fp64 NumPy, 1 thread; "
+            "sample": "%d nb=%d batches (%d positives) of epoch 1, WN18-shaped KG, %s "
+                      "d=%d %s margin %g; oracle/skge_oracle.py fp64 NumPy, 1 thread; "
                       "score+grad+update only (host sampler untimed)"
-                      % (nb_done, npos, {"transe": "TransE-L1", "hole": "HolE",
-                                         "rescal": "RESCAL"}[model], d, margin),
+                      % (nb_done, nb, npos, {"transe": "TransE-L1", "hole": "HolE",
+                                             "rescal": "RESCAL"}[model], d,
+                         {"adagrad": "AdaGrad", "sgd": "SGD"}[opt], margin),
             "e2e_value": npos / t_all}
 
 
@@ -153,14 +154,18 @@ def main():
     ap.add_argument("--nb", type=int, default=100, help="nbatches (reference geometry)")
     ap.add_argument("--d", type=int, default=200)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--opt", choices=["adagrad", "sgd"], default=None,
+                    help="updater (default: AdaGrad; config 1: SGD)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--acc", choices=["auto", "f32"], default="auto",
                     help="accumulator encoding (auto: exact packed int16x4 for TransE-L1)")
     ap.add_argument("--reps", type=int, default=1, help="relation accumulator copies")
     ap.add_argument("--large-nb", type=int, default=2,
                     help="also time this nbatches (large-batch detail line); 0 = skip")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
-                    help="2: WN18 TransE d=200 (the headline); 3: WN18 HolE d=200; 4: WN18 "
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
+                    help="1: WN18 TransE d=50 SGD (BASELINE configs[0], the reference CLI's "
+                         "run_transe.py shape); "
+                         "2: WN18 TransE d=200 (the headline); 3: WN18 HolE d=200; 4: WN18 "
                          "RESCAL d=200 (pairwise, device pair loop); 5: synthetic |E|=50M "
                          "|R|=10k d=512, B=131072 per GPU (BASELINE.json configs[4])")
     ap.add_argument("--c5-scale", type=float, default=1.0,
@@ -174,6 +179,15 @@ def main():
                          "(skge_amd.shard; RCCL all-to-all row fetch + contribution "
                          "reduce-scatter, relation sums all-reduced) instead of replicas")
     args = ap.parse_args()
+    if args.config == 1:
+        # BASELINE configs[0]: TransE on WN18, ncomp=50, nb=100, margin 2.0, SGD
+        # (run_transe_wn18.sh:3-5 / run_transe.py; the reference CLI itself
+        # passes no param_update, i.e. AdaGrad: --opt adagrad times that)
+        args.d = 50
+        if args.opt is None:
+            args.opt = "sgd"
+    if args.opt is None:
+        args.opt = "adagrad"
     if args.config == 5 and args.shard:
         return run_config5_sharded(args)
     if args.config == 5:
@@ -198,7 +212,8 @@ def main():
     np.random.seed(42 + rank)
     model = S.TransE((N_ENT, N_ENT, N_REL), d, l1=True)
     model.add_hyperparam("margin", 2.0)
-    upd = {pid: S.AdaGrad(p, 0.1) for pid, p in model.params.items()}
+    Upd = S.SGD if args.opt == "sgd" else S.AdaGrad
+    upd = {pid: Upd(p, 0.1) for pid, p in model.params.items()}
     kg = DeviceKG(trip, dev)
     runner = EpochRunner(model, upd, kg, nbatches=nb, seed=1234 + rank,
                          force_f32=args.acc == "f32", replicas=args.reps)
@@ -244,9 +259,10 @@ def main():
         p.data.copy_(init[pid])
         upd[pid].reset()
     torch.cuda.synchronize()
+    opt_k = 4 if args.opt == "sgd" else 12     # k = 4 (SGD) / 12 (AdaGrad)
     prof = pipe_profile(runner, kg, nb, d, epochs=args.steps,
-                        gpu_ms_per_epoch=gpu_ms / args.steps) if runner.pipelined else \
-        kernel_profile(model, upd, kg, nb, d, st, runner)
+                        gpu_ms_per_epoch=gpu_ms / args.steps, opt_k=opt_k) if runner.pipelined else \
+        kernel_profile(model, upd, kg, nb, d, st, runner, opt_k=opt_k)
     meas = None
     if runner.pipelined and not args.no_roofline:
         # the same per-launch row traffic without the path's
@@ -259,14 +275,18 @@ def main():
         s_us, s_b, s_gbs = measured_roofline(dev, N_ENT, d, 262144, 5, 0, 0, launches=10, reps=3)
         h_us, h_b, h_gbs = measured_roofline(dev, 5_000_000, d, 262144, 5, 0, 0, launches=10,
                                              reps=3)
+        sg = s_gbs
         meas = {"kernel": "k_roofline (skge_roofline_gather)",
+                "frac_of_streaming_gather": round(prof["dominant"]["achieved_gbs"] / sg, 4),
                 "geometry": "per launch: %d waves x 5 random %d-B row gathers + %d atomic rows "
                             "each, %d rows read+written (20d B), WN18 table"
                             % (npos, 4 * d, int(round(geo["atomic_rows"] / max(npos, 1))),
                                int(round(geo["applied_rows"]))),
                 "avg_launch_us": round(m_us, 3), "bytes_per_launch": round(m_b),
                 "GB_s": round(m_gbs, 1),
-                "frac": round(prof["dominant"]["achieved_gbs"] / m_gbs, 4),
+                "frac": round(prof["dominant"].get("impl_gbs", prof["dominant"]["achieved_gbs"])
+                              / m_gbs, 4),
+                "frac_note": "implementation bytes / the same bytes moved without dependencies",
                 "streaming_gather_GB_s": {"wn18_table_33MB": round(s_gbs, 1),
                                           "table_4GB": round(h_gbs, 1)}}
 
@@ -298,10 +318,13 @@ def main():
             upd[pid].reset()
         torch.cuda.synchronize()
         p2 = pipe_profile(r2, kg, args.large_nb, d, epochs=e2,
-                          gpu_ms_per_epoch=f0.elapsed_time(f1) / e2) if r2.pipelined else \
-            kernel_profile(model, upd, kg, args.large_nb, d, r2.stream, r2)
+                          gpu_ms_per_epoch=f0.elapsed_time(f1) / e2, opt_k=opt_k) if r2.pipelined \
+            else kernel_profile(model, upd, kg, args.large_nb, d, r2.stream, r2, opt_k=opt_k)
         k2 = p2["dominant"]
+        sgl = meas["streaming_gather_GB_s"]["wn18_table_33MB"] if meas else None
         large = {"nbatches": args.large_nb, "batch": N_TRIPLES // args.large_nb,
+                 "frac_of_streaming_gather": round(k2["achieved_gbs"] / sgl, 4) if sgl else None,
+                 "epoch_GB_s_8d": round(p2["epoch_bytes"] / (t2 / e2) / 1e9, 1),
                  "value": round(N_TRIPLES * e2 / t2, 1), "unit": "triples/s",
                  "ms_per_epoch": round(1000.0 * t2 / e2, 4),
                  "kernel": k2["name"], "achieved_GB_s": round(k2["achieved_gbs"], 1),
@@ -311,13 +334,16 @@ def main():
         del r2
 
     if rank == 0:
-        cpu = None if args.no_cpu else cpu_baseline(trip, d, nb, args.cpu_seconds)
+        cpu = None if args.no_cpu else cpu_baseline(trip, d, nb, args.cpu_seconds, opt=args.opt)
         k = prof["dominant"]
         kname = {"transe_sample_grad": "sample_grad", "accum_apply": "k_apply",
                  "pipe_batch": "k_pipe_batch"}[k["name"]]
         traffic, traffic_src = pmc_traffic(kname)
         line = {
-            "metric": "triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X",
+            "metric": "triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X"
+                      if args.config == 2 else
+                      "triples/sec (score+grad+update), WN18 TransE d=%d %s (BASELINE configs[0])"
+                      % (d, args.opt),
             "value": round(value, 1),
             "unit": "triples/s",
             "n_gpus": world,
@@ -330,9 +356,10 @@ def main():
             "dtype": "f32",
             "data": "synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442 uniform, RandomState(rank)); "
                     "random-init params (nunif, seed 42)",
-            "config": {"workload": "TransE-L1 d=%d PairwiseStochasticTrainer+AdaGrad, WN18 shape, "
+            "config": {"workload": "TransE-L1 d=%d PairwiseStochasticTrainer+%s, WN18 shape, "
                                    "nb=%d (B=%d), margin 2.0, lr 0.1, device RandomModeSampler(1,[0,1]); "
-                                   "step = 1 epoch" % (d, nb, N_TRIPLES // nb),
+                                   "step = 1 epoch" % (d, {"sgd": "SGD", "adagrad": "AdaGrad"}[args.opt],
+                                                       nb, N_TRIPLES // nb),
                        "global_batch": N_TRIPLES // nb, "parallelism": "replicas%d" % world},
             "roofline": {"bound": "hbm", "kernel": k["name"],
                          "achieved": round(k["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
@@ -340,6 +367,9 @@ def main():
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,
                          "bytes_per_launch": round(k["bytes_per_launch"]),
+                         "bytes_formula": prof.get("formula"),
+                         "impl_bytes_per_launch": round(k.get("impl_bytes_per_launch",
+                                                              k["bytes_per_launch"])),
                          "avg_launch_us": round(k["avg_us"], 3),
                          "avg_launch_source": "timed-region HIP events (graph replays) minus "
                                               "the draw/advance launches, per batch launch",
@@ -387,7 +417,7 @@ def _apply_bytes(d, rows, packed=True):
     return (16 * d + (4 * d if packed else 8 * d)) * rows
 
 
-def pipe_profile(runner, kg, nb, d, epochs=1, gpu_ms_per_epoch=None, hole=False):
+def pipe_profile(runner, kg, nb, d, epochs=1, gpu_ms_per_epoch=None, hole=False, opt_k=12):
     """Pipelined runner: `epochs` eager epochs with HIP events around every
     launch and the kernel's own per-launch counters (skge_pipe_runner_profile,
     on the runner's stream), started from the same state as the timed region.
@@ -419,18 +449,21 @@ def pipe_profile(runner, kg, nb, d, epochs=1, gpu_ms_per_epoch=None, hole=False)
             t_pipe += float(us[i])
             if cnt:
                 total += algorithmic_bytes(d, cnt, 2 * cnt, 0, 0)
-            total += 12 * d * (UE + UR)
+            total += opt_k * d * (UE + UR)
             geo += (cnt, 2.5 * V if hole else min(5 * cnt, 2 * V + 3 * cnt), UE + UR, 1)
     eager_us = t_pipe / (n * epochs)
     avg_us = eager_us
     if gpu_ms_per_epoch is not None:
         avg_us = (1000.0 * gpu_ms_per_epoch - t_other / epochs) / n
-    bpl = b_pipe / (n * epochs)
+    bpl = b_pipe / (n * epochs)       # implementation bytes (packed sums, atomics)
+    apl = total / (n * epochs)        # SURVEY 8(d) algorithmic bytes
     kern = {("hole_pipe" if hole else "pipe_batch"): {
                            "name": "hole_pipe" if hole else "pipe_batch", "avg_us": avg_us,
                            "launches": n,
-                           "eager_avg_us": eager_us, "bytes_per_launch": bpl,
-                           "achieved_gbs": bpl / (avg_us * 1e-6) / 1e9},
+                           "eager_avg_us": eager_us, "bytes_per_launch": apl,
+                           "achieved_gbs": apl / (avg_us * 1e-6) / 1e9,
+                           "impl_bytes_per_launch": bpl,
+                           "impl_gbs": bpl / (avg_us * 1e-6) / 1e9},
             # per positive: triple 12 B, two filter words 8 B, record 20 B
             "epoch_sample": {"name": "epoch_sample", "avg_us": us0 / epochs, "launches": 1,
                              "bytes_per_launch": 40.0 * T,
@@ -438,7 +471,12 @@ def pipe_profile(runner, kg, nb, d, epochs=1, gpu_ms_per_epoch=None, hole=False)
     g = geo / geo[3]
     return {"kernels": kern, "dominant": kern["hole_pipe" if hole else "pipe_batch"],
             "epoch_bytes": total / epochs,
-            "geometry": {"positives": g[0], "atomic_rows": g[1], "applied_rows": g[2]}}
+            "geometry": {"positives": g[0], "atomic_rows": g[1], "applied_rows": g[2]},
+            # the 8(d) formula's inputs per launch (averaged over the profiled
+            # epochs' n launches): B positives scored, P = 2B pairs, U rows applied
+            "formula": {"launches": n, "B": g[0], "P": 2.0 * g[0], "U": g[2], "d": d,
+                        "k": opt_k, "bytes_per_launch": apl,
+                        "expr": "4d(3B+P) + k d U + 20B"}}
 
 
 def measured_roofline(dev, rows, d, n_gather, rows_per_wave, atom_rows, n_rmw, launches=101,
@@ -484,6 +522,45 @@ def measured_roofline(dev, rows, d, n_gather, rows_per_wave, atom_rows, n_rmw, l
 
 
 N5, M5, D5, T5, B5 = 50_000_000, 10_000, 512, 100_000_000, 131072
+
+
+def cpu_baseline_config5(seconds=10.0, n_ent=1_000_000, n_rel=10_000, d=512, batch=10_000):
+    """The oracle on the config-5 model at SURVEY 6's scaled-down shape (the
+    full 50M x 512 fp64 table and its state, 205 GB, are not a CPU sample):
+    TransE-L1 d=512 AdaGrad margin 2.0, |E|=1M |R|=10k, batches of 10k
+    positives with their RandomModeSampler negatives (untimed), consecutive
+    batches until `seconds` of score+grad+update time."""
+    from oracle import skge_oracle as O
+    rs = np.random.RandomState(5)
+    T = 6 * batch
+    trip = np.stack([rs.randint(n_ent, size=T), rs.randint(n_ent, size=T),
+                     rs.randint(n_rel, size=T)], axis=1)
+    tset = set(map(tuple, trip.tolist()))
+    bnd = np.sqrt(6) / np.sqrt(n_ent + d)
+    E = rs.uniform(-bnd, bnd, size=(n_ent, d))
+    E /= np.sqrt((E ** 2).sum(axis=1))[:, None]
+    bnd = np.sqrt(6) / np.sqrt(n_rel + d)
+    params = {"E": E, "R": rs.uniform(-bnd, bnd, size=(n_rel, d))}
+    state = {k: np.zeros_like(v) for k, v in params.items()}
+    np.random.seed(42)
+    t_step, npos, nbat = 0.0, 0, 0
+    for a in range(0, T, batch):
+        pairs = O.random_mode_sample(trip[a:a + batch], tset, (n_ent, n_ent, n_rel))
+        pos = np.array([p for p, _ in pairs])
+        neg = np.array([q for _, q in pairs])
+        t0 = time.perf_counter()
+        O.pairwise_step("transe", params, state, pos, neg, 0.1, 2.0, "adagrad", l1=True)
+        t_step += time.perf_counter() - t0
+        npos += min(batch, T - a)
+        nbat += 1
+        if t_step > seconds:
+            break
+    return {"value": npos / t_step, "unit": "triples/s", "cores": 1, "kind": "port",
+            "sample": "%d batches of %d positives, TransE-L1 d=%d AdaGrad margin 2.0 at the "
+                      "SURVEY 6 scaled-down config-5 shape (|E|=%d |R|=%d; the 50M-row fp64 "
+                      "table and state do not make a CPU sample); oracle/skge_oracle.py fp64 "
+                      "NumPy, 1 thread; score+grad+update only (host sampler untimed)"
+                      % (nbat, batch, d, n_ent, n_rel)}
 
 
 def make_config5_kg(n_ent, n_rel, n_triples, dev, seed):
@@ -570,7 +647,7 @@ def run_config5(args):
                          "unit": "GB/s", "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 4),
                          "traffic": None, "bytes_per_launch": round(k["bytes_per_launch"]),
                          "avg_launch_us": round(k["avg_us"], 3)},
-            "cpu_baseline": None,
+            "cpu_baseline": None if args.no_cpu else cpu_baseline_config5(args.cpu_seconds),
             "detail": {"runner": "pipelined" if runner.pipelined else "two-launch",
                        "accumulator": "int16x4 exact" if runner.packed else "fp32",
                        "build_s": round(t_build, 1),
@@ -657,7 +734,7 @@ def run_config5_sharded(args):
                          "unit": "GB/s", "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 4),
                          "traffic": None, "bytes_per_launch": round(k["bytes_per_launch"]),
                          "avg_launch_us": round(k["avg_us"], 3)},
-            "cpu_baseline": None,
+            "cpu_baseline": None if args.no_cpu else cpu_baseline_config5(args.cpu_seconds),
             "detail": {"runner": "row-sharded (skge_amd.shard)",
                        "build_s": round(t_build, 1),
                        "violations_per_pair": round(nviol / (2.0 * T_r * (args.warmup + args.steps)), 4),
@@ -889,7 +966,7 @@ def run_config34(args):
         dist.destroy_process_group()
 
 
-def kernel_profile(model, upd, kg, nb, d, st, runner):
+def kernel_profile(model, upd, kg, nb, d, st, runner, opt_k=12):
     """Launch one epoch eagerly with HIP events around every kernel (on the
     stream the kernels run on) and count the algorithmic bytes of each launch
     from the touched-row counts."""
@@ -904,7 +981,8 @@ def kernel_profile(model, upd, kg, nb, d, st, runner):
     bs = T // nb
     sp = L.stream_ptr(st)
     times = {"transe_sample_grad": [], "accum_apply": []}
-    bytes_ = {"transe_sample_grad": 0.0, "accum_apply": 0.0}
+    bytes_ = {"transe_sample_grad": 0.0, "accum_apply": 0.0}     # SURVEY 8(d) share
+    impl = {"transe_sample_grad": 0.0, "accum_apply": 0.0}       # implementation bytes
     total = 0.0
     accE, accR = runner.accE, runner.accR
     with torch.cuda.stream(st):
@@ -928,18 +1006,21 @@ def kernel_profile(model, upd, kg, nb, d, st, runner):
             times["transe_sample_grad"].append(e[0].elapsed_time(e[1]) * 1e3)
             times["accum_apply"].append(e[2].elapsed_time(e[3]) * 1e3)
             P = 2 * cnt
-            b_sg = _score_bytes(d, cnt, V, runner.packed)
-            b_ap = _apply_bytes(d, UE + UR, runner.packed)
-            bytes_["transe_sample_grad"] += b_sg
-            bytes_["accum_apply"] += b_ap
-            total += algorithmic_bytes(d, cnt, P, UE, UR)
+            impl["transe_sample_grad"] += _score_bytes(d, cnt, V, runner.packed)
+            impl["accum_apply"] += _apply_bytes(d, UE + UR, runner.packed)
+            # 8(d): the gathers + indices are the scoring kernel's, k d U the apply's
+            bytes_["transe_sample_grad"] += algorithmic_bytes(d, cnt, P, 0, 0)
+            bytes_["accum_apply"] += float(opt_k) * d * (UE + UR)
+            total += algorithmic_bytes(d, cnt, P, UE, UR, opt_k)
     kern = {}
     for n in times:
         t = np.array(times[n])
         avg = float(t.mean())
         bpl = bytes_[n] / len(t)
+        ipl = impl[n] / len(t)
         kern[n] = {"name": n, "avg_us": avg, "launches": len(t), "bytes_per_launch": bpl,
-                   "achieved_gbs": bpl / (avg * 1e-6) / 1e9}
+                   "achieved_gbs": bpl / (avg * 1e-6) / 1e9, "impl_bytes_per_launch": ipl,
+                   "impl_gbs": ipl / (avg * 1e-6) / 1e9}
     dom = max(kern.values(), key=lambda v: v["avg_us"])
     return {"kernels": kern, "dominant": dom, "epoch_bytes": total}
 

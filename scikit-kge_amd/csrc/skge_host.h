@@ -70,6 +70,13 @@ inline int check_table(const skge_table_t* t, const char* name, bool need_acc) {
                  "%s: unknown accumulator mode %d", name, t->acc_mode);
   SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 || (t->width % 4 == 0 && t->width <= 1024),
                  "%s: packed accumulator needs width %% 4 == 0 and <= 1024", name);
+  // packed sums are TransE-L1's exact integer sign sums: no regularisation
+  // terms and the occurrence count as the divisor (the packed applies' fast
+  // AdaGrad step / projection forms are argued for exactly that case,
+  // skge_device.h adagrad_step_fast)
+  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 ||
+                     (t->rin == 0.0f && t->rout == 0.0f && t->fixed_div <= 0.0f),
+                 "%s: packed accumulator needs rin == rout == 0 and no fixed divisor", name);
   if (need_acc) {
     SKGE_CHECK_ARG(t->acc_sum && t->acc_cnt, "%s: accumulator buffers missing", name);
   }

@@ -1930,15 +1930,23 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
 }
 
 // the in-front W step's epoch end: W / state back into the caller's buffers
-// when the other buffer is current (k_rescal_w_sync), then cur = 0
+// when the other buffer is current (k_rescal_w_sync), then cur = 0.  n = M d^2
+// elements: float4 body + a scalar tail (M d^2 need not be a multiple of 4,
+// e.g. d = 25, M = 7)
 __global__ __launch_bounds__(256) void k_rescal_w_sync(const int* __restrict__ cur, float* W0,
                                                        float* A0, const float* __restrict__ W1,
-                                                       const float* __restrict__ A1, long long n4) {
+                                                       const float* __restrict__ A1, long long n) {
   if (*cur == 0) return;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (long long)gridDim.x * blockDim.x) {
+  const long long n4 = n >> 2;
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (long long i = tid; i < n4; i += (long long)gridDim.x * blockDim.x) {
     reinterpret_cast<float4*>(W0)[i] = reinterpret_cast<const float4*>(W1)[i];
     if (A0) reinterpret_cast<float4*>(A0)[i] = reinterpret_cast<const float4*>(A1)[i];
+  }
+  const long long t = 4 * n4 + tid;   // <= 3 tail elements, threads 0..2 of block 0
+  if (t < n) {
+    W0[t] = W1[t];
+    if (A0) A0[t] = A1[t];
   }
 }
 __global__ void k_rescal_w_reset(int* cur) { *cur = 0; }
@@ -1946,10 +1954,9 @@ __global__ void k_rescal_w_reset(int* cur) { *cur = 0; }
 int skge::rescal_w_sync(hipStream_t st, const WStep& w) {
   if (!w.cur) return SKGE_OK;
   const long long n = (long long)w.M * w.d * w.d;
-  SKGE_CHECK_ARG(n % 4 == 0, "W sync: M d^2 %% 4 != 0");
-  const long long blocks = std::min<long long>((n / 4 + 255) / 256, 2048);
+  const long long blocks = std::max<long long>(1, std::min<long long>((n / 4 + 255) / 256, 2048));
   hipLaunchKernelGGL(k_rescal_w_sync, dim3((unsigned)blocks), dim3(256), 0, st, w.cur, w.W,
-                     w.A, w.W1, w.A1, n / 4);
+                     w.A, w.W1, w.A1, n);
   hipLaunchKernelGGL(k_rescal_w_reset, dim3(1), dim3(1), 0, st, w.cur);
   SKGE_CHECK_LAUNCH("rescal W sync");
   return SKGE_OK;

@@ -466,14 +466,19 @@ def device_sampler_args(trainer, xs, ys):
     """(eligible, ntries, reason): whether PairwiseStochasticTrainer.fit with
     device_loop=True may run the device loop, whose sampler draws what
     RandomModeSampler(1, [0, 1], xs, sz).sample would (skge/sample.py:28-46,
-    skge/base.py:426): every y must be +1 (the labelled-negatives branch,
-    samplef None with y = -1 rows, skge/base.py:1350-1357, pairs given
-    negatives instead) and samplef must be None or such a sampler's sample."""
+    skge/base.py:426).  Needed: every y is +1, samplef is such a sampler's
+    sample, and the sampler rejects against the same training triples the
+    device loop does (its xs == the fit's xs).  samplef None is the
+    reference's labelled-negatives branch (skge/base.py:1350-1357: positives
+    paired with the given y != 1 rows; with none it builds no pairs), which
+    the device loop does not mirror."""
     if ys is not None and not np.all(np.asarray(ys) == 1):
         return False, trainer.ntries, "labelled negatives (y != 1)"
     f = trainer.samplef
     if f is None:
-        return True, trainer.ntries, ""
+        return False, trainer.ntries, ("samplef is None (the labelled-negatives branch, "
+                                       "skge/base.py:1350-1357); pass samplef="
+                                       "RandomModeSampler(1, [0, 1], xs, sz).sample")
     from .sample import RandomModeSampler
     smp = getattr(f, "__self__", None)
     if not isinstance(smp, RandomModeSampler) or getattr(f, "__func__", None) is not \
@@ -485,6 +490,11 @@ def device_sampler_args(trainer, xs, ys):
     n_ent = trainer.model.E.rows
     if tuple(smp.sz[:2]) != (n_ent, n_ent):
         return False, trainer.ntries, "sampler sizes %r differ from the model's" % (smp.sz,)
+    fit_set = set(tuple(int(v) for v in x) for x in
+                  np.asarray(xs, dtype=np.int64).reshape(-1, 3).tolist())
+    if fit_set != smp.xs:
+        return False, trainer.ntries, ("the sampler's rejection set differs from the fit's "
+                                       "triples (the device sampler rejects against xs)")
     return True, smp.ntries, ""
 
 
@@ -498,9 +508,15 @@ def device_optim(trainer, xs, ntries=None):
     if trainer._nviol_dev is None:
         trainer._nviol_dev = torch.zeros(1, dtype=torch.int32, device=dev)
     kg = DeviceKG(xs, dev)
+    which = trainer.device_runner
+    if which == "auto" and trainer.file_gradients is not None:
+        # file_grad's #(violations) / #(updates) columns need the per-row
+        # counters, which only the pair loop keeps (file_grad=None: the
+        # fused / pipelined runners)
+        which = "pairs"
     runner = make_runner(model, trainer._updaters, kg, trainer.nbatches, seed=trainer.seed,
                          ntries=trainer.ntries if ntries is None else ntries,
-                         nviol_total=trainer._nviol_dev, runner=trainer.device_runner)
+                         nviol_total=trainer._nviol_dev, runner=which)
     trainer._runner = runner
     with torch.cuda.stream(runner.stream):
         for trainer.epoch in range(1, trainer.max_epochs + 1):

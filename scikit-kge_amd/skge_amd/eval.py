@@ -47,20 +47,22 @@ class FilteredRankingEval(object):
             idx[p].append((s, o))
         self.idx = dict(idx)
         self._true = triples_array(true_triples)
-        self._kg = None
-        self._answers = None
+        self._kg = {}        # per device: the known-triple set
+        self._answers = {}   # per device: the known-answer CSR
         self.last_ranks = None
 
     def _known_set(self, device):
-        if self._kg is None:
-            self._kg = DeviceKG(self._true, device)
-        return self._kg
+        key = str(torch.device(device))
+        if key not in self._kg:
+            self._kg[key] = DeviceKG(self._true, device)
+        return self._kg[key]
 
     def _known_answers(self, q, device):
         """Per query (s, o, p) its other known tails {o' != o: (s, o', p) known}
         and heads {s' != s: (s', o, p) known}, as int32 CSR on the device (the
         filter of skge/base.py:913-1031 as lists: a handful per query)."""
-        if self._answers is None:
+        key = str(torch.device(device))
+        if key not in self._answers:
             tails, heads = defaultdict(set), defaultdict(set)
             for s, o, p in self._true.tolist():
                 tails[(s, p)].add(o)
@@ -73,8 +75,8 @@ class FilteredRankingEval(object):
                 hoff.append(len(hent))
             as_dev = lambda v: torch.as_tensor(np.asarray(v if v else [0], dtype=np.int32),
                                                device=device)
-            self._answers = (as_dev(toff), as_dev(tent), as_dev(hoff), as_dev(hent))
-        return self._answers
+            self._answers[key] = (as_dev(toff), as_dev(tent), as_dev(hoff), as_dev(hent))
+        return self._answers[key]
 
     def ranks(self, model):
         """[n, 4] int array: tail raw, tail filtered, head raw, head filtered,

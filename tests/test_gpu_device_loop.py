@@ -245,11 +245,14 @@ def test_trainer_device_loop_fit():
     m = S.TransE((400, 400, 6), 32)
     trip, _ = make_kg(400, 6, 3000)
     seen = []
+    xs = [tuple(x) for x in trip.tolist()]
     tr = S.PairwiseStochasticTrainer(m, nbatches=10, max_epochs=3, learning_rate=0.1, margin=2.0,
                                      device_loop=True, file_grad=None, file_embed=None,
+                                     samplef=S.RandomModeSampler(1, [0, 1], xs, (400, 400, 6)).sample,
                                      post_epoch=[lambda t: seen.append((t.epoch, t.nviolations))
                                                  or True])
-    tr.fit([tuple(x) for x in trip.tolist()], [1] * len(trip))
+    tr.fit(xs, [1] * len(trip))
+    assert tr._on_device
     assert [e for e, _ in seen] == [1, 2, 3]
     assert all(v > 0 for _, v in seen)
 

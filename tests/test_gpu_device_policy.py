@@ -107,11 +107,13 @@ def test_forced_packed_overflow_stops_fit_before_callbacks(monkeypatch):
                              seed=kw["seed"], ntries=kw["ntries"], nviol_total=kw["nviol_total"])
 
     monkeypatch.setattr(D, "make_runner", forced)
+    xs = [tuple(x) for x in trip.tolist()]
     tr = S.PairwiseStochasticTrainer(m, nbatches=1, max_epochs=3, margin=1e9, device_loop=True,
                                      file_grad=None, file_embed=None,
+                                     samplef=S.RandomModeSampler(1, [0, 1], xs, (13000, 13000, 5)).sample,
                                      post_epoch=[lambda t: seen.append(t.epoch) or True])
     with pytest.raises(L.SkgeError, match="32767"):
-        tr.fit([tuple(x) for x in trip.tolist()], [1] * len(trip))
+        tr.fit(xs, [1] * len(trip))
     assert seen == []
     monkeypatch.setattr(D, "make_runner", orig)
     L.lib().skge_device_error(L.stream_ptr(), 1)   # leave the global error word clean
@@ -168,6 +170,44 @@ def test_device_loop_reference_sampler_runs_on_device():
                                      samplef=smp.sample, file_grad=None, file_embed=None)
     tr.fit(xs, [1] * len(xs))
     assert tr._runner is not None and tr._on_device
+
+
+def test_device_loop_without_sampler_or_with_foreign_set_stays_on_host():
+    """samplef None is the reference's labelled-negatives branch and a sampler
+    over another triple set rejects other draws: neither runs the device loop."""
+    import skge_amd as S
+    trip, _ = make_kg(60, 4, 300, seed=4)
+    xs = [tuple(x) for x in trip.tolist()]
+    np.random.seed(42)
+    m = S.TransE((60, 60, 4), 16)
+    tr = S.PairwiseStochasticTrainer(m, nbatches=4, max_epochs=1, margin=1.0, device_loop=True,
+                                     file_grad=None, file_embed=None)
+    from skge_amd.device import device_sampler_args
+    ok, _, why = device_sampler_args(tr, xs, [1] * len(xs))
+    assert not ok and "samplef is None" in why
+    smp = S.RandomModeSampler(1, [0, 1], xs[:-5], (60, 60, 4))   # train minus five triples
+    tr2 = S.PairwiseStochasticTrainer(m, nbatches=4, max_epochs=1, margin=1.0, device_loop=True,
+                                      samplef=smp.sample, file_grad=None, file_embed=None)
+    ok, _, why = device_sampler_args(tr2, xs, [1] * len(xs))
+    assert not ok and "rejection set" in why
+
+
+def test_device_loop_file_grad_auto_keeps_counters(tmp_path):
+    """device_runner='auto' with file_grad set: the pair loop, whose per-row
+    counters fill the #(violations) / #(updates) columns."""
+    import skge_amd as S
+    from skge_amd.device import PairLoopRunner
+    trip, _ = make_kg(60, 4, 300, seed=4)
+    xs = [tuple(x) for x in trip.tolist()]
+    for mk in (lambda: S.TransE((60, 60, 4), 16), lambda: S.HolE((60, 60, 4), 16)):
+        np.random.seed(42)
+        m = mk()
+        tr = S.PairwiseStochasticTrainer(m, nbatches=4, max_epochs=1, margin=1.0, device_loop=True,
+                                         samplef=S.RandomModeSampler(1, [0, 1], xs, (60, 60, 4)).sample,
+                                         file_grad=str(tmp_path / "g.txt"), file_embed=None)
+        tr.fit(xs, [1] * len(xs))
+        assert isinstance(tr._runner, PairLoopRunner)
+        assert int(np.asarray(m.E.updateCounts).sum()) > 0
 
 
 def test_outputs_neighbours_accumulate_and_branches(tmp_path):

@@ -179,6 +179,8 @@ def test_trainer_device_loop_any_model(kind):
     seen = []
     tr = S.PairwiseStochasticTrainer(m, nbatches=10, max_epochs=3, learning_rate=0.1,
                                      margin=0.2, device_loop=True, device_runner="pairs",
+                                     samplef=S.RandomModeSampler(1, [0, 1], xs,
+                                                                 (n_ent, n_ent, n_rel)).sample,
                                      file_grad=None, file_embed=None,
                                      post_epoch=[lambda t: seen.append(t.nviolations) or True])
     tr.fit(xs, [1] * len(xs))
@@ -435,6 +437,7 @@ def test_hole_device_loop_auto_selects_pipelined_runner():
     xs = make_kg(200, 5, 1500)
     m = make_model("hole", (200, 200, 5), 16)
     tr = S.PairwiseStochasticTrainer(m, nbatches=10, max_epochs=2, margin=0.2, device_loop=True,
+                                     samplef=S.RandomModeSampler(1, [0, 1], xs, (200, 200, 5)).sample,
                                      file_grad=None, file_embed=None)
     tr.fit(xs, [1] * len(xs))
     assert isinstance(tr._runner, HolePipeRunner)
@@ -584,6 +587,7 @@ def test_rescal_combined_dw_matches_three_items(n_ent, n_rel, T, d, nb, monkeypa
     (300, 5, 2000, 30, 3, "adagrad"),        # d % 4 != 0
     (40943, 18, 14140, 200, 10, "sgd"),      # WN18 entity / relation counts, d, batch size
     (40943, 18, 14140, 200, 9, "sgd"),       # odd number of batches: W ends in the 2nd buffer
+    (300, 7, 2000, 25, 5, "adagrad"),        # odd d, M d^2 % 4 == 3: the W sync's scalar tail
 ])
 def test_rescal_in_front_w_step_matches_apply_side(n_ent, n_rel, T, d, nb, opt, monkeypatch):
     """The W step inside the fused front (written speculatively into a second

@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 import torch
 
+import parity_util
 from golden_util import Case, case_names
 
 pytestmark = pytest.mark.gpu
@@ -29,8 +30,7 @@ def _np(t):
 
 
 def close(got, want, what):
-    np.testing.assert_allclose(_np(got).astype(np.float64), np.asarray(want, dtype=np.float64),
-                               rtol=RTOL, atol=ATOL, err_msg=what)
+    parity_util.check(got, want, what)
 
 
 def build(c):
@@ -61,14 +61,8 @@ def close_adagrad(got, want, p2, lr, what, grad_rounding=None):
     element).  So each element is allowed 1e-5 + 1e-5|want| plus that
     propagated rounding, lr * GRAD_ROUNDING / H.  Elements with a normal
     gradient (H >~ 1e-3) keep the plain 1e-5 bar."""
-    got = _np(got).astype(np.float64)
-    want = np.asarray(want, dtype=np.float64)
-    H = np.maximum(np.sqrt(np.asarray(p2, dtype=np.float64)), 1e-7)
-    e = GRAD_ROUNDING if grad_rounding is None else grad_rounding
-    tol = ATOL + RTOL * np.abs(want) + lr * e / H
-    bad = np.abs(got - want) > tol
-    assert not bad.any(), "%s: %d elements off, max excess %g" % (
-        what, int(bad.sum()), float(np.max(np.abs(got - want) - tol)))
+    parity_util.check(got, want, what, lr=lr, p2=p2,
+                      grad_rounding=GRAD_ROUNDING if grad_rounding is None else grad_rounding)
 
 
 def check_after(c, b, bt, m, upd):

@@ -17,6 +17,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
+import parity_util
 from oracle import skge_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -95,10 +96,11 @@ def _oracle_union(E, R, recs, batches, lr=0.1, margin=2.0):
     return params, state, nv
 
 
-def test_single_rank_batches_match_oracle():
+@pytest.mark.parametrize("d", [200, 512])      # 512: the config-5 width
+def test_single_rank_batches_match_oracle(d):
     from skge_amd.shard import ShardedRunner
     from test_gpu_device_loop import make_kg
-    n_ent, n_rel, d = 300, 5, 200
+    n_ent, n_rel = 300, 5
     trip, _ = make_kg(n_ent, n_rel, 2000)
     E, R = _init_tables(n_ent, n_rel, d, 1)
     dev = torch.device("cuda", 0)
@@ -113,9 +115,10 @@ def test_single_rank_batches_match_oracle():
     params, state, nv = _oracle_union(E, R, [(r.rec.cpu().numpy(), r.rec_n1.cpu().numpy())],
                                       batches)
     assert int(r.nviol_total.item()) == nv > 0
-    np.testing.assert_allclose(r.E.data.cpu().numpy(), params["E"], rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(r.R.data.cpu().numpy(), params["R"], rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(r.updE.p2.cpu().numpy(), state["E"], rtol=1e-5, atol=1e-5)
+    parity_util.check(r.E.data, params["E"], "shard d%d E" % d, lr=0.1, p2=state["E"])
+    parity_util.check(r.R.data, params["R"], "shard d%d R" % d, lr=0.1, p2=state["R"])
+    parity_util.check(r.updE.p2, state["E"], "shard d%d p2 E" % d)
+    parity_util.check(r.updR.p2, state["R"], "shard d%d p2 R" % d)
 
 
 def _free_port():
@@ -126,11 +129,11 @@ def _free_port():
     return port
 
 
-N2, M2, D2, T2 = 400, 6, 128, 3000
+N2, M2, T2 = 400, 6, 3000
 BATCHES2 = [(0, 300), (300, 300)]
 
 
-def _two_rank_worker(rank, world, port, out):
+def _two_rank_worker(rank, world, port, out, D2):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank))
     for p in (ROOT, os.path.join(ROOT, "scikit-kge_amd"), os.path.join(ROOT, "tests")):
@@ -158,11 +161,12 @@ def _two_rank_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_two_ranks_on_one_gpu_match_union_oracle():
+@pytest.mark.parametrize("D2", [128, 512])     # 512: the config-5 width
+def test_two_ranks_on_one_gpu_match_union_oracle(D2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_two_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_two_rank_worker, args=(r, 2, port, q, D2)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=100) for _ in procs), key=lambda x: x[0])
@@ -174,5 +178,5 @@ def test_two_ranks_on_one_gpu_match_union_oracle():
     assert res[0][5] + res[1][5] == nv > 0
     assert np.array_equal(res[0][3], res[1][3])          # both ranks assembled the same table
     assert np.array_equal(res[0][4], res[1][4])          # relation replicas identical
-    np.testing.assert_allclose(res[0][3], params["E"], rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(res[0][4], params["R"], rtol=1e-5, atol=1e-5)
+    parity_util.check(res[0][3], params["E"], "shard 2 ranks d%d E" % D2, lr=0.1, p2=state["E"])
+    parity_util.check(res[0][4], params["R"], "shard 2 ranks d%d R" % D2, lr=0.1, p2=state["R"])
