@@ -10,9 +10,11 @@ mode 1 corrupts o), margin 2.0, lr 0.1 -- run by the native hipGraph epoch
 runner (device permutation, device sampler, fused score+scatter, fused
 mean+AdaGrad+normalize).  value = positive triples fully processed per second.
 
-Multi-GPU: one process per GPU (torchrun); the WN18 tables do not need
-sharding, so every rank trains an independent replica on its own KG
-(DESIGN.md "replicas only"); value = all ranks' triples / max-over-ranks time.
+Multi-GPU (configs 1/2): one process per GPU (torchrun), ONE model trained
+data parallel (skge_amd.dp: every rank scores a slice of each union batch, the
+records are all-gathered over RCCL, every rank applies the whole batch; the
+replicas stay bitwise equal to one GPU's run); value = that model's positive
+triples per second, max-over-ranks time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--nb 100]
 """
@@ -174,6 +176,10 @@ def main():
                     help="skip the measured gather roofline (skge_roofline_gather)")
     ap.add_argument("--runner", default="auto", choices=["auto", "pairs", "hole_pipe"],
                     help="configs 3/4: device runner (auto: HolE pipelined where it applies)")
+    ap.add_argument("--dp-batch", choices=["per-gpu", "global"], default="per-gpu",
+                    help="configs 1/2 on N > 1 GPUs (one model, data parallel): 'per-gpu' keeps "
+                         "the reference's 1414 positives per GPU (union batch N x 1414, nb = "
+                         "nb / N); 'global' keeps the union batch at nb (1414 / N per GPU)")
     ap.add_argument("--shard", action="store_true",
                     help="config 5 only: row-shard E and its AdaGrad state over the ranks "
                          "(skge_amd.shard; RCCL all-to-all row fetch + contribution "
@@ -194,6 +200,8 @@ def main():
         return run_config5(args)
     if args.config in (3, 4):
         return run_config34(args)
+    if dist_env()[0] > 1:
+        return run_dp(args)
 
     import torch
     import torch.distributed as dist
@@ -397,6 +405,98 @@ def main():
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_dp(args):
+    """Configs 1/2 on N > 1 GPUs: ONE TransE-L1 model, data parallel
+    (skge_amd.dp.DataParallelRunner): every rank holds the
+    whole WN18 model, scores its slice of each union batch, the slices'
+    records are all-gathered over RCCL and every rank scatters + applies the
+    whole batch, so all replicas equal one GPU's run on the union batches bit
+    for bit.  value = the ONE model's positive triples per second (one epoch
+    of the KG per step, max over ranks)."""
+    import torch
+    import torch.distributed as dist
+    world, rank, local = dist_env()
+    dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    import skge_amd as S
+    from skge_amd.device import DeviceKG
+    from skge_amd.dp import DataParallelRunner
+    d = args.d
+    nb = max(1, args.nb // world) if args.dp_batch == "per-gpu" else args.nb
+    trip = make_wn18_kg(seed=0)              # ONE model: the same KG on every rank
+    np.random.seed(42)
+    model = S.TransE((N_ENT, N_ENT, N_REL), d, l1=True)
+    model.add_hyperparam("margin", 2.0)
+    Upd = S.SGD if args.opt == "sgd" else S.AdaGrad
+    upd = {pid: Upd(p, 0.1) for pid, p in model.params.items()}
+    kg = DeviceKG(trip, dev)
+    runner = DataParallelRunner(model, upd, kg, nb, seed=1234)
+    init = {pid: p.data.clone() for pid, p in model.params.items()}
+    runner.run(max(args.warmup, 1))          # the first epoch also captures the graph
+    runner.synchronize()
+    for pid, p in model.params.items():      # timed epochs start from the initial tables
+        p.data.copy_(init[pid])
+        upd[pid].reset()
+    runner.nviol_total.zero_()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(runner.stream)
+    runner.run(args.steps)
+    ev1.record(runner.stream)
+    runner.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    dist.barrier()
+    elapsed = max_over_ranks(elapsed, world, dev)
+    gpu_ms = ev0.elapsed_time(ev1)
+    nviol = runner.total_violations()
+    # replicas identical: a checksum of every rank's E must agree
+    ck = torch.tensor([float(model.E.data.double().sum().item()),
+                       float(model.R.data.double().sum().item())], dtype=torch.float64, device=dev)
+    cks = [torch.zeros_like(ck) for _ in range(world)]
+    dist.all_gather(cks, ck)
+    same = all(torch.equal(c, cks[0]) for c in cks)
+    value = N_TRIPLES * args.steps / elapsed
+    bs = N_TRIPLES // nb
+    if rank == 0:
+        line = {
+            "metric": "triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X"
+                      if args.config == 2 else
+                      "triples/sec (score+grad+update), WN18 TransE d=%d %s (BASELINE configs[0])"
+                      % (d, args.opt),
+            "value": round(value, 1), "unit": "triples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442 uniform, RandomState(0)), "
+                    "the same on every rank; random-init params (nunif, seed 42)",
+            "config": {"workload": "ONE TransE-L1 d=%d model, PairwiseStochasticTrainer+%s, WN18 "
+                                   "shape, union batch %d positives (nb=%d; %s), margin 2.0, lr 0.1, "
+                                   "device RandomModeSampler(1,[0,1]); data parallel over %d GPUs: "
+                                   "slice scoring, RCCL all-gather of the records, replicated "
+                                   "scatter + apply; step = 1 epoch"
+                                   % (d, {"sgd": "SGD", "adagrad": "AdaGrad"}[args.opt], bs, nb,
+                                      "~%d per GPU" % (bs // world), world),
+                       "global_batch": bs, "parallelism": "dp%d" % world},
+            "roofline": None,
+            "cpu_baseline": None,
+            "detail": {"runner": "DataParallelRunner (skge_amd.dp)",
+                       "captured_graph": runner.graph is not None,
+                       "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
+                       "batches_per_epoch": len(runner.batches),
+                       "us_per_union_batch": round(1e6 * elapsed / args.steps / len(runner.batches), 2),
+                       "violations_per_pair": round(nviol / (2.0 * N_TRIPLES * args.steps), 4),
+                       "replicas_identical": bool(same),
+                       "record_bytes_per_positive": runner.rec_bytes},
+        }
+        print(json.dumps(line))
+    dist.destroy_process_group()
 
 
 def _score_bytes(d, cnt, V, packed=True, hole=False):

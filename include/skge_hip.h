@@ -61,6 +61,15 @@ enum {
                           flag larger counts, skge_device_error bit 2) -- produced
                           only by skge_transe_sample_grad / the pipelined runner with
                           l1 != 0 and width % 4 == 0 */
+  SKGE_ACC_FX64 = 3,   /* the deterministic reduce mode (float-valued models, off by
+                          default): acc_sum is int64 [rows][width] fixed point with 40
+                          fractional bits; every contribution is rounded once to that
+                          grid and added with an exact integer atomic, so the sums --
+                          and the parameters after the apply -- are the same bits run
+                          to run whatever order the adds arrive in (the reference's
+                          CSR mat-vec is deterministic too, skge/util.py:53-101).
+                          Entity / narrow relation tables (width <= 1024, one copy) of
+                          the per-batch paths and the device pair loop */
   SKGE_ACC_I32X2 = 2   /* pipelined runner's RELATION table only: the same exact sums
                           with 32-bit fields, two elements per int64 (a hot
                           relation's per-batch count passes 32767 long before any
@@ -102,7 +111,7 @@ typedef struct skge_table {
   int rows;
   int width;
   int touched_cap;     /* capacity of acc_touched (slots) */
-  int acc_mode;        /* SKGE_ACC_F32 | SKGE_ACC_I16X4 */
+  int acc_mode;        /* SKGE_ACC_F32 | SKGE_ACC_I16X4 | SKGE_ACC_FX64 */
   int acc_replicas;    /* dense tables only: acc_sum / acc_cnt hold this many
                           copies ([replicas][rows][...]); producers spread their
                           adds over the copies (fewer same-address atomics on
@@ -254,6 +263,37 @@ int skge_transe_sample_grad(void *stream, int l1, const skge_table_t *ent,
                             const void *set, int64_t set_capacity, int64_t start, int count,
                             uint64_t seed, const uint64_t *epoch_key, float margin, int ntries,
                             int *nviol, int *nviol_total, int *neg_out);
+
+/*
+ * Data-parallel TransE-L1 (one model over G ranks; SURVEY.md 8(e) for WN18,
+ * replacing one process's PairwiseStochasticTrainer._process_batch +
+ * _batch_step, skge/base.py:1394-1427 and 1306-1316).  Every rank holds the
+ * whole model and draws the same epoch order and negatives (seed, epoch_key);
+ * the union batch [start, start + count) is split in slices [lo, hi).
+ *   skge_dp_score   scores the slice (sampler, L1 scores, strict margin test,
+ *                   sign sub-gradients, skge/transe.py:48-122) and writes one
+ *                   record per positive into rec_out[(w - lo)]: header
+ *                   {s, o, p, v0 | v1 << 1, s', o', 0, 0} int32 + for a
+ *                   violating positive its sign vectors gp, g0, g1 as 2-bit
+ *                   ternary codes, one uint32 per quad; violations into the
+ *                   64 sharded counters vshards (skge_shard_fold_violations);
+ *   (the caller all-gathers the G slices' records: RCCL)
+ *   skge_dp_scatter adds the whole batch's records into ent / rel's packed
+ *                   (SKGE_ACC_I16X4) accumulators with the slot map of
+ *                   skge_transe_sample_grad (ent 4w+{s,o,s',o'}, rel w): the
+ *                   counts and exact sums one GPU computes for the union
+ *                   batch, so skge_accum_apply then updates every replica
+ *                   bitwise like the one-GPU step.
+ * Record stride: skge_dp_record_bytes(d) (0 if d % 4 != 0).
+ */
+size_t skge_dp_record_bytes(int d);
+int skge_dp_score(void *stream, const skge_table_t *ent, const skge_table_t *rel, int d,
+                  const int *trip, int64_t T, const void *set, int64_t set_capacity,
+                  int64_t start, int count, int lo, int hi, uint64_t seed,
+                  const uint64_t *epoch_key, float margin, int ntries, int *vshards,
+                  void *rec_out);
+int skge_dp_scatter(void *stream, const skge_table_t *ent, const skge_table_t *rel, int d,
+                    int64_t start, int count, const void *records);
 
 /* perm_out[j] = perm_epoch(j) for j < n (tests / host-side replay). */
 int skge_epoch_permutation(void *stream, int64_t T, uint64_t seed, const uint64_t *epoch_key,

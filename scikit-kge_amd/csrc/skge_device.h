@@ -110,11 +110,22 @@ struct Accum {
   int rows;
 };
 
-enum AccMode : int { ACC_F32 = 0, ACC_I16X4 = 1, ACC_I32X2 = 2 };
+enum AccMode : int { ACC_F32 = 0, ACC_I16X4 = 1, ACC_I32X2 = 2, ACC_FX64 = 3 };
 
 // accumulator dwords per row
 __device__ __host__ __forceinline__ int acc_row_dwords(int mode, int width) {
-  return mode == ACC_I16X4 ? (width >> 1) : width;
+  return mode == ACC_I16X4 ? (width >> 1) : (mode == ACC_FX64 ? 2 * width : width);
+}
+
+// ACC_FX64 (the deterministic reduce mode): a float contribution becomes a
+// 64-bit fixed-point integer with 40 fractional bits (one rounding, to the
+// nearest multiple of 2^-40 ~ 9.1e-13, deterministic), sums are exact integer
+// atomics -- the same bits whatever order the adds arrive in -- and the apply
+// converts the sum back once.  |sum| < 2^23 holds for any gradient sum here.
+constexpr float FX_SCALE = 1099511627776.0f;            // 2^40
+__device__ __forceinline__ long long fx_enc(float v) { return __float2ll_rn(v * FX_SCALE); }
+__device__ __forceinline__ float fx_dec(long long x) {
+  return (float)((double)x * (1.0 / 1099511627776.0));
 }
 
 // the copy a producer item adds into (dense replicated tables)
@@ -200,8 +211,17 @@ __device__ __forceinline__ int sel4(int l, int a, int b, int c, int d) {
 
 template <int KM>
 __device__ __forceinline__ void acc_row(const Accum& a, int row, const float (&v)[KM], int d) {
-  float* base = a.sum + (size_t)row * a.width;
   const int l = lane_id();
+  if (a.mode == ACC_FX64) {   // deterministic: exact fixed-point integer sums
+    unsigned long long* base = reinterpret_cast<unsigned long long*>(a.sum) + (size_t)row * a.width;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int e = l + 64 * k;
+      if (e < d && v[k] != 0.0f) atomicAdd(base + e, (unsigned long long)fx_enc(v[k]));
+    }
+    return;
+  }
+  float* base = a.sum + (size_t)row * a.width;
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     const int e = l + 64 * k;

@@ -7,6 +7,7 @@
 // shuffle, and the sampler draws come from a counter-based generator.  The
 // arithmetic per pair is the same as skge_pair_grad's (parity-tested by
 // replaying the recorded negatives through the oracle).
+#include <algorithm>
 #include <vector>
 
 #include "skge_host.h"
@@ -192,57 +193,58 @@ __global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
   count_violations(a, nv);
 }
 
-// TransE-L1 variant with exact packed int16x4 accumulation (ACC_I16X4) and the
-// quad row layout: the sign contributions are small integers, so four
-// elements share one 64-bit integer atomic, and every row gather / row atomic
-// is a single 16-byte-per-lane wave-instruction (d <= 256).
+// TransE-L1, one positive in the quad row layout: the permuted triple, its
+// RandomModeSampler negatives (mode 0 corrupts s, mode 1 corrupts o), the
+// three L1 scores, the strict margin tests and the sign sub-gradients of the
+// positive (gp) and of both negatives (g0, g1) (skge/transe.py:32-46, 73,
+// 103-117).  Shared by the packed two-launch kernel and the data-parallel
+// scorer, so both make bitwise the same decisions.
+struct PosL1 {
+  int s, o, p, neg0, neg1, v0, v1;
+};
 template <int KQ>
-__global__ __launch_bounds__(256) void k_transe_l1_sample_grad_i16(SampleArgs a) {
-  const int wpb = blockDim.x >> 6;
+__device__ __forceinline__ PosL1 transe_l1_front(const SampleArgs& a, const Perm& pm,
+                                                 uint64_t skey, long long j, float4 (&gp)[KQ],
+                                                 float4 (&g0)[KQ], float4 (&g1)[KQ]) {
   const int l = lane_id();
   const int d = a.d;
-  const uint64_t ek = *a.epoch_key;
-  const Perm pm = {(uint64_t)a.T, a.half, epoch_perm_key(a.seed, ek)};
-  const uint64_t skey = epoch_sample_key(a.seed, ek);
-  int nv = 0;
-  for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < a.count; w += gridDim.x * wpb) {
-    const long long j = a.start + w;
 #ifndef SKGE_ABL_NO_PERM
-    const long long t = (long long)perm_index((uint64_t)j, pm);
+  const long long t = (long long)perm_index((uint64_t)j, pm);
 #else
-    const long long t = j;
+  const long long t = j;
 #endif
-    // first tries of both modes do not depend on the positive: their rows load
-    // in the same memory round trip as the triple
-    const int cand0 = draw(skey, j, 0, 0, a.n_ent), cand1 = draw(skey, j, 1, 0, a.n_ent);
-    float4 fs[KQ], fo[KQ];
-    load_row4<KQ>(a.E, cand0, d, fs);
-    load_row4<KQ>(a.E, cand1, d, fo);
-    const int s = __builtin_amdgcn_readfirstlane(a.trip[3 * t]);
-    const int o = __builtin_amdgcn_readfirstlane(a.trip[3 * t + 1]);
-    const int p = __builtin_amdgcn_readfirstlane(a.trip[3 * t + 2]);
-    float4 es[KQ], eo[KQ], rp[KQ];
-    load_row4<KQ>(a.E, s, d, es);
-    load_row4<KQ>(a.E, o, d, eo);
-    load_row4<KQ>(a.R, p, d, rp);
-    bool ok = true;
+  // first tries of both modes do not depend on the positive: their rows load
+  // in the same memory round trip as the triple
+  const int cand0 = draw(skey, j, 0, 0, a.n_ent), cand1 = draw(skey, j, 1, 0, a.n_ent);
+  float4 fs[KQ], fo[KQ];
+  load_row4<KQ>(a.E, cand0, d, fs);
+  load_row4<KQ>(a.E, cand1, d, fo);
+  PosL1 r;
+  r.s = __builtin_amdgcn_readfirstlane(a.trip[3 * t]);
+  r.o = __builtin_amdgcn_readfirstlane(a.trip[3 * t + 1]);
+  r.p = __builtin_amdgcn_readfirstlane(a.trip[3 * t + 2]);
+  const int s = r.s, o = r.o, p = r.p;
+  float4 es[KQ], eo[KQ], rp[KQ];
+  load_row4<KQ>(a.E, s, d, es);
+  load_row4<KQ>(a.E, o, d, eo);
+  load_row4<KQ>(a.R, p, d, rp);
+  bool ok = true;
 #ifndef SKGE_ABL_NO_FILTER
-    if (l < 2) ok = l == 0 ? !set_contains(a.set, cand0, o, p) : !set_contains(a.set, s, cand1, p);
+  if (l < 2) ok = l == 0 ? !set_contains(a.set, cand0, o, p) : !set_contains(a.set, s, cand1, p);
 #endif
-    const uint64_t okm = __ballot(ok);
-    int neg0 = (okm & 1ull) ? cand0 : -1;
-    int neg1 = (okm & 2ull) ? cand1 : -1;
-    if (neg0 < 0 || neg1 < 0) {   // rare: a first draw hit a training triple
-      sample_rest(a, skey, j, s, o, p, 1, neg0, neg1);
-      neg0 = __builtin_amdgcn_readfirstlane(neg0);
-      neg1 = __builtin_amdgcn_readfirstlane(neg1);
-      if (neg0 >= 0 && neg0 != cand0) load_row4<KQ>(a.E, neg0, d, fs);
-      if (neg1 >= 0 && neg1 != cand1) load_row4<KQ>(a.E, neg1, d, fo);
-    }
-    float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
-    float4 gp[KQ], g0[KQ], g1[KQ];
+  const uint64_t okm = __ballot(ok);
+  int neg0 = (okm & 1ull) ? cand0 : -1;
+  int neg1 = (okm & 2ull) ? cand1 : -1;
+  if (neg0 < 0 || neg1 < 0) {   // rare: a first draw hit a training triple
+    sample_rest(a, skey, j, s, o, p, 1, neg0, neg1);
+    neg0 = __builtin_amdgcn_readfirstlane(neg0);
+    neg1 = __builtin_amdgcn_readfirstlane(neg1);
+    if (neg0 >= 0 && neg0 != cand0) load_row4<KQ>(a.E, neg0, d, fs);
+    if (neg1 >= 0 && neg1 != cand1) load_row4<KQ>(a.E, neg1, d, fo);
+  }
+  float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
 #pragma unroll
-    for (int m = 0; m < KQ; ++m) {
+  for (int m = 0; m < KQ; ++m) {
 #define SKGE_EL(X)                                                                    \
   {                                                                                   \
     const float vp = (es[m].X + rp[m].X) - eo[m].X;   /* transe.py:32 */              \
@@ -255,59 +257,173 @@ __global__ __launch_bounds__(256) void k_transe_l1_sample_grad_i16(SampleArgs a)
     g0[m].X = signf_np((eo[m].X - rp[m].X) - fs[m].X);    /* transe.py:104,117 */     \
     g1[m].X = signf_np((fo[m].X - rp[m].X) - es[m].X);                                \
   }
-      SKGE_EL(x)
-      SKGE_EL(y)
-      SKGE_EL(z)
-      SKGE_EL(w)
+    SKGE_EL(x)
+    SKGE_EL(y)
+    SKGE_EL(z)
+    SKGE_EL(w)
 #undef SKGE_EL
+  }
+  const float pscore = -wave_sum(ps);
+  const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
+  r.neg0 = neg0;
+  r.neg1 = neg1;
+  r.v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // strict >, transe.py:73
+  r.v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
+  return r;
+}
+
+// One positive's occurrence counts, touched slots (entity slots
+// 4w+{s,o,s',o'}, relation slot w) and exact packed contributions:
+// pair 0 lists (sp,op,sn,on) = (s,o,s',o), pair 1 = (s,o,s,o')
+// (skge/transe.py:128-160 before the segment mean).
+template <int KQ>
+__device__ __forceinline__ void transe_l1_commit(const SampleArgs& a, long long j, int w,
+                                                 const PosL1& r, const float4 (&gp)[KQ],
+                                                 const float4 (&g0)[KQ], const float4 (&g1)[KQ]) {
+  const int l = lane_id();
+  const int d = a.d;
+  const int v0 = r.v0, v1 = r.v1;
+  {
+    const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
+    const int rE = sel4(l, r.s, r.o, r.neg0, r.neg1);
+    const Accum aR = replica(a.accR, j);
+    if (l < 5) {
+      const bool ent = l < 4;
+      commit_slot(ent ? a.accE.cnt : aR.cnt, ent ? a.accE.touched : aR.touched,
+                  ent ? rE : r.p, ent ? cE : 2 * (v0 + v1), ent ? 4 * w + l : w);
     }
-    const float pscore = -wave_sum(ps);
-    const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
-    const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // strict >, transe.py:73
-    const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
-    if (a.neg_out && l == 0) {
-      a.neg_out[2 * (long long)w] = neg0;
-      a.neg_out[2 * (long long)w + 1] = neg1;
-    }
-    {
-      // occurrence counts + touched slots (entity slots 4w+{s,o,s',o'}):
-      // pair 0 lists (sp,op,sn,on) = (s,o,s',o), pair 1 = (s,o,s,o')
-      const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
-      const int rE = sel4(l, s, o, neg0, neg1);
-      const Accum aR = replica(a.accR, j);
-      if (l < 5) {
-        const bool ent = l < 4;
-        commit_slot(ent ? a.accE.cnt : aR.cnt, ent ? a.accE.touched : aR.touched,
-                    ent ? rE : p, ent ? cE : 2 * (v0 + v1), ent ? 4 * w + l : w);
-      }
-    }
-    if (v0 + v1 == 0) continue;
-    nv += v0 + v1;
-    const float fv0 = (float)v0, fv1 = (float)v1;
-    float4 cs[KQ], co[KQ], c0[KQ], c1[KQ], cr[KQ];
+  }
+  if (v0 + v1 == 0) return;
+  const float fv0 = (float)v0, fv1 = (float)v1;
+  float4 cs[KQ], co[KQ], c0[KQ], c1[KQ], cr[KQ];
 #pragma unroll
-    for (int m = 0; m < KQ; ++m) {
+  for (int m = 0; m < KQ; ++m) {
 #define SKGE_CO(X)                                                   \
   cs[m].X = fv0 * gp[m].X + fv1 * (gp[m].X + g1[m].X);               \
   co[m].X = -(fv0 * (gp[m].X + g0[m].X) + fv1 * gp[m].X);            \
   c0[m].X = g0[m].X;                                                 \
   c1[m].X = -g1[m].X;                                                \
   cr[m].X = fv0 * (gp[m].X + g0[m].X) + fv1 * (gp[m].X + g1[m].X);
-      SKGE_CO(x)
-      SKGE_CO(y)
-      SKGE_CO(z)
-      SKGE_CO(w)
+    SKGE_CO(x)
+    SKGE_CO(y)
+    SKGE_CO(z)
+    SKGE_CO(w)
 #undef SKGE_CO
-    }
+  }
 #ifndef SKGE_ABL_NO_ATOM   // timing-only ablation builds (tools/ablate.sh)
-    acc_row4_i16<KQ>(a.accE, s, cs, d);
-    acc_row4_i16<KQ>(a.accE, o, co, d);
-    if (v0) acc_row4_i16<KQ>(a.accE, neg0, c0, d);
-    if (v1) acc_row4_i16<KQ>(a.accE, neg1, c1, d);
-    acc_row4_i16<KQ>(replica(a.accR, j), p, cr, d);
+  acc_row4_i16<KQ>(a.accE, r.s, cs, d);
+  acc_row4_i16<KQ>(a.accE, r.o, co, d);
+  if (v0) acc_row4_i16<KQ>(a.accE, r.neg0, c0, d);
+  if (v1) acc_row4_i16<KQ>(a.accE, r.neg1, c1, d);
+  acc_row4_i16<KQ>(replica(a.accR, j), r.p, cr, d);
 #endif
+}
+
+// TransE-L1 variant with exact packed int16x4 accumulation (ACC_I16X4) and the
+// quad row layout: the sign contributions are small integers, so four
+// elements share one 64-bit integer atomic, and every row gather / row atomic
+// is a single 16-byte-per-lane wave-instruction (d <= 256).
+template <int KQ>
+__global__ __launch_bounds__(256) void k_transe_l1_sample_grad_i16(SampleArgs a) {
+  const int wpb = blockDim.x >> 6;
+  const int l = lane_id();
+  const uint64_t ek = *a.epoch_key;
+  const Perm pm = {(uint64_t)a.T, a.half, epoch_perm_key(a.seed, ek)};
+  const uint64_t skey = epoch_sample_key(a.seed, ek);
+  int nv = 0;
+  for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < a.count; w += gridDim.x * wpb) {
+    const long long j = a.start + w;
+    float4 gp[KQ], g0[KQ], g1[KQ];
+    const PosL1 r = transe_l1_front<KQ>(a, pm, skey, j, gp, g0, g1);
+    if (a.neg_out && l == 0) {
+      a.neg_out[2 * (long long)w] = r.neg0;
+      a.neg_out[2 * (long long)w + 1] = r.neg1;
+    }
+    nv += r.v0 + r.v1;
+    transe_l1_commit<KQ>(a, j, w, r, gp, g0, g1);
   }
   count_violations(a, nv);
+}
+
+// ---- data-parallel TransE-L1 (one model over G ranks) ----
+// Every rank holds the whole model and draws the same epoch order and
+// negatives; rank g scores positives [lo, hi) of each (union) batch and writes
+// one record per positive: header {s, o, p, flags = v0 | v1 << 1} {neg0, neg1}
+// and, for a violating positive, its three sign vectors gp, g0, g1 as 2-bit
+// ternary codes (0: 0, 1: +1, 2: -1), one 32-bit word per quad q holding
+// (gp, g0, g1) bytes of its four elements.  The records of all ranks are
+// all-gathered (RCCL) and every rank scatters the whole batch with
+// transe_l1_commit -- the same counts, slots and exact packed sums as one GPU
+// scoring the union batch -- then applies it: the replicas stay bitwise equal
+// to the one-GPU run.
+__host__ __device__ inline int dp_record_words(int d) { return 8 + (((d >> 2) + 3) & ~3); }
+
+__device__ __forceinline__ uint32_t tern4(const float4& v) {
+  auto t = [](float x) -> uint32_t { return x > 0.0f ? 1u : (x < 0.0f ? 2u : 0u); };
+  return t(v.x) | (t(v.y) << 2) | (t(v.z) << 4) | (t(v.w) << 6);
+}
+__device__ __forceinline__ float4 untern4(uint32_t b) {
+  auto u = [](uint32_t c) -> float { return (float)(int)(c & 1u) - (float)(int)((c >> 1) & 1u); };
+  return make_float4(u(b), u(b >> 2), u(b >> 4), u(b >> 6));
+}
+
+template <int KQ>
+__global__ __launch_bounds__(256) void k_dp_score(SampleArgs a, int lo, int hi, uint32_t* rec) {
+  const int wpb = blockDim.x >> 6;
+  const int l = lane_id();
+  const int nq = a.d >> 2, rw = dp_record_words(a.d);
+  const uint64_t ek = *a.epoch_key;
+  const Perm pm = {(uint64_t)a.T, a.half, epoch_perm_key(a.seed, ek)};
+  const uint64_t skey = epoch_sample_key(a.seed, ek);
+  int nv = 0;
+  for (int w = lo + blockIdx.x * wpb + (threadIdx.x >> 6); w < hi; w += gridDim.x * wpb) {
+    const long long j = a.start + w;
+    float4 gp[KQ], g0[KQ], g1[KQ];
+    const PosL1 r = transe_l1_front<KQ>(a, pm, skey, j, gp, g0, g1);
+    nv += r.v0 + r.v1;
+    uint32_t* out = rec + (size_t)(w - lo) * rw;
+    if (l < 8) {
+      const int h = sel4(l & 3, r.s, r.o, r.p, r.v0 | (r.v1 << 1));
+      out[l] = (uint32_t)(l < 4 ? h : (l == 4 ? r.neg0 : (l == 5 ? r.neg1 : 0)));
+    }
+    if (r.v0 + r.v1) {
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) {
+        const int q = 64 * m + l;
+        if (q < nq) out[8 + q] = tern4(gp[m]) | (tern4(g0[m]) << 8) | (tern4(g1[m]) << 16);
+      }
+    }
+  }
+  if (lane_id() == 0 && nv) atomicAdd(shard_of(a.vshards), nv);
+}
+
+template <int KQ>
+__global__ __launch_bounds__(256) void k_dp_scatter(SampleArgs a, const uint32_t* __restrict__ rec) {
+  const int wpb = blockDim.x >> 6;
+  const int l = lane_id();
+  const int nq = a.d >> 2, rw = dp_record_words(a.d);
+  for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < a.count; w += gridDim.x * wpb) {
+    const uint32_t* in = rec + (size_t)w * rw;
+    PosL1 r;
+    r.s = (int)__builtin_amdgcn_readfirstlane(in[0]);
+    r.o = (int)__builtin_amdgcn_readfirstlane(in[1]);
+    r.p = (int)__builtin_amdgcn_readfirstlane(in[2]);
+    const int fl = (int)__builtin_amdgcn_readfirstlane(in[3]);
+    r.neg0 = (int)__builtin_amdgcn_readfirstlane(in[4]);
+    r.neg1 = (int)__builtin_amdgcn_readfirstlane(in[5]);
+    r.v0 = fl & 1;
+    r.v1 = (fl >> 1) & 1;
+    float4 gp[KQ], g0[KQ], g1[KQ];
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+      const int q = 64 * m + l;
+      const uint32_t x = (fl && q < nq) ? in[8 + q] : 0u;
+      gp[m] = untern4(x & 0xFFu);
+      g0[m] = untern4((x >> 8) & 0xFFu);
+      g1[m] = untern4((x >> 16) & 0xFFu);
+    }
+    transe_l1_commit<KQ>(a, a.start + w, w, r, gp, g0, g1);
+  }
 }
 
 __global__ void k_perm(long long T, int half, uint64_t seed, const uint64_t* ekp, long long* out,
@@ -347,7 +463,7 @@ static int launch_sample(const SampleArgs& a, bool l1, hipStream_t st) {
     SKGE_CHECK_LAUNCH("transe l1 packed sample grad");
     return SKGE_OK;
   }
-  if (a.accR.mode != ACC_F32) {
+  if (a.accR.mode != ACC_F32 && a.accR.mode != ACC_FX64) {
     set_error("mixed accumulator modes");
     return SKGE_EINVAL;
   }
@@ -465,6 +581,77 @@ extern "C" int skge_transe_sample_grad(void* stream, int l1, const skge_table_t*
   a.count = count;
   a.neg_out = neg_out;
   return launch_sample(a, l1 != 0, as_stream(stream));
+}
+
+extern "C" size_t skge_dp_record_bytes(int d) {
+  return d > 0 && (d & 3) == 0 ? 4 * (size_t)dp_record_words(d) : 0;
+}
+
+static int dp_kq(int d) { return (d / 4 + 63) / 64; }
+
+extern "C" int skge_dp_score(void* stream, const skge_table_t* ent, const skge_table_t* rel, int d,
+                             const int* trip, int64_t T, const void* set_slots,
+                             int64_t set_capacity, int64_t start, int count, int lo, int hi,
+                             uint64_t seed, const uint64_t* epoch_key, float margin, int ntries,
+                             int* vshards, void* rec_out) {
+  SampleArgs a;
+  int rc = fill_sample_args(a, 1, ent, rel, d, trip, T, set_slots, set_capacity, seed, epoch_key,
+                            margin, ntries, nullptr, nullptr);
+  if (rc) return rc;
+  SKGE_CHECK_ARG((d & 3) == 0 && d <= 1024, "data-parallel TransE-L1 needs d %% 4 == 0, d <= 1024");
+  SKGE_CHECK_ARG(start >= 0 && count >= 0 && start + count <= T, "batch out of range");
+  SKGE_CHECK_ARG(0 <= lo && lo <= hi && hi <= count, "slice [lo, hi) out of the batch");
+  SKGE_CHECK_ARG(vshards && (rec_out || lo == hi), "NULL argument");
+  if (lo == hi) return SKGE_OK;
+  a.start = start;
+  a.count = count;
+  a.vshards = vshards;
+  const int n = hi - lo;
+  const int blocks = std::max(1, std::min((n + 3) / 4, 16384));
+  hipStream_t st = as_stream(stream);
+  const int kq = dp_kq(d);
+#define SKGE_DS(K) \
+  hipLaunchKernelGGL((k_dp_score<K>), dim3(blocks), dim3(256), 0, st, a, lo, hi, (uint32_t*)rec_out)
+  if (kq <= 1) SKGE_DS(1);
+  else if (kq <= 2) SKGE_DS(2);
+  else SKGE_DS(4);
+#undef SKGE_DS
+  SKGE_CHECK_LAUNCH("data-parallel score");
+  return SKGE_OK;
+}
+
+extern "C" int skge_dp_scatter(void* stream, const skge_table_t* ent, const skge_table_t* rel,
+                               int d, int64_t start, int count, const void* records) {
+  int rc;
+  if ((rc = check_table(ent, "ent", true)) || (rc = check_table(rel, "rel", true)) ||
+      (rc = check_single(ent, "ent")))
+    return rc;
+  SKGE_CHECK_ARG(ent->acc_mode == SKGE_ACC_I16X4 && rel->acc_mode == SKGE_ACC_I16X4,
+                 "data-parallel scatter needs packed (int16x4) accumulators");
+  SKGE_CHECK_ARG(ent->width == d && rel->width == d && (d & 3) == 0 && d <= 1024, "bad width");
+  SKGE_CHECK_ARG(start >= 0 && count >= 0, "bad batch");
+  if (count == 0) return SKGE_OK;
+  SKGE_CHECK_ARG(records, "NULL records");
+  if ((rc = check_slots(ent, 4ll * count, "ent")) || (rc = check_slots(rel, count, "rel"))) return rc;
+  SampleArgs a = SampleArgs{};
+  a.E = ent->param;
+  a.R = rel->param;
+  a.accE = accum_of(ent);
+  a.accR = accum_of(rel);
+  a.d = d;
+  a.start = start;
+  a.count = count;
+  const int blocks = std::max(1, std::min((count + 3) / 4, 16384));
+  hipStream_t st = as_stream(stream);
+  const int kq = dp_kq(d);
+#define SKGE_DC(K) \
+  hipLaunchKernelGGL((k_dp_scatter<K>), dim3(blocks), dim3(256), 0, st, a, (const uint32_t*)records)
+  if (kq <= 1) SKGE_DC(1);
+  else if (kq <= 2) SKGE_DC(2);
+  else SKGE_DC(4);
+#undef SKGE_DC
+  SKGE_CHECK_LAUNCH("data-parallel scatter");
+  return SKGE_OK;
 }
 
 extern "C" int skge_epoch_permutation(void* stream, int64_t T, uint64_t seed,

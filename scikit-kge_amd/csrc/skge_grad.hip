@@ -811,8 +811,10 @@ bool hole_use_fft(int d) {
 
 bool hole_pos_ok(int af, const skge_table_t* ent, const skge_table_t* rel, int d) {
   return af >= 0 && af <= 3 && d % 4 == 0 && d >= 4 && d <= 256 && ent && rel &&
-         ent->width == d && rel->width == d && ent->acc_mode == SKGE_ACC_F32 &&
-         rel->acc_mode == SKGE_ACC_F32 && ent->acc_replicas <= 1 && ent->acc_sum &&
+         ent->width == d && rel->width == d &&
+         (ent->acc_mode == SKGE_ACC_F32 || ent->acc_mode == SKGE_ACC_FX64) &&
+         (rel->acc_mode == SKGE_ACC_F32 || rel->acc_mode == SKGE_ACC_FX64) &&
+         ent->acc_replicas <= 1 && ent->acc_sum &&
          ent->acc_cnt && rel->acc_sum && rel->acc_cnt;
 }
 

@@ -66,8 +66,12 @@ inline int check_table(const skge_table_t* t, const char* name, bool need_acc) {
   SKGE_CHECK_ARG(t != nullptr, "%s: table is NULL", name);
   SKGE_CHECK_ARG(t->param != nullptr, "%s: param is NULL", name);
   SKGE_CHECK_ARG(t->rows > 0 && t->width > 0, "%s: bad shape %d x %d", name, t->rows, t->width);
-  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 || t->acc_mode == SKGE_ACC_I16X4,
+  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 || t->acc_mode == SKGE_ACC_I16X4 ||
+                     t->acc_mode == SKGE_ACC_FX64,
                  "%s: unknown accumulator mode %d", name, t->acc_mode);
+  SKGE_CHECK_ARG(t->acc_mode != SKGE_ACC_FX64 || (t->width <= 1024 && t->acc_replicas <= 1),
+                 "%s: the deterministic (fixed-point) accumulator needs width <= 1024 and one "
+                 "copy", name);
   SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 || (t->width % 4 == 0 && t->width <= 1024),
                  "%s: packed accumulator needs width %% 4 == 0 and <= 1024", name);
   // packed sums are TransE-L1's exact integer sign sums: no regularisation
@@ -96,7 +100,10 @@ inline int check_single(const skge_table_t* t, const char* name) {
 
 // producers that only write fp32 accumulators
 inline int check_f32(const skge_table_t* t, const char* name) {
-  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32, "%s: this producer needs an fp32 accumulator", name);
+  // float-valued sums: fp32 atomics, or the deterministic fixed-point form
+  // (producers add through acc_row, which handles both)
+  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 || t->acc_mode == SKGE_ACC_FX64,
+                 "%s: this producer needs an fp32 (or fixed-point) accumulator", name);
   return SKGE_OK;
 }
 

@@ -98,20 +98,27 @@ template <int KM>
 __device__ __forceinline__ void mean_row(const TableDev& t, int row, int c, float (&g)[KM]) {
   const int l = lane_id();
   const int w = t.width;
+  const bool fx = t.acc.mode == ACC_FX64;
   float* srow = t.acc.sum + (size_t)row * w;
+  long long* xrow = reinterpret_cast<long long*>(t.acc.sum) + (size_t)row * w;
   const float* prow = t.P + (size_t)row * w;
   const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     const int e = l + 64 * k;
     const int ec = e < w ? e : w - 1;
-    const float sv = srow[ec], pv = prow[ec];
+    const float sv = fx ? fx_dec(xrow[ec]) : srow[ec], pv = prow[ec];
     g[k] = e < w ? (sv + t.rin * pv) / div + t.rout * pv : 0.0f;
   }
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     const int e = l + 64 * k;
-    if (e < w) srow[e] = 0.0f;
+    if (e < w) {
+      if (fx)
+        xrow[e] = 0;
+      else
+        srow[e] = 0.0f;
+    }
   }
   if (l == 0) t.acc.cnt[row] = 0;
 }
@@ -127,7 +134,9 @@ __device__ __forceinline__ void apply_row(const TableDev& t, int row, bool upd) 
   int c = 0;
   if (l == 0) c = atomicExch(t.acc.cnt + row, 0);
   const int w = t.width;
+  const bool fx = t.acc.mode == ACC_FX64;   // deterministic fixed-point sums
   float* __restrict__ srow = t.acc.sum + (size_t)row * w;
+  long long* __restrict__ xrow = reinterpret_cast<long long*>(t.acc.sum) + (size_t)row * w;
   float* __restrict__ prow = t.P + (size_t)row * w;
   float* __restrict__ arow = t.A ? t.A + (size_t)row * w : nullptr;
   const bool ada = t.opt == OPT_ADAGRAD;
@@ -137,7 +146,7 @@ __device__ __forceinline__ void apply_row(const TableDev& t, int row, bool upd) 
     const int e = l + 64 * k;
     const bool in = e < w;
     const int ec = in ? e : w - 1;   // unconditional loads (see load_row)
-    const float sv = srow[ec], pv = prow[ec];
+    const float sv = fx ? fx_dec(xrow[ec]) : srow[ec], pv = prow[ec];
     const float av = ada ? arow[ec] : 0.0f;
     s[k] = in ? sv : 0.0f;
     p[k] = in ? pv : 0.0f;
@@ -172,7 +181,10 @@ __device__ __forceinline__ void apply_row(const TableDev& t, int row, bool upd) 
   for (int k = 0; k < KM; ++k) {
     const int e = l + 64 * k;
     if (e < w) {
-      srow[e] = 0.0f;
+      if (fx)
+        xrow[e] = 0;
+      else
+        srow[e] = 0.0f;
       if (upd) {
         prow[e] = p[k];
         if (ada) arow[e] = a[k];

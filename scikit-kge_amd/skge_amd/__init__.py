@@ -4,7 +4,7 @@ Drop-in for skge's model / updater / trainer protocol: TransE, HolE, RESCAL,
 StochasticTrainer, PairwiseStochasticTrainer, SGD, AdaGrad,
 RandomModeSampler.  Every numeric step runs in libskgehip.so."""
 from .version import __version__
-from .base import Model, StochasticTrainer, PairwiseStochasticTrainer
+from .base import Model, StochasticTrainer, PairwiseStochasticTrainer, set_deterministic, deterministic
 from .transe import TransE
 from .hole import HolE
 from .rescal import RESCAL

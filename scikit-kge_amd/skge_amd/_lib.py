@@ -18,7 +18,7 @@ SKGE_TRANSE_L1, SKGE_TRANSE_L2, SKGE_HOLE, SKGE_RESCAL = 0, 1, 2, 3
 SKGE_AF_LINEAR, SKGE_AF_SIGMOID, SKGE_AF_TANH, SKGE_AF_RELU = 0, 1, 2, 3
 SKGE_SGD, SKGE_ADAGRAD = 0, 1
 SKGE_POST_NONE, SKGE_POST_NORMALIZE, SKGE_POST_NORMLESS1 = 0, 1, 2
-SKGE_ACC_F32, SKGE_ACC_I16X4, SKGE_ACC_I32X2 = 0, 1, 2
+SKGE_ACC_F32, SKGE_ACC_I16X4, SKGE_ACC_I32X2, SKGE_ACC_FX64 = 0, 1, 2, 3
 SKGE_PIPE_LAZY = 1
 
 c_p = ctypes.c_void_p
@@ -97,6 +97,10 @@ SIGNATURES = {
     "skge_shard_score": (c_i, [c_p, T_P, c_i, c_p, c_p, c_i64, c_i, c_p, c_p, c_f, c_p, c_p]),
     "skge_shard_accum": (c_i, [c_p, T_P, c_i, c_p, c_p, c_i64]),
     "skge_shard_fold_violations": (c_i, [c_p, c_p, c_p]),
+    "skge_dp_record_bytes": (c_sz, [c_i]),
+    "skge_dp_score": (c_i, [c_p, T_P, T_P, c_i, c_p, c_i64, c_p, c_i64, c_i64, c_i, c_i, c_i,
+                            c_u64, c_p, c_f, c_i, c_p, c_p]),
+    "skge_dp_scatter": (c_i, [c_p, T_P, T_P, c_i, c_i64, c_i, c_p]),
     "skge_roofline_gather": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i,
                                    ctypes.c_uint32, c_p]),
 }

@@ -14,6 +14,7 @@ numeric step of a batch runs as HIP kernels through libskgehip.so:
   scatter, update -- captured once into a hipGraph by a native runner.
 """
 import logging
+import os
 import pickle
 import timeit
 import warnings
@@ -36,6 +37,24 @@ _DEF_MAX_EPOCHS = 1000
 _DEF_MARGIN = 1.0
 _FILE_GRADIENTS = "gradients.txt"
 _FILE_EMBEDDINGS = "embeddings.txt"
+
+
+_DETERMINISTIC = [os.environ.get("SKGE_DETERMINISTIC", "0") == "1"]
+
+
+def set_deterministic(flag=True):
+    """The deterministic reduce mode (off by default; env SKGE_DETERMINISTIC=1):
+    models created afterwards sum their float gradient contributions as exact
+    64-bit fixed-point integers (SKGE_ACC_FX64) instead of fp32 atomics, so
+    HolE / RESCAL / TransE-L2 parameters are bitwise reproducible run to run,
+    like the reference's CSR mat-vec (skge/util.py:53-101).  Costs 8 B of
+    atomic traffic per element instead of 4; the device loops then run the
+    pair loop (the pipelined HolE runner keeps fp32 sums)."""
+    _DETERMINISTIC[0] = bool(flag)
+
+
+def deterministic():
+    return _DETERMINISTIC[0]
 
 
 class Model(object):
@@ -120,8 +139,13 @@ class Model(object):
             # and spread over copies when rows are very few (pair i adds into
             # copy i mod replicas; the apply / collect fold them)
             reps = 16 if p.rows <= 256 else (4 if p.rows <= 4096 else 1)
+            mode = L.SKGE_ACC_F32
+            if deterministic() and p.width <= 1024 and len(p.shape) == 2:
+                # exact fixed-point sums (one copy): bitwise reproducible
+                # (RESCAL's W sums are plain stores in a fixed order already)
+                mode, reps = L.SKGE_ACC_FX64, 1
             acc = Accumulator(p.rows, p.width, p.data.device, dense=dense,
-                              replicas=reps if dense else 1)
+                              replicas=reps if dense else 1, mode=mode)
             self._acc[pid] = acc
         return acc
 

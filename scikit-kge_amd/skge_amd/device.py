@@ -207,9 +207,12 @@ class EpochRunner(object):
     def _tables(self, model, updaters, packed, rel_replicas, rel_w32=False):
         """The runner's own accumulators (captured by its graph) and tables."""
         from .param import Accumulator
+        from .base import deterministic
         dev = model.device
         E, R = model.params["E"], model.params["R"]
         mode = L.SKGE_ACC_I16X4 if packed else L.SKGE_ACC_F32
+        if not packed and deterministic():   # exact fixed-point sums, one copy
+            mode, rel_replicas = L.SKGE_ACC_FX64, 1
         bs = self.kg.T // self.nbatches
         self.accE = Accumulator(E.rows, E.width, dev, slots=4 * bs, mode=mode)
         # relation rows are hot (every positive adds to one of |R| rows): the
@@ -447,9 +450,10 @@ def make_runner(model, updaters, kg, nbatches, seed=0, ntries=100, nviol_total=N
     HolE -> HolePipeRunner where it applies, RESCAL -> PairLoopRunner),
     'epoch', 'hole_pipe' or 'pairs'."""
     from .transe import TransE
+    from .base import deterministic
     if runner == "auto":
         runner = "epoch" if isinstance(model, TransE) else \
-            ("hole_pipe" if HolePipeRunner.eligible(model) else "pairs")
+            ("hole_pipe" if HolePipeRunner.eligible(model) and not deterministic() else "pairs")
     if runner == "hole_pipe":
         return HolePipeRunner(model, updaters, kg, nbatches, seed=seed, ntries=ntries,
                               nviol_total=nviol_total)

@@ -288,8 +288,10 @@ class Accumulator(object):
                  replicas=1):
         self.rows, self.width, self.mode = rows, width, mode
         self.replicas = replicas if dense else 1
-        # int16x4 mode packs four elements per 8 bytes: width / 2 dwords per row
-        dw = width // 2 if mode == L.SKGE_ACC_I16X4 else width
+        # int16x4 mode packs four elements per 8 bytes: width / 2 dwords per row;
+        # the deterministic fixed-point mode keeps one int64 per element
+        dw = width // 2 if mode == L.SKGE_ACC_I16X4 else \
+            (2 * width if mode == L.SKGE_ACC_FX64 else width)
         self.sum = torch.zeros(self.replicas * rows * dw, dtype=torch.float32, device=device)
         self.cnt = torch.zeros(self.replicas * rows, dtype=torch.int32, device=device)
         self.touched = None if dense else \

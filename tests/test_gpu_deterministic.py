@@ -1,0 +1,84 @@
+"""The deterministic reduce mode (skge_amd.set_deterministic, SKGE_ACC_FX64).
+
+The reference's segment mean is a CSR mat-vec (skge/util.py:53-101): the same
+inputs give the same bits every run.  The default fp32-atomic accumulators of
+the float-valued models (HolE, RESCAL entity rows, TransE-L2) add in arrival
+order, so E is not run-to-run reproducible there.  With the mode on, every
+contribution is rounded once to a 2^-40 fixed-point grid and summed with exact
+integer atomics: two runs of the same epochs must give the same bits, and the
+step must still match the fp64 oracle within the 1e-5 bar.
+"""
+import numpy as np
+import pytest
+import torch
+
+import parity_util
+from oracle import skge_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def det():
+    import skge_amd as S
+    S.set_deterministic(True)
+    yield S
+    S.set_deterministic(False)
+
+
+def _pair_loop(S, kind, xs, n_ent, n_rel, d, nb, epochs=2):
+    from skge_amd import _lib as L
+    from skge_amd.device import DeviceKG, make_runner
+    np.random.seed(42)
+    m = (S.HolE if kind == "hole" else S.RESCAL)((n_ent, n_ent, n_rel), d, rparam=0.05)
+    m.add_hyperparam("margin", 0.2)
+    upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
+    r = make_runner(m, upd, DeviceKG(xs, m.device), nb, seed=3)
+    assert type(r).__name__ == "PairLoopRunner"
+    assert m.accumulator("E").mode == L.SKGE_ACC_FX64
+    with torch.cuda.stream(r.stream):
+        r.run(epochs)
+    r.synchronize()
+    return int(r.nviol_total.item()), {pid: p.data.cpu().numpy().copy()
+                                       for pid, p in m.params.items()}
+
+
+@pytest.mark.parametrize("kind", ["hole", "rescal"])
+def test_pair_loop_bitwise_reproducible(det, kind):
+    from test_gpu_pairloop import make_kg
+    n_ent, n_rel, T, d, nb = 40943, 18, 14140, 200, 10   # WN18 rows, d, batch size
+    xs = make_kg(n_ent, n_rel, T, seed=4)
+    a = _pair_loop(det, kind, xs, n_ent, n_rel, d, nb)
+    b = _pair_loop(det, kind, xs, n_ent, n_rel, d, nb)
+    assert a[0] == b[0] > 0
+    for pid in a[1]:
+        assert np.array_equal(a[1][pid], b[1][pid]), pid
+
+
+def test_transe_l2_epoch_runner_bitwise_reproducible(det):
+    from skge_amd import _lib as L
+    from skge_amd.device import DeviceKG, EpochRunner
+    from test_gpu_device_loop import make_kg
+    trip, _ = make_kg(3000, 11, 12000)
+    out = []
+    for _ in range(2):
+        np.random.seed(7)
+        m = det.TransE((3000, 3000, 11), 64, l1=False)
+        m.add_hyperparam("margin", 2.0)
+        upd = {pid: det.AdaGrad(p, 0.1) for pid, p in m.params.items()}
+        r = EpochRunner(m, upd, DeviceKG(trip, m.device), nbatches=6, seed=2)
+        assert not r.packed and r.accE.mode == L.SKGE_ACC_FX64
+        r.run(2)
+        r.synchronize()
+        out.append((int(r.nviol_total.item()), m.E.data.cpu().numpy().copy(),
+                    m.R.data.cpu().numpy().copy()))
+    assert out[0][0] == out[1][0] > 0
+    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])
+
+
+@pytest.mark.parametrize("kind", ["hole", "rescal"])
+def test_deterministic_step_matches_oracle(det, kind):
+    """The fixed-point sums still meet the 1e-5 bar against the fp64 oracle
+    (per batch from the device state, as tests/test_gpu_models.py)."""
+    from test_gpu_models import _run
+    _run(kind, 400, 18, 200, 700 if kind == "rescal" else 500, nb=2)

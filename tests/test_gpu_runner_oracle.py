@@ -11,13 +11,13 @@ Each is checked here DIRECTLY against oracle.pairwise_step
 skge/param.py:140-174), not through another HIP path:
 
   WN18's entity and relation counts (N = 40943, M = 18), d = 200 and batch
-  size (B = 1414 positives, 2828 pairs); the KG holds 3 x 1414 triples so one
-  epoch is exactly 3 batches.  One epoch is trained first (AdaGrad state
-  non-zero, tables moved), the device state is snapshotted, one more epoch
-  runs, and the oracle replays that epoch's 3 batches -- the pairs the
+  size (B = 1414 positives, 2828 pairs).  The oracle replays the pairs the
   device drew (skge_epoch_sample, the same keyed draws the runners make) in
   the order PairwiseStochasticTrainer._process_batch builds them
-  (skge/base.py:1394-1427) -- from the snapshot.
+  (skge/base.py:1394-1427), from the device state snapshotted before them:
+  (a) AdaGrad, the bench's updater: one batch per epoch, each batch from the
+      device state right before it;
+  (b) one epoch of 3 batches (the pipelined hand-off between batches), SGD.
 
 Bar: violation totals EXACTLY equal; parameters and AdaGrad state within
 1e-5 + 1e-5|x| (+ the propagated AdaGrad rounding lr*1e-8/max(sqrt(p2),1e-7),
@@ -33,11 +33,9 @@ from oracle import skge_oracle as O
 pytestmark = pytest.mark.gpu
 
 N, M, D, B = 40943, 18, 200, 1414
-NB = 3
-T = NB * B
 
 
-def _kg(seed=21):
+def _kg(T, seed=21):
     rs = np.random.RandomState(seed)
     seen, out = set(), []
     while len(out) < T:
@@ -64,76 +62,103 @@ def _pairs(rec, n1, start, count):
 
 def _snapshot(m, upd):
     params = {pid: p.data.detach().cpu().numpy().astype(np.float64) for pid, p in m.params.items()}
-    state = {pid: upd[pid].p2.detach().cpu().numpy().astype(np.float64) for pid in m.params}
+    state = {pid: upd[pid].p2.detach().cpu().numpy().astype(np.float64)
+             for pid in m.params if getattr(upd[pid], "p2", None) is not None}
     return params, state
 
 
-def _replay_and_check(kind, m, upd, runner, kg, seed, **kw):
+def _epoch_vs_oracle(kind, m, upd, runner, kg, seed, epoch, nb, opt, what, **kw):
+    """Run epoch `epoch` (0-based; the runner's key is at it) on the device and
+    replay its batches through the oracle from the device state before it."""
     from skge_amd.device import batch_sizes, epoch_records
-    runner.run(1)                       # epoch 1: moves the tables, fills the AdaGrad state
-    runner.synchronize()
     params, state = _snapshot(m, upd)
+    if opt == "sgd":
+        state = {k: np.zeros_like(v) for k, v in params.items()}
     v0 = int(runner.nviol_total.item())
-    rec, n1 = epoch_records(kg, N, seed, 1)   # epoch 2's draws (epoch key 1)
+    rec, n1 = epoch_records(kg, N, seed, epoch)
     rec, n1 = rec.cpu().numpy(), n1.cpu().numpy()
     runner.run(1)
     runner.synchronize()
     got_v = int(runner.nviol_total.item()) - v0
-    want_v = 0
-    start = 0
-    sizes = batch_sizes(kg.T, NB)
-    assert sizes == [B] * NB
+    want_v, start = 0, 0
+    sizes = batch_sizes(kg.T, nb)
+    assert sizes == [B] * nb
     for c in sizes:
         pos, neg = _pairs(rec, n1, start, c)
         start += c
         assert len(pos) == 2 * c          # WN18-sparse: every negative found
-        want_v += O.pairwise_step(kind, params, state, pos, neg, 0.1, float(m.margin), "adagrad",
-                                  **kw)[2]
-    assert got_v == want_v > 0, (kind, got_v, want_v)
+        want_v += O.pairwise_step(kind, params, state, pos, neg, 0.1, float(m.margin), opt, **kw)[2]
+    assert got_v == want_v > 0, (what, got_v, want_v)
     for pid in m.params:
-        parity_util.check(m.params[pid].data, params[pid], "%s runner %s" % (kind, pid),
-                          lr=0.1, p2=state[pid])
-        parity_util.check(upd[pid].p2, state[pid], "%s runner p2 %s" % (kind, pid))
+        if opt == "adagrad":
+            parity_util.check(m.params[pid].data, params[pid], "%s %s" % (what, pid),
+                              lr=0.1, p2=state[pid])
+            parity_util.check(upd[pid].p2, state[pid], "%s p2 %s" % (what, pid))
+        else:
+            parity_util.check(m.params[pid].data, params[pid], "%s %s" % (what, pid))
     return got_v
 
 
-def _setup(cls, **kw):
+def _setup(cls, T, opt, **kw):
     import skge_amd as S
     from skge_amd.device import DeviceKG
     np.random.seed(42)
     m = cls((N, N, M), D, **kw)
-    upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
-    kg = DeviceKG(_kg(), m.device)
+    U = S.AdaGrad if opt == "adagrad" else S.SGD
+    upd = {pid: U(p, 0.1) for pid, p in m.params.items()}
+    kg = DeviceKG(_kg(T), m.device)
     return m, upd, kg
 
 
-def test_transe_pipelined_runner_vs_oracle():
+def _runner(kind, m, upd, kg, nb, seed):
+    from skge_amd.device import EpochRunner, HolePipeRunner, PairLoopRunner, make_runner
+    if kind == "transe":
+        r = EpochRunner(m, upd, kg, nbatches=nb, seed=seed)
+        assert r.pipelined and r.packed
+    elif kind == "hole":
+        r = HolePipeRunner(m, upd, kg, nb, seed=seed)
+    else:
+        r = make_runner(m, upd, kg, nb, seed=seed)      # auto: the fused-front pair loop
+        assert isinstance(r, PairLoopRunner)
+    return r
+
+
+CASES = {"transe": ("TransE", {"l1": True}, 2.0, {"l1": True}),
+         "hole": ("HolE", {}, 0.2, {"af": O.Sigmoid}),
+         "rescal": ("RESCAL", {}, 0.2, {"af": O.Linear})}
+
+
+@pytest.mark.parametrize("kind", ["transe", "hole", "rescal"])
+def test_runner_adagrad_batches_vs_oracle_from_device_state(kind):
+    """AdaGrad (the bench configuration): one batch of B = 1414 positives per
+    epoch, 3 epochs; every batch replayed from the device state (parameters
+    AND AdaGrad state) right before it, so rounding-level differences of a
+    near-zero first gradient are not compounded through p2 across batches."""
     import skge_amd as S
-    from skge_amd.device import EpochRunner
-    m, upd, kg = _setup(S.TransE, l1=True)
-    m.add_hyperparam("margin", 2.0)
-    r = EpochRunner(m, upd, kg, nbatches=NB, seed=31)
-    assert r.pipelined and r.packed
+    name, ckw, margin, okw = CASES[kind]
+    m, upd, kg = _setup(getattr(S, name), B, "adagrad", **ckw)
+    m.add_hyperparam("margin", margin)
+    r = _runner(kind, m, upd, kg, 1, 41)
     with torch.cuda.stream(r.stream):
-        _replay_and_check("transe", m, upd, r, kg, 31, l1=True)
+        for e in range(3):
+            _epoch_vs_oracle(kind, m, upd, r, kg, 41, e, 1, "adagrad",
+                             "%s runner adagrad e%d" % (kind, e), **okw)
 
 
-def test_hole_pipe_runner_vs_oracle():
+@pytest.mark.parametrize("kind", ["transe", "hole", "rescal"])
+def test_runner_epoch_of_three_batches_vs_oracle(kind):
+    """One epoch of 3 batches (B = 1414): the pipelined hand-off between
+    batches (rows of batch b-1 applied while batch b is scored) in the chain.
+    SGD keeps the 3-batch oracle chain linear (AdaGrad's per-element divisor
+    would compound rounding of near-zero first gradients across batches, see
+    the test above); an epoch is trained first so the tables have moved."""
     import skge_amd as S
-    from skge_amd.device import HolePipeRunner
-    m, upd, kg = _setup(S.HolE)
-    m.add_hyperparam("margin", 0.2)
-    r = HolePipeRunner(m, upd, kg, NB, seed=32)
+    name, ckw, margin, okw = CASES[kind]
+    m, upd, kg = _setup(getattr(S, name), 3 * B, "sgd", **ckw)
+    m.add_hyperparam("margin", margin)
+    r = _runner(kind, m, upd, kg, 3, 42)
     with torch.cuda.stream(r.stream):
-        _replay_and_check("hole", m, upd, r, kg, 32, af=O.Sigmoid)
-
-
-def test_rescal_fused_front_runner_vs_oracle():
-    import skge_amd as S
-    from skge_amd.device import make_runner, PairLoopRunner
-    m, upd, kg = _setup(S.RESCAL)
-    m.add_hyperparam("margin", 0.2)
-    r = make_runner(m, upd, kg, NB, seed=33)          # auto: the fused-front pair loop
-    assert isinstance(r, PairLoopRunner)
-    with torch.cuda.stream(r.stream):
-        _replay_and_check("rescal", m, upd, r, kg, 33, af=O.Linear)
+        r.run(1)
+        r.synchronize()
+        _epoch_vs_oracle(kind, m, upd, r, kg, 42, 1, 3, "sgd", "%s runner sgd 3 batches" % kind,
+                         **okw)
