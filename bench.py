@@ -836,6 +836,8 @@ def run_config5_sharded(args):
                          "avg_launch_us": round(k["avg_us"], 3)},
             "cpu_baseline": None if args.no_cpu else cpu_baseline_config5(args.cpu_seconds),
             "detail": {"runner": "row-sharded (skge_amd.shard)",
+                       "bucket_capacity": runner.C,
+                       "captured_graph": runner.graph is not None,
                        "build_s": round(t_build, 1),
                        "violations_per_pair": round(nviol / (2.0 * T_r * (args.warmup + args.steps)), 4),
                        "phases_ms_per_batch": {n: round(v, 4) for n, v in prof["phases_ms"].items()},
@@ -851,17 +853,18 @@ def run_config5_sharded(args):
 
 def shard_profile(runner, d, nbatch=6):
     """The phases of `nbatch` sharded steps (skge_amd.shard.sharded_step,
-    replayed here with HIP events on the runner stream between phases; the
-    collectives' time shows in the phases that wait for them) and the
-    algorithmic bytes of each HIP kernel: route 52 B per positive (record +
+    replayed here eagerly with HIP events on the runner stream between
+    phases; the collectives' time shows in the phases that wait for them) and
+    the algorithmic bytes of each HIP kernel: route 52 B per positive (record +
     request ids + slots), gather 8d + 4 B per row served, score 20d + 20 B per
     positive (4 fetched rows + R row) + d + 16 B per contribution record + 2d
     per violating positive's R row, accum d + 20 B per record + 4d per
-    non-empty record (packed sums read+written), apply 20d per applied row."""
+    non-empty record (packed sums read+written), apply 20d per applied row.
+    Fixed-capacity layout: every all-to-all moves G x C slots."""
     import torch
     ops, ex, st = runner.ops, runner.ex, runner.stream
-    names = ["route", "split_sizes", "a2a_ids", "gather", "a2a_rows", "score", "a2a_contrib",
-             "accum", "allreduce_R", "apply"]
+    names = ["route", "a2a_ids", "gather", "a2a_rows", "score", "a2a_contrib", "accum",
+             "allreduce_R", "apply"]
     ms = {n: 0.0 for n in names}
     kb = {n: 0.0 for n in ("route", "gather", "score", "accum", "apply")}
     batches = [b for b in runner.batches if b[1] > 0][:nbatch]
@@ -870,38 +873,39 @@ def shard_profile(runner, d, nbatch=6):
         for start, count in batches:
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
             ev[0].record(st)
-            send_ids, req_pos, cnts = ops.route(start, count, ex.G)
+            send_ids, req_pos = ops.route(start, count)
             ev[1].record(st)
-            send, recv = ex.split_sizes(cnts)
+            recv_ids = ex.all_to_all(send_ids, ops.buf("recv_ids"))
             ev[2].record(st)
-            recv_ids = ex.all_to_all(send_ids, send, recv)
-            ev[3].record(st)
             rows = ops.gather(recv_ids)
+            ev[3].record(st)
+            fetched = ex.all_to_all(rows, ops.buf("fetched"))
             ev[4].record(st)
-            fetched = ex.all_to_all(rows, recv, send)
-            ev[5].record(st)
             contrib = ops.score(start, count, fetched, req_pos)
+            ev[5].record(st)
+            rc = ex.all_to_all(contrib, ops.buf("recv_contrib"))
             ev[6].record(st)
-            rc = ex.all_to_all(contrib, send, recv)
-            ev[7].record(st)
             ops.accum(recv_ids, rc)
-            ev[8].record(st)
+            ev[7].record(st)
             for t in ops.rel_sums():
                 ex.all_reduce_(t)
-            ev[9].record(st)
-            nz = int((rc[:, :4].contiguous().view(torch.int32)[:, 0] > 0).sum().item())
+            ev[8].record(st)
+            st.synchronize()
+            valid = recv_ids >= 0
+            nrecv = int(valid.sum().item())
+            nsend = int((send_ids >= 0).sum().item())
+            nz = int(((rc[:, :4].contiguous().view(torch.int32)[:, 0] > 0) & valid).sum().item())
             touched = int((runner.accE.cnt != 0).sum().item()) + int((runner.accR.cnt != 0).sum().item())
-            e_apply = torch.cuda.Event(enable_timing=True)
-            e_apply.record(st)
-            ops.apply(int(sum(recv)))
-            ev[10].record(st)
+            ea = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ea[0].record(st)
+            ops.apply()
+            ea[1].record(st)
             st.synchronize()
             for i, n in enumerate(names):
-                ms[n] += (e_apply if n == "apply" else ev[i]).elapsed_time(ev[i + 1])
-            nrecv = int(sum(recv))
+                ms[n] += ea[0].elapsed_time(ea[1]) if n == "apply" else ev[i].elapsed_time(ev[i + 1])
             kb["route"] += 52.0 * count
             kb["gather"] += (8.0 * d + 4) * nrecv
-            kb["score"] += (20.0 * d + 20) * count + (d + 16.0) * int(sum(send)) + 2.0 * d * count
+            kb["score"] += (20.0 * d + 20) * count + (d + 16.0) * nsend + 2.0 * d * count
             kb["accum"] += (d + 20.0) * nrecv + 4.0 * d * nz
             kb["apply"] += 20.0 * d * touched
     n = max(len(batches), 1)

@@ -447,7 +447,17 @@ size_t skge_shard_route_workspace_bytes(int count, int G);
 int skge_shard_route(void *stream, const int *rec, const int *rec_n1, int64_t start, int count,
                      int G, int *send_ids, int *req_pos, long long *counts, void *workspace,
                      size_t ws_bytes);
-/* Owner side: rows_out[i] = E_shard[ids[i] / G] for i < n ([n][d] fp32). */
+/* The fixed-capacity layout of the graph-capturable step (no host-side split
+ * sizes): send_ids [G][C] = bucket g holds the requests owned by rank g in
+ * request order, unused slots -1 (the all-to-alls then move G equal slices);
+ * req_pos [4*count] = bucket slot of request 4j+k (-1: skipped negative).  A
+ * bucket needing more than C slots sets *err |= 1 (its requests are dropped:
+ * the caller must check *err).  The consumers below skip ids < 0. */
+int skge_shard_route_cap(void *stream, const int *rec, const int *rec_n1, int64_t start,
+                         int count, int G, int C, int *send_ids, int *req_pos, void *workspace,
+                         size_t ws_bytes, int *err);
+/* Owner side: rows_out[i] = E_shard[ids[i] / G] for i < n ([n][d] fp32;
+ * ids[i] < 0: nothing written). */
 int skge_shard_gather(void *stream, const float *E_shard, int d, int G, const int *ids, int64_t n,
                       float *rows_out);
 /* Contribution record of one request: int32 count, pad to 16 B, int8[d]. */
@@ -462,7 +472,7 @@ int skge_shard_score(void *stream, const skge_table_t *rel, int d, const int *re
                      const int *rec_n1, int64_t start, int count, const float *fetched,
                      const int *req_pos, float margin, void *contrib, int *vshards);
 /* Owner side: add the n received records into ent_shard's packed sums (local
- * row ids[i] / G), touched slot i per record; touched_cap >= n. */
+ * row ids[i] / G), touched slot i per record (-1 for ids[i] < 0); touched_cap >= n. */
 int skge_shard_accum(void *stream, const skge_table_t *ent_shard, int G, const int *ids,
                      const void *contrib, int64_t n);
 /* *nviol_total += the violation shards, which are cleared. */

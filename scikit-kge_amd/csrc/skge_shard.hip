@@ -113,14 +113,79 @@ __global__ __launch_bounds__(ROUTE_BLOCK) void k_route_scatter(
   req_pos[i] = off;
 }
 
-// owner side: rows_out[i] = E_shard[ids[i] / G]; one wave per row, 16-B lanes
+// Fixed-capacity layout (graph-capturable step, no host-side split sizes):
+// the send buffer holds G buckets of C request slots each, bucket g = owner g,
+// request order inside a bucket, unused slots -1.  Offsets inside each bucket:
+// the same per-(owner, workgroup) exclusive scan with every bucket starting at
+// 0; a bucket past C raises *err (the runner checks it after the epoch).
+__global__ __launch_bounds__(256) void k_route_scan_cap(int* __restrict__ bcnt, int nblk, int G) {
+  __shared__ int part[256];
+  for (int g = 0; g < G; ++g) {
+    int run = 0;
+    for (int b0 = 0; b0 < nblk; b0 += 256) {
+      const int b = b0 + threadIdx.x;
+      const int v = b < nblk ? bcnt[g * nblk + b] : 0;
+      part[threadIdx.x] = v;
+      __syncthreads();
+      for (int off = 1; off < 256; off <<= 1) {
+        const int t = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += t;
+        __syncthreads();
+      }
+      if (b < nblk) bcnt[g * nblk + b] = run + part[threadIdx.x] - v;
+      run += part[255];
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(ROUTE_BLOCK) void k_route_scatter_cap(
+    const int4* __restrict__ rec, const int* __restrict__ rec_n1, long long start, int cnt, int G,
+    int C, const int* __restrict__ boff, int* __restrict__ send_ids, int* __restrict__ req_pos,
+    int* __restrict__ err) {
+  __shared__ int wcnt[ROUTE_BLOCK / 64][SHARD_MAX_RANKS];
+  const int nblk = gridDim.x;
+  const int l = lane_id(), wv = threadIdx.x >> 6;
+  const long long i = (long long)blockIdx.x * ROUTE_BLOCK + threadIdx.x;
+  const bool in = i < 4ll * cnt;
+  const int id = in ? request_id(rec, rec_n1, start + (i >> 2), (int)(i & 3)) : -1;
+  const int owner = id >= 0 ? id % G : -1;
+  const uint64_t lt = (1ull << l) - 1ull;
+  int rank_in_wave = 0;
+  for (int g = 0; g < G; ++g) {
+    const uint64_t m = __ballot(owner == g);
+    if (owner == g) rank_in_wave = __popcll(m & lt);
+    if (l == 0) wcnt[wv][g] = __popcll(m);
+  }
+  __syncthreads();
+  if (!in) return;
+  if (owner < 0) {
+    req_pos[i] = -1;
+    return;
+  }
+  int off = boff[owner * nblk + blockIdx.x] + rank_in_wave;
+  for (int w = 0; w < wv; ++w) off += wcnt[w][owner];
+  if (off >= C) {            // bucket overflow: flagged, the request dropped
+    atomicOr(err, 1);
+    req_pos[i] = -1;
+    return;
+  }
+  send_ids[owner * C + off] = id;
+  req_pos[i] = owner * C + off;
+}
+
+// owner side: rows_out[i] = E_shard[ids[i] / G] (ids[i] < 0: an unused slot,
+// nothing written); one wave per row, 16-B lanes
 __global__ __launch_bounds__(256) void k_shard_gather(const float* __restrict__ E, int d, int G,
                                                       const int* __restrict__ ids, long long n,
                                                       float* __restrict__ rows_out) {
   const int wpb = blockDim.x >> 6, l = lane_id(), nq = d >> 2;
   for (long long w = (long long)blockIdx.x * wpb + (threadIdx.x >> 6); w < n;
        w += (long long)gridDim.x * wpb) {
-    const int row = __builtin_amdgcn_readfirstlane(ids[w]) / G;
+    const int id = __builtin_amdgcn_readfirstlane(ids[w]);
+    if (id < 0) continue;
+    const int row = id / G;
     const float4* src = reinterpret_cast<const float4*>(E + (size_t)row * d);
     float4* dst = reinterpret_cast<float4*>(rows_out + (size_t)w * d);
     for (int q = l; q < nq; q += 64) dst[q] = src[q];
@@ -264,8 +329,13 @@ __global__ __launch_bounds__(256) void k_shard_accum(Accum acc, int d, int G,
   for (long long w = (long long)blockIdx.x * wpb + (threadIdx.x >> 6); w < n;
        w += (long long)gridDim.x * wpb) {
     const uint8_t* rec = C + (size_t)w * cstride;
+    const int id = __builtin_amdgcn_readfirstlane(ids[w]);
+    if (id < 0) {              // an unused slot of the fixed-capacity layout
+      if (l == 0) acc.touched[w] = -1;
+      continue;
+    }
     const int c = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(rec));
-    const int row = __builtin_amdgcn_readfirstlane(ids[w]) / G;
+    const int row = id / G;
     if (l == 0) commit_slot(acc, row, c, (int)w);
     if (c == 0) continue;
     const uint32_t* pay = reinterpret_cast<const uint32_t*>(rec + 16);
@@ -323,6 +393,30 @@ extern "C" int skge_shard_route(void* stream, const int* rec, const int* rec_n1,
   hipLaunchKernelGGL(k_route_scatter, dim3((unsigned)nblk), dim3(ROUTE_BLOCK), 0, st,
                      (const int4*)rec, rec_n1, (long long)start, count, G, bcnt, send_ids, req_pos);
   SKGE_CHECK_LAUNCH("shard route");
+  return SKGE_OK;
+}
+
+extern "C" int skge_shard_route_cap(void* stream, const int* rec, const int* rec_n1,
+                                    int64_t start, int count, int G, int C, int* send_ids,
+                                    int* req_pos, void* workspace, size_t ws_bytes, int* err) {
+  SKGE_CHECK_ARG(rec && rec_n1 && send_ids && req_pos && err, "NULL argument");
+  SKGE_CHECK_ARG(G >= 1 && G <= SHARD_MAX_RANKS, "G must be 1..%d", SHARD_MAX_RANKS);
+  SKGE_CHECK_ARG(count >= 0 && start >= 0 && C >= 1, "bad batch range / capacity");
+  SKGE_CHECK_ARG(workspace && ws_bytes >= skge_shard_route_workspace_bytes(count, G),
+                 "workspace too small");
+  hipStream_t st = as_stream(stream);
+  SKGE_CHECK_HIP(hipMemsetAsync(send_ids, 0xFF, sizeof(int) * (size_t)G * C, st));   // -1
+  if (count == 0) return SKGE_OK;
+  const long long nblk = (4ll * count + ROUTE_BLOCK - 1) / ROUTE_BLOCK;
+  SKGE_CHECK_ARG(nblk <= (1ll << 30), "batch too large");
+  int* bcnt = (int*)workspace;
+  hipLaunchKernelGGL(k_route_count, dim3((unsigned)nblk), dim3(ROUTE_BLOCK), 0, st,
+                     (const int4*)rec, rec_n1, (long long)start, count, G, bcnt);
+  hipLaunchKernelGGL(k_route_scan_cap, dim3(1), dim3(256), 0, st, bcnt, (int)nblk, G);
+  hipLaunchKernelGGL(k_route_scatter_cap, dim3((unsigned)nblk), dim3(ROUTE_BLOCK), 0, st,
+                     (const int4*)rec, rec_n1, (long long)start, count, G, C, bcnt, send_ids,
+                     req_pos, err);
+  SKGE_CHECK_LAUNCH("shard route (fixed capacity)");
   return SKGE_OK;
 }
 

@@ -92,6 +92,8 @@ SIGNATURES = {
     "skge_pipe_runner_destroy": (None, [c_p]),
     "skge_shard_route_workspace_bytes": (c_sz, [c_i, c_i]),
     "skge_shard_route": (c_i, [c_p, c_p, c_p, c_i64, c_i, c_i, c_p, c_p, c_p, c_p, c_sz]),
+    "skge_shard_route_cap": (c_i, [c_p, c_p, c_p, c_i64, c_i, c_i, c_i, c_p, c_p, c_p, c_sz,
+                                   c_p]),
     "skge_shard_gather": (c_i, [c_p, c_p, c_i, c_i, c_p, c_i64, c_p]),
     "skge_shard_contrib_stride": (ctypes.c_longlong, [c_i]),
     "skge_shard_score": (c_i, [c_p, T_P, c_i, c_p, c_p, c_i64, c_i, c_p, c_p, c_f, c_p, c_p]),

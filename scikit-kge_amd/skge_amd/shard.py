@@ -10,7 +10,8 @@ r % G == g, at local index r // G -- and the relation table R (|R| x d,
 training triples; mini-batch b of the job is the union of every rank's
 batch b, and one step of it is
 
-    route     requests (s, o, s', o') of the rank's positives, by owner  [HIP]
+    route     requests (s, o, s', o') of the rank's positives into G
+              fixed-capacity owner buckets                               [HIP]
     a2a       request ids -> owners                                      [RCCL]
     gather    owners copy the requested rows out of their shard          [HIP]
     a2a       rows -> requesters                                         [RCCL]
@@ -43,7 +44,10 @@ def owned_rows(n_ent, G, rank):
 class Exchange(object):
     """The collectives of one sharded step over a torch.distributed group
     (RCCL under the "nccl" backend; gloo stages device tensors through host
-    memory).  G == 1 needs no process group: every exchange is the identity."""
+    memory).  Every all-to-all moves G EQUAL slices (the fixed-capacity
+    layout), so no split sizes travel to the host and the step is
+    graph-capturable.  G == 1 needs no process group: every exchange is the
+    identity."""
 
     def __init__(self, group=None):
         self.group = group
@@ -54,29 +58,23 @@ class Exchange(object):
         else:
             self.G, self.rank, self.backend = 1, 0, None
 
-    def split_sizes(self, send_counts):
-        """Bucket sizes this rank sends (device int64 [G]) -> (send list,
-        receive list): one tiny all-to-all and ONE host copy per step."""
-        if self.G == 1:
-            c = send_counts.cpu().tolist()
-            return c, c
-        recv = torch.empty_like(send_counts)
-        self._a2a(recv, send_counts, None, None)
-        both = torch.stack([send_counts, recv]).cpu()
-        return both[0].tolist(), both[1].tolist()
-
-    def all_to_all(self, inp, send, recv):
-        """Rows inp[sum(send[:g]) : ...] go to rank g; returns the rows
-        received, grouped by source rank."""
-        if self.G == 1:
-            return inp[:send[0]]
-        out = torch.empty((int(sum(recv)),) + tuple(inp.shape[1:]), dtype=inp.dtype,
-                          device=inp.device)
-        self._a2a(out, inp[:int(sum(send))], recv, send)
+    def all_to_all(self, inp, out=None):
+        """Slice g of inp (G equal slices along dim 0) goes to rank g; returns
+        the G slices received, rank-major (into `out` if given)."""
+        if self.backend is None:
+            return inp
+        if out is None:
+            out = torch.empty_like(inp)
+        if self.backend == "gloo" and inp.is_cuda:
+            h = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(h, inp.cpu(), group=self.group)
+            out.copy_(h)
+        else:
+            dist.all_to_all_single(out, inp, group=self.group)
         return out
 
     def all_reduce_(self, t):
-        if self.G > 1:
+        if self.backend is not None:
             if self.backend == "gloo" and t.is_cuda:
                 h = t.cpu()
                 dist.all_reduce(h, group=self.group)
@@ -85,63 +83,53 @@ class Exchange(object):
                 dist.all_reduce(t, group=self.group)
         return t
 
-    def _a2a(self, out, inp, out_splits, in_splits):
-        if self.backend == "gloo" and inp.is_cuda:
-            h = torch.empty(out.shape, dtype=out.dtype)
-            dist.all_to_all_single(h, inp.cpu(), out_splits, in_splits, group=self.group)
-            out.copy_(h)
-        else:
-            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
-
 
 def sharded_step(ops, ex, start, count):
     """One mini-batch of the sharded job (positives start .. start+count of
     this rank's epoch order); see the module docstring.  `ops` is the
-    rank's compute, `ex` the collectives."""
-    send_ids, req_pos, send_counts = ops.route(start, count, ex.G)
-    send, recv = ex.split_sizes(send_counts)
-    recv_ids = ex.all_to_all(send_ids, send, recv)       # owner side: who wants which row
+    rank's compute, `ex` the collectives.  Fixed-capacity buckets of C
+    request slots per owner: no host read anywhere in the step."""
+    send_ids, req_pos = ops.route(start, count)         # [G * C] ids (-1: unused slot)
+    recv_ids = ex.all_to_all(send_ids, ops.buf("recv_ids"))   # owner side: who wants which row
     rows = ops.gather(recv_ids)
-    fetched = ex.all_to_all(rows, recv, send)            # requester side, send order
+    fetched = ex.all_to_all(rows, ops.buf("fetched"))    # requester side, bucket order
     contrib = ops.score(start, count, fetched, req_pos)  # + this rank's R sums
-    recv_contrib = ex.all_to_all(contrib, send, recv)    # sparse reduce-scatter
+    recv_contrib = ex.all_to_all(contrib, ops.buf("recv_contrib"))   # sparse reduce-scatter
     ops.accum(recv_ids, recv_contrib)
     for t in ops.rel_sums():
         ex.all_reduce_(t)
-    ops.apply(int(sum(recv)))
+    ops.apply()
 
 
 class ShardOps(object):
-    """The HIP compute of one rank (csrc/skge_shard.hip + skge_accum_apply)."""
+    """The HIP compute of one rank (csrc/skge_shard.hip + skge_accum_apply),
+    on buffers allocated once for the fixed capacity C."""
 
     def __init__(self, runner):
         self.r = runner
 
-    def route(self, start, count, G):
+    def buf(self, name):
+        return self.r.bufs[name]
+
+    def route(self, start, count):
         r = self.r
-        n = 4 * count
-        r._grow("send_ids", n, torch.int32)
-        r._grow("req_pos", n, torch.int32)
-        ws_bytes = int(L.lib().skge_shard_route_workspace_bytes(count, G))
-        ws = r._grow("route_ws", ws_bytes, torch.uint8)
-        L.check(L.lib().skge_shard_route(r.sp, L.ptr(r.rec), L.ptr(r.rec_n1), start, count, G,
-                                         L.ptr(r.bufs["send_ids"]), L.ptr(r.bufs["req_pos"]),
-                                         L.ptr(r.send_counts), L.ptr(ws), ws_bytes), "shard route")
-        return r.bufs["send_ids"], r.bufs["req_pos"], r.send_counts
+        b = r.bufs
+        L.check(L.lib().skge_shard_route_cap(r.sp, L.ptr(r.rec), L.ptr(r.rec_n1), start, count,
+                                             r.G, r.C, L.ptr(b["send_ids"]), L.ptr(b["req_pos"]),
+                                             L.ptr(b["route_ws"]), b["route_ws"].numel(),
+                                             L.ptr(r.err)), "shard route")
+        return b["send_ids"], b["req_pos"]
 
     def gather(self, ids):
         r = self.r
-        n = ids.shape[0]
-        rows = r._grow("rows", n * r.d, torch.float32)[:n * r.d].view(n, r.d)
-        L.check(L.lib().skge_shard_gather(r.sp, L.ptr(r.E.data), r.d, r.G, L.ptr(ids), n,
-                                          L.ptr(rows)), "shard gather")
+        rows = r.bufs["rows"]
+        L.check(L.lib().skge_shard_gather(r.sp, L.ptr(r.E.data), r.d, r.G, L.ptr(ids),
+                                          ids.shape[0], L.ptr(rows)), "shard gather")
         return rows
 
     def score(self, start, count, fetched, req_pos):
         r = self.r
-        n = fetched.shape[0]
-        cs = r.cstride
-        C = r._grow("contrib", n * cs, torch.uint8)[:n * cs].view(n, cs)
+        C = r.bufs["contrib"]
         L.check(L.lib().skge_shard_score(r.sp, r.tr, r.d, L.ptr(r.rec), L.ptr(r.rec_n1), start,
                                          count, L.ptr(fetched), L.ptr(req_pos), float(r.margin),
                                          L.ptr(C), L.ptr(r.vshards)), "shard score")
@@ -149,20 +137,34 @@ class ShardOps(object):
 
     def accum(self, ids, contrib):
         r = self.r
-        n = ids.shape[0]
-        r.accE.ensure_slots(n)
-        r.te = r.updE.table(r.accE, counters=False)
-        L.check(L.lib().skge_shard_accum(r.sp, r.te, r.G, L.ptr(ids), L.ptr(contrib), n),
-                "shard accum")
+        L.check(L.lib().skge_shard_accum(r.sp, r.te, r.G, L.ptr(ids), L.ptr(contrib),
+                                         ids.shape[0]), "shard accum")
 
     def rel_sums(self):
         acc = self.r.accR
         return acc.sum.view(torch.int64), acc.cnt   # packed sums add as int64
 
-    def apply(self, n_recv):
+    def apply(self):
         r = self.r
         L.check(L.lib().skge_accum_apply(r.sp, (L.SkgeTable * 2)(r.te, r.tr), 2,
-                                         L.int_array(n_recv, r.R.rows)), "shard apply")
+                                         L.int_array(r.G * r.C, r.R.rows)), "shard apply")
+
+
+def bucket_capacity(trip_local, n_ent, G, batch, sigmas=8.0):
+    """Request slots per owner bucket (the fixed-capacity layout): a batch of
+    `batch` of this rank's positives sends 4 requests each (s, o, s', o');
+    s and o go to owner (id % G) with this rank's exact frequencies f_g, the
+    corruptions uniformly (skge/sample.py:41-46).  mu = batch (2 max_g f_g +
+    2 / G), plus `sigmas` standard deviations and 64; never above 4 batch.
+    The route kernel flags any bucket that still overflows (checked after
+    every epoch)."""
+    batch = int(batch)
+    if G == 1 or batch == 0:
+        return max(4 * batch, 1)
+    so = torch.cat([trip_local[:, 0], trip_local[:, 1]]).long() % G
+    f = torch.bincount(so, minlength=G).double() / max(int(so.numel()), 1)
+    mu = batch * (2.0 * float(f.max().item()) + 2.0 / G)
+    return int(min(4 * batch, np.ceil(mu + sigmas * np.sqrt(mu) + 64)))
 
 
 class ShardedRunner(object):
@@ -177,7 +179,7 @@ class ShardedRunner(object):
     positives take empty batches, which still join the exchanges)."""
 
     def __init__(self, n_ent, E_local, R, trip_local, nbatches, lr=0.1, margin=2.0, seed=0,
-                 ntries=100, group=None, stream=None):
+                 ntries=100, group=None, stream=None, capacity=None, capture=None):
         from .param import AdaGrad, Accumulator, Parameter, normalize
         from .device import DeviceKG
         self.ex = Exchange(group)
@@ -206,8 +208,12 @@ class ShardedRunner(object):
         T_max = self._max_over_ranks(self.T)
         bs = max(T_max // nbatches, 1)
         self.batches = [(s0, max(0, min(bs, self.T - s0))) for s0 in range(0, T_max, bs)]
-        self.accE = Accumulator(self.E.rows, self.d, dev, slots=4 * bs * self.G,
-                                mode=L.SKGE_ACC_I16X4)
+        # fixed-capacity buckets: C request slots per owner (every rank uses the
+        # largest rank's C, so the all-to-all slices are equal)
+        self.C = self._max_over_ranks(bucket_capacity(trip_local, self.n_ent, self.G, bs)
+                                      if capacity is None else int(capacity))
+        n_slots = self.G * self.C
+        self.accE = Accumulator(self.E.rows, self.d, dev, slots=n_slots, mode=L.SKGE_ACC_I16X4)
         # packed relation sums all-reduced over the ranks' batches: positive j
         # adds into copy j mod reps, enough copies that no 16-bit field of the
         # union batch can wrap (the apply folds them, device.relation_replicas)
@@ -221,24 +227,30 @@ class ShardedRunner(object):
         self.te = self.updE.table(self.accE, counters=False)
         self.tr = self.updR.table(self.accR, counters=False)
         self.cstride = int(L.lib().skge_shard_contrib_stride(self.d))
-        self.bufs = {}
-        self.send_counts = torch.zeros(self.G, dtype=torch.int64, device=dev)
+        u8, i32 = torch.uint8, torch.int32
+        ws = int(L.lib().skge_shard_route_workspace_bytes(bs, self.G))
+        self.bufs = {"send_ids": torch.full((n_slots,), -1, dtype=i32, device=dev),
+                     "recv_ids": torch.full((n_slots,), -1, dtype=i32, device=dev),
+                     "req_pos": torch.full((4 * bs,), -1, dtype=i32, device=dev),
+                     "route_ws": torch.zeros(ws, dtype=u8, device=dev),
+                     "rows": torch.zeros((n_slots, self.d), dtype=torch.float32, device=dev),
+                     "fetched": torch.zeros((n_slots, self.d), dtype=torch.float32, device=dev),
+                     "contrib": torch.zeros((n_slots, self.cstride), dtype=u8, device=dev),
+                     "recv_contrib": torch.zeros((n_slots, self.cstride), dtype=u8, device=dev)}
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)   # bucket overflow flag
         self.vshards = torch.zeros(64 * 32, dtype=torch.int32, device=dev)
         self.nviol_total = torch.zeros(1, dtype=torch.int32, device=dev)
         self.epoch_key = torch.zeros(1, dtype=torch.int64, device=dev)
         self.rec = torch.empty((max(self.T, 1), 4), dtype=torch.int32, device=dev)
         self.rec_n1 = torch.empty(max(self.T, 1), dtype=torch.int32, device=dev)
         self.ops = ShardOps(self)
+        if capture is None:
+            capture = self.ex.backend in (None, "nccl")
+        self.capture = bool(capture)
+        self.graph = None
         torch.cuda.current_stream(dev).synchronize()
 
     # ---- helpers ----
-    def _grow(self, name, n, dtype):
-        b = self.bufs.get(name)
-        if b is None or b.numel() < n:
-            b = torch.empty(max(int(n * 1.25), 16), dtype=dtype, device=self.device)
-            self.bufs[name] = b
-        return b
-
     def _max_over_ranks(self, x):
         if self.G == 1:
             return int(x)
@@ -284,17 +296,37 @@ class ShardedRunner(object):
         L.check(L.lib().skge_shard_fold_violations(self.sp, L.ptr(self.vshards),
                                                    L.ptr(self.nviol_total)), "fold")
 
+    def _epoch(self):
+        self.sample_epoch()
+        for start, count in self.batches:
+            sharded_step(self.ops, self.ex, start, count)
+        self.fold_violations()
+        L.check(L.lib().skge_epoch_advance(self.sp, L.ptr(self.epoch_key)), "advance")
+
     def run(self, nepochs=1):
+        """nepochs epochs.  With capture (the "nccl" backend, or one process)
+        the first epoch runs eagerly and is then captured -- kernels and RCCL
+        collectives -- into one CUDA graph that later epochs replay: no host
+        read or host-side size anywhere in an epoch."""
         with torch.cuda.stream(self.stream):
-            for _ in range(nepochs):
-                self.sample_epoch()
-                for start, count in self.batches:
-                    sharded_step(self.ops, self.ex, start, count)
-                self.fold_violations()
-                L.check(L.lib().skge_epoch_advance(self.sp, L.ptr(self.epoch_key)), "advance")
+            for _ in range(int(nepochs)):
+                if not self.capture:
+                    self._epoch()
+                elif self.graph is None:
+                    self._epoch()
+                    self.stream.synchronize()
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=self.stream):
+                        self._epoch()
+                    self.graph = g
+                else:
+                    self.graph.replay()
 
     def synchronize(self):
         self.stream.synchronize()
+        if int(self.err.item()):
+            raise L.SkgeError("sharded runner: an owner bucket overflowed its %d request slots "
+                              "(skewed rows); pass a larger capacity" % self.C)
         rc = L.lib().skge_device_error(self.sp, 1)
         if rc & 2:
             raise L.SkgeError("sharded runner: a row's per-batch count exceeded 32767 "

@@ -25,11 +25,31 @@ def route(rec, rec_n1, start, count, G):
     return send_ids.astype(np.int32), req_pos.astype(np.int32), np.array(counts, dtype=np.int64)
 
 
+def route_cap(rec, rec_n1, start, count, G, C):
+    """The fixed-capacity layout of skge_shard_route_cap: bucket g = slots
+    [g C, (g + 1) C) holds the requests owned by rank g in request order,
+    unused slots -1; req_pos = bucket slot of each request (-1: skipped)."""
+    ids, pos, counts = route(rec, rec_n1, start, count, G)
+    send = np.full(G * C, -1, dtype=np.int32)
+    base = np.concatenate([[0], np.cumsum(counts)])[:-1]
+    out_pos = np.full(pos.shape, -1, dtype=np.int32)
+    for g in range(G):
+        assert counts[g] <= C, "bucket overflow"
+        send[g * C:g * C + counts[g]] = ids[base[g]:base[g] + counts[g]]
+    for i, p in enumerate(pos):
+        if p >= 0:
+            g = int(np.searchsorted(base, p, side="right") - 1)
+            out_pos[i] = g * C + (p - base[g])
+    return send, out_pos
+
+
 class NumpyShardOps(object):
     """Rank compute of one sharded step in float64 (d columns; the
-    contribution record is [count, c_0 .. c_{d-1}] as float64)."""
+    contribution record is [count, c_0 .. c_{d-1}] as float64), in the
+    fixed-capacity layout (C slots per owner bucket)."""
 
-    def __init__(self, rec, rec_n1, E_local, R, G, margin, lr):
+    def __init__(self, rec, rec_n1, E_local, R, G, margin, lr, C):
+        self.C = C
         self.rec, self.rec_n1 = rec, rec_n1
         self.E, self.R = E_local.astype(np.float64).copy(), R.astype(np.float64).copy()
         self.AE, self.AR = np.zeros_like(self.E), np.zeros_like(self.R)
@@ -40,12 +60,19 @@ class NumpyShardOps(object):
         self.cntR = torch.zeros(len(self.R), dtype=torch.int64)
         self.nviol = 0
 
-    def route(self, start, count, G):
-        s, p, c = route(self.rec, self.rec_n1, start, count, G)
-        return torch.from_numpy(s), torch.from_numpy(p), torch.from_numpy(c)
+    def buf(self, name):
+        return None
+
+    def route(self, start, count):
+        s, p = route_cap(self.rec, self.rec_n1, start, count, self.G, self.C)
+        return torch.from_numpy(s), torch.from_numpy(p)
 
     def gather(self, ids):
-        return torch.from_numpy(self.E[ids.numpy().astype(np.int64) // self.G])
+        i = ids.numpy().astype(np.int64)
+        out = np.zeros((len(i), self.d))
+        ok = i >= 0
+        out[ok] = self.E[i[ok] // self.G]
+        return torch.from_numpy(out)
 
     def score(self, start, count, fetched, req_pos):
         F = fetched.numpy()
@@ -87,7 +114,7 @@ class NumpyShardOps(object):
     def accum(self, ids, contrib):
         C = contrib.numpy()
         for i, gid in enumerate(ids.numpy()):
-            if C[i, 0]:
+            if gid >= 0 and C[i, 0]:
                 row = int(gid) // self.G
                 self.sumE[row] += C[i, 1:]
                 self.cntE[row] += int(C[i, 0])
@@ -106,7 +133,7 @@ class NumpyShardOps(object):
         S[rows] = 0.0
         cnt[rows] = 0
 
-    def apply(self, n_recv):
+    def apply(self):
         self._adagrad_normalize(self.E, self.AE, self.sumE, self.cntE, self.lr, True)
         self._adagrad_normalize(self.R, self.AR, self.sumR.numpy(), self.cntR.numpy(), self.lr,
                                 False)

@@ -49,6 +49,63 @@ def test_route_matches_numpy_layout(G, count, start):
     assert np.array_equal(pos.cpu().numpy()[:4 * count], want_pos)
 
 
+@pytest.mark.parametrize("G,count,start,C", [(1, 37, 0, 148), (2, 1000, 3, 2100), (3, 257, 10, 400),
+                                             (8, 4096, 0, 2200), (2, 0, 0, 8)])
+def test_route_cap_matches_numpy_layout(G, count, start, C):
+    from skge_amd import _lib as L
+    from shard_numpy import random_records, route_cap
+    rec, rec_n1 = random_records(np.random.RandomState(G + count), 5000, 997, 9, skip=0.2)
+    dev = torch.device("cuda", 0)
+    r = torch.as_tensor(rec, device=dev)
+    r1 = torch.as_tensor(rec_n1, device=dev)
+    ids = torch.full((G * C,), -9, dtype=torch.int32, device=dev)
+    pos = torch.full((max(4 * count, 1),), -9, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    wsb = int(L.lib().skge_shard_route_workspace_bytes(count, G))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    L.check(L.lib().skge_shard_route_cap(L.stream_ptr(), L.ptr(r), L.ptr(r1), start, count, G, C,
+                                         L.ptr(ids), L.ptr(pos), L.ptr(ws), wsb, L.ptr(err)))
+    want_ids, want_pos = route_cap(rec, rec_n1, start, count, G, C)
+    assert int(err.item()) == 0
+    assert np.array_equal(ids.cpu().numpy(), want_ids)
+    assert np.array_equal(pos.cpu().numpy()[:4 * count], want_pos)
+
+
+def test_sharded_runner_captured_epochs_equal_eager():
+    """The fixed-capacity epoch captured in one graph (no host read per batch)
+    trains bit for bit like the same epochs issued eagerly."""
+    from skge_amd.shard import ShardedRunner
+    from test_gpu_device_loop import make_kg
+    n_ent, n_rel, d = 700, 6, 128
+    trip, _ = make_kg(n_ent, n_rel, 4000)
+    E, R = _init_tables(n_ent, n_rel, d, 3)
+    out = []
+    for cap in (True, False):
+        dev = torch.device("cuda", 0)
+        r = ShardedRunner(n_ent, torch.as_tensor(E, device=dev), torch.as_tensor(R, device=dev),
+                          torch.as_tensor(trip, device=dev), 9, seed=4, capture=cap)
+        r.run(3)
+        r.synchronize()
+        assert (r.graph is not None) == cap
+        out.append((int(r.nviol_total.item()), r.E.data.cpu().numpy(), r.R.data.cpu().numpy()))
+    assert out[0][0] == out[1][0] > 0
+    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])
+
+
+def test_sharded_bucket_overflow_is_reported():
+    from skge_amd import _lib as L
+    from skge_amd.shard import ShardedRunner
+    from test_gpu_device_loop import make_kg
+    trip, _ = make_kg(300, 5, 2000)
+    E, R = _init_tables(300, 5, 32, 1)
+    dev = torch.device("cuda", 0)
+    r = ShardedRunner(300, torch.as_tensor(E, device=dev), torch.as_tensor(R, device=dev),
+                      torch.as_tensor(trip, device=dev), 8, seed=5, capacity=64)
+    r.run(1)
+    with pytest.raises(L.SkgeError, match="overflowed"):
+        r.synchronize()
+
+
 def _init_tables(n_ent, n_rel, d, seed):
     rs = np.random.RandomState(seed)
     E = rs.uniform(-0.3, 0.3, size=(n_ent, d))

@@ -49,7 +49,9 @@ def _worker(rank, world, port, batches, out):
     dist.init_process_group("gloo", init_method="env://")
     E, R, recs = _problem(world)
     rec, rec_n1 = recs[rank]
-    ops = NumpyShardOps(rec, rec_n1, E[rank::world], R, world, MARGIN, LR)
+    # fixed-capacity buckets: the largest batch's request count fits any bucket
+    C = 4 * max(c for _, c in batches)
+    ops = NumpyShardOps(rec, rec_n1, E[rank::world], R, world, MARGIN, LR, C)
     ex = Exchange()
     snaps = []
     for start, count in batches:
@@ -96,6 +98,17 @@ def test_sharded_protocol_matches_union_batch(world, batches):
             np.testing.assert_allclose(snaps[b][1], params["R"], rtol=0, atol=1e-12)
         np.testing.assert_allclose(full, params["E"], rtol=0, atol=1e-12)
     assert sum(r[2] for r in res) == nviol
+
+
+def test_route_cap_layout_fixed_buckets():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from shard_numpy import route_cap
+    rec = np.array([[0, 1, 0, 2], [3, 4, 1, -1], [5, 0, 0, 1]], dtype=np.int32)
+    rec_n1 = np.array([7, 2, -1], dtype=np.int32)
+    send, pos = route_cap(rec, rec_n1, 0, 3, 2, 6)
+    # requests: 0 1 2 7 | 3 4 -1 2 | 5 0 1 -1 -> owner 0: 0 2 4 2 0, owner 1: 1 7 3 5 1
+    assert send.tolist() == [0, 2, 4, 2, 0, -1, 1, 7, 3, 5, 1, -1]
+    assert pos.tolist() == [0, 6, 1, 7, 8, 2, -1, 3, 9, 4, 10, -1]
 
 
 def test_route_layout_is_owner_major_and_stable():
