@@ -78,7 +78,7 @@ inline int check_table(const skge_table_t* t, const char* name, bool need_acc) {
   // terms and the occurrence count as the divisor (the packed applies' fast
   // AdaGrad step / projection forms are argued for exactly that case,
   // skge_device.h adagrad_step_fast)
-  SKGE_CHECK_ARG(t->acc_mode == SKGE_ACC_F32 ||
+  SKGE_CHECK_ARG(t->acc_mode != SKGE_ACC_I16X4 ||
                      (t->rin == 0.0f && t->rout == 0.0f && t->fixed_div <= 0.0f),
                  "%s: packed accumulator needs rin == rout == 0 and no fixed divisor", name);
   if (need_acc) {

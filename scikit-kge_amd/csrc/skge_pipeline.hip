@@ -592,7 +592,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
         SKGE_CO(w)
 #undef SKGE_CO
       }
-      Accum aE;
+      Accum aE = {};   // mode ACC_F32 (0), one copy
       aE.sum = reinterpret_cast<float*>(esum);
       acc_row4_i16<KQ>(aE, s, cs, d);
       acc_row4_i16<KQ>(aE, o, co, d);
@@ -895,7 +895,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_lazy_batch(PipeA
         SKGE_CO(w)
 #undef SKGE_CO
       }
-      Accum aE;
+      Accum aE = {};   // mode ACC_F32 (0), one copy
       aE.sum = reinterpret_cast<float*>(esum);
       acc_row4_i16<KQ>(aE, s, cs, d);
       acc_row4_i16<KQ>(aE, o, co, d);
@@ -1110,7 +1110,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_own_batch(PipeAr
   ((K) == 0 ? fv0 * gp4[M].X + fv1 * (gp4[M].X + g1[M].X)                               \
    : (K) == 1 ? -(fv0 * (gp4[M].X + g0[M].X) + fv1 * gp4[M].X)                          \
    : (K) == 2 ? g0[M].X : -g1[M].X)
-    Accum aE;
+    Accum aE = {};   // mode ACC_F32 (0), one copy
     aE.sum = reinterpret_cast<float*>(esum);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {   // shared rows with contributions: memory-side adds
@@ -1583,7 +1583,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
   }
   float* const wb = FFT ? smem + 2 * d + wave * hole_fft_wave_floats(d) : nullptr;
   const HolePosLds L(FFT ? smem : smem + wave * hole_pos_lds_floats(d), d);
-  Accum aE;
+  Accum aE = {};   // mode ACC_F32 (0), one copy
   aE.sum = reinterpret_cast<float*>(a.E.sum[cp]);
   aE.width = d;
   const int rstride = 2 * a.R.rw;   // floats per relation accumulator row
@@ -1674,7 +1674,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     nv += v0 + v1;
     const float gpf = -af_g_given_f(a.af, pf);   // hole.py:66
     const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
-    Accum aR;
+    Accum aR = {};   // mode ACC_F32 (0), one copy
     aR.sum = racc + (size_t)p * rstride;
     aR.width = d;
     if constexpr (FFT) {
