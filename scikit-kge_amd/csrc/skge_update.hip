@@ -841,8 +841,9 @@ int apply_with_wstep(hipStream_t st, const skge_table_t* ent, int nslots, const 
   int rc = check_table(ent, "ent", true);
   if (rc) return rc;
   if ((rc = check_slots(ent, nslots, "ent"))) return rc;
-  SKGE_CHECK_ARG(ent->acc_mode == SKGE_ACC_F32 && ent->acc_replicas <= 1,
-                 "W step beside the apply: single fp32 entity accumulator");
+  SKGE_CHECK_ARG((ent->acc_mode == SKGE_ACC_F32 || ent->acc_mode == SKGE_ACC_FX64) &&
+                     ent->acc_replicas <= 1,
+                 "W step beside the apply: single fp32 (or fixed-point) entity accumulator");
   SKGE_CHECK_ARG(ent->opt == SKGE_SGD || ent->state, "AdaGrad needs state");
   SKGE_CHECK_ARG(w.opt == SKGE_SGD || w.A, "AdaGrad needs state");
   const int nt = (w.d + WS_T - 1) / WS_T;

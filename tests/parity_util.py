@@ -56,3 +56,79 @@ def check(got, want, what, lr=None, p2=None, grad_rounding=GRAD_ROUNDING, atol=A
         raise AssertionError("%s: %d of %d elements past tol/%g, headroom %.3g, max |err| %.3g"
                              % (what, int(bad.sum()), got.size, min_headroom, h, emax))
     return h
+
+
+ROW_ULPS = 2.0 ** -22   # 4 fp32 ulps (u = 2^-24) of a gradient row's 2-norm
+
+
+def grad_rounding(shape, grads):
+    """Per-element absolute rounding bound of the fp32 gradient: GRAD_ROUNDING
+    plus 4 ulps of the element's ROW norm (the oracle's own gradient rows,
+    (g, idx)).  A row of d-term dot products (RESCAL's W E_o / E_s W) or of
+    FFT correlations (HolE) carries absolute error of a few ulps of the row's
+    magnitude, not of the element's -- an element near zero inherits it."""
+    eps = np.full(shape, GRAD_ROUNDING)
+    if grads is not None:
+        g, idx = grads
+        g = np.asarray(g, dtype=np.float64).reshape(len(idx), -1)
+        rown = np.sqrt((g ** 2).sum(axis=1))
+        eps.reshape(shape[0], -1)[np.asarray(idx)] += ROW_ULPS * rown[:, None]
+    return eps
+
+
+def check_step(got, want, before, grads, p2_after, lr, what, post=None, opt="adagrad",
+               min_headroom=1.0):
+    """Parameters after one updater step (+ projection) from `before`, against
+    the oracle's `want`.  Per element
+
+      a   = lr * eps / H              (AdaGrad: the gradient rounding eps,
+                                       grad_rounding(), through the divisor
+                                       H = max(sqrt(p2), 1e-7); at most 2 lr,
+                                       a sign flip of a near-zero gradient)
+      tol = ATOL + RTOL |want| + a
+
+    and, for a projected row (post 'normalize' / 'normless1', skge/param.py:
+    161-174), the projection's scale moves every element of the row when any
+    element moves: + |want| * dss / ss (normless1, ss >= 1) or |want| * dss /
+    (2 ss) (normalize), dss = sum over the row of 2 |pre| a + a^2, pre the
+    oracle's row before the projection."""
+    want = np.asarray(want, dtype=np.float64)
+    eps = grad_rounding(want.shape, grads)
+    if opt == "adagrad":
+        H = np.maximum(np.sqrt(np.asarray(_np(p2_after), dtype=np.float64)), 1e-7)
+        a = np.minimum(lr * eps / H, 2.0 * lr)
+    else:
+        a = lr * eps
+    tol = ATOL + RTOL * np.abs(want) + a
+    if post is not None and grads is not None:
+        g, idx = grads
+        idx = np.asarray(idx)
+        g = np.asarray(g, dtype=np.float64).reshape(want[idx].shape)
+        b = np.asarray(before, dtype=np.float64)[idx]
+        if opt == "adagrad":
+            step = lr * g / np.maximum(np.sqrt(np.asarray(_np(p2_after), dtype=np.float64)[idx]),
+                                       1e-7)
+        else:
+            step = lr * g
+        pre = b - step
+        flat = lambda x: x.reshape(len(idx), -1)
+        ss = (flat(pre) ** 2).sum(axis=1)
+        ar = flat(a[idx])
+        dss = (2.0 * np.abs(flat(pre)) * ar + ar ** 2).sum(axis=1)
+        if post == "normless1":
+            rel = np.where(ss >= 1.0, dss / np.maximum(ss, 1.0), 0.0)
+        else:
+            rel = dss / (2.0 * np.maximum(ss, 1e-30))
+        extra = np.abs(flat(want[idx])) * rel[:, None]
+        tol.reshape(want.shape[0], -1)[idx] += extra
+    got = _np(got).astype(np.float64)
+    h, emax = headroom(got, want, tol)
+    RECORDS.append((what, h, emax, int(got.size)))
+    if not h >= min_headroom:
+        bad = np.abs(got - want) > tol / min_headroom
+        raise AssertionError("%s: %d of %d elements past tol/%g, headroom %.3g, max |err| %.3g"
+                             % (what, int(bad.sum()), got.size, min_headroom, h, emax))
+    return h
+
+
+POSTS = {"transe": {"E": "normalize"}, "hole": {"E": "normless1"}, "rescal": {}}

@@ -1,14 +1,15 @@
 """Fused explicit-pair steps of every model on random batches at sizes the
 golden fixtures do not reach (many relations, ragged d, duplicate rows), vs
 the oracle; RESCAL runs on the relation-grouped fp32 MFMA path for d <= 480
-(skge_rescal.hip).  Tolerances as tests/test_gpu_parity.py (1e-5 + 1e-5|x|,
-plus the propagated AdaGrad rounding lr*e/max(sqrt(p2),1e-7)); violation
-counts exact."""
+(skge_rescal.hip).  Tolerances 1e-5 + 1e-5|x| plus, for the AdaGrad steps,
+the fp32 gradient rounding propagated through the step and the projection
+(tests/parity_util.py check_step); violation counts exact."""
 import numpy as np
 import pytest
 import torch
 
 from oracle import skge_oracle as O
+import parity_util
 from test_gpu_parity import close, close_adagrad
 
 pytestmark = pytest.mark.gpu
@@ -61,12 +62,15 @@ def _run(name, n_ent, n_rel, d, P, nb, rparam=0.0, seed=5):
         m._pairwise_step(torch.as_tensor(pos, device=m.device), torch.as_tensor(neg, device=m.device),
                          upd, nviol)
         kw = {"rparam": rparam} if name != "transe" else {"l1": True}
-        _, _, nv, _ = O.pairwise_step(name, params, state, pos, neg, 0.1, float(m.margin),
-                                      "adagrad", **kw)
+        before = {k: v.copy() for k, v in params.items()}
+        _, _, nv, grads = O.pairwise_step(name, params, state, pos, neg, 0.1, float(m.margin),
+                                          "adagrad", **kw)
         assert int(nviol.item()) == nv, (name, b)
         for pid in m.params:
-            close_adagrad(m.params[pid].data, params[pid], state[pid], 0.1,
-                          "%s b%d %s" % (name, b, pid))
+            parity_util.check_step(m.params[pid].data, params[pid], before[pid],
+                                   grads[pid] if grads else None, state[pid], 0.1,
+                                   "%s b%d %s" % (name, b, pid),
+                                   post=parity_util.POSTS[name].get(pid))
             close(upd[pid].p2, state[pid], "%s b%d p2 %s" % (name, b, pid))
     return m
 

@@ -20,8 +20,11 @@ skge/param.py:140-174), not through another HIP path:
   (b) one epoch of 3 batches (the pipelined hand-off between batches), SGD.
 
 Bar: violation totals EXACTLY equal; parameters and AdaGrad state within
-1e-5 + 1e-5|x| (+ the propagated AdaGrad rounding lr*1e-8/max(sqrt(p2),1e-7),
-tests/parity_util.py), headroom recorded.
+1e-5 + 1e-5|x|, plus for one AdaGrad step the gradient's fp32 rounding
+propagated through the step and the row projection (parity_util.check_step:
+lr * eps / max(sqrt(p2), 1e-7), eps = 1e-8 + 4 ulps of the gradient row's
+norm; a projected row's scale carries its elements' allowance to the whole
+row), headroom recorded.
 """
 import numpy as np
 import pytest
@@ -87,15 +90,23 @@ def _epoch_vs_oracle(kind, m, upd, runner, kg, seed, epoch, nb, opt, what, **kw)
         pos, neg = _pairs(rec, n1, start, c)
         start += c
         assert len(pos) == 2 * c          # WN18-sparse: every negative found
-        want_v += O.pairwise_step(kind, params, state, pos, neg, 0.1, float(m.margin), opt, **kw)[2]
+        before = {k: v.copy() for k, v in params.items()}
+        _, _, nv, grads = O.pairwise_step(kind, params, state, pos, neg, 0.1, float(m.margin),
+                                          opt, **kw)
+        want_v += nv
     assert got_v == want_v > 0, (what, got_v, want_v)
     for pid in m.params:
-        if opt == "adagrad":
-            parity_util.check(m.params[pid].data, params[pid], "%s %s" % (what, pid),
-                              lr=0.1, p2=state[pid])
-            parity_util.check(upd[pid].p2, state[pid], "%s p2 %s" % (what, pid))
+        if nb == 1:     # one step from the snapshot: the step-aware bound (parity_util.check_step)
+            parity_util.check_step(m.params[pid].data, params[pid], before[pid],
+                                   grads[pid] if grads else None, state[pid], 0.1,
+                                   "%s %s" % (what, pid), post=parity_util.POSTS[kind].get(pid),
+                                   opt=opt)
         else:
-            parity_util.check(m.params[pid].data, params[pid], "%s %s" % (what, pid))
+            parity_util.check(m.params[pid].data, params[pid], "%s %s" % (what, pid),
+                              lr=0.1 if opt == "adagrad" else None,
+                              p2=state[pid] if opt == "adagrad" else None)
+        if opt == "adagrad":
+            parity_util.check(upd[pid].p2, state[pid], "%s p2 %s" % (what, pid))
     return got_v
 
 
