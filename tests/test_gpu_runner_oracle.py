@@ -94,7 +94,7 @@ def _epoch_vs_oracle(kind, m, upd, runner, kg, seed, epoch, nb, opt, what, **kw)
         _, _, nv, grads = O.pairwise_step(kind, params, state, pos, neg, 0.1, float(m.margin),
                                           opt, **kw)
         want_v += nv
-    assert got_v == want_v > 0, (what, got_v, want_v)
+    assert got_v == want_v, (what, got_v, want_v)
     for pid in m.params:
         if nb == 1:     # one step from the snapshot: the step-aware bound (parity_util.check_step)
             parity_util.check_step(m.params[pid].data, params[pid], before[pid],
@@ -151,9 +151,9 @@ def test_runner_adagrad_batches_vs_oracle_from_device_state(kind):
     m.add_hyperparam("margin", margin)
     r = _runner(kind, m, upd, kg, 1, 41)
     with torch.cuda.stream(r.stream):
-        for e in range(3):
-            _epoch_vs_oracle(kind, m, upd, r, kg, 41, e, 1, "adagrad",
-                             "%s runner adagrad e%d" % (kind, e), **okw)
+        viol = [_epoch_vs_oracle(kind, m, upd, r, kg, 41, e, 1, "adagrad",
+                                 "%s runner adagrad e%d" % (kind, e), **okw) for e in range(3)]
+    assert viol[0] > 0      # (a later epoch may separate every pair by the margin)
 
 
 @pytest.mark.parametrize("kind", ["transe", "hole", "rescal"])
@@ -171,5 +171,5 @@ def test_runner_epoch_of_three_batches_vs_oracle(kind):
     with torch.cuda.stream(r.stream):
         r.run(1)
         r.synchronize()
-        _epoch_vs_oracle(kind, m, upd, r, kg, 42, 1, 3, "sgd", "%s runner sgd 3 batches" % kind,
-                         **okw)
+        assert _epoch_vs_oracle(kind, m, upd, r, kg, 42, 1, 3, "sgd",
+                                "%s runner sgd 3 batches" % kind, **okw) > 0
