@@ -70,6 +70,11 @@ enum {
                           CSR mat-vec is deterministic too, skge/util.py:53-101).
                           Entity / narrow relation tables (width <= 1024, one copy) of
                           the per-batch paths and the device pair loop */
+  SKGE_ACC_I8X4 = 4,   /* pipelined TransE-L1 runner's ENTITY table only: the exact sums
+                          in four 8-bit fields per uint32 (acc_sum [rows][width/4]
+                          dwords, one 32-bit integer atomic per quad), exact while a
+                          row's per-batch count is <= 127 (the runner flags larger
+                          counts); half the atomic bytes of int16x4 */
   SKGE_ACC_I32X2 = 2   /* pipelined runner's RELATION table only: the same exact sums
                           with 32-bit fields, two elements per int64 (a hot
                           relation's per-batch count passes 32767 long before any
@@ -111,7 +116,7 @@ typedef struct skge_table {
   int rows;
   int width;
   int touched_cap;     /* capacity of acc_touched (slots) */
-  int acc_mode;        /* SKGE_ACC_F32 | SKGE_ACC_I16X4 | SKGE_ACC_FX64 */
+  int acc_mode;        /* SKGE_ACC_F32 | SKGE_ACC_I16X4 | SKGE_ACC_FX64 (| runner-only modes) */
   int acc_replicas;    /* dense tables only: acc_sum / acc_cnt hold this many
                           copies ([replicas][rows][...]); producers spread their
                           adds over the copies (fewer same-address atomics on

@@ -110,11 +110,12 @@ struct Accum {
   int rows;
 };
 
-enum AccMode : int { ACC_F32 = 0, ACC_I16X4 = 1, ACC_I32X2 = 2, ACC_FX64 = 3 };
+enum AccMode : int { ACC_F32 = 0, ACC_I16X4 = 1, ACC_I32X2 = 2, ACC_FX64 = 3, ACC_I8X4 = 4 };
 
 // accumulator dwords per row
 __device__ __host__ __forceinline__ int acc_row_dwords(int mode, int width) {
-  return mode == ACC_I16X4 ? (width >> 1) : (mode == ACC_FX64 ? 2 * width : width);
+  return mode == ACC_I16X4 ? (width >> 1)
+                           : (mode == ACC_FX64 ? 2 * width : (mode == ACC_I8X4 ? (width >> 2) : width));
 }
 
 // ACC_FX64 (the deterministic reduce mode): a float contribution becomes a
@@ -324,6 +325,37 @@ __device__ __forceinline__ float4 unpack_i16x4(unsigned long long u) {
   const long long f2 = (short)(x & 0xFFFF);
   x = (x - f2) >> 16;
   return make_float4((float)f0, (float)f1, (float)f2, (float)x);
+}
+
+// four int8 fields per uint32 (the same carry/borrow scheme, 8-bit fields): a
+// TransE-L1 entity row whose per-batch count is <= 127 has every field total
+// within +-127, so the wrapped 32-bit sum read as int32 is the exact packed
+// sum -- half the atomic and accumulator bytes of int16x4
+__device__ __forceinline__ unsigned int pack_i8x4_sum(const float4& c) {
+  const int v = (((int)c.w * 256 + (int)c.z) * 256 + (int)c.y) * 256 + (int)c.x;
+  return (unsigned int)v;
+}
+__device__ __forceinline__ float4 unpack_i8x4_sum(unsigned int u) {
+  int x = (int)u;
+  const int f0 = (signed char)(x & 0xFF);
+  x = (x - f0) >> 8;
+  const int f1 = (signed char)(x & 0xFF);
+  x = (x - f1) >> 8;
+  const int f2 = (signed char)(x & 0xFF);
+  x = (x - f2) >> 8;
+  return make_float4((float)f0, (float)f1, (float)f2, (float)x);
+}
+
+template <int KQ>
+__device__ __forceinline__ void acc_row4_i8(unsigned int* sum, int row, const float4 (&c)[KQ],
+                                            int d) {
+  unsigned int* base = sum + (size_t)row * (d >> 2);
+  const int l = lane_id(), nq = d >> 2;
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l;
+    if (q < nq) atomicAdd(base + q, pack_i8x4_sum(c[m]));
+  }
 }
 
 // two int32 fields per int64 (the same carry/borrow scheme, 32-bit fields):

@@ -64,6 +64,9 @@ struct PipeTab {               // entity table
   int* cnt[2];
   int* touched[2];             // slot records of the batch
   int* pend[2];                // [rows]: id of the launch that last accumulated into the row
+  int* own[2];                 // large batches, [rows] by batch parity: a slot naming the row
+                               // (plain stores, one survives): the A role applies a row from
+                               // that slot only, so duplicate slots cost no claim
   int* done;                   // [rows]: id of the launch whose update of the row was last applied
                                // (lazy: whose first reader of the row has published it)
   int* claim;                  // lazy only, [rows]: id of the last launch that claimed the row
@@ -230,24 +233,46 @@ __device__ __forceinline__ void row_update(const UpdParams& t, int c, int d,
 // it as launch `gp` (write-through stores, drain, done word).  The row's sums,
 // parameters and state are loaded in the same memory round trip as the claim:
 // nobody writes them before the claim is won, and a loser discards them.
-template <int KQ>
+template <int KQ, bool E8 = false>
 __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int row, int d, int gp) {
   const int l = lane_id(), nq = d >> 2;
   int c = 0;
   if (l == 0) c = atomicExch(t.cnt[pp] + row, 0);
   unsigned long long* srow = t.sum[pp] + (size_t)row * nq;
+  unsigned int* srow8 = reinterpret_cast<unsigned int*>(t.sum[pp]) + (size_t)row * nq;
   unsigned long long sv[KQ];
   float4 p[KQ], a[KQ];
-  load_upd_row<KQ>(t.P + (size_t)row * d, t.A ? t.A + (size_t)row * d : nullptr, srow, d, p, a,
-                   sv);
+  if (E8) {   // int8x4 sums: one dword per quad, re-packed as int16x4 for row_update
+    unsigned int s8[KQ];
+    const float4* prow = reinterpret_cast<const float4*>(t.P + (size_t)row * d);
+    const float4* arow = reinterpret_cast<const float4*>(t.A + (size_t)row * d);
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+      const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
+      s8[m] = srow8[qc];
+      p[m] = prow[qc];
+      a[m] = t.A ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) sv[m] = pack_i16x4(unpack_i8x4_sum(s8[m]));
+  } else {
+    load_upd_row<KQ>(t.P + (size_t)row * d, t.A ? t.A + (size_t)row * d : nullptr, srow, d, p, a,
+                     sv);
+  }
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row
-  if (c > PACKED_MAX && l == 0) atomicOr(t.err, ERR_PACKED);   // a 16-bit field may have wrapped
+  // a field may have wrapped: 16-bit fields past 32767, 8-bit fields past 127
+  if (c > (E8 ? 127 : PACKED_MAX) && l == 0) atomicOr(t.err, ERR_PACKED);
   row_update<KQ, false>(t.u, c, d, sv, sv, p, a);
 #pragma unroll
   for (int m = 0; m < KQ; ++m) {
     const int q = 64 * m + l;
-    if (q < nq) srow[q] = 0ull;
+    if (q < nq) {
+      if (E8)
+        srow8[q] = 0u;
+      else
+        srow[q] = 0ull;
+    }
   }
   store_row4_sc1<KQ>(t.P, row, d, p);
   if (t.A) store_row4_sc1<KQ>(t.A, row, d, a);
@@ -307,11 +332,11 @@ __device__ __forceinline__ void claim_and_apply2(const PipeTab& t, int pp, int r
 // B role: make sure launch gp's update of entity `row` (pending at launch
 // start) has landed -- apply it if nobody has claimed it yet, else wait for
 // its publisher
-template <int KQ>
+template <int KQ, bool E8 = false>
 __device__ __forceinline__ void ensure_applied(const PipeTab& t, int pp, int row, int d, int gp,
                                                int* err) {
   if (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gp) return;
-  claim_and_apply<KQ>(t, pp, row, d, gp);
+  claim_and_apply<KQ, E8>(t, pp, row, d, gp);
   unsigned spins = 0;
   while (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gp) {
     __builtin_amdgcn_s_sleep(2);
@@ -425,7 +450,7 @@ __device__ __forceinline__ void rel_publish(const PipeArgs& a, int w, int rd, in
 #define SKGE_PIPE_ASLOTS 1   // entity slots per A-role wave (1 or 2)
 #endif
 constexpr int ASLOTS = SKGE_PIPE_ASLOTS;
-template <int KQ, bool W32>
+template <int KQ, bool W32, bool E8>
 __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
@@ -443,7 +468,10 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
   if ((int)blockIdx.x < a.nA) {
     // ---- A role: write R_b, then apply the previous batch's entity rows ----
     const int nR = a.R.rows;
-    const int total = nR + (a.prev_slots + ASLOTS - 1) / ASLOTS;   // relation rows, slot groups
+    // owner marks (large batches): items are groups of 64 slots, scanned
+    // lane-parallel; else one slot (ASLOTS) per item
+    const int* const ownp = a.E.own[pp];
+    const int total = nR + (ownp ? (a.prev_slots + 63) / 64 : (a.prev_slots + ASLOTS - 1) / ASLOTS);
     const int wa = blk_a * wpb + (threadIdx.x >> 6);
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
     if (a.b == a.nb1 && wa == 0)   // the flush: fold the epoch's violation count
@@ -451,6 +479,19 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
     for (int w = wa; w < total; w += a.nA * wpb) {
       if (w < nR) {
         rel_publish<KQ, W32>(a, w, rd, rw, ra_prev, ra_old);
+      } else if (ownp) {
+        // 64 slots: their rows and owner marks in two vector loads; only the
+        // slot each row's owner mark names applies it (no claim on duplicates)
+        const int i = 64 * (w - nR) + l;
+        const int r = i < a.prev_slots ? a.E.touched[pp][i] : -1;
+        const bool mine = r >= 0 && ownp[r] == i;
+        uint64_t m = __ballot(mine);
+        while (m) {
+          const int k = __ffsll((unsigned long long)m) - 1;
+          m &= m - 1;
+          const int row = __builtin_amdgcn_readlane(r, k);
+          claim_and_apply<KQ, E8>(a.E, pp, row, d, gp);
+        }
       } else {
         if (ASLOTS == 2) {
           const int i0 = 2 * (w - nR);
@@ -461,7 +502,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
         } else {
           const int row = __builtin_amdgcn_readfirstlane(a.E.touched[pp][w - nR]);
 #ifndef SKGE_PIPE_ABL_NOAPPLY_E   // timing-only ablation: entity rows never updated
-          if (row >= 0) claim_and_apply<KQ>(a.E, pp, row, d, gp);
+          if (row >= 0) claim_and_apply<KQ, E8>(a.E, pp, row, d, gp);
 #else
           if (row >= 0 && l == 0) a.E.cnt[pp][row] = 0;
 #endif
@@ -479,6 +520,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
   int* const cnt_cp = opaque_ptr(a.E.cnt[cp]);
   int* const tch_cp = opaque_ptr(a.E.touched[cp]);
   int* const pend_cp = opaque_ptr(a.E.pend[cp]);
+  int* const own_cp = a.E.own[cp];
   unsigned long long* const racc = opaque_ptr(a.R.acc[ra_cur]);
   unsigned long long* const esum = opaque_ptr(a.E.sum[cp]);
   // the batch's records through buffer descriptors built once (not pointers
@@ -528,7 +570,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) {
         if (!((pend >> k) & 1ull)) continue;
-        ensure_applied<KQ>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err);
+        ensure_applied<KQ, E8>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err);
       }
       if (pend & 1ull) load_row4_sc1<KQ>(a.E.P, s, d, es);
       if (pend & 2ull) load_row4_sc1<KQ>(a.E.P, o, d, eo);
@@ -569,7 +611,10 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
       const int rE = sel4(l, s, o, neg0, neg1);
       if (l < 4) {
         commit_slot(cnt_cp, tch_cp, rE, cE, 4 * w + l);
-        if (cE > 0) pend_cp[rE] = g;
+        if (cE > 0) {
+          pend_cp[rE] = g;
+          if (own_cp) own_cp[rE] = 4 * w + l;   // large batches: this slot may own the row
+        }
       } else if (l == 4 && v0 + v1 > 0) {
         atomicAdd(racc + (size_t)p * a.R.rw + rcw, (unsigned long long)(2 * (v0 + v1)));
       }
@@ -592,12 +637,20 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
         SKGE_CO(w)
 #undef SKGE_CO
       }
-      Accum aE = {};   // mode ACC_F32 (0), one copy
-      aE.sum = reinterpret_cast<float*>(esum);
-      acc_row4_i16<KQ>(aE, s, cs, d);
-      acc_row4_i16<KQ>(aE, o, co, d);
-      if (v0) acc_row4_i16<KQ>(aE, neg0, c0, d);
-      if (v1) acc_row4_i16<KQ>(aE, neg1, c1, d);
+      if (E8) {   // int8x4 sums: one 32-bit atomic per quad
+        unsigned int* es8 = reinterpret_cast<unsigned int*>(esum);
+        acc_row4_i8<KQ>(es8, s, cs, d);
+        acc_row4_i8<KQ>(es8, o, co, d);
+        if (v0) acc_row4_i8<KQ>(es8, neg0, c0, d);
+        if (v1) acc_row4_i8<KQ>(es8, neg1, c1, d);
+      } else {
+        Accum aE = {};   // mode ACC_F32 (0), one copy
+        aE.sum = reinterpret_cast<float*>(esum);
+        acc_row4_i16<KQ>(aE, s, cs, d);
+        acc_row4_i16<KQ>(aE, o, co, d);
+        if (v0) acc_row4_i16<KQ>(aE, neg0, c0, d);
+        if (v1) acc_row4_i16<KQ>(aE, neg1, c1, d);
+      }
       // relation sums: rows of rw words; int32x2 (two words per quad) when a
       // hot relation's batch total could pass 16 bits
       unsigned long long* rrow = racc + (size_t)p * a.R.rw;
@@ -1775,6 +1828,7 @@ struct skge_pipe_runner {
   std::vector<PipeArgs> batch;     // nb1 batches + the flush
   std::vector<int> grid;
   bool w32 = false;                // int32x2 relation sums
+  bool e8 = false;                 // int8x4 entity sums (SKGE_ACC_I8X4: per-batch counts <= 127)
   bool lazy = false;               // SKGE_PIPE_LAZY: entity rows applied by their next reader
   bool owner = false;              // SKGE_PIPE_OWNER: rows updated by their batch's last reference
   bool hole = false;               // HolE pairwise (k_hole_pipe, fp32 sums)
@@ -1837,9 +1891,12 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
     } else if (r->owner) {                                                                       \
       if (r->w32) hipLaunchKernelGGL((k_own_batch<K, true>), gr, bl, 0, st, a);                  \
       else hipLaunchKernelGGL((k_own_batch<K, false>), gr, bl, 0, st, a);                        \
+    } else if (r->e8) {                                                                          \
+      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true>), gr, bl, 0, st, a);           \
+      else hipLaunchKernelGGL((k_pipe_batch<K, false, true>), gr, bl, 0, st, a);                 \
     } else {                                                                                     \
-      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true>), gr, bl, 0, st, a);                 \
-      else hipLaunchKernelGGL((k_pipe_batch<K, false>), gr, bl, 0, st, a);                       \
+      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false>), gr, bl, 0, st, a);          \
+      else hipLaunchKernelGGL((k_pipe_batch<K, false, false>), gr, bl, 0, st, a);                \
     }                                                                                            \
   } while (0)
     if (r->hole) {
@@ -1882,7 +1939,9 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   }
   skge_table_t relc = *rel;   // the relation encoding is the runner's own (checked below)
   if (relc.acc_mode == SKGE_ACC_I32X2) relc.acc_mode = SKGE_ACC_I16X4;
-  if (check_table(ent, "ent", true) || check_table(&relc, "rel", true)) return nullptr;
+  skge_table_t entc = *ent;   // int8x4 entity sums: the runner's own encoding too
+  if (entc.acc_mode == SKGE_ACC_I8X4) entc.acc_mode = SKGE_ACC_I16X4;
+  if (check_table(&entc, "ent", true) || check_table(&relc, "rel", true)) return nullptr;
   if (hole) {   // HolE: fp32 sums, quad rows (d % 4 == 0, d <= 256)
     if (ent->acc_mode != SKGE_ACC_F32 || rel->acc_mode != SKGE_ACC_F32 || d % 4 || d < 4 ||
         d > 256 || ent->width != d || rel->width != d || ent->acc_touched == nullptr ||
@@ -1893,7 +1952,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
                 "gates");
       return nullptr;
     }
-  } else if (ent->acc_mode != SKGE_ACC_I16X4 ||
+  } else if ((ent->acc_mode != SKGE_ACC_I16X4 && !(ent->acc_mode == SKGE_ACC_I8X4 && !lazy)) ||
       (rel->acc_mode != SKGE_ACC_I16X4 && rel->acc_mode != SKGE_ACC_I32X2) || d % 4 || d > 1024 ||
       ent->width != d || rel->width != d || (ent->acc_touched == nullptr && !lazy) ||
       rel->acc_touched != nullptr || rel->acc_replicas > 1 || ent->acc_replicas > 1 ||
@@ -1920,9 +1979,10 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   skge_pipe_runner* r = new skge_pipe_runner();
   r->lazy = lazy;
   r->hole = hole;
+  r->e8 = !hole && ent->acc_mode == SKGE_ACC_I8X4;
   {
     const char* ow = getenv("SKGE_PIPE_OWNER");   // A/B: entity rows by their last reference
-    r->owner = !hole && !lazy && ow && atoi(ow) != 0;
+    r->owner = !hole && !lazy && !r->e8 && ow && atoi(ow) != 0;
   }
   const int nq = d / 4;
   PipeArgs a = {};
@@ -1953,12 +2013,20 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
       t.claim = (int*)dalloc(r, (size_t)N * 4);
       ok = ok && t.claim;
     } else {      // a second accumulator copy, slot records and batch marks
-      t.sum[1] = (unsigned long long*)dalloc(r, (size_t)N * nq * (hole ? 16 : 8));
+      t.sum[1] = (unsigned long long*)dalloc(r, (size_t)N * nq * (hole ? 16 : (r->e8 ? 4 : 8)));
       t.cnt[1] = (int*)dalloc(r, (size_t)N * 4);
       t.touched[1] = (int*)dalloc(r, (size_t)4 * bs * 4);
       t.pend[0] = (int*)dalloc(r, (size_t)N * 4);
       t.pend[1] = (int*)dalloc(r, (size_t)N * 4);
       ok = ok && t.sum[1] && t.cnt[1] && t.touched[1] && t.pend[0] && t.pend[1];
+      // large batches (more than 16k slots): owner marks, the A role scans its
+      // slots 64 at a time (SKGE_PIPE_OWNMARK=0: one slot per item, as below)
+      const char* om = getenv("SKGE_PIPE_OWNMARK");
+      if (!hole && 4 * bs > 4 * 4096 && !(om && atoi(om) == 0)) {
+        t.own[0] = (int*)dalloc(r, (size_t)N * 4);
+        t.own[1] = (int*)dalloc(r, (size_t)N * 4);
+        ok = ok && t.own[0] && t.own[1];
+      }
     }
     if (r->owner) {   // reference words by batch parity
       t.refs[0] = (unsigned long long*)dalloc(r, (size_t)N * 8);
@@ -2053,10 +2121,13 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     a.prev_slots = 4 * prev;
     // A role: every relation row, then the previous batch's entity slots (lazy:
     // no entity rows, except the flush's sweep over all rows in 64-row chunks)
+    const bool grouped = a.E.own[0] != nullptr;   // owner marks: 64-slot groups
     const int a_items =
         rel->rows + (hole ? (4 * prev + HGROUP - 1) / HGROUP
                           : lazy ? (b == nb1 ? (ent->rows + 63) / 64 : 0)
-                                 : r->owner ? 0 : (4 * prev + ASLOTS - 1) / ASLOTS);
+                                 : r->owner ? 0
+                                            : grouped ? (4 * prev + 63) / 64
+                                                      : (4 * prev + ASLOTS - 1) / ASLOTS);
     constexpr int WPB = SKGE_PIPE_WG / 64;
     // HolE: the apply waves loop over their items within the residency the
     // scoring waves leave (SKGE_HPIPE_OCC waves per SIMD: 2 at ~180 VGPRs; the
@@ -2078,7 +2149,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     // workgroups instead of one wave per slot (the scoring waves then find the
     // chip's residency free; nb = 2 on WN18: 284 -> 304-310 M triples/s, same run);
     // at the reference's batch size one wave per slot is faster (148 vs 142 M)
-    if (!hole && !lazy && b < nb1 && a_items > 4 * 4096) a_cap = 768;
+    if (!hole && !lazy && !grouped && b < nb1 && a_items > 4 * 4096) a_cap = 768;
     if (!hole && !lazy && b < nb1 && getenv("SKGE_PIPE_ACAP"))   // A/B switch (TransE)
       a_cap = std::max(1, atoi(getenv("SKGE_PIPE_ACAP")));
     a.nA = std::max(1, std::min((a_items + WPB - 1) / WPB, std::min(a_cap, 16384)));

@@ -167,8 +167,13 @@ class EpochRunner(object):
         lib = L.lib()
         if can_pipe:
             # relation sums in 16-bit fields while a relation's per-batch count
-            # fits them (faster: half the atomics), else int32x2
-            self._tables(model, updaters, packed, 1, rel_w32=rel_reps != 1)
+            # fits them (faster: half the atomics), else int32x2; entity sums in
+            # 8-bit fields while every entity's per-batch count is <= 127 (half
+            # the atomic bytes again; the apply checks every count)
+            e8 = (not want_lazy and self.count_bound <= 127 and
+                  _os.environ.get("SKGE_PIPE_E8", "1") != "0")
+            self._tables(model, updaters, packed, 1, rel_w32=rel_reps != 1, ent_i8=e8)
+            self.ent_i8 = e8
             self.lazy = want_lazy
             h = lib.skge_pipe_runner_create_ex(
                 L.stream_ptr(self.stream), self.te, self.tr, model.d, L.ptr(kg.trip), kg.T,
@@ -204,7 +209,7 @@ class EpochRunner(object):
         self.handle = h
         self.nlaunches = lib.skge_runner_nlaunches(h)
 
-    def _tables(self, model, updaters, packed, rel_replicas, rel_w32=False):
+    def _tables(self, model, updaters, packed, rel_replicas, rel_w32=False, ent_i8=False):
         """The runner's own accumulators (captured by its graph) and tables."""
         from .param import Accumulator
         from .base import deterministic
@@ -214,7 +219,8 @@ class EpochRunner(object):
         if not packed and deterministic():   # exact fixed-point sums, one copy
             mode, rel_replicas = L.SKGE_ACC_FX64, 1
         bs = self.kg.T // self.nbatches
-        self.accE = Accumulator(E.rows, E.width, dev, slots=4 * bs, mode=mode)
+        self.accE = Accumulator(E.rows, E.width, dev, slots=4 * bs,
+                                mode=L.SKGE_ACC_I8X4 if ent_i8 else mode)
         # relation rows are hot (every positive adds to one of |R| rows): the
         # two-launch runner spreads the adds over `rel_replicas` copies, the
         # pipelined one keeps 32-bit fields (rel_w32)

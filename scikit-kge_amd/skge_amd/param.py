@@ -291,7 +291,8 @@ class Accumulator(object):
         # int16x4 mode packs four elements per 8 bytes: width / 2 dwords per row;
         # the deterministic fixed-point mode keeps one int64 per element
         dw = width // 2 if mode == L.SKGE_ACC_I16X4 else \
-            (2 * width if mode == L.SKGE_ACC_FX64 else width)
+            (2 * width if mode == L.SKGE_ACC_FX64 else
+             (width // 4 if mode == L.SKGE_ACC_I8X4 else width))
         self.sum = torch.zeros(self.replicas * rows * dw, dtype=torch.float32, device=device)
         self.cnt = torch.zeros(self.replicas * rows, dtype=torch.int32, device=device)
         self.touched = None if dense else \

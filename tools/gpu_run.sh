@@ -37,7 +37,7 @@ for st in ${STEPS:-tests smoke bench}; do
         run ${TAG}_tests$n ${TTEST:-900} python -u -m pytest ${arg:-tests} -m gpu -q -rf -p no:cacheprovider \
           --timeout ${TIMEOUT1:-300} --timeout-method thread ${PYTEST_ARGS:-}
       fi
-      rc=$?; [ $rc -gt 1 ] && exit $rc ;;
+      rc=$?; if [ $rc -gt 1 ]; then exit $rc; fi ;;
     smoke)
       run ${TAG}_smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
@@ -61,3 +61,4 @@ for st in ${STEPS:-tests smoke bench}; do
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
+exit 0
