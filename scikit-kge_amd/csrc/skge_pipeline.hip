@@ -281,6 +281,73 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
   if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
 }
 
+// Large batches: up to GRP_ROWS owner rows of a 64-slot group at once -- all
+// claims in one atomic instruction (lane j claims row j), all rows' loads in
+// one round trip, every claimed row updated and stored write-through, ONE
+// drain, then the done words -- instead of a claim / load / store / drain
+// chain per row.
+constexpr int GRP_ROWS = 8;
+template <int KQ, bool E8>
+__device__ __forceinline__ void claim_and_apply_rows(const PipeTab& t, int pp, int rl, int n,
+                                                     int d, int gp) {
+  const int l = lane_id(), nq = d >> 2;
+  int c = 0;
+  if (l < n) c = atomicExch(t.cnt[pp] + rl, 0);   // lane j holds row j (j < n)
+  float4 p[GRP_ROWS][KQ], a[GRP_ROWS][KQ];
+  unsigned long long sv[GRP_ROWS][KQ];
+  int row[GRP_ROWS];
+#pragma unroll
+  for (int j = 0; j < GRP_ROWS; ++j) {
+    row[j] = __builtin_amdgcn_readlane(rl, j < n ? j : 0);
+    const float4* prow = reinterpret_cast<const float4*>(t.P + (size_t)row[j] * d);
+    const float4* arow = reinterpret_cast<const float4*>(t.A + (size_t)row[j] * d);
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+      const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
+      if (E8)
+        sv[j][m] = reinterpret_cast<const unsigned int*>(t.sum[pp])[(size_t)row[j] * nq + qc];
+      else
+        sv[j][m] = t.sum[pp][(size_t)row[j] * nq + qc];
+      p[j][m] = prow[qc];
+      a[j][m] = t.A ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+  }
+  int any = 0;
+#pragma unroll
+  for (int j = 0; j < GRP_ROWS; ++j) {
+    const int cj = __builtin_amdgcn_readlane(c, j);
+    if (j >= n || cj == 0) continue;   // past the rows, or another wave owns the row
+    any = 1;
+    if (cj > (E8 ? 127 : PACKED_MAX) && l == 0) atomicOr(t.err, ERR_PACKED);
+    if (E8) {
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) sv[j][m] = pack_i16x4(unpack_i8x4_sum((unsigned int)sv[j][m]));
+    }
+    row_update<KQ, false>(t.u, cj, d, sv[j], sv[j], p[j], a[j]);
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+      const int q = 64 * m + l;
+      if (q < nq) {
+        if (E8)
+          reinterpret_cast<unsigned int*>(t.sum[pp])[(size_t)row[j] * nq + q] = 0u;
+        else
+          t.sum[pp][(size_t)row[j] * nq + q] = 0ull;
+      }
+    }
+    store_row4_sc1<KQ>(t.P, row[j], d, p[j]);
+    if (t.A) store_row4_sc1<KQ>(t.A, row[j], d, a[j]);
+  }
+  if (!any) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+  if (l < n && c != 0) __hip_atomic_store(t.done + rl, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t.claims && l == 0) {
+    int k = 0;
+#pragma unroll
+    for (int j = 0; j < GRP_ROWS; ++j) k += (j < n && __builtin_amdgcn_readlane(c, j) != 0);
+    atomicAdd(shard_of(t.claims), k);
+  }
+}
+
 // Two slot-recorded rows per A wave (SKGE_PIPE_ASLOTS 2): both claims (lanes 0
 // and 1 of one atomic instruction) and both rows' loads in one round trip, the
 // claimed rows applied and stored write-through, ONE drain, then both done
@@ -450,7 +517,7 @@ __device__ __forceinline__ void rel_publish(const PipeArgs& a, int w, int rd, in
 #define SKGE_PIPE_ASLOTS 1   // entity slots per A-role wave (1 or 2)
 #endif
 constexpr int ASLOTS = SKGE_PIPE_ASLOTS;
-template <int KQ, bool W32, bool E8>
+template <int KQ, bool W32, bool E8, bool GRP = false>
 __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
@@ -486,11 +553,34 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
         const int r = i < a.prev_slots ? a.E.touched[pp][i] : -1;
         const bool mine = r >= 0 && ownp[r] == i;
         uint64_t m = __ballot(mine);
-        while (m) {
-          const int k = __ffsll((unsigned long long)m) - 1;
-          m &= m - 1;
-          const int row = __builtin_amdgcn_readlane(r, k);
-          claim_and_apply<KQ, E8>(a.E, pp, row, d, gp);
+        if (GRP) {   // GRP_ROWS owner rows per round trip
+          while (m) {
+            // compact the next GRP_ROWS owners into lanes 0..n-1
+            const int rank = __popcll(m & ((1ull << l) - 1ull));
+            const bool take = ((m >> l) & 1ull) && rank < GRP_ROWS;
+            const uint64_t tk = __ballot(take);
+            const int n = __popcll(tk);
+            // lane j < n receives the row of the j-th taken lane
+            int src = 0;
+            {
+              uint64_t t2 = tk;
+              for (int j = 0; j < GRP_ROWS && t2; ++j) {
+                const int k = __ffsll((unsigned long long)t2) - 1;
+                t2 &= t2 - 1;
+                if (l == j) src = k;
+              }
+            }
+            const int rl = __builtin_amdgcn_ds_bpermute(src << 2, r);
+            claim_and_apply_rows<KQ, E8>(a.E, pp, rl, n, d, gp);
+            m &= ~tk;
+          }
+        } else {
+          while (m) {
+            const int k = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            const int row = __builtin_amdgcn_readlane(r, k);
+            claim_and_apply<KQ, E8>(a.E, pp, row, d, gp);
+          }
         }
       } else {
         if (ASLOTS == 2) {
@@ -637,6 +727,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
         SKGE_CO(w)
 #undef SKGE_CO
       }
+#ifndef SKGE_PIPE_ABL_NO_EATOM   // timing-only ablation (tools/ablate.sh): entity atomics dropped
       if (E8) {   // int8x4 sums: one 32-bit atomic per quad
         unsigned int* es8 = reinterpret_cast<unsigned int*>(esum);
         acc_row4_i8<KQ>(es8, s, cs, d);
@@ -651,9 +742,13 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
         if (v0) acc_row4_i16<KQ>(aE, neg0, c0, d);
         if (v1) acc_row4_i16<KQ>(aE, neg1, c1, d);
       }
+#endif
       // relation sums: rows of rw words; int32x2 (two words per quad) when a
       // hot relation's batch total could pass 16 bits
       unsigned long long* rrow = racc + (size_t)p * a.R.rw;
+#ifdef SKGE_PIPE_ABL_NO_RATOM   // timing-only ablation: relation atomics dropped
+      if (rrow) continue;
+#endif
 #pragma unroll
       for (int m = 0; m < KQ; ++m) {
         const int q = 64 * m + l;
@@ -1829,6 +1924,7 @@ struct skge_pipe_runner {
   std::vector<int> grid;
   bool w32 = false;                // int32x2 relation sums
   bool e8 = false;                 // int8x4 entity sums (SKGE_ACC_I8X4: per-batch counts <= 127)
+  bool grp = true;                 // owner marks: GRP_ROWS rows per apply round trip
   bool lazy = false;               // SKGE_PIPE_LAZY: entity rows applied by their next reader
   bool owner = false;              // SKGE_PIPE_OWNER: rows updated by their batch's last reference
   bool hole = false;               // HolE pairwise (k_hole_pipe, fp32 sums)
@@ -1891,6 +1987,14 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
     } else if (r->owner) {                                                                       \
       if (r->w32) hipLaunchKernelGGL((k_own_batch<K, true>), gr, bl, 0, st, a);                  \
       else hipLaunchKernelGGL((k_own_batch<K, false>), gr, bl, 0, st, a);                        \
+    } else if (a.E.own[0] && r->grp) {   /* large batches: grouped owner-row apply */             \
+      if (r->e8) {                                                                               \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, true>), gr, bl, 0, st, a);   \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, true, true>), gr, bl, 0, st, a);         \
+      } else {                                                                                   \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true>), gr, bl, 0, st, a);  \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true>), gr, bl, 0, st, a);        \
+      }                                                                                          \
     } else if (r->e8) {                                                                          \
       if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true>), gr, bl, 0, st, a);           \
       else hipLaunchKernelGGL((k_pipe_batch<K, false, true>), gr, bl, 0, st, a);                 \
@@ -1980,6 +2084,10 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   r->lazy = lazy;
   r->hole = hole;
   r->e8 = !hole && ent->acc_mode == SKGE_ACC_I8X4;
+  {
+    const char* gr = getenv("SKGE_PIPE_GRP");   // A/B: 0 = one owner row per round trip
+    r->grp = !(gr && atoi(gr) == 0);
+  }
   {
     const char* ow = getenv("SKGE_PIPE_OWNER");   // A/B: entity rows by their last reference
     r->owner = !hole && !lazy && !r->e8 && ow && atoi(ow) != 0;

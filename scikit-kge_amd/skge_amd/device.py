@@ -49,7 +49,7 @@ def _bincount_max(col, n):
     return torch.bincount(col.long(), minlength=n)
 
 
-def packed_count_bound(kg, n_ent, batch):
+def packed_count_bound(kg, n_ent, batch, tail=None):
     """Upper bound on an ENTITY row's per-batch occurrence count in the
     TransE-L1 device loops (the count bounds every 16-bit field of its packed
     sums, csrc/skge_pipeline.hip).  A positive adds at most 3 to each of its s
@@ -63,8 +63,16 @@ def packed_count_bound(kg, n_ent, batch):
     occ = _bincount_max(kg.trip[:, 0], n_ent) + _bincount_max(kg.trip[:, 1], n_ent)
     det = 3 * min(int(occ.max().item()), 2 * int(batch))
     lam = 2.0 * batch / max(n_ent, 1)
-    corr = min(2 * int(batch), int(math.ceil(_tail(lam))))
+    corr = min(2 * int(batch), int(math.ceil((tail or _tail)(lam))))
     return det + corr
+
+
+def _tail8(mu):
+    """A tighter tail for the int8x4 entity sums' choice (mu + 8 sqrt(mu) +
+    20: a Poisson count passes it with probability < 1e-15): the choice only
+    trades atomic bytes, and a count past 127 is still caught by the apply
+    (the runner raises, use SKGE_PIPE_E8=0)."""
+    return mu + 8.0 * math.sqrt(mu) + 20.0
 
 
 def _tail(mu):
@@ -170,7 +178,7 @@ class EpochRunner(object):
             # fits them (faster: half the atomics), else int32x2; entity sums in
             # 8-bit fields while every entity's per-batch count is <= 127 (half
             # the atomic bytes again; the apply checks every count)
-            e8 = (not want_lazy and self.count_bound <= 127 and
+            e8 = (not want_lazy and packed_count_bound(kg, model.E.rows, bs, _tail8) <= 127 and
                   _os.environ.get("SKGE_PIPE_E8", "1") != "0")
             self._tables(model, updaters, packed, 1, rel_w32=rel_reps != 1, ent_i8=e8)
             self.ent_i8 = e8

@@ -1,7 +1,8 @@
+# A/B of pipelined-runner switches (bench.py default config, nb=100 + the nb=2 detail line)
 set -u
-cd $GRAFT_REPO_ROOT
-true
-run() { # name env... 
+cd ${GRAFT_REPO_ROOT:-$(dirname "$0")/..}
+mkdir -p gpurun_out
+run() { # name env...
   local n=$1; shift
   env "$@" timeout -k 10 150 python bench.py --steps 20 --warmup 3 --no-cpu --no-roofline --large-nb 2 > gpurun_out/ab_$n.log 2>&1 || return 1
   python3 - "$n" <<'PY'
@@ -10,7 +11,8 @@ l=[x for x in open("gpurun_out/ab_%s.log" % n) if x.startswith("{")][0]; j=json.
 print(n, round(j["value"]/1e6,2), j["roofline"]["avg_launch_us"], round(j["detail"]["large_batch"]["value"]/1e6,2), j["detail"]["large_batch"]["ms_per_epoch"])
 PY
 }
-run new SKGE_PIPE_E8=1 SKGE_PIPE_OWNMARK=1 || exit 1
-run old SKGE_PIPE_E8=0 SKGE_PIPE_OWNMARK=0 || exit 1
-run new2 SKGE_PIPE_E8=1 SKGE_PIPE_OWNMARK=1 || exit 1
-run old2 SKGE_PIPE_E8=0 SKGE_PIPE_OWNMARK=0 || exit 1
+# AB: ';'-separated specs "name VAR=value ...", default grouped vs ungrouped applies
+IFS=';' read -ra specs <<< "${AB:-grp SKGE_PIPE_GRP=1;nogrp SKGE_PIPE_GRP=0}"
+for spec in "${specs[@]}"; do
+  run $spec || exit 1
+done
