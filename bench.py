@@ -49,22 +49,24 @@ def make_wn18_kg(n_ent=N_ENT, n_rel=N_REL, n_triples=N_TRIPLES, seed=0):
     return out.astype(np.int32)
 
 
-def pmc_traffic(kernel_substr):
+def pmc_traffic(kernel_substr, fname="pmc.json"):
     """Per-launch HBM-side traffic of a kernel from the newest committed rocprofv3
-    PMC summary (profiles/*/pmc.json, made by tools/gpu_profile.sh): 2*FETCH_SIZE
-    + WRITE_SIZE per the gfx950 correction in MI355X_MICROARCH.md "HBM"."""
+    PMC summary (profiles/<round>/<fname>, made by `tools/gpu_run.sh pmc` +
+    tools/pmc_summary.py; pmc.json for the default line, pmc_c<k>.json for
+    config k): 2*FETCH_SIZE + WRITE_SIZE per the gfx950 correction in
+    MI355X_MICROARCH.md "HBM"."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc.json")))
-    if not files:
-        return None, None
-    data = json.load(open(files[-1]))
-    for name, e in data.items():
-        if kernel_substr in name and "traffic_bytes_per_launch" in e:
-            grids = [g for g in e.get("by_grid", {}).values() if "traffic_bytes_per_launch" in g]
-            if grids:   # the geometry launched most (the nb=100 epochs, not the detail lines)
-                g = max(grids, key=lambda x: x["calls"])
-                return g["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
-            return e["traffic_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", fname)))
+    for f in reversed(files):
+        data = json.load(open(f))
+        for name, e in data.items():
+            if kernel_substr in name and "traffic_bytes_per_launch" in e:
+                grids = [g for g in e.get("by_grid", {}).values()
+                         if "traffic_bytes_per_launch" in g]
+                if grids:   # the geometry launched most (the timed epochs, not the detail lines)
+                    g = max(grids, key=lambda x: x["calls"])
+                    return g["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
+                return e["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
     return None, None
 
 
@@ -684,6 +686,11 @@ def make_config5_kg(n_ent, n_rel, n_triples, dev, seed):
     return out
 
 
+# kernel_profile's names -> the HIP kernel names rocprofv3 reports
+PMC_KERNEL = {"transe_sample_grad": "k_transe_l1_sample_grad", "accum_apply": "k_apply",
+              "pipe_batch": "k_pipe_batch"}
+
+
 def run_config5(args):
     """BASELINE.json configs[4] on one GPU per rank: TransE-L1 d=512, |E|=50M,
     |R|=10k, T=100M synthetic triples, B=131072 positives per batch, AdaGrad.
@@ -729,6 +736,7 @@ def run_config5(args):
         kernel_profile(model, upd, kg, nb, d, runner.stream, runner)
     k = prof["dominant"]
     if rank == 0:
+        traffic, traffic_src = pmc_traffic(PMC_KERNEL.get(k["name"], k["name"]), "pmc_c5.json")
         line = {
             "metric": "triples/sec (score+grad+update), synthetic TransE |E|=50M |R|=10k d=512, "
                       "B=131072 per GPU (BASELINE configs[4])",
@@ -745,7 +753,9 @@ def run_config5(args):
             "roofline": {"bound": "hbm", "kernel": k["name"],
                          "achieved": round(k["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 4),
-                         "traffic": None, "bytes_per_launch": round(k["bytes_per_launch"]),
+                         "traffic": None if traffic is None else round(traffic),
+                         "traffic_source": traffic_src,
+                         "bytes_per_launch": round(k["bytes_per_launch"]),
                          "avg_launch_us": round(k["avg_us"], 3)},
             "cpu_baseline": None if args.no_cpu else cpu_baseline_config5(args.cpu_seconds),
             "detail": {"runner": "pipelined" if runner.pipelined else "two-launch",
@@ -1028,6 +1038,9 @@ def run_config34(args):
     if rank == 0:
         cpu = None if args.no_cpu else cpu_baseline(trip, d, nb, args.cpu_seconds, kind, margin)
         name = {"hole": "HolE", "rescal": "RESCAL"}[kind]
+        tkern = "k_hole_pipe" if prof is not None else (
+            "k_rescal_front" if kind == "rescal" else "k_hole")
+        traffic, traffic_src = pmc_traffic(tkern, "pmc_c%d.json" % args.config)
         line = {
             "metric": "triples/sec (score+grad+update), WN18 %s d=%d pairwise, 1 MI355X "
                       "(BASELINE configs[%d])" % (name, d, args.config - 1),
@@ -1047,7 +1060,8 @@ def run_config34(args):
                           "achieved": round(prof["dominant"]["achieved_gbs"], 1),
                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(prof["dominant"]["achieved_gbs"] / HBM_PEAK_GBS, 4),
-                          "traffic": None,
+                          "traffic": None if traffic is None else round(traffic),
+                          "traffic_source": traffic_src,
                           "bytes_per_launch": round(prof["dominant"]["bytes_per_launch"]),
                           "avg_launch_us": round(prof["dominant"]["avg_us"], 3),
                           "note": "row gathers, fp32 atomic rows (2.5 V lower bound) and "
@@ -1056,7 +1070,10 @@ def run_config34(args):
                          if prof is not None else
                          {"bound": "valu" if kind == "hole" else "mfma", "kernel": "whole step",
                           "achieved": round(tfs, 2), "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
-                          "frac": round(tfs / FP32_PEAK_TFS, 4), "traffic": None}),
+                          "frac": round(tfs / FP32_PEAK_TFS, 4),
+                          # HBM bytes per launch of the step's dominant kernel (rocprofv3 PMC)
+                          "traffic": None if traffic is None else round(traffic),
+                          "traffic_kernel": tkern, "traffic_source": traffic_src}),
             "cpu_baseline": cpu,
             "detail": {"violations_per_pair": round(V / float(P), 4),
                        "direct_form_TFLOP_s": round(tfs, 2),   # model_flops at the timed rate
