@@ -1,6 +1,7 @@
-"""bench.py's multi-GPU (replicas) bookkeeping on CPU: a world-size-2 gloo job
-checks the rank environment, the max-over-ranks timing and the whole-job
-value (replicas only, weak scaling)."""
+"""bench.py's multi-GPU bookkeeping on CPU: a world-size-2 gloo job checks the
+rank environment, the max-over-ranks timing and the whole-job value (the
+config-5 replica lines; configs 1/2 at N > 1 run the one-model data-parallel
+runner, DESIGN.md section 6, whose protocol tests/test_dp_protocol.py covers)."""
 import os
 import socket
 import sys
