@@ -611,7 +611,9 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
   int* const tch_cp = opaque_ptr(a.E.touched[cp]);
   int* const pend_cp = opaque_ptr(a.E.pend[cp]);
   int* const own_cp = a.E.own[cp];
-  unsigned long long* const racc = opaque_ptr(a.R.acc[ra_cur]);
+  unsigned long long* const racc0 = opaque_ptr(a.R.acc[ra_cur]);
+  const size_t rrep = (size_t)a.R.rows * a.R.rw;   // words per relation replica
+  const int rmask = a.R.reps - 1;                  // reps: a power of two (k_rel_fold)
   unsigned long long* const esum = opaque_ptr(a.E.sum[cp]);
   // the batch's records through buffer descriptors built once (not pointers
   // re-loaded from the kernarg segment on the wave's first dependent chain)
@@ -621,6 +623,9 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
       const_cast<int*>(a.rec_n1 + a.start), 0, a.count * 4, 0x00020000);
   int nv = 0;
   for (int w = blk_b * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
+    // large batches: positive w adds its relation sums into replica w % reps
+    // (k_rel_fold folds them after the launch), spreading the hot rows' atomics
+    unsigned long long* const racc = racc0 + (size_t)(w & rmask) * rrep;
     unsigned long long tt[4];
     if (a.trace) tt[0] = now_10ns();
     const u32x4 rx = __builtin_amdgcn_raw_buffer_load_b128(rec_rs, w * 16, 0, 0);
@@ -1857,6 +1862,28 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
 
 __global__ void k_pipe_advance(uint64_t* ek) { *ek += 1; }
 
+// Large TransE batches (RelTab::reps > 1): after batch launch g, fold the
+// relation accumulator copy g % 3's replicas 1..reps-1 into replica 0 (the
+// only one rel_row / rel_publish read) and zero them.  Packed integer sums
+// add exactly in any order, so the result is bitwise the single-copy one.
+// At nb = 2 on WN18 the ~25k violating positives of a batch add 1.6 KB each
+// into 18 rows; one copy serialised those atomics on ~2k addresses
+// (timing-only ablation without them: 0.370 -> 0.300 ms per epoch).
+__global__ __launch_bounds__(256) void k_rel_fold(PipeArgs a) {
+  const int g = launch_id(a);
+  unsigned long long* acc = a.R.acc[g % 3];
+  const size_t rrep = (size_t)a.R.rows * a.R.rw;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < rrep;
+       i += (size_t)gridDim.x * blockDim.x) {
+    unsigned long long s = acc[i];
+    for (int k = 1; k < a.R.reps; ++k) {
+      s += acc[k * rrep + i];
+      acc[k * rrep + i] = 0ull;
+    }
+    acc[i] = s;
+  }
+}
+
 // draw every negative of the epoch: one thread per positive, the same draws and
 // first-accepted-try rule as k_transe_sample_grad (skge/sample.py:41-46)
 __global__ void k_epoch_sample(const int* __restrict__ trip, long long T, int half, uint64_t seed,
@@ -1929,6 +1956,7 @@ struct skge_pipe_runner {
   bool owner = false;              // SKGE_PIPE_OWNER: rows updated by their batch's last reference
   bool hole = false;               // HolE pairwise (k_hole_pipe, fp32 sums)
   bool fft = false;                // HolE: correlations in the frequency domain (skge_hole_fft.h)
+  bool rfold = false;              // TransE: relation sums in replicas, k_rel_fold after each batch
   size_t lds = 0;                  // HolE: dynamic LDS per workgroup
   int nlaunch() const { return (int)batch.size() + 2; }
 };
@@ -2021,6 +2049,11 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
     else if (r->kq <= 2) SKGE_PB(2);
     else SKGE_PB(4);
 #undef SKGE_PB
+    if (r->rfold && a.count > 0) {
+      const size_t words = (size_t)a.R.rows * a.R.rw;
+      hipLaunchKernelGGL(k_rel_fold, dim3((unsigned)std::min<size_t>((words + 255) / 256, 4096)),
+                         dim3(256), 0, st, a);
+    }
     if (ev) (void)hipEventRecord(ev[i + 1], st);
   }
   hipLaunchKernelGGL(k_pipe_advance, dim3(1), dim3(1), 0, st, r->epoch_key);
@@ -2152,6 +2185,18 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     if (hole)
       while (q.reps < 32 && (long long)q.reps * 2048 < bs) q.reps *= 2;
     if (hole && getenv("SKGE_HPIPE_RREPS")) q.reps = std::max(1, atoi(getenv("SKGE_HPIPE_RREPS")));
+    // TransE, large batches (the A role's owner-mark regime): the same spread,
+    // one replica per ~256 expected adds into a row (bs / M), <= 16, folded by
+    // k_rel_fold after every batch launch (WN18 nb = 2: 16; nb = 100: 1)
+    if (!hole && !lazy && !r->owner && 4 * bs > 4 * 4096) {
+      const long long per_row = bs / std::max(1, M);
+      while (q.reps < 16 && (long long)q.reps * 256 < per_row) q.reps *= 2;
+    }
+    if (!hole && !lazy && !r->owner && getenv("SKGE_PIPE_RREPS")) {   // A/B switch (power of 2)
+      q.reps = 1;
+      while (2 * q.reps <= std::min(64, atoi(getenv("SKGE_PIPE_RREPS")))) q.reps *= 2;
+    }
+    r->rfold = !hole && q.reps > 1;
     r->w32 = rel->acc_mode == SKGE_ACC_I32X2;
     // 8-B words per relation row: sums + count, whole 128-B lines (HolE: d
     // floats, then the count as an int)

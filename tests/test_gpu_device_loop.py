@@ -222,6 +222,7 @@ def _runner_result(n_ent, n_rel, T, d, nb, pipelined, epochs=2, seed=11, trip=No
     (1000, 5, 4000, 1024, 8),     # widest packed row
     (40943, 18, 141442, 200, 100),  # WN18 geometry
     (20000, 11, 40000, 64, 2),    # large batch: the apply waves loop over their slots
+    (40943, 18, 141442, 200, 2),  # WN18 at nb = 2: relation sums in 16 replicas (k_rel_fold)
 ])
 def test_pipelined_runner_bitwise_equals_two_launch(n_ent, n_rel, T, d, nb, monkeypatch):
     """The pipelined runner (one launch per batch, cross-workgroup hand-off of

@@ -9,6 +9,7 @@
 #   stats[:<bench.py args>]               rocprofv3 --kernel-trace --stats of a bench command
 #   pmc[:<bench.py args>]                 kernel-trace stats, then FETCH_SIZE and WRITE_SIZE passes
 #                                         (separate runs) + tools/pmc_summary.py
+#   tool:<script>[,<args>]                python tools/<script> (or bash for .sh) under a time limit
 # Arguments after ':' use ',' for spaces (e.g. bench:--config,3,--steps,5).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -58,6 +59,13 @@ for st in ${STEPS:-tests smoke bench}; do
       run ${TAG}_pmcw$n 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv \
         -d $D/write -o run -- python3 bench.py ${arg:---steps 20 --warmup 3 --no-cpu} || exit $?
       python3 tools/pmc_summary.py $D > $D/pmc.json && echo "pmc summary: $D/pmc.json" ;;
+    tool)   # tool:<script under tools/>,<args>  (python scripts and .sh drivers)
+      set -- $arg
+      scr=$1; shift
+      case $scr in
+        *.sh) run ${TAG}_tool$n ${TTOOL:-600} bash tools/$scr "$@" || exit $? ;;
+        *) run ${TAG}_tool$n ${TTOOL:-600} python -u tools/$scr "$@" || exit $? ;;
+      esac ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
