@@ -745,8 +745,6 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
   const int row = wave * 16 + (l & 15), kq = l >> 4;
-  const bool rlive = 16 * wave < cnt;                 // wave-uniform
-  const int ncq = min(4, (d - c0 + 15) >> 4);        // live 16-column groups
   load_step(0);
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
@@ -758,43 +756,25 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
 #else
     // B[k4 + kq][16 q + c]: product 0 at sB[(16 q + c)(KS + 4) + k4 + kq]
     // (banks 36 c + kq: distinct), product 1 at sB[(k4 + kq)(GC + 4) + 16 q + c]
-    // Only live blocks are contracted: a wave whose 16 triples are past the
-    // tile's count, 16-column groups past d and the k past d of the last step
-    // hold staged zeros (their MFMAs would add exact zeros), so they are
-    // skipped -- at d = 200 the 4 x 64 columns and 7 x 32 k of the grid
-    // shrink to 13 x 16 and 50 x 4.
-    if (rlive) {
-      const int kend = min(KS, d - ks * KS);
-      if (prod == 0) {
-        const float* b0 = &sB[buf][(l & 15) * (KS + 4) + kq];
-        auto mm0 = [&](int ke, int nqv) {
+    if (prod == 0) {
+      const float* b0 = &sB[buf][(l & 15) * (KS + 4) + kq];
 #pragma unroll
-          for (int k4 = 0; k4 < ke; k4 += 4) {
-            const float a = sA[buf][row][k4 + kq];
+      for (int k4 = 0; k4 < KS; k4 += 4) {
+        const float a = sA[buf][row][k4 + kq];
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (q < nqv)
-                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b0[q * 16 * (KS + 4) + k4],
-                                                              acc[q], 0, 0, 0);
-          }
-        };
-        if (kend == KS && ncq == 4) mm0(KS, 4);
-        else mm0(kend, ncq);
-      } else {
-        const float* b1 = &sB[buf][kq * (GC + 4) + (l & 15)];
-        auto mm1 = [&](int ke, int nqv) {
+        for (int q = 0; q < 4; ++q)
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b0[q * 16 * (KS + 4) + k4], acc[q], 0,
+                                                        0, 0);
+      }
+    } else {
+      const float* b1 = &sB[buf][kq * (GC + 4) + (l & 15)];
 #pragma unroll
-          for (int k4 = 0; k4 < ke; k4 += 4) {
-            const float a = sA[buf][row][k4 + kq];
+      for (int k4 = 0; k4 < KS; k4 += 4) {
+        const float a = sA[buf][row][k4 + kq];
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (q < nqv)
-                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b1[k4 * (GC + 4) + q * 16],
-                                                              acc[q], 0, 0, 0);
-          }
-        };
-        if (kend == KS && ncq == 4) mm1(KS, 4);
-        else mm1(kend, ncq);
+        for (int q = 0; q < 4; ++q)
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b1[k4 * (GC + 4) + q * 16], acc[q], 0,
+                                                        0, 0);
       }
     }
 #endif
@@ -1097,28 +1077,6 @@ constexpr int WG_FPT = WG_T / WG_TPI;     // row floats per thread and operand
 #endif
 constexpr int WG_PF = SKGE_RS_WG_PF;      // chunks of items loaded together
 
-// one staged chunk of a dW tile: acc[j] += A^T B over the chunk's mm items
-// for wave `wave`'s 16 rows and the tile's ncj live 16-column groups (groups
-// past d hold staged zeros: their MFMAs would add exact zeros, so the edge
-// tiles of d = 200 contract 13 x 13 blocks of 16 instead of 16 x 16)
-__device__ __forceinline__ void wg_contract(const float (*sEs)[WG_T + 4],
-                                            const float (*sEo)[WG_T + 4], int mm, int ncj,
-                                            int wave, int l, f32x4 (&acc)[4]) {
-  auto run = [&](int nj) {
-    for (int k0 = 0; k0 < mm; k0 += 4) {
-      const int ik = k0 + (l >> 4);
-      const float av_ = sEs[ik][16 * wave + (l & 15)];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (j < nj)
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av_, sEo[ik][16 * j + (l & 15)], acc[j],
-                                                        0, 0, 0);
-    }
-  };
-  if (ncj == 4) run(4);
-  else run(ncj);
-}
-
 template <bool APPLY, bool VEC>
 __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restrict__ E, int d,
                                                            RescalWs ws, Accum accW, WApply wa) {
@@ -1142,8 +1100,6 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
   __shared__ float sEs[2][WG_CH][WG_T + 4];
   __shared__ float sEo[2][WG_CH][WG_T + 4];
   const int r0 = rt * WG_T, c0 = ct * WG_T;
-  const bool wlive = r0 + 16 * wave < d;              // wave-uniform
-  const int ncj = min(4, (d - c0 + 15) >> 4);        // live 16-column groups
   f32x4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -1232,7 +1188,14 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
 #ifdef SKGE_ABL_WG_NOMFMA   // timing-only ablation (tools/ablate.sh): no contraction
       if (mm < 0)
 #endif
-      if (wlive) wg_contract(sEs[buf], sEo[buf], mm, ncj, wave, l, acc);
+      for (int k0 = 0; k0 < mm; k0 += 4) {
+        const int ik = k0 + (l >> 4);
+        const float av_ = sEs[buf][ik][16 * wave + (l & 15)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av_, sEo[buf][ik][16 * j + (l & 15)],
+                                                        acc[j], 0, 0, 0);
+      }
     }
   }
   // D[row 4g + reg][col] of accumulator j (os / in above: out-of-range
@@ -1304,8 +1267,6 @@ __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__
   const int cnt = COMB ? ws.n01[p] : cntb;
   const int nch = (cnt + WG_CH - 1) / WG_CH, ngr = (nch + WG_PF - 1) / WG_PF;
   const int r0 = rt * WG_T, c0 = ct * WG_T;
-  const bool wlive = r0 + 16 * wave < d;              // wave-uniform
-  const int ncj = min(4, (d - c0 + 15) >> 4);        // live 16-column groups
   // IF: the W updater's operands, element e = 4 j + reg of the tile: row r0 +
   // 16 wave + 4 (l >> 4) + reg, column c0 + 16 j + (l & 15) (as
   // k_rescal_wgrad_mfma); loaded after the contraction (held across it they
@@ -1411,7 +1372,14 @@ __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__
       }
       __syncthreads();
       const int mm = min(WG_CH, cnt - b * WG_CH);
-      if (wlive) wg_contract(sEs, sEo, mm, ncj, wave, l, acc);
+      for (int k0 = 0; k0 < mm; k0 += 4) {
+        const int ik = k0 + (l >> 4);
+        const float av_ = sEs[ik][16 * wave + (l & 15)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av_, sEo[ik][16 * j + (l & 15)], acc[j], 0,
+                                                        0, 0);
+      }
     }
   }
   if (IF) {   // the W updater's step (skge/param.py:115-155) into the other buffer
