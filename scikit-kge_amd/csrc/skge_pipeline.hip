@@ -286,7 +286,10 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
 // one round trip, every claimed row updated and stored write-through, ONE
 // drain, then the done words -- instead of a claim / load / store / drain
 // chain per row.
-constexpr int GRP_ROWS = 8;
+#ifndef SKGE_PIPE_GRP_ROWS
+#define SKGE_PIPE_GRP_ROWS 8
+#endif
+constexpr int GRP_ROWS = SKGE_PIPE_GRP_ROWS;
 template <int KQ, bool E8>
 __device__ __forceinline__ void claim_and_apply_rows(const PipeTab& t, int pp, int rl, int n,
                                                      int d, int gp) {
@@ -647,8 +650,16 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
     load_row4<KQ>(a.E.P, o, d, eo);
     load_row4<KQ>(a.E.P, n0r, d, fs);
     load_row4<KQ>(a.E.P, n1r, d, fo);
-    int mark = 0;
-    if (l < 4) mark = a.E.pend[pp][sel4(l, s, o, n0r, n1r)];
+    // pending marks and the rows' done words in the same round trip: a pending
+    // row whose update is already published needs only the re-read below (at
+    // nb = 2 every row is pending; one done check per row in sequence had cost
+    // ~1.9 us per wave)
+    int mark = 0, dn = 0;
+    if (l < 4) {
+      const int rr = sel4(l, s, o, n0r, n1r);
+      mark = a.E.pend[pp][rr];
+      dn = __hip_atomic_load(a.E.done + rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     {
       float4 ra[KQ];
       int c;
@@ -659,12 +670,13 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
 #else
     const uint64_t pend = __ballot(mark == gp) & 0xfull;
 #endif
+    const uint64_t unpub = pend & ~__ballot(dn == gp);   // pending and not yet published
     if (a.trace) tt[1] = now_10ns();
     if (pend) {   // some entity rows have an update of batch b-1 outstanding
       // one (not unrolled) copy of the claim/apply/wait code keeps registers low
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) {
-        if (!((pend >> k) & 1ull)) continue;
+        if (!((unpub >> k) & 1ull)) continue;
         ensure_applied<KQ, E8>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err);
       }
       if (pend & 1ull) load_row4_sc1<KQ>(a.E.P, s, d, es);
