@@ -287,7 +287,7 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
 // drain, then the done words -- instead of a claim / load / store / drain
 // chain per row.
 #ifndef SKGE_PIPE_GRP_ROWS
-#define SKGE_PIPE_GRP_ROWS 8
+#define SKGE_PIPE_GRP_ROWS 4   // WN18 nb = 2, same box: 8 rows 467 M, 4 rows 482-488 M (124 -> 85 VGPRs)
 #endif
 constexpr int GRP_ROWS = SKGE_PIPE_GRP_ROWS;
 template <int KQ, bool E8>
