@@ -174,6 +174,60 @@ __device__ __forceinline__ float2* fft_run(float2* b0, float2* b1, int M, int nt
   return x;
 }
 
+// The same stages for a compile-time transform length M and signal count NT
+// (round 3; the device loops' d = 200 -> M = 100): the butterfly indices come
+// from divisions by constants and every pass of a stage is unrolled (no loop
+// control, no float-reciprocal index arithmetic).  Same arithmetic in the same
+// order as fft_stage, so the same bits.
+template <int R, bool INV, int M, int NT, int P>
+__device__ __forceinline__ void fft_stage_c(const float2* x, float2* y, const float2* tw) {
+  constexpr int T = M / R, n = NT * T, stw = 2 * M / (P * R), NP = (n + 63) / 64;
+  int l = lane_id();
+  // opaque: the lane-constant index arithmetic stays here instead of being
+  // hoisted out of the caller's loop into ~40 long-lived registers
+  asm volatile("" : "+v"(l));
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int b = l + 64 * j;
+    if (64 * (j + 1) <= n || b < n) {
+      const int tr = b / T, i = b - tr * T;
+      const int ip = i / P, k = i - ip * P;
+      const float2* xs = x + tr * M + i;
+      float2 u[R], v[R];
+#pragma unroll
+      for (int q = 0; q < R; ++q) u[q] = xs[q * T];
+      if (P > 1) {
+#pragma unroll
+        for (int q = 1; q < R; ++q) {
+          float2 w = tw[q * k * stw];
+          if (INV) w.y = -w.y;
+          u[q] = cmul(u[q], w);
+        }
+      }
+      fft_dft<R, INV>(u, v);
+      float2* ys = y + tr * M + ip * P * R + k;
+#pragma unroll
+      for (int t = 0; t < R; ++t) ys[t * P] = v[t];
+    }
+  }
+}
+
+// fft_run for a compile-time M and NT (the radix order of fft_run: 4s, a 2,
+// 3s, 5s)
+template <int M, int NT, bool INV, int P = 1, int MR = M>
+__device__ __forceinline__ float2* fft_run_c(float2* x, float2* y, const float2* tw) {
+  if constexpr (MR == 1) {
+    __builtin_amdgcn_wave_barrier();
+    return x;
+  } else {
+    constexpr int R = MR % 4 == 0 ? 4 : (MR % 2 == 0 ? 2 : (MR % 3 == 0 ? 3 : 5));
+    static_assert(MR % R == 0, "the transform length must factor into 2, 3 and 5");
+    __builtin_amdgcn_wave_barrier();
+    fft_stage_c<R, INV, M, NT, P>(x, y, tw);
+    return fft_run_c<M, NT, INV, P * R, MR / R>(y, x, tw);
+  }
+}
+
 // quad-layout real row -> complex signal t of buffer b (z[2l], z[2l+1])
 __device__ __forceinline__ void fft_put_row(float2* b, int M, int t, const float4& v, int d) {
   const int l = lane_id();
@@ -249,7 +303,8 @@ __device__ __forceinline__ HoleSpec hole_fft_forward(float* wbuf, const float2* 
   fft_put_row(b0, M, 2, fs, d);
   fft_put_row(b0, M, 3, eo, d);
   fft_put_row(b0, M, 4, fo, d);
-  const float2* Z = fft_run<false>(b0, b1, M, 5, tw, d);
+  const float2* Z = M == 100 ? fft_run_c<100, 5, false>(b0, b1, tw)
+                             : fft_run<false>(b0, b1, M, 5, tw, d);
   HoleSpec h;
   h.k = lane_id();
   h.on = h.k <= M / 2;
@@ -309,7 +364,14 @@ __device__ __forceinline__ const float* hole_fft_rows(float* wbuf, const float2*
     if (v0) fft_real_inv_pair(b0 + (t++) * M, M, k, tw, H[3][0], H[3][1]);
     if (v1) fft_real_inv_pair(b0 + t * M, M, k, tw, H[4][0], H[4][1]);
   }
-  return reinterpret_cast<const float*>(fft_run<true>(b0, b1, M, nt, tw, d));
+  float2* z;
+  if (M == 100 && nt == 5)
+    z = fft_run_c<100, 5, true>(b0, b1, tw);
+  else if (M == 100 && nt == 4)
+    z = fft_run_c<100, 4, true>(b0, b1, tw);
+  else
+    z = fft_run<true>(b0, b1, M, nt, tw, d);
+  return reinterpret_cast<const float*>(z);
 }
 
 // row t of hole_fft_rows' output, scaled by 1/M, added into accumulator row
