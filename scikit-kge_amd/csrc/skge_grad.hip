@@ -574,7 +574,8 @@ __device__ __forceinline__ bool hole_pair_fft(const PairArgs& a, int i, float* w
   fft_put_row(b0, M, 3, rn[0], d);
   fft_put_row(b0, M, 4, fs[0], d);
   fft_put_row(b0, M, 5, fo[0], d);
-  const float2* Z = fft_run<false>(b0, b1, M, 6, tw, d);
+  const float2* Z = M == 100 ? fft_run_c<100, 6, false>(b0, b1, tw)
+                             : fft_run<false>(b0, b1, M, 6, tw, d);
   const int k = l;
   const bool on_ = k <= M / 2;
   float2 X[6][2];
@@ -611,7 +612,8 @@ __device__ __forceinline__ bool hole_pair_fft(const PairArgs& a, int i, float* w
 #pragma unroll
     for (int t = 0; t < 6; ++t) fft_real_inv_pair(b0 + t * M, M, k, tw, X[t][0], X[t][1]);
   }
-  const float* z = reinterpret_cast<const float*>(fft_run<true>(b0, b1, M, 6, tw, d));
+  const float* z = reinterpret_cast<const float*>(
+      M == 100 ? fft_run_c<100, 6, true>(b0, b1, tw) : fft_run<true>(b0, b1, M, 6, tw, d));
   const float sc = 2.0f / (float)d;   // 1/M
   float x[KM], y[KM];
   auto rows = [&](int t0) {
@@ -1001,7 +1003,8 @@ __global__ __launch_bounds__(256) void k_hole_triple_fft(PairArgs a) {
     fft_put_row(b0, M, 0, rp[0], d);
     fft_put_row(b0, M, 1, es[0], d);
     fft_put_row(b0, M, 2, eo[0], d);
-    const float2* Z = fft_run<false>(b0, b1, M, 3, tw, d);
+    const float2* Z = M == 100 ? fft_run_c<100, 3, false>(b0, b1, tw)
+                               : fft_run<false>(b0, b1, M, 3, tw, d);
     const int k = l;
     const bool on = k <= M / 2;
     float2 X[3][2];
@@ -1027,7 +1030,8 @@ __global__ __launch_bounds__(256) void k_hole_triple_fft(PairArgs a) {
 #pragma unroll
       for (int t = 0; t < 3; ++t) fft_real_inv_pair(b0 + t * M, M, k, tw, X[t][0], X[t][1]);
     }
-    const float* z = reinterpret_cast<const float*>(fft_run<true>(b0, b1, M, 3, tw, d));
+    const float* z = reinterpret_cast<const float*>(
+        M == 100 ? fft_run_c<100, 3, true>(b0, b1, tw) : fft_run<true>(b0, b1, M, 3, tw, d));
     const float sc = 2.0f / (float)d;   // 1/M
     float x[KM], yv[KM];
 #pragma unroll
