@@ -141,10 +141,20 @@ class EpochRunner(object):
         bs = kg.T // nbatches
         self.nbatches = nbatches
         self._auto = pipelined is None
+        # d % 4 != 0 (e.g. the reference's d = 50): the packed / pipelined
+        # runners work on quads, so they run on zero-padded copies of the
+        # tables (width rounded up to 4), copied in and out around every run().
+        # A zero column stays zero (TransE-L1: sign(0) = 0 contributions, AdaGrad
+        # and the projection leave 0 at 0) and adds nothing to a score or norm,
+        # so the padded step is the d-wide step.
+        self.d_pad = (model.d + 3) // 4 * 4
+        self._pad = (bool(model.l1) and model.d % 4 != 0 and not force_f32 and replicas <= 1
+                     and pipelined is not False and packed is not False
+                     and _os.environ.get("SKGE_PIPE_PAD", "1") != "0")
         # TransE-L1 sign contributions are small integers: exact packed int16x4
         # sums while every row's per-batch count stays <= 32767 (the applies
         # flag a larger count, checked by synchronize())
-        can_pack = bool(model.l1) and model.d % 4 == 0 and not force_f32
+        can_pack = bool(model.l1) and (model.d % 4 == 0 or self._pad) and not force_f32
         self.count_bound = packed_count_bound(kg, model.E.rows, bs) if can_pack else 0
         auto_packed = packed is None
         if packed is None:
@@ -180,11 +190,13 @@ class EpochRunner(object):
             # the atomic bytes again; the apply checks every count)
             e8 = (not want_lazy and packed_count_bound(kg, model.E.rows, bs, _tail8) <= 127 and
                   _os.environ.get("SKGE_PIPE_E8", "1") != "0")
-            self._tables(model, updaters, packed, 1, rel_w32=rel_reps != 1, ent_i8=e8)
+            self._tables(model, updaters, packed, 1, rel_w32=rel_reps != 1, ent_i8=e8,
+                         pad=self._pad)
             self.ent_i8 = e8
             self.lazy = want_lazy
             h = lib.skge_pipe_runner_create_ex(
-                L.stream_ptr(self.stream), self.te, self.tr, model.d, L.ptr(kg.trip), kg.T,
+                L.stream_ptr(self.stream), self.te, self.tr,
+                self.d_pad if self._pad else model.d, L.ptr(kg.trip), kg.T,
                 L.ptr(kg.slots), kg.capacity, int(nbatches), int(seed) & (2 ** 64 - 1),
                 L.ptr(self.epoch_key), float(model.margin), int(ntries), L.ptr(self.nviol_total),
                 L.SKGE_PIPE_LAZY if self.lazy else 0)
@@ -201,6 +213,10 @@ class EpochRunner(object):
             torch.cuda.empty_cache()
         self.pipelined = False
         self.lazy = False
+        if self._pad:   # the two-launch runner takes any d: no padded copies
+            self._pad = False
+            packed = packed and model.d % 4 == 0
+            rel_reps = relation_replicas(kg, model.R.rows, bs) if packed else 1
         if packed and rel_reps == 0:
             if not auto_packed:
                 raise ValueError("packed sums: a relation's per-batch count exceeds what 32 "
@@ -217,12 +233,30 @@ class EpochRunner(object):
         self.handle = h
         self.nlaunches = lib.skge_runner_nlaunches(h)
 
-    def _tables(self, model, updaters, packed, rel_replicas, rel_w32=False, ent_i8=False):
-        """The runner's own accumulators (captured by its graph) and tables."""
-        from .param import Accumulator
+    def _tables(self, model, updaters, packed, rel_replicas, rel_w32=False, ent_i8=False,
+                pad=False):
+        """The runner's own accumulators (captured by its graph) and tables
+        (pad: over zero-padded copies of the parameters and AdaGrad states)."""
+        from .param import Accumulator, table_struct, post_code
         from .base import deterministic
         dev = model.device
         E, R = model.params["E"], model.params["R"]
+        if pad:
+            class _Padded(object):   # what table_struct reads of a Parameter
+                def __init__(self, rows, width):
+                    self.rows, self.width = rows, width
+                    self.data = torch.zeros((rows, width), dtype=torch.float32, device=dev)
+            self._padded = []
+            tabs = {}
+            for pid, P in (("E", E), ("R", R)):
+                u = updaters[pid]
+                pp = _Padded(P.rows, self.d_pad)
+                st = u.state()
+                sp = None if st is None else torch.zeros_like(pp.data)
+                self._padded.append((P, pp.data, st, sp))
+                tabs[pid] = (u, pp, sp)
+            E = tabs["E"][1]
+            R = tabs["R"][1]
         mode = L.SKGE_ACC_I16X4 if packed else L.SKGE_ACC_F32
         if not packed and deterministic():   # exact fixed-point sums, one copy
             mode, rel_replicas = L.SKGE_ACC_FX64, 1
@@ -236,13 +270,47 @@ class EpochRunner(object):
                                 dense=True, replicas=rel_replicas)
         self.rel_w32 = rel_w32
         self.packed = packed
+        if pad:
+            def tab(pid, acc):
+                u, pp, sp = tabs[pid]
+                return table_struct(pp, sp, acc, opt=u.opt, post=post_code(u.param.post),
+                                    lr=float(u.learning_rate))
+            self.te = tab("E", self.accE)
+            self.tr = tab("R", self.accR)
+            return
         self.te = updaters["E"].table(self.accE, counters=False)
         self.tr = updaters["R"].table(self.accR, counters=False)
+
+    def _pad_in(self):
+        """Padded tables: the model's parameters / states into the copies
+        (ordered after the caller's stream)."""
+        if not getattr(self, "_pad", False):
+            return
+        d = self.model.d
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            for P, Pp, st, sp in self._padded:
+                Pp[:, :d].copy_(P.data)
+                if st is not None:
+                    sp[:, :d].copy_(st)
+
+    def _pad_out(self):
+        if not getattr(self, "_pad", False):
+            return
+        d = self.model.d
+        with torch.cuda.stream(self.stream):
+            for P, Pp, st, sp in self._padded:
+                P.data.copy_(Pp[:, :d])
+                if st is not None:
+                    st.copy_(sp[:, :d])
+        torch.cuda.current_stream().wait_stream(self.stream)
 
     def run(self, nepochs=1):
         lib = L.lib()
         fn = lib.skge_pipe_runner_run if self.pipelined else lib.skge_runner_run
+        self._pad_in()
         L.check(fn(self.handle, L.stream_ptr(self.stream), int(nepochs)), "runner run")
+        self._pad_out()
 
     def profile(self, trace_launch=None):
         """Pipelined runner only: one eager epoch with HIP events around every
@@ -258,10 +326,12 @@ class EpochRunner(object):
         stats = np.zeros((n, 3), dtype=np.int32)
         tr = np.zeros(2 + 6 * self.kg.T + 8 * self.kg.T + 64, dtype=np.uint64) \
             if trace_launch else None
+        self._pad_in()
         L.check(L.lib().skge_pipe_runner_profile(
             self.handle, L.stream_ptr(self.stream), us.ctypes.data, stats.ctypes.data, n,
             int(trace_launch or 0), None if tr is None else tr.ctypes.data,
             0 if tr is None else len(tr)), "runner profile")
+        self._pad_out()
         if trace_launch:
             return us, stats, tr
         return us, stats
