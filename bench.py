@@ -279,18 +279,20 @@ def main():
         # dependencies, and the streaming random-row gather rate of the table
         geo = prof["geometry"]
         npos = int(round(geo["positives"]))
-        m_us, m_b, m_gbs = measured_roofline(dev, N_ENT, d, npos, 5,
+        # d % 4 != 0: the runner moves its zero-padded rows (quad layout)
+        dr = runner.d_pad if getattr(runner, "_pad", False) else d
+        m_us, m_b, m_gbs = measured_roofline(dev, N_ENT, dr, npos, 5,
                                              int(round(geo["atomic_rows"] / max(npos, 1))),
                                              int(round(geo["applied_rows"])))
-        s_us, s_b, s_gbs = measured_roofline(dev, N_ENT, d, 262144, 5, 0, 0, launches=10, reps=3)
-        h_us, h_b, h_gbs = measured_roofline(dev, 5_000_000, d, 262144, 5, 0, 0, launches=10,
+        s_us, s_b, s_gbs = measured_roofline(dev, N_ENT, dr, 262144, 5, 0, 0, launches=10, reps=3)
+        h_us, h_b, h_gbs = measured_roofline(dev, 5_000_000, dr, 262144, 5, 0, 0, launches=10,
                                              reps=3)
         sg = s_gbs
         meas = {"kernel": "k_roofline (skge_roofline_gather)",
                 "frac_of_streaming_gather": round(prof["dominant"]["achieved_gbs"] / sg, 4),
                 "geometry": "per launch: %d waves x 5 random %d-B row gathers + %d atomic rows "
                             "each, %d rows read+written (20d B), WN18 table"
-                            % (npos, 4 * d, int(round(geo["atomic_rows"] / max(npos, 1))),
+                            % (npos, 4 * dr, int(round(geo["atomic_rows"] / max(npos, 1))),
                                int(round(geo["applied_rows"]))),
                 "avg_launch_us": round(m_us, 3), "bytes_per_launch": round(m_b),
                 "GB_s": round(m_gbs, 1),
