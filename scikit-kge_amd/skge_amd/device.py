@@ -326,12 +326,12 @@ class EpochRunner(object):
         stats = np.zeros((n, 3), dtype=np.int32)
         tr = np.zeros(2 + 6 * self.kg.T + 8 * self.kg.T + 64, dtype=np.uint64) \
             if trace_launch else None
-        self._pad_in()
+        EpochRunner._pad_in(self)   # (also HolePipeRunner.profile: no padded tables there)
         L.check(L.lib().skge_pipe_runner_profile(
             self.handle, L.stream_ptr(self.stream), us.ctypes.data, stats.ctypes.data, n,
             int(trace_launch or 0), None if tr is None else tr.ctypes.data,
             0 if tr is None else len(tr)), "runner profile")
-        self._pad_out()
+        EpochRunner._pad_out(self)
         if trace_launch:
             return us, stats, tr
         return us, stats
