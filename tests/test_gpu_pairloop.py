@@ -329,6 +329,32 @@ def test_hole_pipelined_runner_relation_replicas_forced(monkeypatch):
         np.testing.assert_allclose(b[2][pid], a[2][pid], rtol=RTOL, atol=ATOL, err_msg=pid)
 
 
+def test_hole_pipelined_runner_profile_trains_like_run():
+    """HolePipeRunner.profile() (the bench's per-launch timing: one eager
+    epoch with events) trains exactly like run(1) on a twin model and returns
+    one duration per launch."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, HolePipeRunner
+    xs = make_kg(300, 7, 2000, seed=3)
+    outs = []
+    for prof in (False, True):
+        m = make_model("hole", (300, 300, 7), 32)
+        m.add_hyperparam("margin", 0.2)
+        upd = {pid: S.SGD(p, 0.1) for pid, p in m.params.items()}
+        r = HolePipeRunner(m, upd, DeviceKG(xs, m.device), 7, seed=9)
+        if prof:
+            us, stats = r.profile()
+            assert len(us) == r.nlaunches and (us > 0).all()
+        else:
+            r.run(1)
+        r.synchronize()
+        outs.append((int(r.nviol_total.item()),
+                     {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}))
+    assert outs[0][0] > 0 and abs(outs[0][0] - outs[1][0]) <= 2   # float atomics: a tie or two
+    for pid in outs[0][1]:
+        np.testing.assert_allclose(outs[1][1][pid], outs[0][1][pid], rtol=RTOL, atol=ATOL)
+
+
 def test_rescal_split_k_dw_matches_fused(monkeypatch):
     """RESCAL dW split over K (batches with >= 4 groups of 128 items per
     relation: partial tiles summed in split order by a finishing kernel)
