@@ -84,6 +84,7 @@ struct RelTab {                // relation table
   unsigned long long* acc[3];  // [rows][rw]: int16x4 sums in words [0, d/4), count in word d/4
                                // (w32: int32x2 sums in words [0, d/2), count in word d/2)
   int rows, rw;
+  int folded;                  // replicas folded into replica 0 after each batch (k_rel_fold*)
   int reps;                    // HolE: accumulator replicas per copy (row p of replica k at
                                // k * rows + p); positive w adds into replica w % reps
   UpdParams u;
@@ -1630,7 +1631,8 @@ __device__ __forceinline__ void rel_row_f(const RelTab& t, int row, int d, int r
   load_f32_row<KQ>(t.P[rd] + (size_t)row * d, t.A[rd] ? t.A[rd] + (size_t)row * d : nullptr,
                    acc, 0, d, p, a, sm);
   c = __builtin_amdgcn_readfirstlane(__float_as_int(acc[d]));
-  for (int k = 1; k < t.reps; ++k) {   // large batches: the replicas, in a fixed order
+  const int nrep = t.folded ? 1 : t.reps;   // folded: replica 0 holds the sum
+  for (int k = 1; k < nrep; ++k) {   // large batches: the replicas, in a fixed order
     const float* ak = reinterpret_cast<const float*>(t.acc[ra] +
                                                      ((size_t)k * t.rows + row) * t.rw);
     const float4* ak4 = reinterpret_cast<const float4*>(ak);
@@ -1874,6 +1876,37 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
 
 __global__ void k_pipe_advance(uint64_t* ek) { *ek += 1; }
 
+// HolE, large batches: the fp32 form of k_rel_fold -- float e of row p summed
+// over the replicas in index order (the order rel_row_f's readers used, so the
+// same bits), the count word (float index d of the row) as an int; replicas
+// 1..reps-1 zeroed.  The readers then load replica 0 alone instead of every
+// replica (nb = 2: 16-32 replicas of 800 B per scoring wave).
+__global__ __launch_bounds__(256) void k_rel_fold_f(PipeArgs a) {
+  const int g = launch_id(a);
+  float* acc = reinterpret_cast<float*>(a.R.acc[g % 3]);
+  const int rstride = 2 * a.R.rw, d = a.d;
+  const size_t rrep = (size_t)a.R.rows * rstride;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < rrep;
+       i += (size_t)gridDim.x * blockDim.x) {
+    if ((int)(i % rstride) == d) {   // the count
+      int* ai = reinterpret_cast<int*>(acc);
+      int c = ai[i];
+      for (int k = 1; k < a.R.reps; ++k) {
+        c += ai[k * rrep + i];
+        ai[k * rrep + i] = 0;
+      }
+      ai[i] = c;
+    } else {
+      float v = acc[i];
+      for (int k = 1; k < a.R.reps; ++k) {
+        v += acc[k * rrep + i];
+        acc[k * rrep + i] = 0.0f;
+      }
+      acc[i] = v;
+    }
+  }
+}
+
 // Large TransE batches (RelTab::reps > 1): after batch launch g, fold the
 // relation accumulator copy g % 3's replicas 1..reps-1 into replica 0 (the
 // only one rel_row / rel_publish read) and zero them.  Packed integer sums
@@ -2063,8 +2096,12 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
 #undef SKGE_PB
     if (r->rfold && a.count > 0) {
       const size_t words = (size_t)a.R.rows * a.R.rw;
-      hipLaunchKernelGGL(k_rel_fold, dim3((unsigned)std::min<size_t>((words + 255) / 256, 4096)),
-                         dim3(256), 0, st, a);
+      if (r->hole)   // fp32 sums + an int count per row
+        hipLaunchKernelGGL(k_rel_fold_f, dim3((unsigned)std::min<size_t>((2 * words + 255) / 256, 4096)),
+                           dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL(k_rel_fold, dim3((unsigned)std::min<size_t>((words + 255) / 256, 4096)),
+                           dim3(256), 0, st, a);
     }
     if (ev) (void)hipEventRecord(ev[i + 1], st);
   }
@@ -2208,7 +2245,8 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
       q.reps = 1;
       while (2 * q.reps <= std::min(64, atoi(getenv("SKGE_PIPE_RREPS")))) q.reps *= 2;
     }
-    r->rfold = !hole && q.reps > 1;
+    r->rfold = q.reps > 1;
+    q.folded = r->rfold ? 1 : 0;
     r->w32 = rel->acc_mode == SKGE_ACC_I32X2;
     // 8-B words per relation row: sums + count, whole 128-B lines (HolE: d
     // floats, then the count as an int)
@@ -2318,7 +2356,9 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     if (!hole && !lazy && b < nb1 && getenv("SKGE_PIPE_ACAP"))   // A/B switch (TransE)
       a_cap = std::max(1, atoi(getenv("SKGE_PIPE_ACAP")));
     a.nA = std::max(1, std::min((a_items + WPB - 1) / WPB, std::min(a_cap, 16384)));
-    const int nBb = std::max(1, std::min((a.count + WPB - 1) / WPB, 16384));
+    int b_cap = 16384;
+    if (!hole && getenv("SKGE_PIPE_BCAP")) b_cap = std::max(1, atoi(getenv("SKGE_PIPE_BCAP")));   // A/B
+    const int nBb = std::max(1, std::min((a.count + WPB - 1) / WPB, b_cap));
     r->batch.push_back(a);
     r->grid.push_back(a.nA + (a.count > 0 ? nBb : 0));
     prev = a.count;
