@@ -350,7 +350,9 @@ def main():
         k = prof["dominant"]
         kname = {"transe_sample_grad": "sample_grad", "accum_apply": "k_apply",
                  "pipe_batch": "k_pipe_batch"}[k["name"]]
-        traffic, traffic_src = pmc_traffic(kname)
+        # config 1's own PMC pass (pmc_c1.json: d=50 padded to 52, SGD), not config 2's
+        traffic, traffic_src = pmc_traffic(kname, "pmc.json" if args.config == 2 else
+                                           "pmc_c%d.json" % args.config)
         line = {
             "metric": "triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X"
                       if args.config == 2 else
