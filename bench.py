@@ -10,11 +10,20 @@ mode 1 corrupts o), margin 2.0, lr 0.1 -- run by the native hipGraph epoch
 runner (device permutation, device sampler, fused score+scatter, fused
 mean+AdaGrad+normalize).  value = positive triples fully processed per second.
 
-Multi-GPU (configs 1/2): one process per GPU (torchrun), ONE model trained
-data parallel (skge_amd.dp: every rank scores a slice of each union batch, the
-records are all-gathered over RCCL, every rank applies the whole batch; the
-replicas stay bitwise equal to one GPU's run); value = that model's positive
-triples per second, max-over-ranks time.
+Multi-GPU: one process per GPU.  `--gpus N` without a torchrun environment
+starts the N ranks itself (torch.distributed.run as a child process, before
+anything touches a GPU); under torchrun it checks WORLD_SIZE == N.  Configs
+1-4 (WN18, 33 MB tables): N independent replicas by default -- the north star
+replicates the table and exchanges gradients only once |E| d outgrows one
+GPU's HBM, so there is no data-path collective (scaling "weak", value = all
+replicas' positives / the slowest rank's time).  The one-model data-parallel
+runner (skge_amd.dp: slice scoring, RCCL all-gather of records, replicated
+scatter + apply) is measured beside it in `detail.one_model_dp` (union batch
+1414: strong scaling; union batch N x 1414 with the one-GPU run at the same
+union batch), or as the line itself with `--mode dp`.  Config 5 `--shard`:
+the row-sharded table (RCCL all-to-all + reduce-scatter of contributions).
+`--dry-run`: the launcher, rendezvous and max-over-ranks bookkeeping on CPU
+(gloo), no GPU (tests/test_bench_dist.py).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--nb 100]
 """
@@ -74,6 +83,75 @@ def dist_env():
     """(world, rank, local_rank) from the torchrun environment (1, 0, 0 alone)."""
     return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
             int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def free_port():
+    import socket
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` outside torchrun: run this script as N ranks under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) in a
+    CHILD process -- this parent never touches a GPU (no exec from a process
+    that has) -- forward its output and return its exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def acc_label(acc):
+    """Encoding of an accumulator's sums."""
+    from skge_amd import _lib as L
+    return {L.SKGE_ACC_F32: "fp32", L.SKGE_ACC_I16X4: "int16x4 exact",
+            L.SKGE_ACC_I32X2: "int32x2 exact", L.SKGE_ACC_FX64: "fixed-point int64 exact",
+            L.SKGE_ACC_I8X4: "int8x4 exact"}[int(acc.mode)]
+
+
+def run_dry(args):
+    """--dry-run: the multi-rank bookkeeping without a GPU -- rendezvous over
+    gloo, barrier-bracketed timing of a NumPy stand-in step, max over ranks,
+    the whole-job value and ONE line from rank 0 (not a measurement)."""
+    import torch
+    import torch.distributed as dist
+    world, rank, _ = dist_env()
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    rs = np.random.RandomState(rank)
+    x = rs.rand(4096, 64)
+    for _ in range(args.warmup):
+        np.abs(x).sum()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        np.abs(x + 1.0).sum()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(elapsed, world)
+    ranks = [rank]
+    if world > 1:
+        out = [None] * world
+        dist.all_gather_object(out, rank)
+        ranks = out
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run (launcher bookkeeping, no GPU)", "dry_run": True,
+                          "value": replica_value(4096 * args.steps, world, elapsed),
+                          "unit": "rows/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
+                          "scaling": "weak", "detail": {"ranks": ranks}}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def max_over_ranks(x, world, device="cpu"):
@@ -178,10 +256,16 @@ def main():
                     help="skip the measured gather roofline (skge_roofline_gather)")
     ap.add_argument("--runner", default="auto", choices=["auto", "pairs", "hole_pipe"],
                     help="configs 3/4: device runner (auto: HolE pipelined where it applies)")
-    ap.add_argument("--dp-batch", choices=["per-gpu", "global"], default="per-gpu",
-                    help="configs 1/2 on N > 1 GPUs (one model, data parallel): 'per-gpu' keeps "
-                         "the reference's 1414 positives per GPU (union batch N x 1414, nb = "
-                         "nb / N); 'global' keeps the union batch at nb (1414 / N per GPU)")
+    ap.add_argument("--mode", choices=["replicas", "dp"], default="replicas",
+                    help="configs 1/2 on N > 1 GPUs: 'replicas' (default; N independent "
+                         "models, no exchange, one-model DP measured in detail) or 'dp' (the "
+                         "line is the one-model data-parallel runner)")
+    ap.add_argument("--dp-batch", choices=["per-gpu", "global"], default="global",
+                    help="--mode dp: 'global' (default) keeps the union batch at the reference's "
+                         "1414 (1414 / N per GPU: strong scaling); 'per-gpu' keeps 1414 per GPU "
+                         "(union batch N x 1414, nb = nb / N: a larger batch, weak scaling)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only: the multi-rank launcher and bookkeeping over gloo")
     ap.add_argument("--shard", action="store_true",
                     help="config 5 only: row-shard E and its AdaGrad state over the ranks "
                          "(skge_amd.shard; RCCL all-to-all row fetch + contribution "
@@ -196,13 +280,21 @@ def main():
             args.opt = "sgd"
     if args.opt is None:
         args.opt = "adagrad"
+    world = dist_env()[0]
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (launch N ranks with --gpus N)"
+                         % (args.gpus, world))
+    if args.dry_run:
+        return run_dry(args)
     if args.config == 5 and args.shard:
         return run_config5_sharded(args)
     if args.config == 5:
         return run_config5(args)
     if args.config in (3, 4):
         return run_config34(args)
-    if dist_env()[0] > 1:
+    if world > 1 and args.mode == "dp":
         return run_dp(args)
 
     import torch
@@ -260,6 +352,7 @@ def main():
     nviol = int(runner.nviol_total.item())
     positives = N_TRIPLES * args.steps
     value = replica_value(positives, world, elapsed)
+    rank_value = positives / (t1 - t0)      # this replica alone
 
     # ---- per-kernel timing (HIP events on the runner stream, eager launches of
     # one more epoch, outside the timed region) for the roofline.  The tables
@@ -345,6 +438,26 @@ def main():
                  "runner": "pipelined" if r2.pipelined else "two-launch"}
         del r2
 
+    pipelined, nlaunches = runner.pipelined, runner.nlaunches
+    acc_names = {"entity": acc_label(runner.accE), "relation": acc_label(runner.accR)}
+    launch_us_max = max_over_ranks(prof["dominant"]["avg_us"], world, dev)
+    one_model = None
+    if world > 1:
+        # the one-model data-parallel runner beside the replicas:
+        # union batch = the reference's 1414 (strong scaling), and 1414 per GPU
+        # (union batch N x 1414) with the one-GPU runner at that union batch
+        del runner
+        torch.cuda.synchronize()
+        g = measure_dp(args, dev, nb, args.warmup, args.steps)
+        nb_w = max(1, nb // world)
+        w = measure_dp(args, dev, nb_w, args.warmup, args.steps, profile=False)
+        same = one_gpu_value(args, dev, nb_w)
+        one_model = {"global_batch": dict(g, scaling="strong",
+                                          vs_one_gpu=round(g["value"] / rank_value, 4)),
+                     "per_gpu_batch": dict(w, scaling="weak (union batch grows with N)",
+                                           one_gpu_same_geometry=same,
+                                           vs_one_gpu_same_geometry=round(w["value"] /
+                                                                          same["value"], 4))}
     if rank == 0:
         cpu = None if args.no_cpu else cpu_baseline(trip, d, nb, args.cpu_seconds, opt=args.opt)
         k = prof["dominant"]
@@ -365,9 +478,9 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
             "higher_is_better": True,
-            # one model, one epoch per step at every N (N > 1: run_dp, the same
-            # model data parallel over the GPUs)
-            "scaling": "strong",
+            # one replica per GPU, one epoch of its own KG per step: per-GPU
+            # work fixed as N grows (the one-model DP runner: detail.one_model_dp)
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442 uniform, RandomState(0)); "
@@ -375,8 +488,13 @@ def main():
             "config": {"workload": "TransE-L1 d=%d PairwiseStochasticTrainer+%s, WN18 shape, "
                                    "nb=%d (B=%d), margin 2.0, lr 0.1, device RandomModeSampler(1,[0,1]); "
                                    "step = 1 epoch" % (d, {"sgd": "SGD", "adagrad": "AdaGrad"}[args.opt],
-                                                       nb, N_TRIPLES // nb),
-                       "global_batch": N_TRIPLES // nb, "parallelism": "dp%d" % world},
+                                                       nb, N_TRIPLES // nb) +
+                                   ("" if world == 1 else
+                                    "; %d independent replicas (one per GPU, each its own KG "
+                                    "and model; no exchange: the 33 MB table is replicated, "
+                                    "north_star)" % world),
+                       "global_batch": N_TRIPLES // nb,
+                       "parallelism": "replicas%d" % world if world > 1 else "1gpu"},
             "roofline": {"bound": "hbm", "kernel": k["name"],
                          "achieved": round(k["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 4),
@@ -390,6 +508,7 @@ def main():
                          "avg_launch_source": "timed-region HIP events (graph replays) minus "
                                               "the draw/advance launches, per batch launch",
                          "eager_avg_launch_us": round(k.get("eager_avg_us", k["avg_us"]), 3),
+                         "avg_launch_us_max_over_ranks": round(launch_us_max, 3),
                          "measured": meas},
             "cpu_baseline": cpu,
             "detail": {
@@ -404,10 +523,12 @@ def main():
                                 "GB_s": round(v["achieved_gbs"], 1)}
                             for n, v in prof["kernels"].items()},
                 "step_algorithmic_GB_s": round(prof["epoch_bytes"] / (elapsed / args.steps) / 1e9, 1),
-                "launches_per_step": runner.nlaunches,
-                "runner": "pipelined (1 launch/batch)" if runner.pipelined else "two-launch",
-                "accumulator": "int16x4 exact" if runner.packed else "fp32",
+                "launches_per_step": nlaunches,
+                "runner": "pipelined (1 launch/batch)" if pipelined else "two-launch",
+                "accumulator": acc_names,
+                "per_replica_value": round(rank_value, 1),
                 "large_batch": large,
+                "one_model_dp": one_model,
             },
         }
         print(json.dumps(line))
@@ -415,25 +536,24 @@ def main():
         dist.destroy_process_group()
 
 
-def run_dp(args):
-    """Configs 1/2 on N > 1 GPUs: ONE TransE-L1 model, data parallel
-    (skge_amd.dp.DataParallelRunner): every rank holds the
-    whole WN18 model, scores its slice of each union batch, the slices'
+def measure_dp(args, dev, nb, warmup, steps, profile=True):
+    """ONE TransE-L1 model trained data parallel over the ranks
+    (skge_amd.dp.DataParallelRunner; reference semantics
+    skge/base.py:1394-1427, 1306-1316): every rank holds the whole WN18 model,
+    scores its slice of each union batch (nb batches per epoch), the slices'
     records are all-gathered over RCCL and every rank scatters + applies the
     whole batch, so all replicas equal one GPU's run on the union batches bit
-    for bit.  value = the ONE model's positive triples per second (one epoch
-    of the KG per step, max over ranks)."""
+    for bit.  Timed epochs start from the initial tables; max over ranks.
+    profile: one more eager epoch with HIP events between the phases of every
+    union batch (score / all-gather / scatter / apply on the runner stream) and
+    the rows each batch applied, for the per-rank roofline."""
     import torch
     import torch.distributed as dist
-    world, rank, local = dist_env()
-    dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
     import skge_amd as S
     from skge_amd.device import DeviceKG
-    from skge_amd.dp import DataParallelRunner
+    from skge_amd.dp import DataParallelRunner, dp_step, slice_of
+    world = dist.get_world_size()
     d = args.d
-    nb = max(1, args.nb // world) if args.dp_batch == "per-gpu" else args.nb
     trip = make_wn18_kg(seed=0)              # ONE model: the same KG on every rank
     np.random.seed(42)
     model = S.TransE((N_ENT, N_ENT, N_REL), d, l1=True)
@@ -443,19 +563,23 @@ def run_dp(args):
     kg = DeviceKG(trip, dev)
     runner = DataParallelRunner(model, upd, kg, nb, seed=1234)
     init = {pid: p.data.clone() for pid, p in model.params.items()}
-    runner.run(max(args.warmup, 1))          # the first epoch also captures the graph
+
+    def rollback():
+        for pid, p in model.params.items():
+            p.data.copy_(init[pid])
+            upd[pid].reset()
+        runner.nviol_total.zero_()
+        torch.cuda.synchronize()
+
+    runner.run(max(warmup, 1))               # the first epoch also captures the graph
     runner.synchronize()
-    for pid, p in model.params.items():      # timed epochs start from the initial tables
-        p.data.copy_(init[pid])
-        upd[pid].reset()
-    runner.nviol_total.zero_()
-    torch.cuda.synchronize()
+    rollback()
     dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(runner.stream)
-    runner.run(args.steps)
+    runner.run(steps)
     ev1.record(runner.stream)
     runner.synchronize()
     torch.cuda.synchronize()
@@ -464,47 +588,169 @@ def run_dp(args):
     elapsed = max_over_ranks(elapsed, world, dev)
     gpu_ms = ev0.elapsed_time(ev1)
     nviol = runner.total_violations()
-    # replicas identical: a checksum of every rank's E must agree
+    # replicas identical: every rank's tables must agree
     ck = torch.tensor([float(model.E.data.double().sum().item()),
                        float(model.R.data.double().sum().item())], dtype=torch.float64, device=dev)
     cks = [torch.zeros_like(ck) for _ in range(world)]
     dist.all_gather(cks, ck)
     same = all(torch.equal(c, cks[0]) for c in cks)
-    value = N_TRIPLES * args.steps / elapsed
     bs = N_TRIPLES // nb
+    out = {"union_batch": bs, "nb": nb, "per_gpu_batch": -(-bs // world),
+           "value": round(N_TRIPLES * steps / elapsed, 1), "unit": "triples/s",
+           "ms_per_step": round(1000.0 * elapsed / steps, 4),
+           "gpu_event_ms_per_step": round(gpu_ms / steps, 4),
+           "us_per_union_batch": round(1e6 * elapsed / steps / len(runner.batches), 2),
+           "violations_per_pair": round(nviol / (2.0 * N_TRIPLES * steps), 4),
+           "replicas_identical": bool(same), "captured_graph": runner.graph is not None,
+           "record_bytes_per_positive": runner.rec_bytes}
+    if profile:
+        rollback()
+        out["phases"] = dp_profile(runner, args, world)
+    del runner
+    return out
+
+
+def dp_profile(runner, args, world):
+    """Per-rank phases of one eager data-parallel epoch (HIP events on the
+    runner stream; the all-gather's time is the RCCL collective's, incl. its
+    wait for the slowest rank) and their algorithmic bytes (SURVEY 8(d),
+    per rank): score 4d x 5 rows + 20 B per positive of the rank's slice + its
+    records written; all-gather G x share records received; scatter the union
+    batch's records read (its packed atomics are implementation bytes, not
+    8(d)'s); apply k d U."""
+    import torch
+    d, k = runner.d, (4 if args.opt == "sgd" else 12)
+    rb = runner.rec_bytes
+    ops, ex, st = runner.ops, runner.ex, runner.stream
+    from skge_amd.dp import slice_of
+    names = ("score", "all_gather", "scatter", "apply")
+    ms = dict.fromkeys(names, 0.0)
+    by = dict.fromkeys(names, 0.0)
+    runner._pad_in()
+    nbat = 0
+    with torch.cuda.stream(st):
+        for start, count in runner.batches:
+            share, lo, hi = slice_of(count, ex.G, ex.rank)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+            ev[0].record(st)
+            send = ops.score(start, count, lo, hi, share)
+            ev[1].record(st)
+            recs = ops.gathered(ex, send, share)
+            ev[2].record(st)
+            ops.scatter(start, count, recs)
+            ev[3].record(st)
+            st.synchronize()
+            U = int((runner.accE.cnt != 0).sum().item()) + int((runner.accR.cnt != 0).sum().item())
+            ea = torch.cuda.Event(enable_timing=True)
+            ea.record(st)
+            ops.apply(count)
+            ev[4].record(st)
+            st.synchronize()
+            for i, n in enumerate(names):
+                ms[n] += (ea if n == "apply" else ev[i]).elapsed_time(ev[i + 1])
+            by["score"] += (hi - lo) * (4.0 * d * 5 + 20 + rb)
+            by["all_gather"] += ex.G * share * rb
+            by["scatter"] += count * rb
+            by["apply"] += k * d * U
+            nbat += 1
+    runner._pad_out()
+    ph = {}
+    for n in names:
+        us = 1000.0 * ms[n] / nbat
+        b = by[n] / nbat
+        ph[n] = {"us_per_batch": round(us, 3), "bytes_per_batch": round(b),
+                 "GB_s": round(b / (us * 1e-6) / 1e9, 1) if us > 0 else None}
+    return ph
+
+
+def run_dp(args):
+    """--mode dp on N > 1 GPUs: the line is ONE model trained data parallel
+    (measure_dp).  --dp-batch global: union batch = the reference's 1414
+    (strong scaling); per-gpu: 1414 per GPU (union batch N x 1414, weak), with
+    the one-GPU pipelined runner at that union batch beside it."""
+    import torch
+    import torch.distributed as dist
+    world, rank, local = dist_env()
+    dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    nb = max(1, args.nb // world) if args.dp_batch == "per-gpu" else args.nb
+    m = measure_dp(args, dev, nb, args.warmup, args.steps)
+    same_geo = one_gpu_value(args, dev, nb) if args.dp_batch == "per-gpu" else None
+    bs = N_TRIPLES // nb
+    d = args.d
     if rank == 0:
+        ph = m["phases"]
+        dom = max(("score", "scatter", "apply"), key=lambda n: ph[n]["us_per_batch"])
+        cpu = None if args.no_cpu else cpu_baseline(make_wn18_kg(seed=0), d, args.nb,
+                                                    args.cpu_seconds, opt=args.opt)
         line = {
             "metric": "triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X"
                       if args.config == 2 else
                       "triples/sec (score+grad+update), WN18 TransE d=%d %s (BASELINE configs[0])"
                       % (d, args.opt),
-            "value": round(value, 1), "unit": "triples/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "value": m["value"], "unit": "triples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": m["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": "strong" if args.dp_batch == "global" else "weak",
+            "vs_baseline": None, "dtype": "f32",
             "data": "synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442 uniform, RandomState(0)), "
                     "the same on every rank; random-init params (nunif, seed 42)",
             "config": {"workload": "ONE TransE-L1 d=%d model, PairwiseStochasticTrainer+%s, WN18 "
-                                   "shape, union batch %d positives (nb=%d; %s), margin 2.0, lr 0.1, "
-                                   "device RandomModeSampler(1,[0,1]); data parallel over %d GPUs: "
-                                   "slice scoring, RCCL all-gather of the records, replicated "
-                                   "scatter + apply; step = 1 epoch"
+                                   "shape, union batch %d positives (nb=%d; ~%d per GPU), margin "
+                                   "2.0, lr 0.1, device RandomModeSampler(1,[0,1]); data parallel "
+                                   "over %d GPUs: slice scoring, RCCL all-gather of the records, "
+                                   "replicated scatter + apply; step = 1 epoch"
                                    % (d, {"sgd": "SGD", "adagrad": "AdaGrad"}[args.opt], bs, nb,
-                                      "~%d per GPU" % (bs // world), world),
+                                      m["per_gpu_batch"], world),
                        "global_batch": bs, "parallelism": "dp%d" % world},
-            "roofline": None,
-            "cpu_baseline": None,
-            "detail": {"runner": "DataParallelRunner (skge_amd.dp)",
-                       "captured_graph": runner.graph is not None,
-                       "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
-                       "batches_per_epoch": len(runner.batches),
-                       "us_per_union_batch": round(1e6 * elapsed / args.steps / len(runner.batches), 2),
-                       "violations_per_pair": round(nviol / (2.0 * N_TRIPLES * args.steps), 4),
-                       "replicas_identical": bool(same),
-                       "record_bytes_per_positive": runner.rec_bytes},
+            "roofline": {"bound": "hbm", "kernel": "dp_" + dom,
+                         "achieved": ph[dom]["GB_s"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ph[dom]["GB_s"] / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_per_launch": ph[dom]["bytes_per_batch"],
+                         "avg_launch_us": ph[dom]["us_per_batch"],
+                         "phases_per_rank": ph,
+                         "note": "per rank and union batch, eager epoch with HIP events between "
+                                 "phases (bench.dp_profile); all_gather = RCCL over xGMI"},
+            "cpu_baseline": cpu,
+            "detail": dict(m, runner="DataParallelRunner (skge_amd.dp)",
+                           one_gpu_same_geometry=same_geo),
         }
         print(json.dumps(line))
     dist.destroy_process_group()
+
+
+def one_gpu_value(args, dev, nb, epochs=None):
+    """The one-GPU pipelined runner (this rank's GPU alone, no collective) on
+    the same KG, model and union batch as a data-parallel run: what the
+    batch size alone buys, so a scaling curve does not credit it to the GPUs."""
+    import torch
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, EpochRunner
+    epochs = epochs or args.steps
+    trip = make_wn18_kg(seed=0)
+    np.random.seed(42)
+    model = S.TransE((N_ENT, N_ENT, N_REL), args.d, l1=True)
+    model.add_hyperparam("margin", 2.0)
+    Upd = S.SGD if args.opt == "sgd" else S.AdaGrad
+    upd = {pid: Upd(p, 0.1) for pid, p in model.params.items()}
+    r = EpochRunner(model, upd, DeviceKG(trip, dev), nbatches=nb, seed=1234)
+    init = {pid: p.data.clone() for pid, p in model.params.items()}
+    r.run(max(args.warmup, 1))
+    r.synchronize()
+    for pid, p in model.params.items():     # timed epochs start from the initial tables
+        p.data.copy_(init[pid])
+        upd[pid].reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r.run(epochs)
+    r.synchronize()
+    el = time.perf_counter() - t0
+    out = {"nb": nb, "union_batch": N_TRIPLES // nb, "value": round(N_TRIPLES * epochs / el, 1),
+           "ms_per_step": round(1000.0 * el / epochs, 4),
+           "runner": "pipelined" if r.pipelined else "two-launch"}
+    del r
+    return out
 
 
 def _score_bytes(d, cnt, V, packed=True, hole=False):
@@ -765,7 +1011,8 @@ def run_config5(args):
                          "avg_launch_us": round(k["avg_us"], 3)},
             "cpu_baseline": None if args.no_cpu else cpu_baseline_config5(args.cpu_seconds),
             "detail": {"runner": "pipelined" if runner.pipelined else "two-launch",
-                       "accumulator": "int16x4 exact" if runner.packed else "fp32",
+                       "accumulator": {"entity": acc_label(runner.accE),
+                                       "relation": acc_label(runner.accR)},
                        "build_s": round(t_build, 1),
                        "kernels": {n: {"avg_us": round(v["avg_us"], 3), "launches": v["launches"],
                                        "GB_s": round(v["achieved_gbs"], 1)}

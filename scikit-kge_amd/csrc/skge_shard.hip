@@ -207,6 +207,7 @@ __device__ __forceinline__ float4 unpack_i8x4(uint32_t u) {
 template <int KQ>
 __device__ __forceinline__ void store_contrib(uint8_t* __restrict__ C, long long stride, int pos,
                                               int c, const float4 (&v)[KQ], int d) {
+  if (pos < 0) return;       // a request dropped on bucket overflow: no record slot
   uint8_t* rec = C + (size_t)pos * stride;
   const int l = lane_id(), nq = d >> 2;
   if (l == 0) *reinterpret_cast<int*>(rec) = c;
@@ -254,6 +255,21 @@ __global__ __launch_bounds__(256) void k_shard_score(ShardScoreArgs a) {
     const int po_ = __builtin_amdgcn_readfirstlane(a.req_pos[4 * w + 1]);
     const int p0_ = __builtin_amdgcn_readfirstlane(a.req_pos[4 * w + 2]);
     const int p1_ = __builtin_amdgcn_readfirstlane(a.req_pos[4 * w + 3]);
+    // bucket overflow dropped the positive's own s / o row (error flagged by the
+    // route kernel): the positive is skipped whole -- no contributions, no
+    // relation sums, no violations -- rather than scored against a wrong row
+    if (ps_ < 0 || po_ < 0) {
+      // the slots this positive still holds carry a zero count (the record
+      // buffer is reused across batches: a stale count must not be re-added)
+      float4 z[KQ];
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) z[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+      store_contrib<KQ>(a.C, a.cstride, ps_, 0, z, d);
+      store_contrib<KQ>(a.C, a.cstride, po_, 0, z, d);
+      store_contrib<KQ>(a.C, a.cstride, p0_, 0, z, d);
+      store_contrib<KQ>(a.C, a.cstride, p1_, 0, z, d);
+      continue;
+    }
     float4 es[KQ], eo[KQ], fs[KQ], fo[KQ], rp[KQ];
     load_fetched<KQ>(a.F, ps_, d, es);
     load_fetched<KQ>(a.F, po_, d, eo);

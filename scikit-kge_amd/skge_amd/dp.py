@@ -129,6 +129,14 @@ class DPOps(object):
                                          L.int_array(4 * count, count)), "dp apply")
 
 
+class _PaddedParam(object):
+    """What table_struct reads of a Parameter: a zero-padded fp32 copy."""
+
+    def __init__(self, rows, width, dev):
+        self.rows, self.width = rows, width
+        self.data = torch.zeros((rows, width), dtype=torch.float32, device=dev)
+
+
 class DataParallelRunner(object):
     """TransE-L1 PairwiseStochasticTrainer epochs (margin, strict >,
     RandomModeSampler(1, [0, 1]) negatives drawn on the device) of ONE model
@@ -144,10 +152,10 @@ class DataParallelRunner(object):
     def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, group=None, stream=None,
                  capture=None):
         from .transe import TransE
-        from .param import Accumulator
+        from .param import Accumulator, table_struct, post_code
         from .device import packed_count_bound, relation_replicas, PACKED_MAX
-        if not isinstance(model, TransE) or not model.l1 or model.d % 4 or model.d > 1024:
-            raise ValueError("data-parallel runner: TransE-L1 with d % 4 == 0, d <= 1024")
+        if not isinstance(model, TransE) or not model.l1 or model.d > 1024:
+            raise ValueError("data-parallel runner: TransE-L1 with d <= 1024")
         self.ex = DPExchange(group)
         self.G, self.rank = self.ex.G, self.ex.rank
         self.model, self.kg = model, kg
@@ -155,7 +163,13 @@ class DataParallelRunner(object):
         self.device = dev
         self.stream = stream if stream is not None else torch.cuda.Stream(device=dev)
         self.sp = L.stream_ptr(self.stream)
-        self.d = int(model.d)
+        # d % 4 != 0 (the reference's d = 50): the kernels work on quads, so
+        # they run on zero-padded copies of the tables and AdaGrad states (as
+        # device.EpochRunner does), copied in and out around every run().  A
+        # zero column stays zero (sign(0) = 0 contributions, AdaGrad and the
+        # projection keep 0 at 0) and adds nothing to a score or a norm.
+        self.d = (int(model.d) + 3) // 4 * 4
+        self._pad = self.d != int(model.d)
         self.margin = float(model.margin)
         self.seed = int(seed) & (2 ** 64 - 1)
         self.ntries = int(ntries)
@@ -172,11 +186,24 @@ class DataParallelRunner(object):
             raise ValueError("data-parallel runner: a relation's per-batch count exceeds what 32 "
                              "packed accumulator copies hold; use more batches")
         E, R = model.params["E"], model.params["R"]
-        self.accE = Accumulator(E.rows, E.width, dev, slots=4 * bs, mode=L.SKGE_ACC_I16X4)
-        self.accR = Accumulator(R.rows, R.width, dev, mode=L.SKGE_ACC_I16X4, dense=True,
+        self.accE = Accumulator(E.rows, self.d, dev, slots=4 * bs, mode=L.SKGE_ACC_I16X4)
+        self.accR = Accumulator(R.rows, self.d, dev, mode=L.SKGE_ACC_I16X4, dense=True,
                                 replicas=reps)
-        self.te = updaters["E"].table(self.accE, counters=False)
-        self.tr = updaters["R"].table(self.accR, counters=False)
+        if self._pad:
+            self._padded = []
+            tabs = []
+            for pid, acc in (("E", self.accE), ("R", self.accR)):
+                u, P = updaters[pid], model.params[pid]
+                pp = _PaddedParam(P.rows, self.d, dev)
+                st = u.state()
+                sp = None if st is None else torch.zeros_like(pp.data)
+                self._padded.append((P, pp.data, st, sp))
+                tabs.append(table_struct(pp, sp, acc, opt=u.opt, post=post_code(u.param.post),
+                                         lr=float(u.learning_rate)))
+            self.te, self.tr = tabs
+        else:
+            self.te = updaters["E"].table(self.accE, counters=False)
+            self.tr = updaters["R"].table(self.accR, counters=False)
         self.rec_bytes = int(L.lib().skge_dp_record_bytes(self.d))
         share_max = -(-bs // self.G)
         self.send = torch.zeros(max(share_max, 1) * self.rec_bytes, dtype=torch.uint8, device=dev)
@@ -202,7 +229,34 @@ class DataParallelRunner(object):
                                                    L.ptr(self.nviol_total)), "dp fold")
         L.check(L.lib().skge_epoch_advance(self.sp, L.ptr(self.epoch_key)), "dp advance")
 
+    def _pad_in(self):
+        if not self._pad:
+            return
+        d = self.model.d
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            for P, Pp, st, sp in self._padded:
+                Pp[:, :d].copy_(P.data)
+                if st is not None:
+                    sp[:, :d].copy_(st)
+
+    def _pad_out(self):
+        if not self._pad:
+            return
+        d = self.model.d
+        with torch.cuda.stream(self.stream):
+            for P, Pp, st, sp in self._padded:
+                P.data.copy_(Pp[:, :d])
+                if st is not None:
+                    st.copy_(sp[:, :d])
+        torch.cuda.current_stream().wait_stream(self.stream)
+
     def run(self, nepochs=1):
+        self._pad_in()
+        self._run(nepochs)
+        self._pad_out()
+
+    def _run(self, nepochs):
         with torch.cuda.stream(self.stream):
             for _ in range(int(nepochs)):
                 if not self.capture:

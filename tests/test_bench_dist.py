@@ -2,8 +2,10 @@
 rank environment, the max-over-ranks timing and the whole-job value (the
 config-5 replica lines; configs 1/2 at N > 1 run the one-model data-parallel
 runner, DESIGN.md section 6, whose protocol tests/test_dp_protocol.py covers)."""
+import json
 import os
 import socket
+import subprocess
 import sys
 
 import pytest
@@ -61,3 +63,34 @@ def test_single_process_defaults(monkeypatch):
     assert bench.dist_env() == (1, 0, 0)
     assert bench.max_over_ranks(3.5, 1) == 3.5
     assert bench.replica_value(10, 1, 2.0) == 5.0
+
+
+def _bench_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_gpus_n_launches_n_ranks(n):
+    """`bench.py --gpus N` outside torchrun starts N ranks itself (CPU dry mode:
+    gloo, no GPU) and rank 0 alone prints one line with n_gpus == N."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n),
+                        "--dry-run", "--steps", "3", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _bench_lines(r.stdout)
+    assert len(lines) == 1
+    line = lines[0]
+    assert line["n_gpus"] == n and line["dry_run"] is True
+    assert sorted(line["detail"]["ranks"]) == list(range(n))
+    assert line["steps"] == 3 and line["value"] > 0
+
+
+def test_bench_rejects_world_size_mismatch():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4",
+                        "--dry-run"], capture_output=True, text=True, timeout=120, env=env,
+                       cwd=ROOT)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr

@@ -87,6 +87,21 @@ def test_dp_one_process_bitwise_equals_one_gpu_runner(n_ent, n_rel, T, d, nb):
     _same(pipe, want)
 
 
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb", [
+    (500, 7, 3001, 50, 7),          # the reference's d = 50 (BASELINE configs[0])
+    (300, 5, 2000, 13, 5),          # odd width
+])
+def test_dp_padded_width_bitwise_equals_padded_pipelined(n_ent, n_rel, T, d, nb):
+    """d % 4 != 0: the data-parallel runner works on zero-padded tables like
+    the one-GPU pipelined runner, so the two train bit for bit alike."""
+    from test_gpu_device_loop import make_kg
+    trip, _ = make_kg(n_ent, n_rel, T)
+    want = _one_gpu(trip, n_ent, n_rel, d, nb, 2, 5, pipelined=True)
+    got = _dp(trip, n_ent, n_rel, d, nb, 2, 5)
+    assert got["E"].shape[1] == d
+    _same(got, want)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -110,13 +110,16 @@ def _epoch_vs_oracle(kind, m, upd, runner, kg, seed, epoch, nb, opt, what, **kw)
     return got_v
 
 
-def _setup(cls, T, opt, **kw):
+def _setup(cls, T, opt, d=D, lr=0.1, no_post=False, **kw):
     import skge_amd as S
     from skge_amd.device import DeviceKG
     np.random.seed(42)
-    m = cls((N, N, M), D, **kw)
+    m = cls((N, N, M), d, **kw)
+    if no_post:          # gradient probe: the rows' projection off (see test below)
+        for p in m.params.values():
+            p.post = None
     U = S.AdaGrad if opt == "adagrad" else S.SGD
-    upd = {pid: U(p, 0.1) for pid, p in m.params.items()}
+    upd = {pid: U(p, lr) for pid, p in m.params.items()}
     kg = DeviceKG(_kg(T), m.device)
     return m, upd, kg
 
@@ -173,3 +176,80 @@ def test_runner_epoch_of_three_batches_vs_oracle(kind):
         r.synchronize()
         assert _epoch_vs_oracle(kind, m, upd, r, kg, 42, 1, 3, "sgd",
                                 "%s runner sgd 3 batches" % kind, **okw) > 0
+
+
+def test_config1_padded_runner_three_batches_vs_oracle():
+    """BASELINE configs[0] (run_transe_wn18.sh:3-5): TransE-L1 d = 50, SGD, the
+    bench's runner -- the pipelined runner on zero-padded d = 52 tables --
+    one epoch of 3 batches of B = 1414 against the oracle (after a first
+    epoch so the tables have moved)."""
+    import skge_amd as S
+    m, upd, kg = _setup(S.TransE, 3 * B, "sgd", d=50, l1=True)
+    m.add_hyperparam("margin", 2.0)
+    r = _runner("transe", m, upd, kg, 3, 43)
+    assert r._pad and r.d_pad == 52
+    with torch.cuda.stream(r.stream):
+        r.run(1)
+        r.synchronize()
+        assert _epoch_vs_oracle("transe", m, upd, r, kg, 43, 1, 3, "sgd",
+                                "config1 padded runner sgd 3 batches", l1=True) > 0
+
+
+GRAD_CASES = [("transe", 200), ("transe", 50), ("hole", 200), ("rescal", 200)]
+
+
+@pytest.mark.parametrize("kind,d", GRAD_CASES)
+def test_runner_gradients_vs_oracle(kind, d):
+    """Gradient-level parity of the SHIPPED runners (k_pipe_batch incl. config
+    1's padded tables, k_hole_pipe, RESCAL's fused front) at WN18 geometry,
+    at the plain north-star bar 1e-5 + 1e-5|g| -- no AdaGrad amplification term.
+
+    Gradient probe: the same runner with its updaters set to SGD(lr = 1) and
+    the rows' projection off, one batch of B = 1414 positives from the tables
+    after one AdaGrad-free training epoch.  The apply then computes
+    P' = fl(P - g) with g the device's segment mean (accumulated sums / counts,
+    skge/util.py:53-101), so P - P' (exact in fp64) is g to within half an ulp
+    of |P'| (<= 6e-8 here).  Compared with oracle.pairwise_step's (grad, idx)
+    rows (transe.py:48-165, hole.py:44-100, rescal.py:78-139); rows outside
+    idx must be unchanged, violations exactly equal."""
+    import skge_amd as S
+    from skge_amd.device import epoch_records
+    name, ckw, margin, okw = CASES[kind]
+    # warm the tables up with one ordinary epoch (shipped updater, projection on)
+    m0, upd0, kg = _setup(getattr(S, name), B, "sgd", d=d, **ckw)
+    m0.add_hyperparam("margin", margin)
+    r0 = _runner(kind, m0, upd0, kg, 1, 44)
+    r0.run(1)
+    r0.synchronize()
+    warm = {pid: p.data.clone() for pid, p in m0.params.items()}
+    del r0
+    m, upd, _ = _setup(getattr(S, name), 1, "sgd", d=d, lr=1.0, no_post=True, **ckw)
+    m.add_hyperparam("margin", margin)
+    for pid, p in m.params.items():
+        p.data.copy_(warm[pid])
+    r = _runner(kind, m, upd, kg, 1, 44)
+    if kind == "transe":
+        assert r.pipelined and (r._pad == (d % 4 != 0))
+    before = {pid: p.data.detach().cpu().numpy().astype(np.float64) for pid, p in m.params.items()}
+    rec, n1 = epoch_records(kg, N, 44, 0)
+    rec, n1 = rec.cpu().numpy(), n1.cpu().numpy()
+    with torch.cuda.stream(r.stream):
+        r.run(1)
+        r.synchronize()
+    torch.cuda.synchronize()
+    got_v = int(r.nviol_total.item())
+    pos, neg = _pairs(rec, n1, 0, B)
+    params = {k: v.copy() for k, v in before.items()}
+    state = {k: np.zeros_like(v) for k, v in before.items()}
+    _, _, want_v, grads = O.pairwise_step(kind, params, state, pos, neg, 1.0, margin, "sgd", **okw)
+    assert got_v == want_v > 0
+    for pid, p in m.params.items():
+        after = p.data.detach().cpu().numpy().astype(np.float64)
+        g_dev = before[pid] - after
+        rows, idx = grads[pid]
+        idx = np.asarray(idx, dtype=np.int64)
+        mask = np.ones(g_dev.shape[0], dtype=bool)
+        mask[idx] = False
+        assert np.array_equal(after[mask], before[pid][mask]), "%s %s: untouched rows moved" % (kind, pid)
+        parity_util.check(g_dev[idx], np.asarray(rows, dtype=np.float64),
+                          "%s d%d runner gradient %s" % (kind, d, pid))

@@ -101,9 +101,22 @@ def test_sharded_bucket_overflow_is_reported():
     dev = torch.device("cuda", 0)
     r = ShardedRunner(300, torch.as_tensor(E, device=dev), torch.as_tensor(R, device=dev),
                       torch.as_tensor(trip, device=dev), 8, seed=5, capacity=64)
+    # the contribution records live inside a guarded allocation: a record
+    # written for a dropped request (slot -1) would land in the front guard
+    C = r.bufs["contrib"]
+    guard = 4096
+    big = torch.full((C.numel() + 2 * guard,), 0xA5, dtype=torch.uint8, device=dev)
+    r.bufs["contrib"] = big[guard:guard + C.numel()].view(C.shape)
     r.run(1)
     with pytest.raises(L.SkgeError, match="overflowed"):
         r.synchronize()
+    torch.cuda.synchronize()
+    g = big.cpu().numpy()
+    assert (g[:guard] == 0xA5).all() and (g[-guard:] == 0xA5).all()
+    # a skipped positive adds nothing anywhere: tables finite, sums drained
+    assert torch.isfinite(r.E.data).all() and torch.isfinite(r.R.data).all()
+    for acc in (r.accE, r.accR):
+        assert int(acc.cnt.abs().sum().item()) == 0
 
 
 def _init_tables(n_ent, n_rel, d, seed):
