@@ -154,6 +154,32 @@ def run_dry(args):
         dist.destroy_process_group()
 
 
+def setup_ranks():
+    """(world, rank, local, device) of this process: the process group
+    (RCCL, i.e. "nccl"; SKGE_BENCH_BACKEND=gloo for a rehearsal) and its GPU.
+    SKGE_BENCH_ONE_GPU=1 puts every rank on GPU 0 (a multi-rank rehearsal on a
+    one-GPU box; RCCL refuses two ranks on one GPU, so pair it with gloo)."""
+    import torch
+    import torch.distributed as dist
+    world, rank, local = dist_env()
+    if world > 1:
+        dist.init_process_group(os.environ.get("SKGE_BENCH_BACKEND", "nccl"),
+                                init_method="env://")
+    if os.environ.get("SKGE_BENCH_ONE_GPU") == "1":
+        local = 0
+    torch.cuda.set_device(local)
+    return world, rank, local, torch.device("cuda", local)
+
+
+def coll_device(device):
+    """Where a bookkeeping collective's tensor lives: the GPU under RCCL, the
+    host under gloo."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "gloo":
+        return "cpu"
+    return device
+
+
 def max_over_ranks(x, world, device="cpu"):
     """The maximum of a per-rank float over all ranks (the timed region's
     wall clock: the job is done when the slowest replica is)."""
@@ -161,7 +187,7 @@ def max_over_ranks(x, world, device="cpu"):
         return float(x)
     import torch
     import torch.distributed as dist
-    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -299,11 +325,7 @@ def main():
 
     import torch
     import torch.distributed as dist
-    world, rank, local = dist_env()
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    world, rank, local, dev = setup_ranks()
 
     import skge_amd as S
     from skge_amd import _lib as L
@@ -590,7 +612,8 @@ def measure_dp(args, dev, nb, warmup, steps, profile=True):
     nviol = runner.total_violations()
     # replicas identical: every rank's tables must agree
     ck = torch.tensor([float(model.E.data.double().sum().item()),
-                       float(model.R.data.double().sum().item())], dtype=torch.float64, device=dev)
+                       float(model.R.data.double().sum().item())], dtype=torch.float64,
+                      device=coll_device(dev))
     cks = [torch.zeros_like(ck) for _ in range(world)]
     dist.all_gather(cks, ck)
     same = all(torch.equal(c, cks[0]) for c in cks)
@@ -670,10 +693,7 @@ def run_dp(args):
     the one-GPU pipelined runner at that union batch beside it."""
     import torch
     import torch.distributed as dist
-    world, rank, local = dist_env()
-    dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    world, rank, local, dev = setup_ranks()
     nb = max(1, args.nb // world) if args.dp_batch == "per-gpu" else args.nb
     m = measure_dp(args, dev, nb, args.warmup, args.steps)
     same_geo = one_gpu_value(args, dev, nb) if args.dp_batch == "per-gpu" else None
@@ -950,11 +970,7 @@ def run_config5(args):
     MI355X, so N GPUs run replicas (north_star: shard only past 288 GB)."""
     import torch
     import torch.distributed as dist
-    world, rank, local = dist_env()
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    world, rank, local, dev = setup_ranks()
     import skge_amd as S
     from skge_amd.device import DeviceKG, EpochRunner
     n_ent, T = int(N5 * args.c5_scale), int(T5 * args.c5_scale)
@@ -1032,11 +1048,7 @@ def run_config5_sharded(args):
     The dataset and tables are fixed as G grows: scaling "strong"."""
     import torch
     import torch.distributed as dist
-    world, rank, local = dist_env()
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    world, rank, local, dev = setup_ranks()
     from skge_amd.shard import ShardedRunner, owned_rows
     n_ent, T = int(N5 * args.c5_scale), int(T5 * args.c5_scale)
     d, n_rel = D5, M5
@@ -1214,11 +1226,7 @@ def run_config34(args):
     explicit pairs + skge_pair_step per batch, one hipGraph per epoch)."""
     import torch
     import torch.distributed as dist
-    world, rank, local = dist_env()
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    world, rank, local, dev = setup_ranks()
     import skge_amd as S
     from skge_amd.device import DeviceKG, batch_sizes, make_runner
     kind = "hole" if args.config == 3 else "rescal"

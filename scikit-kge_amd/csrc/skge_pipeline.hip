@@ -76,7 +76,11 @@ struct PipeTab {               // entity table
   unsigned long long* refs[2]; // owner mode, [rows] by batch parity: the batch's references to
                                // the row, total (high word, fixed within the launch) and not
                                // yet retired (low word) (k_own_batch)
+  int agrp;                    // > 0: the A role's entity waves in groups of AGRP_WAVES, each
+                               // group over `agrp` slot records (one vector load), its waves
+                               // taking turns over the slots that name a row; 0: one wave per slot
 };
+constexpr int AGRP_WAVES = 4;
 
 struct RelTab {                // relation table
   float* P[2];                 // P[0]: the caller's parameters; P[1]: the other buffer
@@ -521,6 +525,9 @@ __device__ __forceinline__ void rel_publish(const PipeArgs& a, int w, int rd, in
 #define SKGE_PIPE_ASLOTS 1   // entity slots per A-role wave (1 or 2)
 #endif
 constexpr int ASLOTS = SKGE_PIPE_ASLOTS;
+#ifndef SKGE_PIPE_AGRP_DEFAULT
+#define SKGE_PIPE_AGRP_DEFAULT 0   // A/B: SKGE_PIPE_AGRP
+#endif
 template <int KQ, bool W32, bool E8, bool GRP = false>
 __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
@@ -585,6 +592,23 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
             const int row = __builtin_amdgcn_readlane(r, k);
             claim_and_apply<KQ, E8>(a.E, pp, row, d, gp);
           }
+        }
+      } else if (a.E.agrp) {
+        // a group of AGRP_WAVES waves over agrp slots: every wave loads the
+        // group's slot records (one vector load), and the k-th slot naming a
+        // row goes to wave k % AGRP_WAVES -- ~U apply waves are dispatched
+        // instead of one per slot (73% of slots name no row at nb = 100)
+        const int e = w - nR;
+        const int grp = e / AGRP_WAVES, sub = e % AGRP_WAVES;
+        const int i = grp * a.E.agrp + l;
+        const int r = (l < a.E.agrp && i < a.prev_slots) ? a.E.touched[pp][i] : -1;
+        uint64_t m = __ballot(r >= 0);
+        int k = 0;
+        while (m) {
+          const int j = __ffsll((unsigned long long)m) - 1;
+          m &= m - 1;
+          if ((k++ % AGRP_WAVES) == sub)
+            claim_and_apply<KQ, E8>(a.E, pp, __builtin_amdgcn_readlane(r, j), d, gp);
         }
       } else {
         if (ASLOTS == 2) {
@@ -2315,6 +2339,9 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   r->lds = !hole ? 0
            : r->fft ? hole_fft_lds_bytes(d, SKGE_PIPE_WG / 64)
                     : (size_t)(SKGE_PIPE_WG / 64) * hole_pos_lds_floats(d) * sizeof(float);
+  // A-role entity groups (SKGE_PIPE_AGRP: slots per group of AGRP_WAVES waves, <= 64)
+  int agrp = SKGE_PIPE_AGRP_DEFAULT;
+  if (getenv("SKGE_PIPE_AGRP")) agrp = std::max(0, std::min(64, atoi(getenv("SKGE_PIPE_AGRP"))));
   int prev = 0;
   for (int b = 0; b <= nb1; ++b) {   // b == nb1: flush of the last batch (A role only)
     a.b = b;
@@ -2325,12 +2352,14 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     // A role: every relation row, then the previous batch's entity slots (lazy:
     // no entity rows, except the flush's sweep over all rows in 64-row chunks)
     const bool grouped = a.E.own[0] != nullptr;   // owner marks: 64-slot groups
+    a.E.agrp = (!hole && !lazy && !r->owner && !grouped) ? agrp : 0;
     const int a_items =
         rel->rows + (hole ? (4 * prev + HGROUP - 1) / HGROUP
                           : lazy ? (b == nb1 ? (ent->rows + 63) / 64 : 0)
                                  : r->owner ? 0
                                             : grouped ? (4 * prev + 63) / 64
-                                                      : (4 * prev + ASLOTS - 1) / ASLOTS);
+                                                      : a.E.agrp ? AGRP_WAVES * ((4 * prev + a.E.agrp - 1) / a.E.agrp)
+                                                                 : (4 * prev + ASLOTS - 1) / ASLOTS);
     constexpr int WPB = SKGE_PIPE_WG / 64;
     // HolE: the apply waves loop over their items within the residency the
     // scoring waves leave (SKGE_HPIPE_OCC waves per SIMD: 2 at ~180 VGPRs; the

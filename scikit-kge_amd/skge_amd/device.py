@@ -147,7 +147,10 @@ class EpochRunner(object):
         # A zero column stays zero (TransE-L1: sign(0) = 0 contributions, AdaGrad
         # and the projection leave 0 at 0) and adds nothing to a score or norm,
         # so the padded step is the d-wide step.
-        self.d_pad = (model.d + 3) // 4 * 4
+        # padded width: a multiple of 4 (quads); SKGE_PIPE_PAD_TO (A/B) rounds
+        # further, e.g. 32 -> d = 50 runs at 64 (256-B rows on whole 128-B lines)
+        pad_to = max(4, int(_os.environ.get("SKGE_PIPE_PAD_TO", "4")) // 4 * 4)
+        self.d_pad = (model.d + pad_to - 1) // pad_to * pad_to
         self._pad = (bool(model.l1) and model.d % 4 != 0 and not force_f32 and replicas <= 1
                      and pipelined is not False and packed is not False
                      and _os.environ.get("SKGE_PIPE_PAD", "1") != "0")

@@ -215,14 +215,17 @@ def test_runner_gradients_vs_oracle(kind, d):
     import skge_amd as S
     from skge_amd.device import epoch_records
     name, ckw, margin, okw = CASES[kind]
-    # warm the tables up with one ordinary epoch (shipped updater, projection on)
+    # HolE / RESCAL: warm the tables up with one ordinary epoch (shipped updater,
+    # projection on); TransE from its initial tables (after one SGD epoch only
+    # ~10 of its 2828 pairs still violate the margin of 2)
     m0, upd0, kg = _setup(getattr(S, name), B, "sgd", d=d, **ckw)
     m0.add_hyperparam("margin", margin)
-    r0 = _runner(kind, m0, upd0, kg, 1, 44)
-    r0.run(1)
-    r0.synchronize()
+    if kind != "transe":
+        r0 = _runner(kind, m0, upd0, kg, 1, 44)
+        r0.run(1)
+        r0.synchronize()
+        del r0
     warm = {pid: p.data.clone() for pid, p in m0.params.items()}
-    del r0
     m, upd, _ = _setup(getattr(S, name), 1, "sgd", d=d, lr=1.0, no_post=True, **ckw)
     m.add_hyperparam("margin", margin)
     for pid, p in m.params.items():
@@ -242,7 +245,7 @@ def test_runner_gradients_vs_oracle(kind, d):
     params = {k: v.copy() for k, v in before.items()}
     state = {k: np.zeros_like(v) for k, v in before.items()}
     _, _, want_v, grads = O.pairwise_step(kind, params, state, pos, neg, 1.0, margin, "sgd", **okw)
-    assert got_v == want_v > 0
+    assert got_v == want_v > (200 if kind == "transe" else 0)
     for pid, p in m.params.items():
         after = p.data.detach().cpu().numpy().astype(np.float64)
         g_dev = before[pid] - after

@@ -51,7 +51,19 @@ def residuals(E, R, rec, n1):
     return vp, v0, v1
 
 
-def main(batches=10, seed=7):
+def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=40943)
+    ap.add_argument("--m", type=int, default=18)
+    ap.add_argument("--batch", type=int, default=1414)
+    ap.add_argument("--opt", default="sgd", choices=["sgd", "adagrad"])
+    ap.add_argument("--batches", type=int, default=10)
+    ap.add_argument("--tag", default="c1")
+    args = ap.parse_args()
+    global N, M, B
+    N, M, B = args.n, args.m, args.batch
+    batches, seed = args.batches, 7
     import skge_amd as S
     from skge_amd.device import DeviceKG, EpochRunner, epoch_records
     dev = torch.device("cuda", 0)
@@ -62,7 +74,8 @@ def main(batches=10, seed=7):
         np.random.seed(42)
         m = S.TransE((N, N, M), D, l1=True)
         m.add_hyperparam("margin", 2.0)
-        upd = {pid: S.SGD(p, 0.1) for pid, p in m.params.items()}
+        U = S.SGD if args.opt == "sgd" else S.AdaGrad
+        upd = {pid: U(p, 0.1) for pid, p in m.params.items()}
         r = EpochRunner(m, upd, kg, nbatches=1, seed=seed, force_f32=f32)
         runs.append((m, r))
     assert runs[0][1].pipelined and runs[0][1]._pad and not runs[1][1].pipelined
@@ -86,7 +99,7 @@ def main(batches=10, seed=7):
                     runs[1][0].E.data.cpu().numpy())
         dR = np.abs(runs[0][0].R.data.cpu().numpy().astype(np.float64) -
                     runs[1][0].R.data.cpu().numpy())
-        line = {"batch": e, "sign_flips_pos_neg0_neg1": flips,
+        line = {"tag": args.tag, "opt": args.opt, "n": N, "batch_size": B, "batch": e, "sign_flips_pos_neg0_neg1": flips,
                 "components_below_1e-6": near, "margin_decision_flips": dec,
                 "E_elems_gt_1e-5": int((dE > 1e-5).sum()), "E_rows_gt_1e-5": int((dE > 1e-5).any(1).sum()),
                 "E_max": float(dE.max()), "R_elems_gt_1e-5": int((dR > 1e-5).sum()),
@@ -94,7 +107,7 @@ def main(batches=10, seed=7):
         print(json.dumps(line))
         out.append(line)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "diag_pad_div.json"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", "diag_pad_div_%s.json" % args.tag), "w") as f:
         json.dump(out, f, indent=1)
 
 
