@@ -139,8 +139,9 @@ typedef struct skge_table {
 int skge_abi_version(void);
 const char *skge_last_error(void);
 /* Synchronizes the stream and returns the error bits raised by device kernels
- * since the last reset (2 = a packed row's count exceeded 32767); reset != 0
- * clears them. */
+ * since the last reset (2 = a packed row's count exceeded 32767; 4 = an
+ * SKGE_ACC_FX64 sum reached 2^22 in gradient units, half its wrap-around
+ * range); reset != 0 clears them. */
 int skge_device_error(void *stream, int reset);
 
 /*

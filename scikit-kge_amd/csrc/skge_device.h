@@ -122,7 +122,11 @@ __device__ __host__ __forceinline__ int acc_row_dwords(int mode, int width) {
 // 64-bit fixed-point integer with 40 fractional bits (one rounding, to the
 // nearest multiple of 2^-40 ~ 9.1e-13, deterministic), sums are exact integer
 // atomics -- the same bits whatever order the adds arrive in -- and the apply
-// converts the sum back once.  |sum| < 2^23 holds for any gradient sum here.
+// converts the sum back once.  Range: |sum| < 2^23 per element and batch,
+// i.e. (a row's occurrences in the batch) x max |contribution| < 8.4e6 -- WN18
+// RESCAL at nb = 2 (~5e4 pairs of one relation, |E_s E_o| <= 1) stays far
+// inside; the applies flag any decoded sum past 2^22 (skge_device_error bit 4,
+// raised by the runners' synchronize()).
 constexpr float FX_SCALE = 1099511627776.0f;            // 2^40
 __device__ __forceinline__ long long fx_enc(float v) { return __float2ll_rn(v * FX_SCALE); }
 __device__ __forceinline__ float fx_dec(long long x) {

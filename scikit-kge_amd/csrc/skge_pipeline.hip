@@ -76,6 +76,8 @@ struct PipeTab {               // entity table
   unsigned long long* refs[2]; // owner mode, [rows] by batch parity: the batch's references to
                                // the row, total (high word, fixed within the launch) and not
                                // yet retired (low word) (k_own_batch)
+  int a4;                      // 1: one A-role wave per positive's 4 slots, one row per 16-lane
+                               // group (claim_and_apply4; d <= 256)
   int agrp;                    // > 0: the A role's entity waves in groups of AGRP_WAVES, each
                                // group over `agrp` slot records (one vector load), its waves
                                // taking turns over the slots that name a row; 0: one wave per slot
@@ -284,6 +286,130 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
   if (l == 0) __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
+}
+
+// Four slot-recorded rows per A-role wave, in parallel: 16-lane group k holds
+// slot 4i + k's row, lane j of a group quads j, j + 16, j + 32, j + 48 (d <=
+// 256).  Claims (one atomic instruction), loads, updates, write-through stores
+// and the drain are one chain for all four rows -- a wave per positive instead
+// of a wave per slot, with the one-row wave's chain length.  row_update4 is
+// row_update's arithmetic element for element, and its squared-norm reduction
+// follows wave_sum's order exactly (register k of a group holds what lanes 16k
+// .. 16k + 15 hold in the one-row layout; the same four DPP steps per 16-lane
+// row, then (k0 + k1) + (k2 + k3)), so a row gets the same bits whichever
+// wave applies it (the scoring waves' claim_and_apply, or this).
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xb1>(v);
+  v += dpp_f<0x4e>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  return v;   // every lane of the 16-lane row holds the row's total
+}
+
+__device__ __forceinline__ void row_update4(const UpdParams& t, int c, int d,
+                                            const unsigned long long (&sv)[4], float4 (&p)[4],
+                                            float4 (&a)[4]) {
+  const int gl = lane_id() & 15, nq = d >> 2;
+  const bool ada = t.opt == OPT_ADAGRAD;
+  const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
+  float ss[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const bool in = 16 * m + gl < nq;
+    const float4 sm = unpack_i16x4(in ? sv[m] : 0ull);
+    ss[m] = 0.0f;
+#define SKGE_UP(X)                                                      \
+  {                                                                     \
+    const float g = (sm.X + t.rin * p[m].X) / div + t.rout * p[m].X;    \
+    float pv = p[m].X;                                                  \
+    if (ada) {                                                          \
+      a[m].X = a[m].X + g * g;                        /* param.py:147 */\
+      pv = pv - adagrad_step_fast(t.lr, g, a[m].X);   /* 152-155 */     \
+    } else {                                                            \
+      pv = pv - t.lr * g;                             /* param.py:130 */\
+    }                                                                   \
+    p[m].X = in ? pv : 0.0f;                                            \
+    ss[m] += p[m].X * p[m].X;                                           \
+  }
+    SKGE_UP(x)
+    SKGE_UP(y)
+    SKGE_UP(z)
+    SKGE_UP(w)
+#undef SKGE_UP
+  }
+  if (t.post != POST_NONE) {
+    const float tot = (row16_sum(ss[0]) + row16_sum(ss[1])) + (row16_sum(ss[2]) + row16_sum(ss[3]));
+    const float inv = proj_scale_fast(t.post, tot);   // param.py:165-166 / 171-173
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      p[m].x = p[m].x * inv;
+      p[m].y = p[m].y * inv;
+      p[m].z = p[m].z * inv;
+      p[m].w = p[m].w * inv;
+    }
+  }
+}
+
+template <bool E8>
+__device__ __forceinline__ void claim_and_apply4(const PipeTab& t, int pp, int slot0, int nslots,
+                                                 int d, int gp) {
+  const int l = lane_id(), grp = l >> 4, gl = l & 15, nq = d >> 2;
+  const int sl = slot0 + grp;
+  const int row = sl < nslots ? t.touched[pp][sl] : -1;   // lanes of a group: one address
+  if (!__ballot(row >= 0)) return;
+  int c = 0;
+  if (gl == 0 && row >= 0) c = atomicExch(t.cnt[pp] + row, 0);
+  const int rr = row >= 0 ? row : 0;   // (rows past the slots: a valid address, discarded)
+  unsigned long long sv[4];
+  float4 p[4], a[4];
+  const float4* prow = reinterpret_cast<const float4*>(t.P + (size_t)rr * d);
+  const float4* arow = reinterpret_cast<const float4*>(t.A + (size_t)rr * d);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int q = 16 * m + gl, qc = q < nq ? q : nq - 1;
+    if (E8)
+      sv[m] = reinterpret_cast<const unsigned int*>(t.sum[pp])[(size_t)rr * nq + qc];
+    else
+      sv[m] = t.sum[pp][(size_t)rr * nq + qc];
+    p[m] = prow[qc];
+    a[m] = t.A ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  c = __builtin_amdgcn_ds_bpermute(grp << 6, c);   // the group's claim (lane 16 grp)
+  const bool mine = c != 0;
+  if (!__ballot(mine)) return;   // empty slots, or rows other waves own
+  if (mine && gl == 0 && c > (E8 ? 127 : PACKED_MAX)) atomicOr(t.err, ERR_PACKED);
+  if (E8) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) sv[m] = pack_i16x4(unpack_i8x4_sum((unsigned int)sv[m]));
+  }
+  row_update4(t.u, mine ? c : 1, d, sv, p, a);
+  // write-through 16-B stores through descriptors over the whole tables
+  // (per-lane offsets: the four groups' rows differ)
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc(t.P, 0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ars =
+      __builtin_amdgcn_make_buffer_rsrc(t.A ? t.A : t.P, 0, 0x7FFFFFFF, 0x00020000);
+  if (mine) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int q = 16 * m + gl;
+      if (q < nq) {
+        if (E8)
+          reinterpret_cast<unsigned int*>(t.sum[pp])[(size_t)row * nq + q] = 0u;
+        else
+          t.sum[pp][(size_t)row * nq + q] = 0ull;
+        const int off = (row * d + 4 * q) * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&p[m]), prs, off,
+                                               0, AUX_SC1);
+        if (t.A)
+          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&a[m]), ars, off,
+                                                 0, AUX_SC1);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+  if (mine && gl == 0) __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t.claims && l == 0) atomicAdd(shard_of(t.claims), __popcll(__ballot(mine && gl == 0)));
 }
 
 // Large batches: up to GRP_ROWS owner rows of a 64-slot group at once -- all
@@ -525,10 +651,13 @@ __device__ __forceinline__ void rel_publish(const PipeArgs& a, int w, int rd, in
 #define SKGE_PIPE_ASLOTS 1   // entity slots per A-role wave (1 or 2)
 #endif
 constexpr int ASLOTS = SKGE_PIPE_ASLOTS;
+#ifndef SKGE_PIPE_A4_DEFAULT
+#define SKGE_PIPE_A4_DEFAULT 0   // A/B: SKGE_PIPE_A4
+#endif
 #ifndef SKGE_PIPE_AGRP_DEFAULT
 #define SKGE_PIPE_AGRP_DEFAULT 0   // A/B: SKGE_PIPE_AGRP
 #endif
-template <int KQ, bool W32, bool E8, bool GRP = false>
+template <int KQ, bool W32, bool E8, bool GRP = false, bool A4 = false>
 __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
@@ -593,6 +722,9 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
             claim_and_apply<KQ, E8>(a.E, pp, row, d, gp);
           }
         }
+      } else if (A4) {
+        // one wave per positive: its 4 slots, one row per 16-lane group
+        if constexpr (A4 && KQ == 1) claim_and_apply4<E8>(a.E, pp, 4 * (w - nR), a.prev_slots, d, gp);
       } else if (a.E.agrp) {
         // a group of AGRP_WAVES waves over agrp slots: every wave loads the
         // group's slot records (one vector load), and the k-th slot naming a
@@ -2092,6 +2224,14 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
         if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true>), gr, bl, 0, st, a);  \
         else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true>), gr, bl, 0, st, a);        \
       }                                                                                          \
+    } else if (a.E.a4 && K == 1) {   /* one A-role wave per positive (claim_and_apply4) */       \
+      if (r->e8) {                                                                               \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, false, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, true, false, true>), gr, bl, 0, st, a);  \
+      } else {                                                                                   \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, false, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, false, true>), gr, bl, 0, st, a); \
+      }                                                                                          \
     } else if (r->e8) {                                                                          \
       if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true>), gr, bl, 0, st, a);           \
       else hipLaunchKernelGGL((k_pipe_batch<K, false, true>), gr, bl, 0, st, a);                 \
@@ -2342,6 +2482,9 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   // A-role entity groups (SKGE_PIPE_AGRP: slots per group of AGRP_WAVES waves, <= 64)
   int agrp = SKGE_PIPE_AGRP_DEFAULT;
   if (getenv("SKGE_PIPE_AGRP")) agrp = std::max(0, std::min(64, atoi(getenv("SKGE_PIPE_AGRP"))));
+  // one A-role wave per positive, four rows in parallel (SKGE_PIPE_A4, d <= 256)
+  int a4 = SKGE_PIPE_A4_DEFAULT;
+  if (getenv("SKGE_PIPE_A4")) a4 = atoi(getenv("SKGE_PIPE_A4")) != 0;
   int prev = 0;
   for (int b = 0; b <= nb1; ++b) {   // b == nb1: flush of the last batch (A role only)
     a.b = b;
@@ -2353,11 +2496,14 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     // no entity rows, except the flush's sweep over all rows in 64-row chunks)
     const bool grouped = a.E.own[0] != nullptr;   // owner marks: 64-slot groups
     a.E.agrp = (!hole && !lazy && !r->owner && !grouped) ? agrp : 0;
+    a.E.a4 = (!hole && !lazy && !r->owner && !grouped && nq <= 64 &&
+              (long long)ent->rows * d * 4 < (1ll << 31)) ? a4 : 0;   // (table-wide descriptors)
     const int a_items =
         rel->rows + (hole ? (4 * prev + HGROUP - 1) / HGROUP
                           : lazy ? (b == nb1 ? (ent->rows + 63) / 64 : 0)
                                  : r->owner ? 0
                                             : grouped ? (4 * prev + 63) / 64
+                                                      : a.E.a4 ? prev
                                                       : a.E.agrp ? AGRP_WAVES * ((4 * prev + a.E.agrp - 1) / a.E.agrp)
                                                                  : (4 * prev + ASLOTS - 1) / ASLOTS);
     constexpr int WPB = SKGE_PIPE_WG / 64;

@@ -13,7 +13,16 @@ namespace skge {
 
 // error bits raised by apply kernels (read with skge_device_error):
 // 2 = a packed int16x4 row's count exceeded 32767 (its sums may have wrapped)
+// 4 = a deterministic fixed-point (ACC_FX64) sum reached half its range
+//     (|sum| >= 2^22 in gradient units; it wraps at 2^23)
 __device__ int g_skge_dev_err = 0;
+
+// FX64 sums wrap silently past +-2^63 (2^23 in gradient units, FX_SCALE):
+// flag any decoded element at or past half of that range
+__device__ __forceinline__ void fx_check(long long x) {
+  constexpr long long HALF = 1ll << 62;
+  if (x >= HALF || x <= -HALF) atomicOr(&g_skge_dev_err, 4);
+}
 
 struct TableDev {
   float* P;
@@ -108,6 +117,7 @@ __device__ __forceinline__ void mean_row(const TableDev& t, int row, int c, floa
     const int e = l + 64 * k;
     const int ec = e < w ? e : w - 1;
     const float sv = fx ? fx_dec(xrow[ec]) : srow[ec], pv = prow[ec];
+    if (fx) fx_check(xrow[ec]);
     g[k] = e < w ? (sv + t.rin * pv) / div + t.rout * pv : 0.0f;
   }
 #pragma unroll
@@ -154,6 +164,11 @@ __device__ __forceinline__ void apply_row(const TableDev& t, int row, bool upd) 
   }
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row, or a stale slot
+  if (fx) {
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+      if (l + 64 * k < w) fx_check(xrow[l + 64 * k]);
+  }
   if (upd && ada && t.ucnt && l == 0) t.ucnt[row] += 1;   // param.py:149-150
   const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
   float ss = 0.0f;

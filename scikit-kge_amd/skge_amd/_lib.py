@@ -162,3 +162,19 @@ def ptr(t):
     if t is None:
         return None
     return c_p(t.data_ptr())
+
+
+def check_device_error(stream_handle, what="device"):
+    """Read and reset the apply kernels' error word (skge_device_error) and
+    raise on its bits: 2 = a packed row's count passed 32767, 4 = a
+    deterministic fixed-point sum reached half its range."""
+    rc = lib().skge_device_error(stream_handle, 1)
+    if rc < 0:
+        raise SkgeError("%s: %s" % (what, lib().skge_last_error().decode()))
+    if rc & 2:
+        raise SkgeError("%s: a row's per-batch count exceeded 32767 (packed sums may have "
+                        "wrapped); use force_f32=True" % what)
+    if rc & 4:
+        raise SkgeError("%s: a deterministic fixed-point (FX64) sum reached 2^22 -- past 2^23 "
+                        "it wraps; use more batches or the default float sums" % what)
+    return rc

@@ -359,6 +359,8 @@ class StochasticTrainer(object):
             for batch in np.split(idx, batch_idx):
                 bxys = [xys[z] for z in batch]
                 self._process_batch(bxys)
+            if deterministic():   # FX64 sums: range flag of the epoch's applies
+                L.check_device_error(L.stream_ptr(), "trainer")
             for f in self.post_epoch:
                 if not f(self):
                     break

@@ -341,11 +341,8 @@ class EpochRunner(object):
 
     def synchronize(self):
         self.stream.synchronize()
-        if not self.pipelined and self.packed:
-            rc = L.lib().skge_device_error(L.stream_ptr(self.stream), 1)
-            if rc & 2:
-                raise L.SkgeError("epoch runner: a row's per-batch count exceeded 32767 "
-                                  "(packed sums may have wrapped); use force_f32=True")
+        if not self.pipelined:
+            L.check_device_error(L.stream_ptr(self.stream), "epoch runner")
         if self.pipelined:
             rc = L.lib().skge_pipe_runner_error(self.handle, L.stream_ptr(self.stream))
             if rc < 0:
@@ -505,6 +502,7 @@ class PairLoopRunner(object):
 
     def synchronize(self):
         self.stream.synchronize()
+        L.check_device_error(L.stream_ptr(self.stream), "pair-loop runner")
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -82,3 +82,32 @@ def test_deterministic_step_matches_oracle(det, kind):
     (per batch from the device state, as tests/test_gpu_models.py)."""
     from test_gpu_models import _run
     _run(kind, 400, 18, 200, 700 if kind == "rescal" else 500, nb=2)
+
+
+@pytest.mark.parametrize("mag", [1.0, 5.0e6])
+def test_fx64_range_flag(mag):
+    """FX64 sums wrap past 2^23 gradient units.  An apply that
+    decodes a sum at or past 2^22 sets skge_device_error bit 4, which
+    check_device_error (every runner's synchronize) raises; ordinary sums do
+    not."""
+    import skge_amd as S
+    from skge_amd import _lib as L
+    from skge_amd.param import Accumulator, table_struct
+    dev = torch.device("cuda", 0)
+    rows, d = 8, 64
+    P = S.param.Parameter(None, name="W", value=torch.zeros((rows, d), device=dev))
+    acc = Accumulator(rows, d, dev, slots=4, mode=L.SKGE_ACC_FX64)
+    x = acc.sum.view(torch.int64).view(rows, d)
+    x[3] = int(mag * 2 ** 40)           # one row's fixed-point sum, count 1
+    acc.cnt[3] = 1
+    acc.touched[0] = 3
+    t = table_struct(P, None, acc, opt=L.SKGE_SGD, post=L.SKGE_POST_NONE, lr=1.0)
+    L.lib().skge_device_error(L.stream_ptr(), 1)
+    L.check(L.lib().skge_accum_apply(L.stream_ptr(), (L.SkgeTable * 1)(t), 1, L.int_array(4)),
+            "apply")
+    if mag < 2 ** 22:
+        L.check_device_error(L.stream_ptr(), "fx64")
+        assert float(P.data[3, 0].item()) == -mag
+    else:
+        with pytest.raises(L.SkgeError, match="FX64"):
+            L.check_device_error(L.stream_ptr(), "fx64")

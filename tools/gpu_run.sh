@@ -9,6 +9,7 @@
 #   stats[:<bench.py args>]               rocprofv3 --kernel-trace --stats of a bench command
 #   pmc[:<bench.py args>]                 kernel-trace stats, then FETCH_SIZE and WRITE_SIZE passes
 #                                         (separate runs) + tools/pmc_summary.py
+#   pmcx[:<bench.py args>]                one --pmc pass of the counters in $PMCX + tools/pmc_counters.py
 #   tool:<script>[,<args>]                python tools/<script> (or bash for .sh) under a time limit
 # Arguments after ':' use ',' for spaces (e.g. bench:--config,3,--steps,5).
 set -u
@@ -59,6 +60,11 @@ for st in ${STEPS:-tests smoke bench}; do
       run ${TAG}_pmcw$n 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv \
         -d $D/write -o run -- python3 bench.py ${arg:---steps 20 --warmup 3 --no-cpu} || exit $?
       python3 tools/pmc_summary.py $D > $D/pmc.json && echo "pmc summary: $D/pmc.json" ;;
+    pmcx)   # one --pmc pass of the counters in $PMCX (space separated) over a bench command
+      D=gpurun_out/${TAG}_pmcx$n
+      run ${TAG}_pmcx$n 300 rocprofv3 --pmc ${PMCX:-SQ_WAVES SQ_WAVE_CYCLES} --kernel-trace -T \
+        --output-format csv -d $D -o run -- python3 bench.py ${arg:---steps 5 --warmup 2 --no-cpu} || exit $?
+      python3 tools/pmc_counters.py $D > $D/pmc_counters.json && echo "pmc counters: $D/pmc_counters.json" ;;
     tool)   # tool:<script under tools/>,<args>  (python scripts and .sh drivers)
       set -- $arg
       scr=$1; shift
