@@ -37,6 +37,9 @@ constexpr int GC = 64;          // output columns per GEMM tile
 #ifndef SKGE_RS_KS
 #define SKGE_RS_KS 32
 #endif
+#ifndef SKGE_RS_GKS_DEFAULT
+#define SKGE_RS_GKS_DEFAULT 1   // A/B: SKGE_RS_GKS
+#endif
 constexpr int KS = SKGE_RS_KS;  // k per staged step
 constexpr int RS_MAX_D = 1024;  // d of the MFMA path
 constexpr int RS_MAX_M = 8192;  // relations (k_rs_scan keeps 2M+1 ints in LDS)
@@ -81,7 +84,42 @@ struct RescalWs {
   float* W1;
   float* A1;
   int* wcur;
+  // GEMM K split (SKGE_RS_GKS, 1 = off): the WE / EW rows and partial scores
+  // come in gks slices over k, slice k at WE + k * part_stride (spart + k *
+  // spart_stride); consumers add the slices in index order (deterministic)
+  int gks;
+  long long part_stride, spart_stride;
 };
+
+// WE / EW row i of the batch: the K slices summed in slice order
+template <int KM>
+__device__ __forceinline__ void load_row_gk(const float* __restrict__ base, const RescalWs& ws,
+                                            int i, int d, float (&v)[KM]) {
+  load_row<KM>(base, i, d, v);
+  if (ws.gks > 1) {
+    float u[KM];
+    load_row<KM>(base + ws.part_stride, i, d, u);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) v[k] += u[k];
+  }
+}
+// the raw score of item i: the column blocks' partial scores (and their K
+// slices) in a fixed order
+__device__ __forceinline__ float spart_sum(const RescalWs& ws, int i, int ncb) {
+  float r = 0.0f;
+  for (int q = 0; q < ncb; ++q) {
+    r += ws.spart[(size_t)i * ncb + q];
+    if (ws.gks > 1) r += ws.spart[ws.spart_stride + (size_t)i * ncb + q];
+  }
+  return r;
+}
+
+// K slices of the GEMMs (SKGE_RS_GKS: 1 or 2; d needs at least 2 k-steps)
+static int rs_gks(int d) {
+  const char* e = getenv("SKGE_RS_GKS");
+  const int g = e ? atoi(e) : SKGE_RS_GKS_DEFAULT;
+  return g >= 2 && (d + SKGE_RS_KS - 1) / SKGE_RS_KS >= 2 ? 2 : 1;
+}
 
 // the fused front's in-front W step (WStep::cur): W_b is in buffer *cur
 // (0: W0 / A0 = the caller's); the dW workgroups write W_{b+1} into the other
@@ -178,10 +216,14 @@ static size_t rescal_ws_layout(int n, int M, int d, void* base, RescalWs* ws) {
   w.sorted_s = (int*)take((size_t)n * 4);
   w.sorted_o = (int*)take((size_t)n * 4);
   w.bpos = (int*)take((size_t)n * 4);
-  w.spart = (float*)take((size_t)n * ((d + GC - 1) / GC) * 4);
+  const int gks = rs_gks(d);
+  w.gks = gks;
+  w.part_stride = (long long)n * d;
+  w.spart_stride = (long long)n * ((d + GC - 1) / GC);
+  w.spart = (float*)take((size_t)gks * n * ((d + GC - 1) / GC) * 4);
   w.coef = (float*)take((size_t)n * 4);
-  w.WE = (float*)take((size_t)n * d * 4);
-  w.EW = (float*)take((size_t)n * d * 4);
+  w.WE = (float*)take((size_t)gks * n * d * 4);
+  w.EW = (float*)take((size_t)gks * n * d * 4);
   const size_t wpb = rs_wpart_bytes(n, M, d);
   w.wpart = wpb ? (float*)take(wpb) : nullptr;
   w.ecoef = nullptr;
@@ -632,16 +674,20 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
                                                  float (*sA)[RT_ITEMS][KS + 4], float (*sB)[SBN],
                                                  int* s_row, int* s_gid, int* s_es, int* s_es2) {
   const int ncb = (d + GC - 1) / GC;
-  // plain: (tile, product, column block); deduplicated (ws.npos > 0): (tile,
-  // column block), the product-0 tiles first
+  // plain: (tile, product, column block, K slice); deduplicated (ws.npos > 0):
+  // (tile, column block, K slice), the product-0 tiles first
   const bool dedup = ws.npos > 0;
-  const int t = dedup ? bid / ncb : bid / (2 * ncb);
+  const int gks = ws.gks;
+  const int per = (dedup ? ncb : 2 * ncb) * gks;
+  const int t = bid / per;
   // the tile's fields and the tile count in one round trip (t < rs_tmax: the
   // fields are in bounds, read before the check, used after it)
   const int nti = ws.ntiles[0], nt0 = dedup ? ws.ntiles[1] : 0;
   const int p = ws.tile_rel[t], s0 = ws.tile_start[t], cnt = ws.tile_cnt[t];
   if (t >= nti) return;
-  const int rem = dedup ? bid - t * ncb : bid - t * 2 * ncb;
+  const int rem_k = bid - t * per;
+  const int ksl = rem_k % gks;   // this workgroup's K slice
+  const int rem = rem_k / gks;
   const int prod = dedup ? (t < nt0 ? 0 : 1) : rem / ncb;
   const int cb = dedup ? rem : rem - (rem / ncb) * ncb;
   const int tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
@@ -656,7 +702,8 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
   }
   __syncthreads();
   const float* Wp = W + (size_t)p * d * d;
-  const int nk = (d + KS - 1) / KS;
+  const int nk_all = (d + KS - 1) / KS, nks = (nk_all + gks - 1) / gks;
+  const int k_lo = ksl * nks, nk = min(nk_all, k_lo + nks);   // k-steps [k_lo, nk)
   // staging map, 16 consecutive floats of A and of B per thread and k-step:
   //   A[ai][ak..ak+15] = E[row ai][k + ak ..]
   //   product 0: B[k + bk ..][bq] = W[c0 + bq][k + bk ..]   (transposed into LDS)
@@ -745,9 +792,9 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
   const int row = wave * 16 + (l & 15), kq = l >> 4;
-  load_step(0);
-  for (int ks = 0; ks < nk; ++ks) {
-    const int buf = ks & 1;
+  load_step(k_lo);
+  for (int ks = k_lo; ks < nk; ++ks) {
+    const int buf = (ks - k_lo) & 1;
     store_step(buf, ks);
     __syncthreads();   // (also: every wave is done with buf's previous use, step ks - 2)
     if (ks + 1 < nk) load_step(ks + 1);   // in flight during this step's MFMAs
@@ -780,7 +827,8 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
 #endif
   }
   // epilogue: D[row 4g + reg][col] of accumulator q -> triple 16w + 4g + reg, column c0 + 16q + c
-  float* out = prod == 0 ? ws.WE : ws.EW;
+  float* out = (prod == 0 ? ws.WE : ws.EW) + (size_t)ksl * ws.part_stride;
+  float* const spart = ws.spart + (size_t)ksl * ws.spart_stride;
   const int g = l >> 4, c = l & 15;
   float ev[4][4], ev2[4][4];
   // a row with a second subject (deduplicated: a positive's WE row also
@@ -823,7 +871,7 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
       v += __shfl_xor(v, 2, 64);
       v += __shfl_xor(v, 1, 64);
       const int it = wave * 16 + 4 * g + reg;
-      if (c == 0 && it < cnt) ws.spart[(size_t)s_gid[it] * ncb + cb] = v;
+      if (c == 0 && it < cnt) spart[(size_t)s_gid[it] * ncb + cb] = v;
       if (two) {   // the s-corrupted negative (item npos + 2j) of positive j = s_gid
         float v2 = ps2[reg];
         v2 += __shfl_xor(v2, 8, 64);
@@ -831,7 +879,7 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
         v2 += __shfl_xor(v2, 2, 64);
         v2 += __shfl_xor(v2, 1, 64);
         if (c == 0 && it < cnt && s_es2[it] >= 0)
-          ws.spart[(size_t)(ws.npos + 2 * s_gid[it]) * ncb + cb] = v2;
+          spart[(size_t)(ws.npos + 2 * s_gid[it]) * ncb + cb] = v2;
       }
     }
   }
@@ -870,11 +918,7 @@ __global__ __launch_bounds__(256) void k_rescal_scatter(const int* __restrict__ 
       continue;
     }
     const int ncb = (d + GC - 1) / GC;
-    float praw = 0.0f, nraw = 0.0f;
-    for (int q = 0; q < ncb; ++q) {   // fixed order: deterministic
-      praw += ws.spart[(size_t)i * ncb + q];
-      nraw += ws.spart[(size_t)(P + i) * ncb + q];
-    }
+    const float praw = spart_sum(ws, i, ncb), nraw = spart_sum(ws, P + i, ncb);   // fixed order
     const float pf = af_f(af, praw), nf = af_f(af, nraw);
     const float gp = -af_g_given_f(af, pf);   // rescal.py:275 (all pairs)
     const float gn = af_g_given_f(af, nf);
@@ -889,10 +933,10 @@ __global__ __launch_bounds__(256) void k_rescal_scatter(const int* __restrict__ 
     if (!viol) continue;
     ++nv;
     float wep[KM], wen[KM], ewp[KM], ewn[KM], x[KM], y[KM];
-    load_row<KM>(ws.WE, i, d, wep);
-    load_row<KM>(ws.WE, P + i, d, wen);
-    load_row<KM>(ws.EW, i, d, ewp);
-    load_row<KM>(ws.EW, P + i, d, ewn);
+    load_row_gk<KM>(ws.WE, ws, i, d, wep);
+    load_row_gk<KM>(ws.WE, ws, P + i, d, wen);
+    load_row_gk<KM>(ws.EW, ws, i, d, ewp);
+    load_row_gk<KM>(ws.EW, ws, P + i, d, ewn);
     // (sp, sn) <- (gp WEp, gn WEn)                    rescal.py:299-300
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
@@ -943,16 +987,13 @@ __global__ __launch_bounds__(256) void k_rescal_pos_scatter(const int4* __restri
     // positive without a violation discards them): W E_o and E_s W of the
     // positive, E_s' W of (s', o, p), W E_o' of (s, o', p)
     float wep[KM], ewp[KM], ew0[KM], we1[KM];
-    load_row<KM>(ws.WE, j, d, wep);
-    load_row<KM>(ws.EW, j, d, ewp);
-    load_row<KM>(ws.EW, i0, d, ew0);
-    load_row<KM>(ws.WE, i1, d, we1);
-    float praw = 0.0f, raw0 = 0.0f, raw1 = 0.0f;
-    for (int q = 0; q < ncb; ++q) {   // fixed order: deterministic
-      praw += ws.spart[(size_t)j * ncb + q];
-      raw0 += ws.spart[(size_t)i0 * ncb + q];
-      raw1 += ws.spart[(size_t)i1 * ncb + q];
-    }
+    load_row_gk<KM>(ws.WE, ws, j, d, wep);
+    load_row_gk<KM>(ws.EW, ws, j, d, ewp);
+    load_row_gk<KM>(ws.EW, ws, i0, d, ew0);
+    load_row_gk<KM>(ws.WE, ws, i1, d, we1);
+    // fixed order: deterministic
+    const float praw = spart_sum(ws, j, ncb), raw0 = spart_sum(ws, i0, ncb),
+                raw1 = spart_sum(ws, i1, ncb);
     const float pf = af_f(af, praw), f0 = af_f(af, raw0), f1 = af_f(af, raw1);
     const float gp = -af_g_given_f(af, pf);   // rescal.py:275 (all pairs)
     const float g0 = af_g_given_f(af, f0), g1 = af_g_given_f(af, f1);
@@ -979,8 +1020,8 @@ __global__ __launch_bounds__(256) void k_rescal_pos_scatter(const int4* __restri
         ew1[k] = ewp[k];
       }
     } else {
-      load_row<KM>(ws.WE, i0, d, we0);
-      load_row<KM>(ws.EW, i1, d, ew1);
+      load_row_gk<KM>(ws.WE, ws, i0, d, we0);
+      load_row_gk<KM>(ws.EW, ws, i1, d, ew1);
     }
     const float fv0 = (float)v0, fv1 = (float)v1;
 #pragma unroll
@@ -1018,8 +1059,7 @@ __global__ __launch_bounds__(256) void k_rescal_logistic(const int* __restrict__
   for (int i = blockIdx.x * wpb + (threadIdx.x >> 6); i < T; i += gridDim.x * wpb) {
     const int s = __builtin_amdgcn_readfirstlane(trip[3 * i]);
     const int o = __builtin_amdgcn_readfirstlane(trip[3 * i + 1]);
-    float score = 0.0f;
-    for (int q = 0; q < ncb; ++q) score += ws.spart[(size_t)i * ncb + q];   // fixed order
+    const float score = spart_sum(ws, i, ncb);   // fixed order
     const float y = ys[i];
     const float ysc = y * score;
     const float li = fmaxf(-ysc, 0.0f) + log1pf(expf(-fabsf(ysc)));   // logaddexp(0, -ys)
@@ -1033,8 +1073,8 @@ __global__ __launch_bounds__(256) void k_rescal_logistic(const int* __restrict__
       if (l < 2) commit_slot(accE, l == 0 ? s : o, s == o ? (l == 0 ? 2 : 0) : 1, 2 * i + l);
     }
     float we[KM], ew[KM], x[KM], yv[KM];
-    load_row<KM>(ws.WE, i, d, we);
-    load_row<KM>(ws.EW, i, d, ew);
+    load_row_gk<KM>(ws.WE, ws, i, d, we);
+    load_row_gk<KM>(ws.EW, ws, i, d, ew);
 #pragma unroll
     for (int k = 0; k < KM; ++k) {   // rescal.py:65-66 (fs WE over ss, fs EW over os)
       x[k] = fs * we[k];
@@ -1604,8 +1644,8 @@ static int rescal_front(hipStream_t st, const skge_table_t* ent, const skge_tabl
     hipLaunchKernelGGL(k_rs_scatter, dim3(cblocks), dim3(256), 0, st, a, b, na, n, M, ws);
   }
   const int ncb = (d + GC - 1) / GC;
-  const dim3 ggrid((unsigned)(ws.npos > 0 ? rs_tmax_dedup(ws.npos, M) * ncb
-                                          : rs_tmax(n, M) * 2 * ncb));
+  const dim3 ggrid((unsigned)((ws.npos > 0 ? rs_tmax_dedup(ws.npos, M) * ncb
+                                           : rs_tmax(n, M) * 2 * ncb) * ws.gks));
   if ((d & 3) == 0)
     hipLaunchKernelGGL((k_rescal_gemm<true>), ggrid, dim3(256), 0, st, ent->param, rel->param, d,
                        ws);
@@ -1749,10 +1789,14 @@ static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, Resc
     return q;
   };
   RescalWs w;
-  w.spart = (float*)take((size_t)n * ((d + GC - 1) / GC) * 4);
+  const int gks = rs_gks(d);
+  w.gks = gks;
+  w.part_stride = (long long)n * d;
+  w.spart_stride = (long long)n * ((d + GC - 1) / GC);
+  w.spart = (float*)take((size_t)gks * n * ((d + GC - 1) / GC) * 4);
   w.coef = (float*)take((size_t)n * 4);
-  w.WE = (float*)take((size_t)n * d * 4);
-  w.EW = (float*)take((size_t)n * d * 4);
+  w.WE = (float*)take((size_t)gks * n * d * 4);
+  w.EW = (float*)take((size_t)gks * n * d * 4);
   // batches of fewer items use fewer splits; the fused front (Linear) needs
   // partial tiles even at one split
   const size_t wpb = std::max(rs_wpart_bytes(n, M, d), rs_front_wpart_bytes(n, M, d));
@@ -1863,7 +1907,7 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
     const int nt = (d + WG_T - 1) / WG_T, ncb = (d + GC - 1) / GC;
     const int nwg = M * nt * nt * fsplits;
     const dim3 grid((unsigned)(nwg + (w.npos > 0 ? rs_tmax_dedup(count, M) * ncb
-                                                  : rs_tmax(n, M) * 2 * ncb)));
+                                                  : rs_tmax(n, M) * 2 * ncb) * w.gks));
     // workgroup order of the two roles (k_rescal_front_fused): the GEMM grid
     // first (A/B on WN18 d = 200: 29.25 M vs 29.0 M triples/s with the dW
     // grid first, 29.2 M interleaving one dW workgroup in three)

@@ -168,7 +168,8 @@ class DataParallelRunner(object):
         # device.EpochRunner does), copied in and out around every run().  A
         # zero column stays zero (sign(0) = 0 contributions, AdaGrad and the
         # projection keep 0 at 0) and adds nothing to a score or a norm.
-        self.d = (int(model.d) + 3) // 4 * 4
+        from .device import padded_width
+        self.d = int(model.d) if model.d % 4 == 0 else padded_width(int(model.d))
         self._pad = self.d != int(model.d)
         self.margin = float(model.margin)
         self.seed = int(seed) & (2 ** 64 - 1)

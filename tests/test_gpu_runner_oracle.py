@@ -180,14 +180,14 @@ def test_runner_epoch_of_three_batches_vs_oracle(kind):
 
 def test_config1_padded_runner_three_batches_vs_oracle():
     """BASELINE configs[0] (run_transe_wn18.sh:3-5): TransE-L1 d = 50, SGD, the
-    bench's runner -- the pipelined runner on zero-padded d = 52 tables --
+    bench's runner -- the pipelined runner on zero-padded d = 64 tables --
     one epoch of 3 batches of B = 1414 against the oracle (after a first
     epoch so the tables have moved)."""
     import skge_amd as S
     m, upd, kg = _setup(S.TransE, 3 * B, "sgd", d=50, l1=True)
     m.add_hyperparam("margin", 2.0)
     r = _runner("transe", m, upd, kg, 3, 43)
-    assert r._pad and r.d_pad == 52
+    assert r._pad and r.d_pad == 64      # device.padded_width: whole 128-B lines
     with torch.cuda.stream(r.stream):
         r.run(1)
         r.synchronize()
