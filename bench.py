@@ -991,17 +991,24 @@ def run_config5(args):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    runner.run(args.steps)
-    runner.synchronize()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    if runner.pipelined:   # (not at |E| = 50M: the second accumulator copy does not fit)
+        t0 = time.perf_counter()
+        runner.run(args.steps)
+        runner.synchronize()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        prof = None
+    else:
+        # the two-launch epoch's kernel sequence launched eagerly with HIP events
+        # between the kernels: per-kernel device time and applied rows of
+        # exactly the timed epochs (kernels of ~0.3-1 ms: launch cost ~1%)
+        elapsed, prof = eager_epochs(runner, kg, nb, d, args.steps)
     if world > 1:
         dist.barrier()
     elapsed = max_over_ranks(elapsed, world, dev)
     value = replica_value(T * args.steps, world, elapsed)
-    prof = pipe_profile(runner, kg, nb, d) if runner.pipelined else \
-        kernel_profile(model, upd, kg, nb, d, runner.stream, runner)
+    if prof is None:
+        prof = pipe_profile(runner, kg, nb, d)
     k = prof["dominant"]
     if rank == 0:
         traffic, traffic_src = pmc_traffic(PMC_KERNEL.get(k["name"], k["name"]), "pmc_c5.json")
@@ -1024,7 +1031,9 @@ def run_config5(args):
                          "traffic": None if traffic is None else round(traffic),
                          "traffic_source": traffic_src,
                          "bytes_per_launch": round(k["bytes_per_launch"]),
-                         "avg_launch_us": round(k["avg_us"], 3)},
+                         "avg_launch_us": round(k["avg_us"], 3),
+                         "avg_launch_source": prof.get("source"),
+                         "bytes_formula": prof.get("formula")},
             "cpu_baseline": None if args.no_cpu else cpu_baseline_config5(args.cpu_seconds),
             "detail": {"runner": "pipelined" if runner.pipelined else "two-launch",
                        "accumulator": {"entity": acc_label(runner.accE),
@@ -1033,11 +1042,88 @@ def run_config5(args):
                        "kernels": {n: {"avg_us": round(v["avg_us"], 3), "launches": v["launches"],
                                        "GB_s": round(v["achieved_gbs"], 1)}
                                    for n, v in prof["kernels"].items()},
+                       # the kernels' device time per step (<= ms_per_step: the
+                       # rest is launch gaps)
+                       "kernels_ms_per_step": round(sum(v["avg_us"] * v["launches"]
+                                                        for v in prof["kernels"].values()
+                                                        if v["launches"] > 1)
+                                                    / 1000.0 / args.steps, 3),
                        "gpu_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)},
         }
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def eager_epochs(runner, kg, nb, d, epochs, opt_k=12):
+    """`epochs` epochs of the two-launch runner's graph (skge_epoch.hip
+    skge_runner_create: per batch k_transe_*_sample_grad then k_apply, then
+    the epoch-key advance) launched eagerly on the runner's stream, HIP events
+    between the kernels and no host synchronisation until the end; AdaGrad
+    update counters on (skge_table_t.upd_count, param.py:149-150), whose sum is
+    the rows the applies updated.  Returns (wall seconds, profile): per kernel
+    the mean device time over these launches and the SURVEY 8(d) bytes --
+    sample_grad 4d(3B + P) + 20B per batch, k_apply k d U with U the counted
+    rows -- so frac and ms_per_step come from the same epochs."""
+    import torch
+    from skge_amd import _lib as L
+    lib = L.lib()
+    st = runner.stream
+    sp = L.stream_ptr(st)
+    dev = runner.model.device
+    te = L.SkgeTable.from_buffer_copy(runner.te)
+    tr = L.SkgeTable.from_buffer_copy(runner.tr)
+    ucE = torch.zeros(te.rows, dtype=torch.int32, device=dev)
+    ucR = torch.zeros(tr.rows, dtype=torch.int32, device=dev)
+    te.upd_count, tr.upd_count = L.ptr(ucE), L.ptr(ucR)
+    tabs = (L.SkgeTable * 2)(te, tr)
+    nviol = torch.zeros(1, dtype=torch.int32, device=dev)
+    T = kg.T
+    bs = T // nb
+    batches = [(s0, min(bs, T - s0)) for s0 in range(0, T, bs)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
+          for _ in range(epochs * len(batches))]
+    l1 = 1 if runner.model.l1 else 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(st):
+        i = 0
+        for _ in range(epochs):
+            for start, cnt in batches:
+                e = ev[i]
+                i += 1
+                e[0].record(st)
+                L.check(lib.skge_transe_sample_grad(sp, l1, te, tr, d, L.ptr(kg.trip), T,
+                                                    L.ptr(kg.slots), kg.capacity, start, cnt,
+                                                    runner.seed, L.ptr(runner.epoch_key),
+                                                    float(runner.model.margin), runner.ntries,
+                                                    L.ptr(nviol), None, None), "sample_grad")
+                e[1].record(st)
+                L.check(lib.skge_accum_apply(sp, tabs, 2, L.int_array(4 * cnt, cnt)), "apply")
+                e[2].record(st)
+            L.check(lib.skge_epoch_advance(sp, L.ptr(runner.epoch_key)), "advance")
+    st.synchronize()
+    elapsed = time.perf_counter() - t0
+    runner.nviol_total.add_(nviol)
+    n = len(ev)
+    t_s = sum(e[0].elapsed_time(e[1]) for e in ev) * 1e3 / n
+    t_a = sum(e[1].elapsed_time(e[2]) for e in ev) * 1e3 / n
+    U = (int(ucE.sum().item()) + int(ucR.sum().item())) / n
+    b_s = sum(algorithmic_bytes(d, c, 2 * c, 0, 0) for _, c in batches) / len(batches)
+    b_a = float(opt_k) * d * U
+    kern = {"transe_sample_grad": {"name": "transe_sample_grad", "avg_us": t_s, "launches": n,
+                                   "bytes_per_launch": b_s,
+                                   "achieved_gbs": b_s / (t_s * 1e-6) / 1e9},
+            "accum_apply": {"name": "accum_apply", "avg_us": t_a, "launches": n,
+                            "bytes_per_launch": b_a, "achieved_gbs": b_a / (t_a * 1e-6) / 1e9}}
+    B = T / len(batches)
+    return elapsed, {"kernels": kern, "dominant": max(kern.values(), key=lambda v: v["avg_us"]),
+                     "epoch_bytes": (b_s + b_a) * len(batches),
+                     "source": "HIP events between the kernels of the timed epochs (eager "
+                               "launches of the epoch graph's sequence)",
+                     "formula": {"launches_per_epoch": len(batches), "B": B, "P": 2 * B,
+                                 "U_per_apply": U, "d": d, "k": opt_k,
+                                 "expr": "sample_grad 4d(3B+P) + 20B; k_apply k d U"}}
 
 
 def run_config5_sharded(args):

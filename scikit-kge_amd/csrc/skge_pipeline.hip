@@ -671,8 +671,11 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
   const int nB = gridDim.x - a.nA;
   // apply workgroups first: they start the hand-offs the scoring waves may wait
   // on (measured: 6% faster than scoring first, 9% faster than interleaved)
-  const int blk_a = (int)blockIdx.x, blk_b = (int)blockIdx.x - a.nA;
-  if ((int)blockIdx.x < a.nA) {
+  // b_first (A/B, SKGE_PIPE_AFIRST=0): the scoring workgroups dispatched first
+  const int blk = (int)blockIdx.x;
+  const bool is_a = a.b_first ? blk >= nB : blk < a.nA;
+  const int blk_a = a.b_first ? blk - nB : blk, blk_b = a.b_first ? blk : blk - a.nA;
+  if (is_a) {
     // ---- A role: write R_b, then apply the previous batch's entity rows ----
     const int nR = a.R.rows;
     // owner marks (large batches): items are groups of 64 slots, scanned
@@ -2468,6 +2471,8 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   {
     const char* af_env = getenv("SKGE_HPIPE_AFIRST");   // A/B switch: 0 = scoring WGs first
     a.b_first = hole && af_env && atoi(af_env) == 0 ? 1 : 0;   // default: apply WGs first
+    const char* paf = getenv("SKGE_PIPE_AFIRST");   // the same switch for TransE (A/B)
+    if (!hole && paf && atoi(paf) == 0) a.b_first = 1;
   }
   r->fft = hole && hole_use_fft(d);
   a.tw = r->fft ? hole_fft_table(d) : nullptr;

@@ -149,6 +149,7 @@ class EpochRunner(object):
         self.stream = stream if stream is not None else torch.cuda.Stream(device=dev)
         self.kg = kg
         self.model = model
+        self.seed, self.ntries = int(seed) & (2 ** 64 - 1), int(ntries)
         self.epoch_key = torch.zeros(1, dtype=torch.int64, device=dev)
         self.nviol_total = nviol_total if nviol_total is not None else \
             torch.zeros(1, dtype=torch.int32, device=dev)
