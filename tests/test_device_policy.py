@@ -74,3 +74,17 @@ def test_relation_replicas_config5_shape():
                      rs.randint(10000, size=T)], axis=1)
     assert relation_replicas(_kg(trip), 10000, 131072) == 1
     assert relation_replicas(_kg(trip), 10000, 131072, ranks=8) == 1   # the sharded union batch
+
+
+def test_padded_width_whole_lines(monkeypatch):
+    """d % 4 != 0 tables run on zero-padded copies: whole 128-B lines (32
+    floats) when that costs <= 30% more row bytes, else the next quad."""
+    from skge_amd.device import padded_width
+    monkeypatch.delenv("SKGE_PIPE_PAD_TO", raising=False)
+    assert padded_width(50) == 64       # BASELINE configs[0]: 256-B rows
+    assert padded_width(30) == 32
+    assert padded_width(13) == 16       # 32 would be 2.5x the row
+    assert padded_width(97) == 100      # 128 would be +32%
+    assert padded_width(99) == 128      # +29%
+    monkeypatch.setenv("SKGE_PIPE_PAD_TO", "4")
+    assert padded_width(50) == 52       # the round-3 width (A/B switch)
