@@ -657,7 +657,11 @@ constexpr int ASLOTS = SKGE_PIPE_ASLOTS;
 #ifndef SKGE_PIPE_AGRP_DEFAULT
 #define SKGE_PIPE_AGRP_DEFAULT 0   // A/B: SKGE_PIPE_AGRP
 #endif
-template <int KQ, bool W32, bool E8, bool GRP = false, bool A4 = false>
+// ROLE 0: both roles in one grid (nA apply workgroups, then the scoring ones);
+// ROLE 1: apply role only (grid nA); ROLE 2: scoring role only (grid nB) --
+// the split form, two kernels on parallel branches of the epoch graph, each
+// with its own register budget (SKGE_PIPE_SPLIT)
+template <int KQ, bool W32, bool E8, bool GRP = false, bool A4 = false, int ROLE = 0>
 __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
@@ -668,14 +672,15 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
   const int rd = a.b & 1;                // relation buffer holding R_{b-1}
   const int rw = a.b < a.nb1 ? rd ^ 1 : 0;   // ... receiving R_b (the flush: the caller's)
   const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
-  const int nB = gridDim.x - a.nA;
+  const int nB = ROLE == 2 ? (int)gridDim.x : (int)gridDim.x - a.nA;
   // apply workgroups first: they start the hand-offs the scoring waves may wait
   // on (measured: 6% faster than scoring first, 9% faster than interleaved)
   // b_first (A/B, SKGE_PIPE_AFIRST=0): the scoring workgroups dispatched first
   const int blk = (int)blockIdx.x;
-  const bool is_a = a.b_first ? blk >= nB : blk < a.nA;
-  const int blk_a = a.b_first ? blk - nB : blk, blk_b = a.b_first ? blk : blk - a.nA;
-  if (is_a) {
+  const bool is_a = ROLE == 1 || (ROLE == 0 && (a.b_first ? blk >= nB : blk < a.nA));
+  const int blk_a = ROLE == 1 ? blk : (a.b_first ? blk - nB : blk);
+  const int blk_b = ROLE == 2 ? blk : (a.b_first ? blk : blk - a.nA);
+  if (ROLE != 2 && is_a) {
     // ---- A role: write R_b, then apply the previous batch's entity rows ----
     const int nR = a.R.rows;
     // owner marks (large batches): items are groups of 64 slots, scanned
@@ -2161,6 +2166,10 @@ struct skge_pipe_runner {
   bool hole = false;               // HolE pairwise (k_hole_pipe, fp32 sums)
   bool fft = false;                // HolE: correlations in the frequency domain (skge_hole_fft.h)
   bool rfold = false;              // TransE: relation sums in replicas, k_rel_fold after each batch
+  bool split = false;              // SKGE_PIPE_SPLIT: apply and scoring roles as two kernels on
+                                   // parallel branches (large batches: own register budgets)
+  hipStream_t st2 = nullptr;       // split: the scoring kernels' capture stream
+  hipEvent_t fork = nullptr, join = nullptr;
   size_t lds = 0;                  // HolE: dynamic LDS per workgroup
   int nlaunch() const { return (int)batch.size() + 2; }
 };
@@ -2178,6 +2187,9 @@ static void pipe_free(skge_pipe_runner* r) {
   if (!r) return;
   if (r->exec) (void)hipGraphExecDestroy(r->exec);
   if (r->graph) (void)hipGraphDestroy(r->graph);
+  if (r->fork) (void)hipEventDestroy(r->fork);
+  if (r->join) (void)hipEventDestroy(r->join);
+  if (r->st2) (void)hipStreamDestroy(r->st2);
   for (void* p : r->bufs) (void)hipFree(p);
   delete r;
 }
@@ -2219,6 +2231,31 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
     } else if (r->owner) {                                                                       \
       if (r->w32) hipLaunchKernelGGL((k_own_batch<K, true>), gr, bl, 0, st, a);                  \
       else hipLaunchKernelGGL((k_own_batch<K, false>), gr, bl, 0, st, a);                        \
+    } else if (a.E.own[0] && r->grp && r->split && a.count > 0) {                                \
+      /* large batches, split: the apply kernel here, the scoring kernel on st2 (forked and */   \
+      /* joined around the pair), each sized to its own role */                                  \
+      const dim3 ga(a.nA), gb(r->grid[k] - a.nA);                                                \
+      (void)hipEventRecord(r->fork, st);                                                        \
+      (void)hipStreamWaitEvent(r->st2, r->fork, 0);                                             \
+      if (r->e8) {                                                                               \
+        if (r->w32) {                                                                            \
+          hipLaunchKernelGGL((k_pipe_batch<K, true, true, true, false, 2>), gb, bl, 0, r->st2, a); \
+          hipLaunchKernelGGL((k_pipe_batch<K, true, true, true, false, 1>), ga, bl, 0, st, a);   \
+        } else {                                                                                 \
+          hipLaunchKernelGGL((k_pipe_batch<K, false, true, true, false, 2>), gb, bl, 0, r->st2, a); \
+          hipLaunchKernelGGL((k_pipe_batch<K, false, true, true, false, 1>), ga, bl, 0, st, a);  \
+        }                                                                                        \
+      } else {                                                                                   \
+        if (r->w32) {                                                                            \
+          hipLaunchKernelGGL((k_pipe_batch<K, true, false, true, false, 2>), gb, bl, 0, r->st2, a); \
+          hipLaunchKernelGGL((k_pipe_batch<K, true, false, true, false, 1>), ga, bl, 0, st, a);  \
+        } else {                                                                                 \
+          hipLaunchKernelGGL((k_pipe_batch<K, false, false, true, false, 2>), gb, bl, 0, r->st2, a); \
+          hipLaunchKernelGGL((k_pipe_batch<K, false, false, true, false, 1>), ga, bl, 0, st, a); \
+        }                                                                                        \
+      }                                                                                          \
+      (void)hipEventRecord(r->join, r->st2);                                                    \
+      (void)hipStreamWaitEvent(st, r->join, 0);                                                 \
     } else if (a.E.own[0] && r->grp) {   /* large batches: grouped owner-row apply */             \
       if (r->e8) {                                                                               \
         if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, true>), gr, bl, 0, st, a);   \
@@ -2336,6 +2373,17 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   {
     const char* gr = getenv("SKGE_PIPE_GRP");   // A/B: 0 = one owner row per round trip
     r->grp = !(gr && atoi(gr) == 0);
+  }
+  {
+    const char* sp = getenv("SKGE_PIPE_SPLIT");   // A/B: two kernels per large-batch launch
+    r->split = !hole && !lazy && sp && atoi(sp) != 0;
+    if (r->split && (hipStreamCreateWithFlags(&r->st2, hipStreamNonBlocking) != hipSuccess ||
+                     hipEventCreateWithFlags(&r->fork, hipEventDisableTiming) != hipSuccess ||
+                     hipEventCreateWithFlags(&r->join, hipEventDisableTiming) != hipSuccess)) {
+      set_error("pipelined runner: split-mode stream / event creation failed");
+      pipe_free(r);
+      return nullptr;
+    }
   }
   {
     const char* ow = getenv("SKGE_PIPE_OWNER");   // A/B: entity rows by their last reference
