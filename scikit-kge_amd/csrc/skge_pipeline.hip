@@ -2010,6 +2010,10 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     aR.width = d;
     if constexpr (FFT) {
       const float* z = hole_fft_rows(wb, tw, d, hs, v0, v1, gpf, g0, g1);
+      if (a.trace) {   // diagnostics: the inverse transforms done (LDS results waited for)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        tt[3] |= (now_10ns() - tt[3]) << 40;   // (delta in the stamp's high bits)
+      }
       acc_fft_row<KM>(aR, 0, z, 2, d);
       acc_fft_row<KM>(aE, s, z, 0, d);
       acc_fft_row<KM>(aE, o, z, 1, d);

@@ -56,6 +56,8 @@ def main():
             np.percentile(us[1:-1], 90), us.sum(), len(us)))
         nb_, na = int(tr[0]), int(tr[1])
         B = tr[2:2 + 6 * nb_].reshape(nb_, 6).astype(np.int64)
+        inv = B[:, 3] >> 40                   # violating: inverse-transform phase (delta)
+        B[:, 3] = B[:, 3] & ((1 << 40) - 1)
         A = tr[2 + 6 * nb_:2 + 6 * nb_ + 2 * na].reshape(na, 2).astype(np.int64)
         A = A[A[:, 0] > 0]
         t0 = min(B[:, 0].min(), A[:, 0].min() if len(A) else B[:, 0].min())
@@ -74,6 +76,8 @@ def main():
         print("B settle (none pending)  ", pct((B[:, 2] - B[:, 1])[pend == 0]))
         print("B stage+2 corr+scores    ", pct(B[:, 3] - B[:, 2]))
         print("B rows+atomics (viol)    ", pct((B[:, 4] - B[:, 3])[viol == 1]))
+        print("  of which H + inverse   ", pct(inv[viol == 1]))
+        print("  then rows' atomics     ", pct((B[:, 4] - B[:, 3] - inv)[viol == 1]))
         print("B end (not violating)    ", pct((B[:, 4] - t0)[viol == 0]))
         print("B end (violating)        ", pct((B[:, 4] - t0)[viol == 1]))
         if len(A):

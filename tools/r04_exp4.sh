@@ -7,4 +7,5 @@ export TMPDIR=/tmp
 SKGE_PIPE_SPLIT=1 TAG=r04g STEPS="tests:tests/test_gpu_device_loop.py" bash tools/gpu_run.sh || exit $?
 AB="s0 SKGE_PIPE_SPLIT=0;s1 SKGE_PIPE_SPLIT=1;s0b SKGE_PIPE_SPLIT=0;s1b SKGE_PIPE_SPLIT=1" timeout -k 10 400 bash tools/ab_pipe.sh || exit $?
 SKGE_PIPE_SPLIT=1 TAG=r04pt2s STEPS="tool:pipe_trace.py,--nb,2,--launch,2" bash tools/gpu_run.sh || exit $?
+TAG=r04ht2 STEPS="tool:hole_trace.py" bash tools/gpu_run.sh || exit $?
 exit 0
