@@ -1636,9 +1636,12 @@ __device__ __forceinline__ void load_f32_row(const float* P, const float* A, con
   }
 }
 
-template <int KQ>
+// SPEC (spectral entity sums): the summed Z' is inverse-transformed in the
+// wave's buffers (wb, tw) first
+template <int KQ, bool SPEC = false>
 __device__ __forceinline__ void claim_and_apply_f(const PipeTab& t, int pp, int row, int d,
-                                                  int gp) {
+                                                  int gp, float* wb = nullptr,
+                                                  const float2* tw = nullptr) {
   const int l = lane_id(), nq = d >> 2;
   int c = 0;
   if (l == 0) c = atomicExch(t.cnt[pp] + row, 0);
@@ -1647,6 +1650,7 @@ __device__ __forceinline__ void claim_and_apply_f(const PipeTab& t, int pp, int 
   load_f32_row<KQ>(t.P, t.A, S, row, d, p, a, sm);
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row
+  if constexpr (SPEC) spec_to_spatial<KQ>(wb, tw, d, sm);
   row_update_f<KQ>(t.u, c, d, sm, p, a);
   float4* srow = reinterpret_cast<float4*>(S + (size_t)row * d);
 #pragma unroll
@@ -1711,9 +1715,10 @@ __device__ __forceinline__ void claim_and_apply_group_f(const PipeTab& t, int pp
 // slots cost nothing more), and each touched row's claim and loads are issued
 // while the previous row is updated and published, so a wave's rows overlap
 // instead of paying a dependent slot load + claim round trip each.
-template <int KQ>
+template <int KQ, bool SPEC = false>
 __device__ __forceinline__ void apply_slots_f(const PipeTab& t, int pp, int k0, int ks, int ns,
-                                              int d, int gp) {
+                                              int d, int gp, float* wb = nullptr,
+                                              const float2* tw = nullptr) {
   const int l = lane_id(), nq = d >> 2;
   float* S = reinterpret_cast<float*>(t.sum[pp]);
   for (int base = k0; base < ns; base += 64 * ks) {
@@ -1740,6 +1745,7 @@ __device__ __forceinline__ void apply_slots_f(const PipeTab& t, int pp, int k0, 
       }
       c = __builtin_amdgcn_readfirstlane(c);
       if (c != 0) {   // this wave owns the row
+        if constexpr (SPEC) spec_to_spatial<KQ>(wb, tw, d, sm);
         row_update_f<KQ>(t.u, c, d, sm, p, a);
         float4* srow = reinterpret_cast<float4*>(S + (size_t)r * d);
 #pragma unroll
@@ -1765,11 +1771,12 @@ __device__ __forceinline__ void apply_slots_f(const PipeTab& t, int pp, int k0, 
   }
 }
 
-template <int KQ>
+template <int KQ, bool SPEC = false>
 __device__ __forceinline__ void ensure_applied_f(const PipeTab& t, int pp, int row, int d, int gp,
-                                                 int* err) {
+                                                 int* err, float* wb = nullptr,
+                                                 const float2* tw = nullptr) {
   if (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gp) return;
-  claim_and_apply_f<KQ>(t, pp, row, d, gp);
+  claim_and_apply_f<KQ, SPEC>(t, pp, row, d, gp, wb, tw);
   unsigned spins = 0;
   while (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gp) {
     __builtin_amdgcn_s_sleep(2);
@@ -1861,8 +1868,9 @@ __device__ __forceinline__ void rel_publish_f(const PipeArgs& a, int w, int rd, 
 #define SKGE_HPIPE_ATTR
 #endif
 
-template <int KM, bool FFT>
+template <int KM, bool FFT, bool SPEC = false>
 __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(PipeArgs a) {
+  static_assert(!SPEC || FFT, "spectral entity sums need the FFT form");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6;
   const int l = lane_id();
@@ -1882,12 +1890,18 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     const int wa = blk_a * wpb + wave;
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
     if (a.b == a.nb1 && wa == 0) fold_shards(a.nviol_shards, a.nviol_total);
+    float2* const twA = reinterpret_cast<float2*>(smem);
+    float* const wbA = smem + 2 * d + wave * hole_fft_wave_floats(d);
+    if constexpr (SPEC) {   // the appliers' inverse transforms need the twiddles
+      fft_twiddles(twA, a.tw, d);
+      __syncthreads();
+    }
 #if SKGE_HPIPE_SLOTS_PREFETCH
     // items w = wa, wa + S, ...: relation rows w < nR, then entity slots w - nR
     const int S = a.nA * wpb;
     for (int w = wa; w < nR; w += S) rel_publish_f<1>(a, w, rd, rw, ra_prev, ra_old);
     const int k0 = wa >= nR ? wa - nR : wa - nR + ((nR - wa + S - 1) / S) * S;
-    apply_slots_f<1>(a.E, pp, k0, S, a.prev_slots, d, gp);
+    apply_slots_f<1, SPEC>(a.E, pp, k0, S, a.prev_slots, d, gp, wbA, twA);
 #else
     const int total = nR + (a.prev_slots + HGROUP - 1) / HGROUP;   // relation rows, slot groups
     for (int w = wa; w < total; w += a.nA * wpb) {
@@ -1953,7 +1967,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) {
         if (!((pend >> k) & 1ull)) continue;
-        ensure_applied_f<1>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err);
+        ensure_applied_f<1, SPEC>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err, wb, tw);
       }
       if (pend & 1ull) load_row4_sc1<1>(a.E.P, s, d, es);
       if (pend & 2ull) load_row4_sc1<1>(a.E.P, o, d, eo);
@@ -2008,7 +2022,21 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     Accum aR = {};   // mode ACC_F32 (0), one copy
     aR.sum = racc + (size_t)p * rstride;
     aR.width = d;
-    if constexpr (FFT) {
+    if constexpr (SPEC) {
+      int ne;
+      const float* zr = hole_fft_rows_spec(wb, tw, d, hs, v0, v1, gpf, g0, g1, ne);
+      if (a.trace) {   // diagnostics: the inverse transform done (LDS results waited for)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        tt[3] |= (now_10ns() - tt[3]) << 40;
+      }
+      const float* zs = wb;   // the entity rows' Z', signals 0 .. ne - 1
+      acc_fft_row<KM>(aR, 0, zr, 0, d);
+      acc_fft_row<KM>(aE, s, zs, 0, d);
+      acc_fft_row<KM>(aE, o, zs, 1, d);
+      if (v0) acc_fft_row<KM>(aE, neg0, zs, 2, d);
+      if (v1) acc_fft_row<KM>(aE, neg1, zs, 2 + v0, d);
+      (void)ne;
+    } else if constexpr (FFT) {
       const float* z = hole_fft_rows(wb, tw, d, hs, v0, v1, gpf, g0, g1);
       if (a.trace) {   // diagnostics: the inverse transforms done (LDS results waited for)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2170,6 +2198,8 @@ struct skge_pipe_runner {
   bool hole = false;               // HolE pairwise (k_hole_pipe, fp32 sums)
   bool fft = false;                // HolE: correlations in the frequency domain (skge_hole_fft.h)
   bool rfold = false;              // TransE: relation sums in replicas, k_rel_fold after each batch
+  bool spec = false;               // HolE FFT: entity sums as pre-processed half spectra
+                                   // (SKGE_HPIPE_SPEC; hole_fft_rows_spec / spec_to_spatial)
   bool split = false;              // SKGE_PIPE_SPLIT: apply and scoring roles as two kernels on
                                    // parallel branches (large batches: own register budgets)
   hipStream_t st2 = nullptr;       // split: the scoring kernels' capture stream
@@ -2286,10 +2316,12 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
   } while (0)
     if (r->hole) {
       const dim3 gr(r->grid[k]), bl(SKGE_PIPE_WG);
-#define SKGE_HPIPE(K)                                                   \
-  if (r->fft)                                                           \
-    hipLaunchKernelGGL((k_hole_pipe<K, true>), gr, bl, r->lds, st, a);  \
-  else                                                                  \
+#define SKGE_HPIPE(K)                                                          \
+  if (r->fft && r->spec)                                                       \
+    hipLaunchKernelGGL((k_hole_pipe<K, true, true>), gr, bl, r->lds, st, a);   \
+  else if (r->fft)                                                             \
+    hipLaunchKernelGGL((k_hole_pipe<K, true>), gr, bl, r->lds, st, a);         \
+  else                                                                         \
     hipLaunchKernelGGL((k_hole_pipe<K, false>), gr, bl, r->lds, st, a);
       switch (km_for(a.d)) {
         case 1: SKGE_HPIPE(1) break;
@@ -2527,6 +2559,10 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     if (!hole && paf && atoi(paf) == 0) a.b_first = 1;
   }
   r->fft = hole && hole_use_fft(d);
+  {
+    const char* sp = getenv("SKGE_HPIPE_SPEC");   // A/B: spectral entity sums
+    r->spec = r->fft && sp && atoi(sp) != 0;
+  }
   a.tw = r->fft ? hole_fft_table(d) : nullptr;
   if (r->fft && !a.tw) {
     set_error("pipelined runner: HolE FFT twiddle table allocation failed");
@@ -2571,7 +2607,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     // FFT variant (133 VGPRs, 3 waves per SIMD): the cap of a 4-wave residency,
     // measured best on WN18 d = 200 (caps 150 / 250 / 400 / 600 / 800 / 1100:
     // 74.7 / 77.6 / 80.5 / 81.7 / 75.4 / 70.5 M triples/s)
-    const int occ = r->fft ? 4 : SKGE_HPIPE_OCC;
+    const int occ = r->fft ? (r->spec ? 3 : 4) : SKGE_HPIPE_OCC;   // (spec: 149 VGPRs)
     int a_cap = hole && b < nb1 ? std::max(1, (occ * 4 * 256 - (int)((batches[b].second + WPB - 1) / WPB) * WPB) / WPB - 8) : 16384;
     // (large batches: more scoring waves than the chip holds -- they run in
     // rounds anyway -- so the apply waves get a fixed share instead of the
