@@ -2017,6 +2017,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     }
     if (v0 + v1 == 0) continue;
     nv += v0 + v1;
+    unsigned long long inv_dt = 0ull;            // diagnostics: the inverse-transform phase
     const float gpf = -af_g_given_f(a.af, pf);   // hole.py:66
     const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
     Accum aR = {};   // mode ACC_F32 (0), one copy
@@ -2027,7 +2028,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
       const float* zr = hole_fft_rows_spec(wb, tw, d, hs, v0, v1, gpf, g0, g1, ne);
       if (a.trace) {   // diagnostics: the inverse transform done (LDS results waited for)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        tt[3] |= (now_10ns() - tt[3]) << 40;
+        inv_dt = now_10ns() - tt[3];
       }
       const float* zs = wb;   // the entity rows' Z', signals 0 .. ne - 1
       acc_fft_row<KM>(aR, 0, zr, 0, d);
@@ -2040,7 +2041,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
       const float* z = hole_fft_rows(wb, tw, d, hs, v0, v1, gpf, g0, g1);
       if (a.trace) {   // diagnostics: the inverse transforms done (LDS results waited for)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        tt[3] |= (now_10ns() - tt[3]) << 40;   // (delta in the stamp's high bits)
+        inv_dt = now_10ns() - tt[3];   // (reported in the flags word's high bits)
       }
       acc_fft_row<KM>(aR, 0, z, 2, d);
       acc_fft_row<KM>(aE, s, z, 0, d);
@@ -2061,7 +2062,8 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     if (a.trace && l == 0) {   // stamp after issue (no drain)
       unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
       tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
-      tr[5] = pend | (1ull << 8) | ((unsigned long long)v0 << 9) | ((unsigned long long)v1 << 10);
+      tr[5] = pend | (1ull << 8) | ((unsigned long long)v0 << 9) | ((unsigned long long)v1 << 10) |
+              (inv_dt << 16);
     }
   }
   if (l == 0 && nv) {

@@ -56,8 +56,8 @@ def main():
             np.percentile(us[1:-1], 90), us.sum(), len(us)))
         nb_, na = int(tr[0]), int(tr[1])
         B = tr[2:2 + 6 * nb_].reshape(nb_, 6).astype(np.int64)
-        inv = B[:, 3] >> 40                   # violating: inverse-transform phase (delta)
-        B[:, 3] = B[:, 3] & ((1 << 40) - 1)
+        inv = B[:, 5] >> 16                   # violating: inverse-transform phase (10 ns ticks)
+        B[:, 5] = B[:, 5] & 0xffff
         A = tr[2 + 6 * nb_:2 + 6 * nb_ + 2 * na].reshape(na, 2).astype(np.int64)
         A = A[A[:, 0] > 0]
         t0 = min(B[:, 0].min(), A[:, 0].min() if len(A) else B[:, 0].min())
