@@ -464,7 +464,7 @@ def main():
     acc_names = {"entity": acc_label(runner.accE), "relation": acc_label(runner.accR)}
     launch_us_max = max_over_ranks(prof["dominant"]["avg_us"], world, dev)
     one_model = None
-    if world > 1:
+    if world > 1 and os.environ.get("SKGE_BENCH_DP_DETAIL", "1") != "0":
         # the one-model data-parallel runner beside the replicas:
         # union batch = the reference's 1414 (strong scaling), and 1414 per GPU
         # (union batch N x 1414) with the one-GPU runner at that union batch
@@ -553,7 +553,7 @@ def main():
                 "one_model_dp": one_model,
             },
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -736,7 +736,7 @@ def run_dp(args):
             "detail": dict(m, runner="DataParallelRunner (skge_amd.dp)",
                            one_gpu_same_geometry=same_geo),
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     dist.destroy_process_group()
 
 
@@ -1050,7 +1050,7 @@ def run_config5(args):
                                                     / 1000.0 / args.steps, 3),
                        "gpu_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)},
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -1207,7 +1207,7 @@ def run_config5_sharded(args):
                                    for n, v in prof["kernels"].items()},
                        "gpu_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)},
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -1429,7 +1429,7 @@ def run_config34(args):
                        "batches": len(batch_sizes(N_TRIPLES, nb)),
                        "large_batch": large},
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
