@@ -228,6 +228,57 @@ __device__ __forceinline__ float2* fft_run_c(float2* x, float2* y, const float2*
   }
 }
 
+// Pair form (round 4, SKGE_HPIPE_PAIR): the two waves of a 128-thread
+// workgroup run ONE positive's transforms together in the workgroup's
+// buffers -- wave h takes the stage passes j = h, h + 2, ... of
+// fft_stage_c, so each butterfly is the same arithmetic on the same inputs
+// (the same bits as fft_run_c) and a stage boundary is a workgroup barrier.
+template <int R, bool INV, int M, int NT, int P>
+__device__ __forceinline__ void fft_stage_c2(const float2* x, float2* y, const float2* tw, int h) {
+  constexpr int T = M / R, n = NT * T, stw = 2 * M / (P * R), NP = (n + 63) / 64;
+  int l = lane_id();
+  asm volatile("" : "+v"(l));
+#pragma unroll
+  for (int jj = 0; jj < (NP + 1) / 2; ++jj) {
+    const int b = l + 64 * (2 * jj + h);
+    if (b < n) {
+      const int tr = b / T, i = b - tr * T;
+      const int ip = i / P, k = i - ip * P;
+      const float2* xs = x + tr * M + i;
+      float2 u[R], v[R];
+#pragma unroll
+      for (int q = 0; q < R; ++q) u[q] = xs[q * T];
+      if (P > 1) {
+#pragma unroll
+        for (int q = 1; q < R; ++q) {
+          float2 w = tw[q * k * stw];
+          if (INV) w.y = -w.y;
+          u[q] = cmul(u[q], w);
+        }
+      }
+      fft_dft<R, INV>(u, v);
+      float2* ys = y + tr * M + ip * P * R + k;
+#pragma unroll
+      for (int t = 0; t < R; ++t) ys[t * P] = v[t];
+    }
+  }
+}
+
+// fft_run_c over the pair (entered after a barrier that published the
+// inputs; returns after the barrier that publishes the output)
+template <int M, int NT, bool INV, int P = 1, int MR = M>
+__device__ __forceinline__ float2* fft_run_c2(float2* x, float2* y, const float2* tw, int h) {
+  if constexpr (MR == 1) {
+    return x;
+  } else {
+    constexpr int R = MR % 4 == 0 ? 4 : (MR % 2 == 0 ? 2 : (MR % 3 == 0 ? 3 : 5));
+    static_assert(MR % R == 0, "the transform length must factor into 2, 3 and 5");
+    fft_stage_c2<R, INV, M, NT, P>(x, y, tw, h);
+    __syncthreads();
+    return fft_run_c2<M, NT, INV, P * R, MR / R>(y, x, tw, h);
+  }
+}
+
 // quad-layout real row -> complex signal t of buffer b (z[2l], z[2l+1])
 __device__ __forceinline__ void fft_put_row(float2* b, int M, int t, const float4& v, int d) {
   const int l = lane_id();
@@ -290,21 +341,12 @@ struct HoleSpec {
   int k;
   bool on;                                   // lane holds a pair
 };
-__device__ __forceinline__ HoleSpec hole_fft_forward(float* wbuf, const float2* tw, int d,
-                                                     const float4& rp, const float4& es,
-                                                     const float4& fs, const float4& eo,
-                                                     const float4& fo, float& praw, float& raw0,
-                                                     float& raw1) {
+// the spectra at (k, M - k) of the five transformed rows in Z and the three
+// raw scores (hole_fft_forward's second half; the pair form calls it in both
+// waves, which then hold the same values)
+__device__ __forceinline__ HoleSpec hole_fft_spectra(const float2* Z, const float2* tw, int d,
+                                                     float& praw, float& raw0, float& raw1) {
   const int M = d / 2;
-  float2* b0 = reinterpret_cast<float2*>(wbuf);
-  float2* b1 = b0 + 5 * M;
-  fft_put_row(b0, M, 0, rp, d);
-  fft_put_row(b0, M, 1, es, d);
-  fft_put_row(b0, M, 2, fs, d);
-  fft_put_row(b0, M, 3, eo, d);
-  fft_put_row(b0, M, 4, fo, d);
-  const float2* Z = M == 100 ? fft_run_c<100, 5, false>(b0, b1, tw)
-                             : fft_run<false>(b0, b1, M, 5, tw, d);
   HoleSpec h;
   h.k = lane_id();
   h.on = h.k <= M / 2;
@@ -329,41 +371,70 @@ __device__ __forceinline__ HoleSpec hole_fft_forward(float* wbuf, const float2* 
   return h;
 }
 
+__device__ __forceinline__ HoleSpec hole_fft_forward(float* wbuf, const float2* tw, int d,
+                                                     const float4& rp, const float4& es,
+                                                     const float4& fs, const float4& eo,
+                                                     const float4& fo, float& praw, float& raw0,
+                                                     float& raw1) {
+  const int M = d / 2;
+  float2* b0 = reinterpret_cast<float2*>(wbuf);
+  float2* b1 = b0 + 5 * M;
+  fft_put_row(b0, M, 0, rp, d);
+  fft_put_row(b0, M, 1, es, d);
+  fft_put_row(b0, M, 2, fs, d);
+  fft_put_row(b0, M, 3, eo, d);
+  fft_put_row(b0, M, 4, fo, d);
+  const float2* Z = M == 100 ? fft_run_c<100, 5, false>(b0, b1, tw)
+                             : fft_run<false>(b0, b1, M, 5, tw, d);
+  return hole_fft_spectra(Z, tw, d, praw, raw0, raw1);
+}
+
 // Inverse phase of a violating positive: the contribution rows of
 // hole_pos_rows as real rows in LDS -- the inverse transforms' output, whose
 // complex interleave (z_m = x_{2m} + i x_{2m+1}) is the real row in natural
 // order -- times 1/M.  Rows: 0 E[s], 1 E[o], 2 R[p], then E[s'] when v0, then
 // E[o'] when v1.  Returns the buffer (float view, row t at t * d).
+// the inverse transforms' inputs (pre-processed half spectra) of the
+// contribution rows t in [lo, hi): 0 E[s], 1 E[o], 2 R[p], then E[s'] (v0),
+// E[o'] (v1)
+__device__ __forceinline__ void hole_inv_inputs(float2* b0, int M, const float2* tw,
+                                                const HoleSpec& h, int v0, int v1, float gp,
+                                                float g0, float g1, int lo, int hi) {
+  if (!h.on) return;
+  const float cE = (float)(v0 + v1) * gp, cF = v1 ? g1 : 0.0f;   // E[s] row
+  const float cu = (float)(v0 + v1) * gp, cf = v0 ? g0 : 0.0f;   // u = cu E[s] + cf E[s']
+  float2 H[5][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float2 r = h.r[j], eo = h.eo[j], fo = h.fo[j], es = h.es[j];
+    const float2 uh = cadd(cscale(cu, es), cscale(cf, h.fs[j]));
+    H[0][j] = cmulc(r, cadd(cscale(cE, eo), cscale(cF, fo)));          // E[s]
+    H[1][j] = cmul(r, uh);                                            // E[o]
+    H[2][j] = cadd(cmulc(uh, eo), cscale(cF, cmulc(es, fo)));         // R[p]
+    H[3][j] = cscale(g0, cmulc(r, eo));                               // E[s'] (v0)
+    H[4][j] = cscale(g1, cmul(r, es));                                // E[o'] (v1)
+  }
+  const int k = h.k;
+  if (lo <= 0 && 0 < hi) fft_real_inv_pair(b0 + 0 * M, M, k, tw, H[0][0], H[0][1]);
+  if (lo <= 1 && 1 < hi) fft_real_inv_pair(b0 + 1 * M, M, k, tw, H[1][0], H[1][1]);
+  if (lo <= 2 && 2 < hi) fft_real_inv_pair(b0 + 2 * M, M, k, tw, H[2][0], H[2][1]);
+  int t = 3;
+  if (v0) {
+    if (lo <= t && t < hi) fft_real_inv_pair(b0 + t * M, M, k, tw, H[3][0], H[3][1]);
+    ++t;
+  }
+  if (v1 && lo <= t && t < hi) fft_real_inv_pair(b0 + t * M, M, k, tw, H[4][0], H[4][1]);
+}
+
 __device__ __forceinline__ const float* hole_fft_rows(float* wbuf, const float2* tw, int d,
                                                       const HoleSpec& h, int v0, int v1,
                                                       float gp, float g0, float g1) {
   const int M = d / 2;
   float2* b0 = reinterpret_cast<float2*>(wbuf);
   float2* b1 = b0 + 5 * M;
-  const float cE = (float)(v0 + v1) * gp, cF = v1 ? g1 : 0.0f;   // E[s] row
-  const float cu = (float)(v0 + v1) * gp, cf = v0 ? g0 : 0.0f;   // u = cu E[s] + cf E[s']
   const int nt = 3 + v0 + v1;
   __builtin_amdgcn_wave_barrier();   // every lane is done reading the forward buffers
-  if (h.on) {
-    float2 H[5][2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float2 r = h.r[j], eo = h.eo[j], fo = h.fo[j], es = h.es[j];
-      const float2 uh = cadd(cscale(cu, es), cscale(cf, h.fs[j]));
-      H[0][j] = cmulc(r, cadd(cscale(cE, eo), cscale(cF, fo)));          // E[s]
-      H[1][j] = cmul(r, uh);                                            // E[o]
-      H[2][j] = cadd(cmulc(uh, eo), cscale(cF, cmulc(es, fo)));         // R[p]
-      H[3][j] = cscale(g0, cmulc(r, eo));                               // E[s'] (v0)
-      H[4][j] = cscale(g1, cmul(r, es));                                // E[o'] (v1)
-    }
-    const int k = h.k;
-    fft_real_inv_pair(b0 + 0 * M, M, k, tw, H[0][0], H[0][1]);
-    fft_real_inv_pair(b0 + 1 * M, M, k, tw, H[1][0], H[1][1]);
-    fft_real_inv_pair(b0 + 2 * M, M, k, tw, H[2][0], H[2][1]);
-    int t = 3;
-    if (v0) fft_real_inv_pair(b0 + (t++) * M, M, k, tw, H[3][0], H[3][1]);
-    if (v1) fft_real_inv_pair(b0 + t * M, M, k, tw, H[4][0], H[4][1]);
-  }
+  hole_inv_inputs(b0, M, tw, h, v0, v1, gp, g0, g1, 0, 5);
   float2* z;
   if (M == 100 && nt == 5)
     z = fft_run_c<100, 5, true>(b0, b1, tw);
@@ -371,6 +442,23 @@ __device__ __forceinline__ const float* hole_fft_rows(float* wbuf, const float2*
     z = fft_run_c<100, 4, true>(b0, b1, tw);
   else
     z = fft_run<true>(b0, b1, M, nt, tw, d);
+  return reinterpret_cast<const float*>(z);
+}
+
+// Pair form of hole_fft_rows (M = 100): both waves hold the spectra h; wave hw
+// writes its share of the inverse inputs (0: rows 0-2, 1: the negatives'
+// rows), then the pair runs the transforms.  Same bits as hole_fft_rows.
+__device__ __forceinline__ const float* hole_fft_rows_pair(float* wbuf, const float2* tw,
+                                                           const HoleSpec& h, int v0, int v1,
+                                                           float gp, float g0, float g1, int hw) {
+  constexpr int M = 100;
+  float2* b0 = reinterpret_cast<float2*>(wbuf);
+  float2* b1 = b0 + 5 * M;
+  __syncthreads();   // both waves are done reading the forward buffers
+  hole_inv_inputs(b0, M, tw, h, v0, v1, gp, g0, g1, hw ? 3 : 0, hw ? 5 : 3);
+  __syncthreads();
+  float2* z = v0 + v1 == 2 ? fft_run_c2<M, 5, true>(b0, b1, tw, hw)
+                           : fft_run_c2<M, 4, true>(b0, b1, tw, hw);
   return reinterpret_cast<const float*>(z);
 }
 

@@ -1868,9 +1868,114 @@ __device__ __forceinline__ void rel_publish_f(const PipeArgs& a, int w, int rd, 
 #define SKGE_HPIPE_ATTR
 #endif
 
-template <int KM, bool FFT, bool SPEC = false>
+// PAIR (round 4, SKGE_HPIPE_PAIR; FFT at d = 200, no SPEC): 128-thread
+// workgroups, and a scoring workgroup's two waves score ONE positive together
+// -- each loads and settles two of its rows, the transforms' stage passes are
+// split between them (fft_run_c2: the same butterflies, the same bits), both
+// compute the spectra and scores (identical values), and each issues half of
+// the contribution rows' atomics -- so a positive's serial chain is shorter.
+template <int KM>
+__device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* smem, int blk_b,
+                                                     int nB) {
+  const int hw = (int)(threadIdx.x >> 6);   // the wave's half of the pair
+  const int l = lane_id();
+  const int d = a.d;
+  const int g = launch_id(a), gp = g - 1;
+  const int cp = a.b & 1, pp = cp ^ 1;
+  const int rd = a.b & 1;
+  const int ra_prev = (g - 1) % 3, ra_cur = g % 3;
+  float2* const tw = reinterpret_cast<float2*>(smem);
+  fft_twiddles(tw, a.tw, d);
+  float* const wb = smem + 2 * d;   // the pair's two transform buffers
+  float2* const b0 = reinterpret_cast<float2*>(wb);
+  float2* const b1 = b0 + 5 * 100;
+  Accum aE = {};
+  aE.sum = reinterpret_cast<float*>(a.E.sum[cp]);
+  aE.width = d;
+  const int rstride = 2 * a.R.rw;
+  int nv = 0;
+  for (int w = blk_b; w < a.count; w += nB) {
+    float* const racc = reinterpret_cast<float*>(a.R.acc[ra_cur]) +
+                        (size_t)(w % a.R.reps) * a.R.rows * rstride;
+    const long long j = a.start + w;
+    const int4 r4 = a.rec[j];
+    const int r1 = a.rec_n1[j];
+    __builtin_amdgcn_sched_barrier(0);
+    const int s = uni(r4.x), o = uni(r4.y), p = uni(r4.z), neg0 = uni(r4.w);
+    const int neg1 = uni(r1);
+    const int n0r = neg0 >= 0 ? neg0 : s, n1r = neg1 >= 0 ? neg1 : o;
+    // wave 0: R[p], E[s], E[s'] (signals 0-2); wave 1: E[o], E[o'] (3, 4)
+    const int ra_row = hw ? o : s, rb_row = hw ? n1r : n0r;
+    float4 xa[1], xb[1], xr[1];
+    load_row4<1>(a.E.P, ra_row, d, xa);
+    load_row4<1>(a.E.P, rb_row, d, xb);
+    int mark = 0;
+    if (l < 2) mark = a.E.pend[pp][l ? rb_row : ra_row];
+    if (hw == 0) {
+      float4 rav[1];
+      int c;
+      rel_row_f<1>(a.R, p, d, rd, ra_prev, xr, rav, c);
+    }
+    const uint64_t pend = __ballot(mark == gp) & 0x3ull;
+    if (pend) {
+      if (pend & 1ull) ensure_applied_f<1>(a.E, pp, ra_row, d, gp, a.err);
+      if (pend & 2ull) ensure_applied_f<1>(a.E, pp, rb_row, d, gp, a.err);
+      if (pend & 1ull) load_row4_sc1<1>(a.E.P, ra_row, d, xa);
+      if (pend & 2ull) load_row4_sc1<1>(a.E.P, rb_row, d, xb);
+    }
+    __syncthreads();   // the previous positive's buffers are free, the twiddles in place
+    if (hw == 0) {
+      fft_put_row(b0, 100, 0, xr[0], d);
+      fft_put_row(b0, 100, 1, xa[0], d);
+      fft_put_row(b0, 100, 2, xb[0], d);
+    } else {
+      fft_put_row(b0, 100, 3, xa[0], d);
+      fft_put_row(b0, 100, 4, xb[0], d);
+    }
+    __syncthreads();
+    const float2* Z = fft_run_c2<100, 5, false>(b0, b1, tw, hw);
+    float praw, raw0, raw1;
+    const HoleSpec hs = hole_fft_spectra(Z, tw, d, praw, raw0, raw1);
+    const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
+    const int v0 = uni((neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0);   // hole.py:56
+    const int v1 = uni((neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0);
+    if (hw == 0) {
+      const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
+      const int rE = sel4(l, s, o, neg0, neg1);
+      if (l < 4) {
+        commit_slot(a.E.cnt[cp], a.E.touched[cp], rE, cE, 4 * w + l);
+        if (cE > 0) a.E.pend[cp][rE] = g;
+      } else if (l == 4 && v0 + v1 > 0) {
+        atomicAdd(reinterpret_cast<int*>(racc + (size_t)p * rstride + d), 2 * (v0 + v1));
+      }
+      nv += v0 + v1;
+    }
+    if (v0 + v1 == 0) continue;   // (the same in both waves)
+    const float gpf = -af_g_given_f(a.af, pf);   // hole.py:66
+    const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
+    const float* z = hole_fft_rows_pair(wb, tw, hs, v0, v1, gpf, g0, g1, hw);
+    if (hw == 0) {
+      Accum aR = {};
+      aR.sum = racc + (size_t)p * rstride;
+      aR.width = d;
+      acc_fft_row<KM>(aR, 0, z, 2, d);
+      acc_fft_row<KM>(aE, s, z, 0, d);
+    } else {
+      acc_fft_row<KM>(aE, o, z, 1, d);
+      if (v0) acc_fft_row<KM>(aE, neg0, z, 3, d);
+      if (v1) acc_fft_row<KM>(aE, neg1, z, 3 + v0, d);
+    }
+  }
+  if (l == 0 && nv) {
+    atomicAdd(shard_of(a.nviol_shards), nv);
+    if (a.stats_viol) atomicAdd(shard_of(a.stats_viol), nv);
+  }
+}
+
+template <int KM, bool FFT, bool SPEC = false, bool PAIR = false>
 __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(PipeArgs a) {
   static_assert(!SPEC || FFT, "spectral entity sums need the FFT form");
+  static_assert(!PAIR || (FFT && !SPEC), "the pair form is the FFT form's");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6;
   const int l = lane_id();
@@ -1920,6 +2025,10 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
   }
   // ---- B role: score batch b (k_hole_pos's arithmetic), scatter into cp / ra_cur ----
   const int blk_b = a.b_first ? blk : blk - a.nA;
+  if constexpr (PAIR) {
+    hole_pipe_score_pair<KM>(a, smem, blk_b, nB);
+    return;
+  }
   // FFT: the workgroup's twiddle table, then per wave two transform buffers
   float2* const tw = reinterpret_cast<float2*>(smem);
   if constexpr (FFT) {
@@ -2207,6 +2316,7 @@ struct skge_pipe_runner {
   hipStream_t st2 = nullptr;       // split: the scoring kernels' capture stream
   hipEvent_t fork = nullptr, join = nullptr;
   size_t lds = 0;                  // HolE: dynamic LDS per workgroup
+  bool pair = false;               // HolE FFT, d = 200: two waves per positive (SKGE_HPIPE_PAIR)
   int nlaunch() const { return (int)batch.size() + 2; }
 };
 
@@ -2317,9 +2427,11 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
     }                                                                                            \
   } while (0)
     if (r->hole) {
-      const dim3 gr(r->grid[k]), bl(SKGE_PIPE_WG);
+      const dim3 gr(r->grid[k]), bl(r->pair ? 128 : SKGE_PIPE_WG);
 #define SKGE_HPIPE(K)                                                          \
-  if (r->fft && r->spec)                                                       \
+  if (r->pair)                                                                 \
+    hipLaunchKernelGGL((k_hole_pipe<K, true, false, true>), gr, bl, r->lds, st, a); \
+  else if (r->fft && r->spec)                                                  \
     hipLaunchKernelGGL((k_hole_pipe<K, true, true>), gr, bl, r->lds, st, a);   \
   else if (r->fft)                                                             \
     hipLaunchKernelGGL((k_hole_pipe<K, true>), gr, bl, r->lds, st, a);         \
@@ -2565,6 +2677,17 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     const char* sp = getenv("SKGE_HPIPE_SPEC");   // A/B: spectral entity sums
     r->spec = r->fft && sp && atoi(sp) != 0;
   }
+  {
+    // two waves per positive (default while the batch's 2 x B scoring waves fit
+    // the chip's 4-wave-per-SIMD residency; SKGE_HPIPE_PAIR=0/1 forces).  WN18
+    // d = 200, same box: nb = 100 93.7 -> 106.7 M triples/s (14.6 -> 12.8 us per
+    // launch); nb = 2 (70k positives per launch) 157 -> 142 M, so off there
+    const char* pe = getenv("SKGE_HPIPE_PAIR");
+    int64_t maxb = 0;
+    for (const auto& bt : batches) maxb = std::max(maxb, bt.second);
+    const bool fits = 2 * maxb <= 4 * 4 * 256;
+    r->pair = r->fft && !r->spec && d == 200 && (pe ? atoi(pe) != 0 : fits);
+  }
   a.tw = r->fft ? hole_fft_table(d) : nullptr;
   if (r->fft && !a.tw) {
     set_error("pipelined runner: HolE FFT twiddle table allocation failed");
@@ -2572,6 +2695,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     return nullptr;
   }
   r->lds = !hole ? 0
+           : r->pair ? hole_fft_lds_bytes(d, 1)
            : r->fft ? hole_fft_lds_bytes(d, SKGE_PIPE_WG / 64)
                     : (size_t)(SKGE_PIPE_WG / 64) * hole_pos_lds_floats(d) * sizeof(float);
   // A-role entity groups (SKGE_PIPE_AGRP: slots per group of AGRP_WAVES waves, <= 64)
@@ -2601,16 +2725,17 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
                                                       : a.E.a4 ? prev
                                                       : a.E.agrp ? AGRP_WAVES * ((4 * prev + a.E.agrp - 1) / a.E.agrp)
                                                                  : (4 * prev + ASLOTS - 1) / ASLOTS);
-    constexpr int WPB = SKGE_PIPE_WG / 64;
+    const int WPB = r->pair ? 2 : SKGE_PIPE_WG / 64;
     // HolE: the apply waves loop over their items within the residency the
     // scoring waves leave (SKGE_HPIPE_OCC waves per SIMD: 2 at ~180 VGPRs; the
     // flush has the chip to itself)
-    auto nBwaves = [](long long cnt) { return (cnt + WPB - 1) / WPB * WPB; };
+    // (pair: two waves per positive, one positive per workgroup)
+    auto nBwaves = [&](long long cnt) { return r->pair ? 2 * cnt : (cnt + WPB - 1) / WPB * WPB; };
     // FFT variant (133 VGPRs, 3 waves per SIMD): the cap of a 4-wave residency,
     // measured best on WN18 d = 200 (caps 150 / 250 / 400 / 600 / 800 / 1100:
     // 74.7 / 77.6 / 80.5 / 81.7 / 75.4 / 70.5 M triples/s)
     const int occ = r->fft ? (r->spec ? 3 : 4) : SKGE_HPIPE_OCC;   // (spec: 149 VGPRs)
-    int a_cap = hole && b < nb1 ? std::max(1, (occ * 4 * 256 - (int)((batches[b].second + WPB - 1) / WPB) * WPB) / WPB - 8) : 16384;
+    int a_cap = hole && b < nb1 ? std::max(1, (occ * 4 * 256 - (int)nBwaves(batches[b].second)) / WPB - 8) : 16384;
     // (large batches: more scoring waves than the chip holds -- they run in
     // rounds anyway -- so the apply waves get a fixed share instead of the
     // residency left over, which would be none: nb = 2 on WN18 had 4 apply
@@ -2628,7 +2753,8 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     a.nA = std::max(1, std::min((a_items + WPB - 1) / WPB, std::min(a_cap, 16384)));
     int b_cap = 16384;
     if (!hole && getenv("SKGE_PIPE_BCAP")) b_cap = std::max(1, atoi(getenv("SKGE_PIPE_BCAP")));   // A/B
-    const int nBb = std::max(1, std::min((a.count + WPB - 1) / WPB, b_cap));
+    const int nBb = r->pair ? std::max(1, std::min(a.count, 2 * 16384))
+                            : std::max(1, std::min((a.count + WPB - 1) / WPB, b_cap));
     r->batch.push_back(a);
     r->grid.push_back(a.nA + (a.count > 0 ? nBb : 0));
     prev = a.count;
