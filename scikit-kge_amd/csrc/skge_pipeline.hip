@@ -1897,6 +1897,8 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
   for (int w = blk_b; w < a.count; w += nB) {
     float* const racc = reinterpret_cast<float*>(a.R.acc[ra_cur]) +
                         (size_t)(w % a.R.reps) * a.R.rows * rstride;
+    unsigned long long tt[4] = {0ull, 0ull, 0ull, 0ull};   // diagnostics: wave 0's phases
+    if (a.trace) tt[0] = now_10ns();
     const long long j = a.start + w;
     const int4 r4 = a.rec[j];
     const int r1 = a.rec_n1[j];
@@ -1917,12 +1919,14 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
       rel_row_f<1>(a.R, p, d, rd, ra_prev, xr, rav, c);
     }
     const uint64_t pend = __ballot(mark == gp) & 0x3ull;
+    if (a.trace) tt[1] = now_10ns();
     if (pend) {
       if (pend & 1ull) ensure_applied_f<1>(a.E, pp, ra_row, d, gp, a.err);
       if (pend & 2ull) ensure_applied_f<1>(a.E, pp, rb_row, d, gp, a.err);
       if (pend & 1ull) load_row4_sc1<1>(a.E.P, ra_row, d, xa);
       if (pend & 2ull) load_row4_sc1<1>(a.E.P, rb_row, d, xb);
     }
+    if (a.trace) tt[2] = now_10ns();
     __syncthreads();   // the previous positive's buffers are free, the twiddles in place
     if (hw == 0) {
       fft_put_row(b0, 100, 0, xr[0], d);
@@ -1939,6 +1943,17 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
     const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
     const int v0 = uni((neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0);   // hole.py:56
     const int v1 = uni((neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0);
+    if (a.trace) tt[3] = now_10ns();
+    // trace record of positive w (wave 0, lane 0): stamps, then the flags word
+    // (bits 0-1: wave 0's pending rows s, s'; 8 violating; 9 v0; 10 v1; 16+:
+    // the inverse phase in 10 ns ticks)
+    auto stamp = [&](unsigned long long flags) {
+      if (a.trace && hw == 0 && l == 0) {
+        unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
+        tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
+        tr[5] = flags;
+      }
+    };
     if (hw == 0) {
       const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
       const int rE = sel4(l, s, o, neg0, neg1);
@@ -1950,10 +1965,14 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
       }
       nv += v0 + v1;
     }
-    if (v0 + v1 == 0) continue;   // (the same in both waves)
+    if (v0 + v1 == 0) {   // (the same in both waves)
+      stamp(pend);
+      continue;
+    }
     const float gpf = -af_g_given_f(a.af, pf);   // hole.py:66
     const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
     const float* z = hole_fft_rows_pair(wb, tw, hs, v0, v1, gpf, g0, g1, hw);
+    const unsigned long long inv_dt = a.trace ? now_10ns() - tt[3] : 0ull;
     if (hw == 0) {
       Accum aR = {};
       aR.sum = racc + (size_t)p * rstride;
@@ -1965,6 +1984,9 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
       if (v0) acc_fft_row<KM>(aE, neg0, z, 3, d);
       if (v1) acc_fft_row<KM>(aE, neg1, z, 3 + v0, d);
     }
+    __builtin_amdgcn_wave_barrier();
+    stamp(pend | (1ull << 8) | ((unsigned long long)v0 << 9) | ((unsigned long long)v1 << 10) |
+          (inv_dt << 16));
   }
   if (l == 0 && nv) {
     atomicAdd(shard_of(a.nviol_shards), nv);
@@ -2734,7 +2756,8 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     // FFT variant (133 VGPRs, 3 waves per SIMD): the cap of a 4-wave residency,
     // measured best on WN18 d = 200 (caps 150 / 250 / 400 / 600 / 800 / 1100:
     // 74.7 / 77.6 / 80.5 / 81.7 / 75.4 / 70.5 M triples/s)
-    const int occ = r->fft ? (r->spec ? 3 : 4) : SKGE_HPIPE_OCC;   // (spec: 149 VGPRs)
+    const int occ = r->pair ? std::max(4, SKGE_HPIPE_OCC)   // (pair: 114 VGPRs)
+                  : r->fft ? (r->spec ? 3 : 4) : SKGE_HPIPE_OCC;   // (spec: 149 VGPRs)
     int a_cap = hole && b < nb1 ? std::max(1, (occ * 4 * 256 - (int)nBwaves(batches[b].second)) / WPB - 8) : 16384;
     // (large batches: more scoring waves than the chip holds -- they run in
     // rounds anyway -- so the apply waves get a fixed share instead of the

@@ -13,9 +13,6 @@ import argparse
 import os
 import sys
 
-# the per-wave trace is written by the one-wave-per-positive form only
-os.environ.setdefault("SKGE_HPIPE_PAIR", "0")
-
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "scikit-kge_amd"))
 sys.path.insert(0, ROOT)
