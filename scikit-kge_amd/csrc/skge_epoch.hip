@@ -728,14 +728,28 @@ extern "C" skge_runner_t* skge_runner_create(void* stream, int l1, const skge_ta
     return nullptr;
   }
   int rc = SKGE_OK;
+  // large batches: when a batch's entity slot records outnumber the table's
+  // rows, the entity table is applied densely (one wave per row, claimed as
+  // with slots) instead of one wave per slot record -- no duplicate slots whose
+  // waves load a row they then lose the claim for.  WN18 d = 200, same box:
+  // nb = 2 219 -> 254 M triples/s, nb = 10 203 -> 211 M (tools/large_batch_ab.py;
+  // the pipelined runner, the default there, does 605 / 396 M).
+  // SKGE_APPLY_DENSE=0: slot records always.
+  const char* de = getenv("SKGE_APPLY_DENSE");
+  const int dense_mode = de ? atoi(de) : 1;
   for (auto& b : batches) {
     a.start = b.first;
     a.count = (int)b.second;
     a.neg_out = nullptr;
-    const int ns[2] = {(int)(4 * b.second), (int)b.second};
+    int ns[2] = {(int)(4 * b.second), (int)b.second};
     if ((rc = check_slots(ent, ns[0], "ent")) || (rc = check_slots(rel, ns[1], "rel"))) break;
     if ((rc = launch_sample(a, l1 != 0, st))) break;
-    if ((rc = skge_accum_apply(stream, tabs, 2, ns))) break;
+    skge_table_t at[2] = {tabs[0], tabs[1]};
+    if (dense_mode > 0 && ns[0] >= ent->rows) {
+      at[0].acc_touched = nullptr;
+      ns[0] = ent->rows;
+    }
+    if ((rc = skge_accum_apply(stream, at, 2, ns))) break;
     r->nlaunch += 2;
   }
   if (!rc) {
