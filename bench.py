@@ -58,6 +58,45 @@ def make_wn18_kg(n_ent=N_ENT, n_rel=N_REL, n_triples=N_TRIPLES, seed=0):
     return out.astype(np.int32)
 
 
+def make_zipf_kg(n_ent=N_ENT, n_rel=N_REL, n_triples=N_TRIPLES, alpha=1.1, seed=0):
+    """SURVEY 8(d)'s skew variant: entity ids Zipf(alpha) - 1, truncated to
+    [0, n_ent) by redrawing (clipping would pile ~1/3 of the draws onto one
+    id), relations uniform; unique (s, o, p), RandomState(seed).  At WN18's N
+    and alpha 1.1 entity 0 is ~14% of the s / o draws: hot rows, duplicate
+    slots and pending-row hand-offs in nearly every scoring wave."""
+    rs = np.random.RandomState(seed)
+
+    def ids(m):
+        x = np.empty(0, dtype=np.int64)
+        while len(x) < m:
+            z = rs.zipf(alpha, size=2 * (m - len(x)) + 64) - 1
+            x = np.concatenate([x, z[z < n_ent]])
+        return x[:m]
+    out = np.empty((0, 3), dtype=np.int64)
+    while len(out) < n_triples:
+        m = (n_triples - len(out)) * 2 + 1024
+        cand = np.stack([ids(m), ids(m), rs.randint(n_rel, size=m)], axis=1)
+        allt = np.concatenate([out, cand])
+        key = (allt[:, 0] * n_ent + allt[:, 1]) * n_rel + allt[:, 2]
+        _, first = np.unique(key, return_index=True)
+        out = allt[np.sort(first)][:n_triples]
+    return out.astype(np.int32)
+
+
+def bench_kg(args, seed):
+    """The WN18-shaped KG of configs 1-4: uniform, or Zipf-skewed (--skew zipf)."""
+    if getattr(args, "skew", "none") == "zipf":
+        return make_zipf_kg(seed=seed)
+    return make_wn18_kg(seed=seed)
+
+
+def kg_label(args, seed_txt):
+    if getattr(args, "skew", "none") == "zipf":
+        return ("synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442, entity ids Zipf(1.1) "
+                "truncated, %s)" % seed_txt)
+    return "synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442 uniform, %s)" % seed_txt
+
+
 def pmc_traffic(kernel_substr, fname="pmc.json"):
     """Per-launch HBM-side traffic of a kernel from the newest committed rocprofv3
     PMC summary (profiles/<round>/<fname>, made by `tools/gpu_run.sh pmc` +
@@ -262,6 +301,9 @@ def main():
     ap.add_argument("--nb", type=int, default=100, help="nbatches (reference geometry)")
     ap.add_argument("--d", type=int, default=200)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--skew", choices=("none", "zipf"), default="none",
+                    help="configs 1-4: entity ids Zipf(1.1) instead of uniform (SURVEY 8(d)'s "
+                         "skew variant: hot rows, duplicate slots)")
     ap.add_argument("--opt", choices=["adagrad", "sgd"], default=None,
                     help="updater (default: AdaGrad; config 1: SGD)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -332,7 +374,7 @@ def main():
     from skge_amd.device import DeviceKG, EpochRunner
 
     d, nb = args.d, args.nb
-    trip = make_wn18_kg(seed=rank)        # replica r trains on its own KG
+    trip = bench_kg(args, rank)           # replica r trains on its own KG
     np.random.seed(42 + rank)
     model = S.TransE((N_ENT, N_ENT, N_REL), d, l1=True)
     model.add_hyperparam("margin", 2.0)
@@ -505,8 +547,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442 uniform, RandomState(0)); "
-                    "random-init params (nunif, seed 42)",
+            "data": kg_label(args, "RandomState(0)") + "; random-init params (nunif, seed 42)",
             "config": {"workload": "TransE-L1 d=%d PairwiseStochasticTrainer+%s, WN18 shape, "
                                    "nb=%d (B=%d), margin 2.0, lr 0.1, device RandomModeSampler(1,[0,1]); "
                                    "step = 1 epoch" % (d, {"sgd": "SGD", "adagrad": "AdaGrad"}[args.opt],
@@ -576,7 +617,7 @@ def measure_dp(args, dev, nb, warmup, steps, profile=True):
     from skge_amd.dp import DataParallelRunner, dp_step, slice_of
     world = dist.get_world_size()
     d = args.d
-    trip = make_wn18_kg(seed=0)              # ONE model: the same KG on every rank
+    trip = bench_kg(args, 0)              # ONE model: the same KG on every rank
     np.random.seed(42)
     model = S.TransE((N_ENT, N_ENT, N_REL), d, l1=True)
     model.add_hyperparam("margin", 2.0)
@@ -702,7 +743,7 @@ def run_dp(args):
     if rank == 0:
         ph = m["phases"]
         dom = max(("score", "scatter", "apply"), key=lambda n: ph[n]["us_per_batch"])
-        cpu = None if args.no_cpu else cpu_baseline(make_wn18_kg(seed=0), d, args.nb,
+        cpu = None if args.no_cpu else cpu_baseline(bench_kg(args, 0), d, args.nb,
                                                     args.cpu_seconds, opt=args.opt)
         line = {
             "metric": "triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X"
@@ -748,7 +789,7 @@ def one_gpu_value(args, dev, nb, epochs=None):
     import skge_amd as S
     from skge_amd.device import DeviceKG, EpochRunner
     epochs = epochs or args.steps
-    trip = make_wn18_kg(seed=0)
+    trip = bench_kg(args, 0)
     np.random.seed(42)
     model = S.TransE((N_ENT, N_ENT, N_REL), args.d, l1=True)
     model.add_hyperparam("margin", 2.0)
@@ -1317,7 +1358,7 @@ def run_config34(args):
     from skge_amd.device import DeviceKG, batch_sizes, make_runner
     kind = "hole" if args.config == 3 else "rescal"
     d, nb, margin = args.d, args.nb, 0.2
-    trip = make_wn18_kg(seed=rank)
+    trip = bench_kg(args, rank)
     np.random.seed(42 + rank)
     model = (S.HolE if kind == "hole" else S.RESCAL)((N_ENT, N_ENT, N_REL), d)
     model.add_hyperparam("margin", margin)
@@ -1395,8 +1436,7 @@ def run_config34(args):
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442 uniform, "
-                    "RandomState(rank)); random-init params (nunif, seed 42)",
+            "data": kg_label(args, "RandomState(rank)") + "; random-init params (nunif, seed 42)",
             "config": {"workload": "%s d=%d PairwiseStochasticTrainer+AdaGrad, %s, margin %g, "
                                    "lr 0.1, nb=%d (B=%d), device RandomModeSampler(1,[0,1]); "
                                    "step = 1 epoch on the device pair loop"
