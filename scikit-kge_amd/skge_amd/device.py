@@ -54,14 +54,27 @@ def packed_count_bound(kg, n_ent, batch, tail=None):
     TransE-L1 device loops (the count bounds every 16-bit field of its packed
     sums, csrc/skge_pipeline.hip).  A positive adds at most 3 to each of its s
     and o (skge/transe.py:103-136: s is sp of both pairs and sn of the
-    tail-corrupted one) and 1 to each accepted corruption.  The first part is
-    exact from the training triples; the corruptions are uniform draws over
-    the entities (skge/sample.py:41-46), bounded by their Poisson tail
-    (lambda + 12 sqrt(lambda) + 40, lambda = 2 batch / n_ent).  The applies
-    still check every row's count at run time (ERR_PACKED), and device_optim
-    reads that flag after every epoch."""
-    occ = _bincount_max(kg.trip[:, 0], n_ent) + _bincount_max(kg.trip[:, 1], n_ent)
-    det = 3 * min(int(occ.max().item()), 2 * int(batch))
+    tail-corrupted one) and 1 to each accepted corruption.  The first part
+    comes from the training triples: a row that is the subject of c_s of the
+    T triples is the subject of at most min(c_s, B) positives of a batch, and
+    -- the batch being a uniform sample of the triples (the epoch permutation)
+    -- of fewer than the binomial tail mu + 12 sqrt(mu) + 40, mu = c_s B / T,
+    as relation_replicas() bounds the relation rows (round 4: the whole-KG
+    count alone sent skewed KGs to fp32 sums at every batch past ~3k);
+    likewise as object.  The corruptions are uniform draws over the entities
+    (skge/sample.py:41-46), bounded by their Poisson tail (lambda + 12
+    sqrt(lambda) + 40, lambda = 2 batch / n_ent).  The applies still check
+    every row's count at run time (ERR_PACKED), and device_optim reads that
+    flag after every epoch."""
+    T = float(max(int(kg.trip.shape[0]), 1))
+    B = float(min(int(batch), int(kg.trip.shape[0])))
+
+    def per_batch(col):
+        c = _bincount_max(col, n_ent).double()
+        mu = c * (B / T)
+        return torch.minimum(torch.minimum(c, torch.full_like(c, B)), (tail or _tail)(mu))
+    occ = per_batch(kg.trip[:, 0]) + per_batch(kg.trip[:, 1])
+    det = 3 * min(int(math.ceil(float(occ.max().item()))), 2 * int(batch))
     lam = 2.0 * batch / max(n_ent, 1)
     corr = min(2 * int(batch), int(math.ceil((tail or _tail)(lam))))
     return det + corr
@@ -72,14 +85,14 @@ def _tail8(mu):
     20: a Poisson count passes it with probability < 1e-15): the choice only
     trades atomic bytes, and a count past 127 is still caught by the apply
     (the runner raises, use SKGE_PIPE_E8=0)."""
-    return mu + 8.0 * math.sqrt(mu) + 20.0
+    return mu + 8.0 * mu ** 0.5 + 20.0
 
 
 def _tail(mu):
     """Poisson/binomial upper tail used for the random parts of the count
     bounds: mu + 12 sqrt(mu) + 40 (never reached in practice; the applies
     still check every count at run time)."""
-    return mu + 12.0 * math.sqrt(mu) + 40.0
+    return mu + 12.0 * mu ** 0.5 + 40.0
 
 
 def relation_replicas(kg, n_rel, batch, max_reps=32, ranks=1):

@@ -49,7 +49,27 @@ def test_corruption_term_tiny_graph():
                      rs.randint(3, size=40000)], axis=1)
     kg = _kg(trip)
     assert packed_count_bound(kg, 10, 40000) > PACKED_MAX   # -> fp32 sums
-    assert packed_count_bound(kg, 10, 4000) > 3 * 8000   # the triples' part is not batch-bound
+    # a batch of 4000 is a uniform sample of the 40000 triples: ~400 of a row's
+    # ~4000 subject (and object) occurrences land in it, bounded by the
+    # binomial tail, not by the whole-KG count (round 4)
+    b = packed_count_bound(kg, 10, 4000)
+    assert 3 * 2 * 400 + 800 < b <= PACKED_MAX
+
+
+def test_bound_skewed_kg_batch_sample():
+    """Zipf-skewed WN18-sized KG (bench.make_zipf_kg): the hottest row is in
+    ~16% of the triples.  Its per-batch share, not its whole-KG count, bounds
+    the packed fields, so batches up to ~14k positives keep packed sums; at
+    nb = 2 the hot row's ~11k per-batch occurrences (x3) do not fit."""
+    from bench import make_zipf_kg
+    trip = make_zipf_kg(40943, 18, 141442, seed=3)
+    kg = _kg(trip)
+    occ = (np.bincount(trip[:, 0], minlength=40943) + np.bincount(trip[:, 1], minlength=40943))
+    for batch in (1414, 7072, 14144):
+        b = packed_count_bound(kg, 40943, batch)
+        assert b <= PACKED_MAX, batch
+        assert b >= 3 * occ.max() * batch / len(trip)   # above the hot row's mean share
+    assert packed_count_bound(kg, 40943, 70721) > PACKED_MAX
 
 
 def test_relation_replicas_dominant_relation():

@@ -20,8 +20,8 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("n_ent,n_rel,T,d,nb", [
     (2000, 11, 12000, 64, 10),        # hot rows in every batch
     (40943, 18, 141442, 200, 100),    # WN18 geometry, skewed
-    (40943, 18, 141442, 200, 50),     # WN18 skewed at nb = 50 (at nb <= 20 the static count
-                                      # bound 3 min(occurrences, 2B) exceeds 32767: fp32 sums)
+    (40943, 18, 141442, 200, 10),     # WN18 skewed at nb = 10: 14k positives per batch, packed
+                                      # sums from the per-batch (binomial) count bound
 ])
 def test_pipelined_transe_bitwise_equals_two_launch_on_zipf(n_ent, n_rel, T, d, nb):
     from bench import make_zipf_kg
