@@ -662,7 +662,14 @@ constexpr int ASLOTS = SKGE_PIPE_ASLOTS;
 // ROLE 1: apply role only (grid nA); ROLE 2: scoring role only (grid nB) --
 // the split form, two kernels on parallel branches of the epoch graph, each
 // with its own register budget (SKGE_PIPE_SPLIT)
-template <int KQ, bool W32, bool E8, bool GRP = false, bool A4 = false, int ROLE = 0>
+// P2 (round 4, large batches, SKGE_PIPE_P2): each scoring wave scores TWO
+// positives (2i, 2i + 1) side by side -- both records, both positives' rows
+// and marks in the same round trips, lanes 0-3 / 4-7 holding the two
+// positives' row roles -- so a wave's chain of dependent round trips covers
+// two positives and the batch's scoring waves run in half the rounds.  The
+// same per-positive arithmetic, slots and sums as the one-positive loop.
+template <int KQ, bool W32, bool E8, bool GRP = false, bool A4 = false, int ROLE = 0,
+          bool P2 = false>
 __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
@@ -791,6 +798,181 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
   const __amdgpu_buffer_rsrc_t rec1_rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<int*>(a.rec_n1 + a.start), 0, a.count * 4, 0x00020000);
   int nv = 0;
+  if constexpr (P2) {
+    for (int i = blk_b * wpb + (threadIdx.x >> 6); 2 * i < a.count; i += nB * wpb) {
+      const int wv[2] = {2 * i, 2 * i + 1};
+      const bool has1 = wv[1] < a.count;
+      const int w1c = has1 ? wv[1] : wv[0];   // a valid record to load for an absent second
+      const u32x4 rx0 = __builtin_amdgcn_raw_buffer_load_b128(rec_rs, wv[0] * 16, 0, 0);
+      const u32x4 rx1 = __builtin_amdgcn_raw_buffer_load_b128(rec_rs, w1c * 16, 0, 0);
+      const int r10 = (int)__builtin_amdgcn_raw_buffer_load_b32(rec1_rs, wv[0] * 4, 0, 0);
+      const int r11 = (int)__builtin_amdgcn_raw_buffer_load_b32(rec1_rs, w1c * 4, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      int s[2], o[2], p[2], ng0[2], ng1[2], n0r[2], n1r[2];
+      s[0] = __builtin_amdgcn_readfirstlane((int)rx0.x);
+      o[0] = __builtin_amdgcn_readfirstlane((int)rx0.y);
+      p[0] = __builtin_amdgcn_readfirstlane((int)rx0.z);
+      ng0[0] = __builtin_amdgcn_readfirstlane((int)rx0.w);
+      ng1[0] = __builtin_amdgcn_readfirstlane(r10);
+      s[1] = __builtin_amdgcn_readfirstlane((int)rx1.x);
+      o[1] = __builtin_amdgcn_readfirstlane((int)rx1.y);
+      p[1] = __builtin_amdgcn_readfirstlane((int)rx1.z);
+      ng0[1] = __builtin_amdgcn_readfirstlane((int)rx1.w);
+      ng1[1] = __builtin_amdgcn_readfirstlane(r11);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        n0r[u] = ng0[u] >= 0 ? ng0[u] : s[u];
+        n1r[u] = ng1[u] >= 0 ? ng1[u] : o[u];
+      }
+      float4 es[2][KQ], eo[2][KQ], rp[2][KQ], fs[2][KQ], fo[2][KQ];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        load_row4<KQ>(a.E.P, s[u], d, es[u]);
+        load_row4<KQ>(a.E.P, o[u], d, eo[u]);
+        load_row4<KQ>(a.E.P, n0r[u], d, fs[u]);
+        load_row4<KQ>(a.E.P, n1r[u], d, fo[u]);
+      }
+      // lanes 0-3: the first positive's rows (s, o, s', o'), lanes 4-7 the second's
+      int mark = 0, dn = 0;
+      if (l < 8) {
+        const int k = l & 3;
+        const int rr = l < 4 ? sel4(k, s[0], o[0], n0r[0], n1r[0])
+                             : sel4(k, s[1], o[1], n0r[1], n1r[1]);
+        mark = a.E.pend[pp][rr];
+        dn = __hip_atomic_load(a.E.done + rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float4 ra[KQ];
+        int c;
+        rel_row<KQ, W32>(a.R, p[u], d, rd, ra_prev, rp[u], ra, c);
+      }
+      const uint64_t pmask = has1 ? 0xffull : 0xfull;
+      const uint64_t pend = __ballot(mark == gp) & pmask;
+      const uint64_t unpub = pend & ~__ballot(dn == gp);
+      if (pend) {
+#pragma unroll 1
+        for (int k = 0; k < 8; ++k) {
+          if (!((unpub >> k) & 1ull)) continue;
+          const int row = k < 4 ? sel4(k & 3, s[0], o[0], n0r[0], n1r[0])
+                                : sel4(k & 3, s[1], o[1], n0r[1], n1r[1]);
+          ensure_applied<KQ, E8>(a.E, pp, row, d, gp, a.err);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const uint64_t pu = pend >> (4 * u);
+          if (pu & 1ull) load_row4_sc1<KQ>(a.E.P, s[u], d, es[u]);
+          if (pu & 2ull) load_row4_sc1<KQ>(a.E.P, o[u], d, eo[u]);
+          if (pu & 4ull) load_row4_sc1<KQ>(a.E.P, n0r[u], d, fs[u]);
+          if (pu & 8ull) load_row4_sc1<KQ>(a.E.P, n1r[u], d, fo[u]);
+        }
+      }
+      int vv0[2], vv1[2];
+      float4 gp4[2][KQ], g0[2][KQ], g1[2][KQ];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
+#pragma unroll
+        for (int m = 0; m < KQ; ++m) {
+#define SKGE_EL(X)                                                                    \
+  {                                                                                   \
+    const float vp = (es[u][m].X + rp[u][m].X) - eo[u][m].X;   /* transe.py:32 */     \
+    const float v0 = (fs[u][m].X + rp[u][m].X) - eo[u][m].X;                          \
+    const float v1 = (es[u][m].X + rp[u][m].X) - fo[u][m].X;                          \
+    ps += fabsf(vp);                                                                  \
+    n0 += fabsf(v0);                                                                  \
+    n1 += fabsf(v1);                                                                  \
+    gp4[u][m].X = signf_np(-((eo[u][m].X - rp[u][m].X) - es[u][m].X));                \
+    g0[u][m].X = signf_np((eo[u][m].X - rp[u][m].X) - fs[u][m].X);                    \
+    g1[u][m].X = signf_np((fo[u][m].X - rp[u][m].X) - es[u][m].X);                    \
+  }
+          SKGE_EL(x)
+          SKGE_EL(y)
+          SKGE_EL(z)
+          SKGE_EL(w)
+#undef SKGE_EL
+        }
+        const float pscore = -wave_sum(ps);
+        const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
+        const bool live = u == 0 || has1;
+        vv0[u] = (live && ng0[u] >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // transe.py:73
+        vv1[u] = (live && ng1[u] >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
+      }
+      {   // counts, touched slots and pending marks of both positives (per-lane
+          // choices by selects: no dynamically indexed private arrays)
+        const bool second = (l & 4) != 0;
+        const int kk = l & 3;
+        const int v0 = second ? vv0[1] : vv0[0], v1 = second ? vv1[1] : vv1[0];
+        const int cE = sel4(kk, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
+        const int rE = second ? sel4(kk, s[1], o[1], ng0[1], ng1[1])
+                              : sel4(kk, s[0], o[0], ng0[0], ng1[0]);
+        const int slot = 4 * (second ? wv[1] : wv[0]) + kk;
+        const bool lr = l == 8 || (l == 9 && has1);   // the relation count lanes
+        const int ur = l == 9;
+        const int vr = ur ? vv0[1] + vv1[1] : vv0[0] + vv1[0];
+        if (l < 4 || (l < 8 && has1)) {
+          commit_slot(cnt_cp, tch_cp, rE, cE, slot);
+          if (cE > 0) {
+            pend_cp[rE] = g;
+            if (own_cp) own_cp[rE] = slot;
+          }
+        } else if (lr && vr > 0) {
+          const int wr = ur ? wv[1] : wv[0], pr = ur ? p[1] : p[0];
+          unsigned long long* const rac = racc0 + (size_t)(wr & rmask) * rrep;
+          atomicAdd(rac + (size_t)pr * a.R.rw + rcw, (unsigned long long)(2 * vr));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int v0 = vv0[u], v1 = vv1[u];
+        if (v0 + v1 == 0) continue;
+        nv += v0 + v1;
+        const float fv0 = (float)v0, fv1 = (float)v1;
+        float4 cs[KQ], co[KQ], c0[KQ], c1[KQ], cr[KQ];
+#pragma unroll
+        for (int m = 0; m < KQ; ++m) {
+#define SKGE_CO(X)                                                            \
+  cs[m].X = fv0 * gp4[u][m].X + fv1 * (gp4[u][m].X + g1[u][m].X);             \
+  co[m].X = -(fv0 * (gp4[u][m].X + g0[u][m].X) + fv1 * gp4[u][m].X);          \
+  c0[m].X = g0[u][m].X;                                                       \
+  c1[m].X = -g1[u][m].X;                                                      \
+  cr[m].X = fv0 * (gp4[u][m].X + g0[u][m].X) + fv1 * (gp4[u][m].X + g1[u][m].X);
+          SKGE_CO(x)
+          SKGE_CO(y)
+          SKGE_CO(z)
+          SKGE_CO(w)
+#undef SKGE_CO
+        }
+        if (E8) {
+          unsigned int* es8 = reinterpret_cast<unsigned int*>(esum);
+          acc_row4_i8<KQ>(es8, s[u], cs, d);
+          acc_row4_i8<KQ>(es8, o[u], co, d);
+          if (v0) acc_row4_i8<KQ>(es8, ng0[u], c0, d);
+          if (v1) acc_row4_i8<KQ>(es8, ng1[u], c1, d);
+        } else {
+          Accum aE = {};
+          aE.sum = reinterpret_cast<float*>(esum);
+          acc_row4_i16<KQ>(aE, s[u], cs, d);
+          acc_row4_i16<KQ>(aE, o[u], co, d);
+          if (v0) acc_row4_i16<KQ>(aE, ng0[u], c0, d);
+          if (v1) acc_row4_i16<KQ>(aE, ng1[u], c1, d);
+        }
+        unsigned long long* rrow = racc0 + (size_t)(wv[u] & rmask) * rrep + (size_t)p[u] * a.R.rw;
+#pragma unroll
+        for (int m = 0; m < KQ; ++m) {
+          const int q = 64 * m + l;
+          if (q < nq) {
+            if (W32) {
+              atomicAdd(rrow + 2 * q, pack_i32x2(cr[m].x, cr[m].y));
+              atomicAdd(rrow + 2 * q + 1, pack_i32x2(cr[m].z, cr[m].w));
+            } else {
+              atomicAdd(rrow + q, pack_i16x4(cr[m]));
+            }
+          }
+        }
+      }
+    }
+  } else
   for (int w = blk_b * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
     // large batches: positive w adds its relation sums into replica w % reps
     // (k_rel_fold folds them after the launch), spreading the hot rows' atomics
@@ -2341,6 +2523,7 @@ struct skge_pipe_runner {
   hipEvent_t fork = nullptr, join = nullptr;
   size_t lds = 0;                  // HolE: dynamic LDS per workgroup
   bool pair = false;               // HolE FFT, d = 200: two waves per positive (SKGE_HPIPE_PAIR)
+  bool p2 = false;                 // TransE large batches: two positives per scoring wave (SKGE_PIPE_P2)
   int nlaunch() const { return (int)batch.size() + 2; }
 };
 
@@ -2426,6 +2609,14 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
       }                                                                                          \
       (void)hipEventRecord(r->join, r->st2);                                                    \
       (void)hipStreamWaitEvent(st, r->join, 0);                                                 \
+    } else if (a.E.own[0] && r->grp && r->p2) {   /* ... two positives per scoring wave */      \
+      if (r->e8) {                                                                               \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, true, false, 0, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, true, true, false, 0, true>), gr, bl, 0, st, a); \
+      } else {                                                                                   \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true, false, 0, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true, false, 0, true>), gr, bl, 0, st, a); \
+      }                                                                                          \
     } else if (a.E.own[0] && r->grp) {   /* large batches: grouped owner-row apply */             \
       if (r->e8) {                                                                               \
         if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, true>), gr, bl, 0, st, a);   \
@@ -2716,6 +2907,10 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     const char* pr = getenv("SKGE_HPIPE_PAIR_R1");
     a.pair_r1 = pr && atoi(pr) == 0 ? 0 : 1;
   }
+  {
+    const char* p2e = getenv("SKGE_PIPE_P2");   // A/B: two positives per scoring wave
+    r->p2 = !hole && p2e && atoi(p2e) != 0;   // (owner mode, split roles: not combined)
+  }
   a.tw = r->fft ? hole_fft_table(d) : nullptr;
   if (r->fft && !a.tw) {
     set_error("pipelined runner: HolE FFT twiddle table allocation failed");
@@ -2782,8 +2977,11 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     a.nA = std::max(1, std::min((a_items + WPB - 1) / WPB, std::min(a_cap, 16384)));
     int b_cap = 16384;
     if (!hole && getenv("SKGE_PIPE_BCAP")) b_cap = std::max(1, atoi(getenv("SKGE_PIPE_BCAP")));   // A/B
+    // (P2 at large batches: one scoring wave per two positives)
+    const bool p2_here = !hole && r->p2 && grouped && r->grp && !r->split && !r->owner && !lazy;
+    const int b_items = p2_here ? (a.count + 1) / 2 : a.count;
     const int nBb = r->pair ? std::max(1, std::min(a.count, 2 * 16384))
-                            : std::max(1, std::min((a.count + WPB - 1) / WPB, b_cap));
+                            : std::max(1, std::min((b_items + WPB - 1) / WPB, b_cap));
     r->batch.push_back(a);
     r->grid.push_back(a.nA + (a.count > 0 ? nBb : 0));
     prev = a.count;
