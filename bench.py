@@ -505,25 +505,11 @@ def main():
     pipelined, nlaunches = runner.pipelined, runner.nlaunches
     acc_names = {"entity": acc_label(runner.accE), "relation": acc_label(runner.accR)}
     launch_us_max = max_over_ranks(prof["dominant"]["avg_us"], world, dev)
-    one_model = None
-    if world > 1 and os.environ.get("SKGE_BENCH_DP_DETAIL", "1") != "0":
-        # the one-model data-parallel runner beside the replicas (DESIGN.md 6):
-        # union batch = the reference's 1414 (strong scaling), and 1414 per GPU
-        # (union batch N x 1414) with the one-GPU runner at that union batch
-        del runner
-        torch.cuda.synchronize()
-        g = measure_dp(args, dev, nb, args.warmup, args.steps)
-        nb_w = max(1, nb // world)
-        w = measure_dp(args, dev, nb_w, args.warmup, args.steps, profile=False)
-        same = one_gpu_value(args, dev, nb_w)
-        one_model = {"global_batch": dict(g, scaling="strong",
-                                          vs_one_gpu=round(g["value"] / rank_value, 4)),
-                     "per_gpu_batch": dict(w, scaling="weak (union batch grows with N)",
-                                           one_gpu_same_geometry=same,
-                                           vs_one_gpu_same_geometry=round(w["value"] /
-                                                                          same["value"], 4))}
+    line = None
     if rank == 0:
-        cpu = None if args.no_cpu else cpu_baseline(trip, d, nb, args.cpu_seconds, opt=args.opt)
+        # the CPU baseline on rank 0 at N = 1 only (the bench contract)
+        cpu = None if (args.no_cpu or world > 1) else cpu_baseline(trip, d, nb, args.cpu_seconds,
+                                                                   opt=args.opt)
         k = prof["dominant"]
         kname = {"transe_sample_grad": "sample_grad", "accum_apply": "k_apply",
                  "pipe_batch": "k_pipe_batch"}[k["name"]]
@@ -591,12 +577,78 @@ def main():
                 "accumulator": acc_names,
                 "per_replica_value": round(rank_value, 1),
                 "large_batch": large,
-                "one_model_dp": one_model,
+                "one_model_dp": None,
             },
         }
+    dp_failed = False
+    if world > 1 and os.environ.get("SKGE_BENCH_DP_DETAIL", "1") != "0":
+        # the one-model data-parallel runner beside the replicas (DESIGN.md 6):
+        # union batch = the reference's 1414 (strong scaling), and 1414 per GPU
+        # (union batch N x 1414) with the one-GPU runner at that union batch.
+        # Its multi-rank RCCL path has not run on hardware here, so the line is
+        # built first and a watchdog prints it (detail marked) and ends every
+        # rank if the detail does not finish in SKGE_BENCH_DP_TIMEOUT seconds
+        del runner
+        torch.cuda.synchronize()
+        one_model = run_with_watchdog(
+            lambda: dp_detail(args, dev, nb, world, rank_value), line,
+            float(os.environ.get("SKGE_BENCH_DP_TIMEOUT", "240")))
+        dp_failed = isinstance(one_model, dict) and "error" in one_model
+        if line is not None:
+            line["detail"]["one_model_dp"] = one_model
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
+        if dp_failed:
+            os._exit(0)   # ranks may be out of step in a failed collective: no teardown
         dist.destroy_process_group()
+
+
+def dp_detail(args, dev, nb, world, rank_value):
+    """detail.one_model_dp of the replicas line (N > 1)."""
+    g = measure_dp(args, dev, nb, args.warmup, args.steps)
+    nb_w = max(1, nb // world)
+    w = measure_dp(args, dev, nb_w, args.warmup, args.steps, profile=False)
+    same = one_gpu_value(args, dev, nb_w)
+    return {"global_batch": dict(g, scaling="strong",
+                                 vs_one_gpu=round(g["value"] / rank_value, 4)),
+            "per_gpu_batch": dict(w, scaling="weak (union batch grows with N)",
+                                  one_gpu_same_geometry=same,
+                                  vs_one_gpu_same_geometry=round(w["value"] / same["value"], 4))}
+
+
+def run_with_watchdog(fn, line, limit):
+    """fn() with a time limit: an exception becomes {"error": ...}; if fn has
+    not returned after `limit` seconds (a collective that never completes), a
+    watchdog thread prints `line` (rank 0's already built bench line; None on
+    other ranks) with the detail marked as not measured, and ends this rank's
+    process with status 0 -- the main measurement is already in the line."""
+    import threading
+    done = threading.Event()
+    state = {"printed": False}
+    lock = threading.Lock()
+
+    def watchdog():
+        if done.wait(limit):
+            return
+        with lock:
+            if line is not None and not state["printed"]:
+                line["detail"]["one_model_dp"] = {
+                    "error": "did not finish within %g s (multi-rank RCCL path); not measured"
+                             % limit}
+                print(json.dumps(line), flush=True)
+                state["printed"] = True
+        os._exit(0)
+    threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        out = fn()
+    except Exception as e:   # reported in the line, not fatal to the main measurement
+        out = {"error": "%s: %s" % (type(e).__name__, e)}
+    with lock:
+        done.set()
+        if state["printed"]:
+            os._exit(0)
+    return out
 
 
 def measure_dp(args, dev, nb, warmup, steps, profile=True):
