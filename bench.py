@@ -795,8 +795,8 @@ def run_dp(args):
     if rank == 0:
         ph = m["phases"]
         dom = max(("score", "scatter", "apply"), key=lambda n: ph[n]["us_per_batch"])
-        cpu = None if args.no_cpu else cpu_baseline(bench_kg(args, 0), d, args.nb,
-                                                    args.cpu_seconds, opt=args.opt)
+        cpu = None if (args.no_cpu or world > 1) else cpu_baseline(   # N = 1 only
+            bench_kg(args, 0), d, args.nb, args.cpu_seconds, opt=args.opt)
         line = {
             "metric": "triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X"
                       if args.config == 2 else
@@ -1127,7 +1127,8 @@ def run_config5(args):
                          "avg_launch_us": round(k["avg_us"], 3),
                          "avg_launch_source": prof.get("source"),
                          "bytes_formula": prof.get("formula")},
-            "cpu_baseline": None if args.no_cpu else cpu_baseline_config5(args.cpu_seconds),
+            "cpu_baseline": None if (args.no_cpu or world > 1) else
+                            cpu_baseline_config5(args.cpu_seconds),   # N = 1 only
             "detail": {"runner": "pipelined" if runner.pipelined else "two-launch",
                        "accumulator": {"entity": acc_label(runner.accE),
                                        "relation": acc_label(runner.accR)},
@@ -1288,7 +1289,8 @@ def run_config5_sharded(args):
                          "unit": "GB/s", "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 4),
                          "traffic": None, "bytes_per_launch": round(k["bytes_per_launch"]),
                          "avg_launch_us": round(k["avg_us"], 3)},
-            "cpu_baseline": None if args.no_cpu else cpu_baseline_config5(args.cpu_seconds),
+            "cpu_baseline": None if (args.no_cpu or world > 1) else
+                            cpu_baseline_config5(args.cpu_seconds),   # N = 1 only
             "detail": {"runner": "row-sharded (skge_amd.shard)",
                        "bucket_capacity": runner.C,
                        "captured_graph": runner.graph is not None,
@@ -1476,7 +1478,8 @@ def run_config34(args):
                  "runner": type(r2).__name__}
         del r2
     if rank == 0:
-        cpu = None if args.no_cpu else cpu_baseline(trip, d, nb, args.cpu_seconds, kind, margin)
+        cpu = None if (args.no_cpu or world > 1) else cpu_baseline(   # N = 1 only
+            trip, d, nb, args.cpu_seconds, kind, margin)
         name = {"hole": "HolE", "rescal": "RESCAL"}[kind]
         tkern = "k_hole_pipe" if prof is not None else (
             "k_rescal_front" if kind == "rescal" else "k_hole")
