@@ -798,6 +798,14 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
     store_step(buf, ks);
     __syncthreads();   // (also: every wave is done with buf's previous use, step ks - 2)
     if (ks + 1 < nk) load_step(ks + 1);   // in flight during this step's MFMAs
+#ifdef SKGE_ABL_RS_NOPAD   // timing-only upper bound of a d-exact tiling: the edge
+                           // column block (its 48 padding columns at d = 200) skips
+                           // its contraction entirely
+    if (c0 + GC > d) {
+      acc[0][0] += sA[buf][row][kq];
+      continue;
+    }
+#endif
 #ifdef SKGE_ABL_GEMM_NOMFMA   // timing-only ablation: no contraction
     acc[0][0] += sA[buf][row][kq] + sB[buf][kq * (GC + 4) + (l & 15)];
 #else
@@ -1412,6 +1420,9 @@ __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__
       }
       __syncthreads();
       const int mm = min(WG_CH, cnt - b * WG_CH);
+#ifdef SKGE_ABL_RS_NOPAD   // (as above: edge dW tiles skip their contraction)
+      if (r0 + WG_T > d || c0 + WG_T > d) continue;
+#endif
       for (int k0 = 0; k0 < mm; k0 += 4) {
         const int ik = k0 + (l >> 4);
         const float av_ = sEs[ik][16 * wave + (l & 15)];
