@@ -2068,7 +2068,19 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
   const int rd = a.b & 1;
   const int ra_prev = (g - 1) % 3, ra_cur = g % 3;
   float2* const tw = reinterpret_cast<float2*>(smem);
+  // the twiddle table into LDS before the loop.  (SKGE_HPIPE_TW_LATE, A/B:
+  // its global loads issued here and written to LDS just before the first
+  // barrier, overlapping the first record's round trip: 94.4 / 94.6 vs 94.9 M
+  // triples/s, no gain -- not on the critical path)
+  const int t0 = (int)threadIdx.x, t1 = t0 + 128;
+#ifdef SKGE_HPIPE_TW_LATE
+  const float2 twr0 = a.tw[t0 < d ? t0 : 0], twr1 = a.tw[t1 < d ? t1 : 0];
+  bool tw_pending = true;
+#else
+  const float2 twr0 = {}, twr1 = {};
   fft_twiddles(tw, a.tw, d);
+  bool tw_pending = false;
+#endif
   float* const wb = smem + 2 * d;   // the pair's two transform buffers
   float2* const b0 = reinterpret_cast<float2*>(wb);
   float2* const b1 = b0 + 5 * 100;
@@ -2111,6 +2123,11 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
       if (pend & 2ull) load_row4_sc1<1>(a.E.P, rb_row, d, xb);
     }
     if (a.trace) tt[2] = now_10ns();
+    if (tw_pending) {
+      if (t0 < d) tw[t0] = twr0;
+      if (t1 < d) tw[t1] = twr1;
+      tw_pending = false;
+    }
     __syncthreads();   // the previous positive's buffers are free, the twiddles in place
     if (hw == a.pair_r1) fft_put_row(b0, 100, 0, xr[0], d);
     if (hw == 0) {
