@@ -13,17 +13,23 @@ mean+AdaGrad+normalize).  value = positive triples fully processed per second.
 Multi-GPU: one process per GPU.  `--gpus N` without a torchrun environment
 starts the N ranks itself (torch.distributed.run as a child process, before
 anything touches a GPU); under torchrun it checks WORLD_SIZE == N.  Configs
-1-4 (WN18, 33 MB tables): N independent replicas by default -- the north star
-replicates the table and exchanges gradients only once |E| d outgrows one
-GPU's HBM, so there is no data-path collective (scaling "weak", value = all
-replicas' positives / the slowest rank's time).  The one-model data-parallel
-runner (skge_amd.dp: slice scoring, RCCL all-gather of records, replicated
-scatter + apply) is measured beside it in `detail.one_model_dp` (union batch
-1414: strong scaling; union batch N x 1414 with the one-GPU run at the same
-union batch), or as the line itself with `--mode dp`.  Config 5 `--shard`:
-the row-sharded table (RCCL all-to-all + reduce-scatter of contributions).
-`--dry-run`: the launcher, rendezvous and max-over-ranks bookkeeping on CPU
-(gloo), no GPU (tests/test_bench_dist.py).
+1-2 at N > 1 (default `--mode auto` = dp): the line is ONE TransE model
+trained data parallel over the N GPUs on the same KG (skge_amd.dp: every rank
+scores its slice of each union batch of the reference's 1414 positives, RCCL
+all-gather of the records, replicated scatter + apply; strong scaling).  At
+this batch the per-batch all-gather and the replicated apply bound it, so it
+is expected at or below one GPU and reported as such.
+The union batch N x 1414 (with the one-GPU runner at that batch) and N
+independent replicas ("independent jobs": N models on N KGs, no exchange)
+are measured into `detail` only.  `--mode replicas` prints the independent
+jobs as the line, named so in the metric.  Config 5 at N > 1: the
+row-sharded table (`--shard`, RCCL all-to-all + reduce-scatter of
+contributions).  Any multi-rank measurement that raises or does not finish
+within SKGE_BENCH_DP_TIMEOUT seconds ends the job with a non-zero status
+(after rank 0 has printed its line, the failure marked in it).
+`--dry-run`: the launcher, rendezvous, the data-parallel protocol
+(skge_amd.dp.dp_step with a NumPy rank compute, gloo) and the
+max-over-ranks bookkeeping on CPU, no GPU (tests/test_bench_dist.py).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--nb 100]
 """
@@ -158,37 +164,57 @@ def acc_label(acc):
 
 def run_dry(args):
     """--dry-run: the multi-rank bookkeeping without a GPU -- rendezvous over
-    gloo, barrier-bracketed timing of a NumPy stand-in step, max over ranks,
-    the whole-job value and ONE line from rank 0 (not a measurement)."""
-    import torch
+    gloo, the data-parallel protocol of the N > 1 line (skge_amd.dp.dp_step:
+    slice scoring, all-gather, scatter, apply) with the float64 NumPy rank
+    compute of tests/dp_numpy.py on a small KG, barrier-bracketed timing, max
+    over ranks and ONE line from rank 0 with the DP line's shape (not a
+    measurement: "dry_run": true)."""
     import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from dp_numpy import NumpyDPOps
+    from shard_numpy import random_records
+    from skge_amd.dp import DPExchange, dp_step
     world, rank, _ = dist_env()
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
-    rs = np.random.RandomState(rank)
-    x = rs.rand(4096, 64)
+    n_ent, n_rel, d, T, nb = 200, 6, 8, 400, 4
+    rs = np.random.RandomState(0)          # ONE model: the same problem on every rank
+    E = rs.uniform(-0.5, 0.5, size=(n_ent, d))
+    E /= np.sqrt((E ** 2).sum(axis=1))[:, None]
+    R = rs.uniform(-0.5, 0.5, size=(n_rel, d))
+    rec, rec_n1 = random_records(np.random.RandomState(5), T, n_ent, n_rel)
+    ops = NumpyDPOps(rec, rec_n1, E, R, 2.0, 0.1)
+    ex = DPExchange()
+    bs = T // nb
+    batches = [(s0, min(bs, T - s0)) for s0 in range(0, T, bs)]
     for _ in range(args.warmup):
-        np.abs(x).sum()
+        for s0, c in batches:
+            dp_step(ops, ex, s0, c)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        np.abs(x + 1.0).sum()
+        for s0, c in batches:
+            dp_step(ops, ex, s0, c)
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     elapsed = max_over_ranks(elapsed, world)
-    ranks = [rank]
+    ranks, cks = [rank], [float(ops.E.sum())]
     if world > 1:
         out = [None] * world
-        dist.all_gather_object(out, rank)
-        ranks = out
+        dist.all_gather_object(out, (rank, float(ops.E.sum())))
+        ranks, cks = [r for r, _ in out], [c for _, c in out]
     if rank == 0:
-        print(json.dumps({"metric": "dry-run (launcher bookkeeping, no GPU)", "dry_run": True,
-                          "value": replica_value(4096 * args.steps, world, elapsed),
-                          "unit": "rows/s", "n_gpus": world, "steps": args.steps,
-                          "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
-                          "scaling": "weak", "detail": {"ranks": ranks}}))
+        m = {"value": round(T * args.steps / elapsed, 1),
+             "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "union_batch": bs, "nb": nb,
+             "per_gpu_batch": -(-bs // world), "replicas_identical": len(set(cks)) == 1}
+        line = dp_line(args, world, m, None, d=d, nb=nb, workload_kg="dry-run KG (|E|=%d |R|=%d "
+                       "T=%d), float64 NumPy rank compute (tests/dp_numpy.py)" % (n_ent, n_rel, T))
+        line.update(metric="dry-run (launcher and DP-protocol bookkeeping, no GPU)", dry_run=True,
+                    unit="triples/s")
+        line["detail"] = {"ranks": ranks, "dp": m, "backend": "gloo"}
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -208,6 +234,23 @@ def setup_ranks():
         local = 0
     torch.cuda.set_device(local)
     return world, rank, local, torch.device("cuda", local)
+
+
+def rank_setup_info(world, local):
+    """What the job ran on, for the line: the backend, the number of distinct
+    GPUs the ranks used (max over ranks of local index + 1 on one node) and
+    whether it is a one-GPU rehearsal (SKGE_BENCH_ONE_GPU=1: every rank on GPU
+    0, so its numbers are not a scaling point)."""
+    import torch.distributed as dist
+    backend = dist.get_backend() if world > 1 else None
+    devices = int(max_over_ranks(local + 1, world, coll_device("cuda"))) if world > 1 else 1
+    return {"backend": backend, "distinct_gpus": devices,
+            "rehearsal_one_gpu": os.environ.get("SKGE_BENCH_ONE_GPU") == "1"}
+
+
+def parallelism_label(base, info):
+    """base (e.g. 'dp2'), marked when every rank shared one GPU."""
+    return base + ("-on-1gpu-rehearsal" if info.get("rehearsal_one_gpu") else "")
 
 
 def coll_device(device):
@@ -324,10 +367,10 @@ def main():
                     help="skip the measured gather roofline (skge_roofline_gather)")
     ap.add_argument("--runner", default="auto", choices=["auto", "pairs", "hole_pipe"],
                     help="configs 3/4: device runner (auto: HolE pipelined where it applies)")
-    ap.add_argument("--mode", choices=["replicas", "dp"], default="replicas",
-                    help="configs 1/2 on N > 1 GPUs: 'replicas' (default; N independent "
-                         "models, no exchange, one-model DP measured in detail) or 'dp' (the "
-                         "line is the one-model data-parallel runner)")
+    ap.add_argument("--mode", choices=["auto", "replicas", "dp"], default="auto",
+                    help="configs 1/2 on N > 1 GPUs: 'dp' (= auto, the default: the line is ONE "
+                         "model trained data parallel; independent replicas in detail) or "
+                         "'replicas' (the line is N independent jobs, named so in the metric)")
     ap.add_argument("--dp-batch", choices=["per-gpu", "global"], default="global",
                     help="--mode dp: 'global' (default) keeps the union batch at the reference's "
                          "1414 (1414 / N per GPU: strong scaling); 'per-gpu' keeps 1414 per GPU "
@@ -356,18 +399,19 @@ def main():
                          % (args.gpus, world))
     if args.dry_run:
         return run_dry(args)
-    if args.config == 5 and args.shard:
-        return run_config5_sharded(args)
+    if args.config == 5 and (args.shard or (world > 1 and args.mode != "replicas")):
+        return run_config5_sharded(args)     # N > 1: one model, the table row-sharded
     if args.config == 5:
         return run_config5(args)
     if args.config in (3, 4):
         return run_config34(args)
-    if world > 1 and args.mode == "dp":
-        return run_dp(args)
+    if world > 1 and args.mode != "replicas":
+        return run_dp(args)                  # N > 1: one model, data parallel
 
     import torch
     import torch.distributed as dist
     world, rank, local, dev = setup_ranks()
+    info = rank_setup_info(world, local)
 
     import skge_amd as S
     from skge_amd import _lib as L
@@ -517,10 +561,12 @@ def main():
         traffic, traffic_src = pmc_traffic(kname, "pmc.json" if args.config == 2 else
                                            "pmc_c%d.json" % args.config)
         line = {
-            "metric": "triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X"
-                      if args.config == 2 else
-                      "triples/sec (score+grad+update), WN18 TransE d=%d %s (BASELINE configs[0])"
-                      % (d, args.opt),
+            "metric": ("triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X"
+                       if args.config == 2 else
+                       "triples/sec (score+grad+update), WN18 TransE d=%d %s (BASELINE configs[0])"
+                       % (d, args.opt)) +
+                      ("" if world == 1 else " -- %d independent replicas (weak; not one model)"
+                       % world),
             "value": round(value, 1),
             "unit": "triples/s",
             "n_gpus": world,
@@ -528,8 +574,9 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
             "higher_is_better": True,
-            # one replica per GPU, one epoch of its own KG per step: per-GPU
-            # work fixed as N grows (the one-model DP runner: detail.one_model_dp)
+            # --mode replicas at N > 1: one replica per GPU, one epoch of its own
+            # KG per step: per-GPU work fixed as N grows (the default N > 1 line
+            # is the one-model data-parallel run, run_dp)
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
@@ -543,7 +590,8 @@ def main():
                                     "and model; no exchange: the 33 MB table is replicated, "
                                     "north_star)" % world),
                        "global_batch": N_TRIPLES // nb,
-                       "parallelism": "replicas%d" % world if world > 1 else "1gpu"},
+                       "parallelism": parallelism_label("replicas%d" % world, info)
+                       if world > 1 else "1gpu"},
             "roofline": {"bound": "hbm", "kernel": k["name"],
                          "achieved": round(k["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 4),
@@ -577,52 +625,37 @@ def main():
                 "accumulator": acc_names,
                 "per_replica_value": round(rank_value, 1),
                 "large_batch": large,
-                "one_model_dp": None,
+                "rank_setup": info,
             },
         }
-    dp_failed = False
-    if world > 1 and os.environ.get("SKGE_BENCH_DP_DETAIL", "1") != "0":
-        # the one-model data-parallel runner beside the replicas:
-        # union batch = the reference's 1414 (strong scaling), and 1414 per GPU
-        # (union batch N x 1414) with the one-GPU runner at that union batch.
-        # Its multi-rank RCCL path has not run on hardware here, so the line is
-        # built first and a watchdog prints it (detail marked) and ends every
-        # rank if the detail does not finish in SKGE_BENCH_DP_TIMEOUT seconds
-        del runner
-        torch.cuda.synchronize()
-        one_model = run_with_watchdog(
-            lambda: dp_detail(args, dev, nb, world, rank_value), line,
-            float(os.environ.get("SKGE_BENCH_DP_TIMEOUT", "240")))
-        dp_failed = isinstance(one_model, dict) and "error" in one_model
-        if line is not None:
-            line["detail"]["one_model_dp"] = one_model
-    if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
-        if dp_failed:
-            os._exit(0)   # ranks may be out of step in a failed collective: no teardown
         dist.destroy_process_group()
 
 
-def dp_detail(args, dev, nb, world, rank_value):
-    """detail.one_model_dp of the replicas line (N > 1)."""
-    g = measure_dp(args, dev, nb, args.warmup, args.steps)
-    nb_w = max(1, nb // world)
-    w = measure_dp(args, dev, nb_w, args.warmup, args.steps, profile=False)
-    same = one_gpu_value(args, dev, nb_w)
-    return {"global_batch": dict(g, scaling="strong",
-                                 vs_one_gpu=round(g["value"] / rank_value, 4)),
-            "per_gpu_batch": dict(w, scaling="weak (union batch grows with N)",
-                                  one_gpu_same_geometry=same,
-                                  vs_one_gpu_same_geometry=round(w["value"] / same["value"], 4))}
+WATCHDOG_EXIT = 3   # a multi-rank measurement raised or hung: the job failed
 
 
-def run_with_watchdog(fn, line, limit):
-    """fn() with a time limit: an exception becomes {"error": ...}; if fn has
-    not returned after `limit` seconds (a collective that never completes), a
-    watchdog thread prints `line` (rank 0's already built bench line; None on
-    other ranks) with the detail marked as not measured, and ends this rank's
-    process with status 0 -- the main measurement is already in the line."""
+def mark_failure(line, key, msg):
+    """Record a failed measurement in rank 0's line: key None = the line's own
+    value (set to null), else detail[key]."""
+    if line is None:
+        return
+    if key is None:
+        line["value"] = None
+        line["error"] = msg
+    else:
+        line.setdefault("detail", {})[key] = {"error": msg}
+
+
+def run_with_watchdog(fn, line, limit, key=None):
+    """fn() with a time limit.  Returns fn's result, or {"error": ...} if it
+    raised (the caller then prints the line and ends with WATCHDOG_EXIT).  If
+    fn has not returned after `limit` seconds (a collective that never
+    completes), a watchdog thread marks the failure in `line` (rank 0's bench
+    line; None on other ranks) under `key` (see mark_failure), prints it once
+    and ends this rank's process with status WATCHDOG_EXIT -- never 0: a hung
+    GPU collective must not look like a successful run."""
     import threading
     done = threading.Event()
     state = {"printed": False}
@@ -633,22 +666,25 @@ def run_with_watchdog(fn, line, limit):
             return
         with lock:
             if line is not None and not state["printed"]:
-                line["detail"]["one_model_dp"] = {
-                    "error": "did not finish within %g s (multi-rank RCCL path); not measured"
-                             % limit}
+                mark_failure(line, key, "did not finish within %g s (multi-rank collective); "
+                                        "not measured" % limit)
                 print(json.dumps(line), flush=True)
                 state["printed"] = True
-        os._exit(0)
+        os._exit(WATCHDOG_EXIT)
     threading.Thread(target=watchdog, daemon=True).start()
     try:
         out = fn()
-    except Exception as e:   # reported in the line, not fatal to the main measurement
+    except Exception as e:
         out = {"error": "%s: %s" % (type(e).__name__, e)}
     with lock:
         done.set()
         if state["printed"]:
-            os._exit(0)
+            os._exit(WATCHDOG_EXIT)
     return out
+
+
+def failed(x):
+    return isinstance(x, dict) and "error" in x
 
 
 def measure_dp(args, dev, nb, warmup, steps, profile=True):
@@ -779,75 +815,127 @@ def dp_profile(runner, args, world):
     return ph
 
 
+def dp_line(args, world, m, ph, d=None, nb=None, workload_kg=None, info=None):
+    """The N > 1 line of configs 1-2: ONE TransE-L1 model trained data parallel
+    (measure_dp's result m; ph: its per-rank phases, the roofline's source)."""
+    d = d or args.d
+    nb = nb or args.nb
+    bs = m["union_batch"]
+    opt = {"sgd": "SGD", "adagrad": "AdaGrad"}[args.opt]
+    line = {
+        "metric": "triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X"
+                  if args.config == 2 else
+                  "triples/sec (score+grad+update), WN18 TransE d=%d %s (BASELINE configs[0])"
+                  % (d, args.opt),
+        "value": m["value"], "unit": "triples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": m["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "strong" if args.dp_batch == "global" else "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": (workload_kg or "synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442 uniform, "
+                 "RandomState(0))") + ", the same on every rank; random-init params (nunif, seed 42)",
+        "config": {"workload": "ONE TransE-L1 d=%d model, PairwiseStochasticTrainer+%s, union "
+                               "batch %d positives (nb=%d; ~%d per GPU), margin 2.0, lr 0.1, "
+                               "device RandomModeSampler(1,[0,1]); data parallel over %d GPUs: "
+                               "slice scoring, all-gather of the records, replicated scatter + "
+                               "apply; step = 1 epoch" % (d, opt, bs, nb, m["per_gpu_batch"], world),
+                   "global_batch": bs,
+                   "parallelism": parallelism_label("dp%d" % world, info or {})},
+        "roofline": None,
+        "cpu_baseline": None,        # the bench contract: rank 0 at N = 1 only
+        "detail": {"runner": "DataParallelRunner (skge_amd.dp)", "dp": m,
+                   "rank_setup": info},
+    }
+    if ph:
+        dom = max(("score", "scatter", "apply"), key=lambda n: ph[n]["us_per_batch"])
+        line["roofline"] = {
+            "bound": "hbm", "kernel": "dp_" + dom, "achieved": ph[dom]["GB_s"],
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ph[dom]["GB_s"] / HBM_PEAK_GBS, 4) if ph[dom]["GB_s"] else None,
+            "traffic": None, "bytes_per_launch": ph[dom]["bytes_per_batch"],
+            "avg_launch_us": ph[dom]["us_per_batch"], "phases_per_rank": ph,
+            "note": "rank 0, per union batch, eager epoch with HIP events between phases "
+                    "(bench.dp_profile); all_gather = RCCL over xGMI"}
+    return line
+
+
 def run_dp(args):
-    """--mode dp on N > 1 GPUs: the line is ONE model trained data parallel
-    (measure_dp).  --dp-batch global: union batch = the reference's 1414
-    (strong scaling); per-gpu: 1414 per GPU (union batch N x 1414, weak), with
-    the one-GPU pipelined runner at that union batch beside it."""
+    """Configs 1-2 on N > 1 GPUs (the default): the line is ONE model trained
+    data parallel (measure_dp).  --dp-batch global (default): union batch =
+    the reference's 1414 (strong scaling); per-gpu: 1414 per GPU (union batch
+    N x 1414, weak).  detail: the other union batch with the one-GPU
+    pipelined runner at that batch beside it, one GPU alone at the line's
+    batch (vs_one_gpu), and N independent jobs (N models on N KGs, no
+    exchange) -- never the value.  Every multi-rank measurement runs under
+    run_with_watchdog: a failure or hang ends the job with WATCHDOG_EXIT."""
     import torch
     import torch.distributed as dist
     world, rank, local, dev = setup_ranks()
+    info = rank_setup_info(world, local)
+    limit = float(os.environ.get("SKGE_BENCH_DP_TIMEOUT", "300"))
     nb = max(1, args.nb // world) if args.dp_batch == "per-gpu" else args.nb
-    m = measure_dp(args, dev, nb, args.warmup, args.steps)
-    same_geo = one_gpu_value(args, dev, nb) if args.dp_batch == "per-gpu" else None
     bs = N_TRIPLES // nb
-    d = args.d
+    skel = None
     if rank == 0:
-        ph = m["phases"]
-        dom = max(("score", "scatter", "apply"), key=lambda n: ph[n]["us_per_batch"])
-        cpu = None if (args.no_cpu or world > 1) else cpu_baseline(   # N = 1 only
-            bench_kg(args, 0), d, args.nb, args.cpu_seconds, opt=args.opt)
-        line = {
-            "metric": "triples/sec (score+grad+update), WN18 TransE d=200, 1/2/4/8 MI355X"
-                      if args.config == 2 else
-                      "triples/sec (score+grad+update), WN18 TransE d=%d %s (BASELINE configs[0])"
-                      % (d, args.opt),
-            "value": m["value"], "unit": "triples/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": m["ms_per_step"],
-            "higher_is_better": True,
-            "scaling": "strong" if args.dp_batch == "global" else "weak",
-            "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442 uniform, RandomState(0)), "
-                    "the same on every rank; random-init params (nunif, seed 42)",
-            "config": {"workload": "ONE TransE-L1 d=%d model, PairwiseStochasticTrainer+%s, WN18 "
-                                   "shape, union batch %d positives (nb=%d; ~%d per GPU), margin "
-                                   "2.0, lr 0.1, device RandomModeSampler(1,[0,1]); data parallel "
-                                   "over %d GPUs: slice scoring, RCCL all-gather of the records, "
-                                   "replicated scatter + apply; step = 1 epoch"
-                                   % (d, {"sgd": "SGD", "adagrad": "AdaGrad"}[args.opt], bs, nb,
-                                      m["per_gpu_batch"], world),
-                       "global_batch": bs, "parallelism": "dp%d" % world},
-            "roofline": {"bound": "hbm", "kernel": "dp_" + dom,
-                         "achieved": ph[dom]["GB_s"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ph[dom]["GB_s"] / HBM_PEAK_GBS, 4), "traffic": None,
-                         "bytes_per_launch": ph[dom]["bytes_per_batch"],
-                         "avg_launch_us": ph[dom]["us_per_batch"],
-                         "phases_per_rank": ph,
-                         "note": "per rank and union batch, eager epoch with HIP events between "
-                                 "phases (bench.dp_profile); all_gather = RCCL over xGMI"},
-            "cpu_baseline": cpu,
-            "detail": dict(m, runner="DataParallelRunner (skge_amd.dp)",
-                           one_gpu_same_geometry=same_geo),
-        }
+        skel = dp_line(args, world, {"value": None, "ms_per_step": None, "union_batch": bs,
+                                     "per_gpu_batch": -(-bs // world)}, None, nb=nb, info=info)
+    m = run_with_watchdog(lambda: measure_dp(args, dev, nb, args.warmup, args.steps), skel, limit)
+    if failed(m):
+        if rank == 0:
+            mark_failure(skel, None, m["error"])
+            print(json.dumps(skel), flush=True)
+        os._exit(WATCHDOG_EXIT)     # ranks may be out of step in a failed collective
+    line = dp_line(args, world, m, m.get("phases"), nb=nb, info=info) if rank == 0 else None
+    torch.cuda.synchronize()
+
+    def details():
+        out = {}
+        one = one_gpu_value(args, dev, nb)
+        out["one_gpu_same_batch"] = dict(one, vs=None)
+        out["vs_one_gpu"] = round(m["value"] / one["value"], 4)
+        nb2 = args.nb if args.dp_batch == "per-gpu" else max(1, args.nb // world)
+        w = measure_dp(args, dev, nb2, args.warmup, args.steps, profile=False)
+        same = one_gpu_value(args, dev, nb2)
+        out["other_union_batch"] = dict(
+            w, scaling="strong" if nb2 == args.nb else "weak (union batch grows with N)",
+            one_gpu_same_geometry=same,
+            vs_one_gpu_same_geometry=round(w["value"] / same["value"], 4))
+        ind = one_gpu_value(args, dev, args.nb, kg_seed=rank, seed=1234 + rank)
+        el = max_over_ranks(ind["elapsed_s"], world, dev)
+        out["independent_jobs"] = {
+            "what": "%d independent models, one per GPU, each on its own KG, no exchange (job "
+                    "throughput, not one model trained faster)" % world,
+            "value": round(replica_value(N_TRIPLES * ind["epochs"], world, el), 1),
+            "nb": args.nb, "ms_per_step": round(1000.0 * el / ind["epochs"], 4)}
+        return out
+    det = run_with_watchdog(details, line, limit, key="details")
+    if rank == 0:
+        if failed(det):
+            mark_failure(line, "details", det["error"])
+        else:
+            line["detail"].update(det)
         print(json.dumps(line), flush=True)
+    if failed(det):
+        os._exit(WATCHDOG_EXIT)
     dist.destroy_process_group()
 
 
-def one_gpu_value(args, dev, nb, epochs=None):
+def one_gpu_value(args, dev, nb, epochs=None, kg_seed=0, seed=1234):
     """The one-GPU pipelined runner (this rank's GPU alone, no collective) on
     the same KG, model and union batch as a data-parallel run: what the
-    batch size alone buys, so a scaling curve does not credit it to the GPUs."""
+    batch size alone buys, so a scaling curve does not credit it to the GPUs
+    (kg_seed = rank: an independent job on its own KG)."""
     import torch
     import skge_amd as S
     from skge_amd.device import DeviceKG, EpochRunner
     epochs = epochs or args.steps
-    trip = bench_kg(args, 0)
-    np.random.seed(42)
+    trip = bench_kg(args, kg_seed)
+    np.random.seed(42 + kg_seed)
     model = S.TransE((N_ENT, N_ENT, N_REL), args.d, l1=True)
     model.add_hyperparam("margin", 2.0)
     Upd = S.SGD if args.opt == "sgd" else S.AdaGrad
     upd = {pid: Upd(p, 0.1) for pid, p in model.params.items()}
-    r = EpochRunner(model, upd, DeviceKG(trip, dev), nbatches=nb, seed=1234)
+    r = EpochRunner(model, upd, DeviceKG(trip, dev), nbatches=nb, seed=seed)
     init = {pid: p.data.clone() for pid, p in model.params.items()}
     r.run(max(args.warmup, 1))
     r.synchronize()
@@ -860,7 +948,7 @@ def one_gpu_value(args, dev, nb, epochs=None):
     r.synchronize()
     el = time.perf_counter() - t0
     out = {"nb": nb, "union_batch": N_TRIPLES // nb, "value": round(N_TRIPLES * epochs / el, 1),
-           "ms_per_step": round(1000.0 * el / epochs, 4),
+           "ms_per_step": round(1000.0 * el / epochs, 4), "elapsed_s": el, "epochs": epochs,
            "runner": "pipelined" if r.pipelined else "two-launch"}
     del r
     return out
@@ -1107,7 +1195,9 @@ def run_config5(args):
         traffic, traffic_src = pmc_traffic(PMC_KERNEL.get(k["name"], k["name"]), "pmc_c5.json")
         line = {
             "metric": "triples/sec (score+grad+update), synthetic TransE |E|=50M |R|=10k d=512, "
-                      "B=131072 per GPU (BASELINE configs[4])",
+                      "B=131072 per GPU (BASELINE configs[4])" +
+                      ("" if world == 1 else " -- %d independent replicas (weak; not one model)"
+                       % world),
             "value": round(value, 1), "unit": "triples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
@@ -1117,7 +1207,8 @@ def run_config5(args):
             "config": {"workload": "TransE-L1 d=%d PairwiseStochasticTrainer+AdaGrad, margin 2.0, "
                                    "lr 0.1, device RandomModeSampler(1,[0,1]); step = 1 epoch of "
                                    "%d batches" % (d, nb),
-                       "global_batch": T // nb * world, "parallelism": "replicas%d" % world},
+                       "global_batch": T // nb * world,
+                       "parallelism": "replicas%d" % world if world > 1 else "1gpu"},
             "roofline": {"bound": "hbm", "kernel": k["name"],
                          "achieved": round(k["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(k["achieved_gbs"] / HBM_PEAK_GBS, 4),
@@ -1486,7 +1577,9 @@ def run_config34(args):
         traffic, traffic_src = pmc_traffic(tkern, "pmc_c%d.json" % args.config)
         line = {
             "metric": "triples/sec (score+grad+update), WN18 %s d=%d pairwise, 1 MI355X "
-                      "(BASELINE configs[%d])" % (name, d, args.config - 1),
+                      "(BASELINE configs[%d])" % (name, d, args.config - 1) +
+                      ("" if world == 1 else " -- %d independent replicas (weak; not one model: "
+                       "no data-parallel runner for this model)" % world),
             "value": round(value, 1), "unit": "triples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
@@ -1497,7 +1590,8 @@ def run_config34(args):
                                    "step = 1 epoch on the device pair loop"
                                    % (name, d, "Sigmoid" if kind == "hole" else "Linear",
                                       margin, nb, N_TRIPLES // nb),
-                       "global_batch": N_TRIPLES // nb, "parallelism": "replicas%d" % world},
+                       "global_batch": N_TRIPLES // nb,
+                       "parallelism": "replicas%d" % world if world > 1 else "1gpu"},
             "roofline": ({"bound": "hbm", "kernel": "k_hole_pipe",
                           "achieved": round(prof["dominant"]["achieved_gbs"], 1),
                           "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -1,7 +1,9 @@
 """bench.py's multi-GPU bookkeeping on CPU: a world-size-2 gloo job checks the
-rank environment, the max-over-ranks timing and the whole-job value (the
-config-5 replica lines; configs 1/2 at N > 1 run the one-model data-parallel
-runner, DESIGN.md section 6, whose protocol tests/test_dp_protocol.py covers)."""
+rank environment, the max-over-ranks timing and the whole-job value; the
+`--gpus N --dry-run` launcher runs the N > 1 line's data-parallel protocol
+(skge_amd.dp.dp_step with the NumPy rank compute over gloo) and must print ONE
+line shaped like the one-model DP line (parallelism dpN, strong scaling,
+identical replicas).  The protocol's numerics: tests/test_dp_protocol.py."""
 import json
 import os
 import socket
@@ -86,6 +88,11 @@ def test_bench_gpus_n_launches_n_ranks(n):
     assert line["n_gpus"] == n and line["dry_run"] is True
     assert sorted(line["detail"]["ranks"]) == list(range(n))
     assert line["steps"] == 3 and line["value"] > 0
+    # the N > 1 line is ONE model trained data parallel, not N replicas
+    assert line["config"]["parallelism"] == "dp%d" % n
+    assert line["scaling"] == "strong" and line["cpu_baseline"] is None
+    assert line["detail"]["dp"]["replicas_identical"] is True
+    assert "ONE TransE-L1" in line["config"]["workload"]
 
 
 def test_bench_rejects_world_size_mismatch():
