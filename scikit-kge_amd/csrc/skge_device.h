@@ -125,8 +125,10 @@ __device__ __host__ __forceinline__ int acc_row_dwords(int mode, int width) {
 // converts the sum back once.  Range: |sum| < 2^23 per element and batch,
 // i.e. (a row's occurrences in the batch) x max |contribution| < 8.4e6 -- WN18
 // RESCAL at nb = 2 (~5e4 pairs of one relation, |E_s E_o| <= 1) stays far
-// inside; the applies flag any decoded sum past 2^22 (skge_device_error bit 4,
-// raised by the runners' synchronize()).
+// inside; the applies flag any decoded sum at or past 2^22 (skge_device_error
+// bit 4, raised by the runners' synchronize()) -- a partial guard: a true sum
+// in [2^22, 3*2^22) is caught wrapped or not, one past 3*2^22 can wrap back
+// below 2^22 unflagged.
 constexpr float FX_SCALE = 1099511627776.0f;            // 2^40
 __device__ __forceinline__ long long fx_enc(float v) { return __float2ll_rn(v * FX_SCALE); }
 __device__ __forceinline__ float fx_dec(long long x) {

@@ -97,9 +97,32 @@ struct RelTab {                // relation table
   int* updated;                // profile only: rows with a nonzero count (sharded)
 };
 
+// The fused TransE runner's entity table (k_pipe_fused, round 5).  Rows live
+// in one of two buffers; a row updated in launch g is written to the buffer
+// its previous value is NOT in, so the pre-update value stays readable for
+// the whole launch.  Sums, counts and slot records rotate over three copies
+// by launch id: launch g adds into copy g % 3, reads and applies copy
+// (g - 1) % 3 and zeroes copy (g - 2) % 3 (the copy launch g + 1 adds into).
+struct FusedTab {
+  float* P[2];        // P[0]: the caller's parameters; P[1]: the runner's second buffer
+  float* A[2];        // AdaGrad state, likewise (nullptr: SGD)
+  void* sum[3];       // exact packed sums (int8x4 / int16x4) by launch id % 3
+  int* cnt[3];
+  int* touched[3];    // slot records by launch id % 3: row | buffer << 30 (the buffer
+                      // holding the row after that launch), -1: no row
+  int4* meta;         // [rows]: x / y: id of the last even / odd launch that accumulated
+                      // into the row; z: (id of the launch that last wrote the row << 1) |
+                      // the buffer it wrote; w: id of the last launch that claimed its apply
+};
+constexpr int SLOT_BUF = 1 << 30;
+
 struct PipeArgs {
   PipeTab E;
   RelTab R;
+  FusedTab F;                  // fused runner (k_pipe_fused) only
+  int pprev_slots;             // fused: slots of the launch before the previous one (zeroed)
+  int nwork;                   // fused: work items (max of this, the previous and the
+                               // pre-previous launch's positives)
   const int4* rec;             // [T]: (s, o, p, s') of the epoch's positive j
   const int* rec_n1;           // [T]: o'
   long long start;             // B role: this batch's positives [start, start + count)
@@ -185,11 +208,13 @@ __device__ __forceinline__ void load_upd_row(const float* P, const float* A,
 // mean + AdaGrad / SGD + projection; the same arithmetic as apply_row_i16
 // (skge_update.hip) and the reference (skge/param.py:130, 147-155;
 // skge/transe.py normalize).  Lanes past the row end with zeros.
-template <int KQ, bool W32>
-__device__ __forceinline__ void row_update(const UpdParams& t, int c, int d,
-                                           const unsigned long long (&sv)[KQ],
-                                           const unsigned long long (&sw)[KQ], float4 (&p)[KQ],
-                                           float4 (&a)[KQ]) {
+// (row_update_s: the same from the sums already decoded to floats, zero past
+// the row -- the fused runner's form; every packed apply shares this code, so
+// a row's update has the same bits whichever kernel computes it)
+template <int KQ>
+__device__ __forceinline__ void row_update_s(const UpdParams& t, int c, int d,
+                                             const float4 (&sms)[KQ], float4 (&p)[KQ],
+                                             float4 (&a)[KQ]) {
   const int l = lane_id(), nq = d >> 2;
   const bool ada = t.opt == OPT_ADAGRAD;
   const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
@@ -197,13 +222,7 @@ __device__ __forceinline__ void row_update(const UpdParams& t, int c, int d,
 #pragma unroll
   for (int m = 0; m < KQ; ++m) {
     const bool in = 64 * m + l < nq;
-    float4 sm;
-    if (W32) {   // int32x2 sums: quad q in words sv (elements 0, 1) and sw (2, 3)
-      const float2 lo = unpack_i32x2(in ? sv[m] : 0ull), hi = unpack_i32x2(in ? sw[m] : 0ull);
-      sm = make_float4(lo.x, lo.y, hi.x, hi.y);
-    } else {     // int16x4 sums
-      sm = unpack_i16x4(in ? sv[m] : 0ull);
-    }
+    const float4 sm = sms[m];
 #define SKGE_UP(X)                                                      \
   {                                                                     \
     const float g = (sm.X + t.rin * p[m].X) / div + t.rout * p[m].X;    \
@@ -234,6 +253,26 @@ __device__ __forceinline__ void row_update(const UpdParams& t, int c, int d,
       p[m].w = p[m].w * inv;
     }
   }
+}
+
+template <int KQ, bool W32>
+__device__ __forceinline__ void row_update(const UpdParams& t, int c, int d,
+                                           const unsigned long long (&sv)[KQ],
+                                           const unsigned long long (&sw)[KQ], float4 (&p)[KQ],
+                                           float4 (&a)[KQ]) {
+  const int l = lane_id(), nq = d >> 2;
+  float4 sm[KQ];
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const bool in = 64 * m + l < nq;
+    if (W32) {   // int32x2 sums: quad q in words sv (elements 0, 1) and sw (2, 3)
+      const float2 lo = unpack_i32x2(in ? sv[m] : 0ull), hi = unpack_i32x2(in ? sw[m] : 0ull);
+      sm[m] = make_float4(lo.x, lo.y, hi.x, hi.y);
+    } else {     // int16x4 sums
+      sm[m] = unpack_i16x4(in ? sv[m] : 0ull);
+    }
+  }
+  row_update_s<KQ>(t, c, d, sm, p, a);
 }
 
 // Claim a pending entity row's update (the first wave to swap its count out
@@ -1138,6 +1177,389 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
   if (l == 0 && nv) {
     atomicAdd(shard_of(a.nviol_shards), nv);
     if (a.stats_viol) atomicAdd(shard_of(a.stats_viol), nv);
+  }
+}
+
+// ---- fused runner (round 5): one kind of wave, no hand-offs ----
+//
+// k_pipe_batch gives each launch two roles: apply waves for batch b-1's rows
+// (dispatched first) and scoring waves that WAIT for any row batch b-1
+// touched (claim / done word / write-through re-read).  Its per-wave traces
+// put the scoring waves' start at ~3.2 us (p50) behind ~1.4k apply
+// workgroups, with ~30% of them settling a pending row.  k_pipe_fused has one
+// kind of wave and nothing waits:
+//
+//   * work item w scores positive w of batch b, applies launch g-1's slot
+//     records 4w..4w+3 (claimed through the row's meta word) and zeroes the
+//     rows of launch g-2's slot records 4w..4w+3 (the accumulator copy launch
+//     g+1 adds into) -- one workgroup per four positives instead of one per
+//     positive plus one per slot record;
+//   * a scoring wave that reads a row batch b-1 touched computes that row's
+//     update itself from its pre-update value, state, sums and count
+//     (row_update_s, the applier's arithmetic: the same bits) instead of
+//     waiting for its publication.  The pre-update value stays readable all
+//     launch because the applier writes the row's OTHER buffer (FusedTab);
+//   * the buffer holding a row is its meta word z (launch id and buffer of the
+//     last write), loaded with its pending mark in the round trip that loads
+//     the row -- from both buffers, two 16-B loads per lane instead of a
+//     dependent third round trip.
+//
+// Relation rows as in k_pipe_batch (double-buffered and recomputed by every
+// scoring wave; items 0..nR-1 publish them for the next launch).  After a
+// runner's epochs k_fused_fin copies rows living in buffer 1 back into the
+// caller's tables and clears the meta words.
+
+template <int KQ, bool E8>
+__device__ __forceinline__ void load_sums_raw(const void* S, int row, int d,
+                                              unsigned long long (&sv)[KQ]) {
+  const int l = lane_id(), nq = d >> 2;
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
+    if (E8)
+      sv[m] = reinterpret_cast<const unsigned int*>(S)[(size_t)row * nq + qc];
+    else
+      sv[m] = reinterpret_cast<const unsigned long long*>(S)[(size_t)row * nq + qc];
+  }
+}
+
+// packed sums -> floats (exact small integers), zero past the row
+template <int KQ, bool E8>
+__device__ __forceinline__ void decode_sums(const unsigned long long (&sv)[KQ], int d,
+                                            float4 (&sm)[KQ]) {
+  const int l = lane_id(), nq = d >> 2;
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const bool in = 64 * m + l < nq;
+    sm[m] = E8 ? unpack_i8x4_sum(in ? (unsigned int)sv[m] : 0u) : unpack_i16x4(in ? sv[m] : 0ull);
+  }
+}
+
+// P (and A) of a row from buffer b, clamped unconditional loads
+template <int KQ>
+__device__ __forceinline__ void load_pa(const FusedTab& F, int b, int row, int d,
+                                        float4 (&p)[KQ], float4 (&av)[KQ]) {
+  const int l = lane_id(), nq = d >> 2;
+  const float4* prow = reinterpret_cast<const float4*>(F.P[b] + (size_t)row * d);
+  const float4* arow = reinterpret_cast<const float4*>((F.A[0] ? F.A[b] : F.P[b]) + (size_t)row * d);
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
+    p[m] = prow[qc];
+    av[m] = F.A[0] ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+}
+
+template <int KQ, bool E8>
+__device__ __forceinline__ void zero_sums_row(void* S, int* cnt, int row, int d) {
+  const int l = lane_id(), nq = d >> 2;
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l;
+    if (q < nq) {
+      if (E8)
+        reinterpret_cast<unsigned int*>(S)[(size_t)row * nq + q] = 0u;
+      else
+        reinterpret_cast<unsigned long long*>(S)[(size_t)row * nq + q] = 0ull;
+    }
+  }
+  if (l == 0) cnt[row] = 0;
+}
+
+template <int KQ>
+__device__ __forceinline__ void store_row4(float* T, int row, int d, const float4 (&v)[KQ]) {
+  const int l = lane_id(), nq = d >> 2;
+  float4* base = reinterpret_cast<float4*>(T + (size_t)row * d);
+#pragma unroll
+  for (int m = 0; m < KQ; ++m)
+    if (64 * m + l < nq) base[64 * m + l] = v[m];
+}
+
+template <int KQ, bool W32, bool E8>
+__global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
+  const int wpb = blockDim.x >> 6;
+  const int l = lane_id();
+  const int d = a.d, nq = d >> 2;
+  const int rcw = W32 ? 2 * nq : nq;   // relation accumulator: the count word
+  const int g = launch_id(a), gp = g - 1;
+  const int k0 = g % 3, k1 = (g + 2) % 3, k2 = (g + 1) % 3;   // copies of launches g, g-1, g-2
+  const int rd = a.b & 1;                    // relation buffer holding R_{b-1}
+  const int rw = a.b < a.nb1 ? rd ^ 1 : 0;   // ... receiving R_b (the flush: the caller's)
+  const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
+  const bool flush = a.b == a.nb1;
+  const bool ada = a.F.A[0] != nullptr;
+  const int nR = a.R.rows;
+  const int w0 = (int)blockIdx.x * wpb + (int)(threadIdx.x >> 6);
+  const int nwv = (int)gridDim.x * wpb;
+  if (flush && w0 == 0) fold_shards(a.nviol_shards, a.nviol_total);   // the epoch's violations
+  unsigned long long* const racc0 = opaque_ptr(a.R.acc[ra_cur]);
+  const size_t rrep = (size_t)a.R.rows * a.R.rw;   // words per relation replica
+  const int rmask = a.R.reps - 1;
+  void* const esum = opaque_ptr(a.F.sum[k0]);
+  const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int4*>(a.rec + a.start), 0, a.count * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rec1_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int*>(a.rec_n1 + a.start), 0, a.count * 4, 0x00020000);
+  int nv = 0, napp = 0;
+  for (int item = w0; item < nR + a.nwork; item += nwv) {
+    if (item < nR) {   // relation row `item`: R_b for the next launch, old sums cleared
+      rel_publish<KQ, W32>(a, item, rd, rw, ra_prev, ra_old);
+      continue;
+    }
+    const int w = item - nR;
+    const bool sc = w < a.count;
+    unsigned long long tt[4] = {0ull, 0ull, 0ull, 0ull};
+    if (a.trace) tt[0] = now_10ns();
+    // ---- round trip 1: the record; slot records 4w..4w+3 of launch g-1 (lanes
+    // 0-3: applied here) and of launch g-2 (lanes 4-7: their rows zeroed) ----
+    u32x4 rx = {0u, 0u, 0u, 0u};
+    int r1v = -1;
+    if (sc) {
+      rx = __builtin_amdgcn_raw_buffer_load_b128(rec_rs, w * 16, 0, 0);
+      r1v = (int)__builtin_amdgcn_raw_buffer_load_b32(rec1_rs, w * 4, 0, 0);
+    }
+    int sl = -1;
+    {
+      const int i = 4 * w + (l & 3);
+      const bool lo = l < 4;
+      if (lo ? i < a.prev_slots : (l < 8 && i < a.pprev_slots))
+        sl = (lo ? a.F.touched[k1] : a.F.touched[k2])[i];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int s = uni((int)rx.x), o = uni((int)rx.y), p = uni((int)rx.z);
+    const int neg0 = uni((int)rx.w), neg1 = uni(r1v);
+    const int n0r = neg0 >= 0 ? neg0 : s, n1r = neg1 >= 0 ? neg1 : o;
+    // launch g-2's rows: zero their sums and counts (copy k2: read by nobody in
+    // this launch, added into by the next)
+#pragma unroll
+    for (int j = 4; j < 8; ++j) {
+      const int v = __builtin_amdgcn_readlane(sl, j);
+      if (v >= 0) zero_sums_row<KQ, E8>(a.F.sum[k2], a.F.cnt[k2], v & (SLOT_BUF - 1), d);
+    }
+    // ---- round trip 2: the scoring rows from both buffers, their meta words,
+    // launch g-1's rows named by this item's slots (claim, value, state, sums,
+    // count) and the relation row ----
+    float4 x0[4][KQ], x1[4][KQ];
+    int4 mt = make_int4(0, 0, 0, 0);
+    if (sc) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = sel4(k, s, o, n0r, n1r);
+        load_row4<KQ>(a.F.P[0], r, d, x0[k]);
+        load_row4<KQ>(a.F.P[1], r, d, x1[k]);
+      }
+      if (l < 4) mt = a.F.meta[sel4(l, s, o, n0r, n1r)];
+    }
+    int won = 0, cl = 0;
+    if (l < 4 && sl >= 0) {
+      const int r = sl & (SLOT_BUF - 1);
+      won = atomicExch(&a.F.meta[r].w, g) != g;   // the first of its slots to get here applies it
+      cl = a.F.cnt[k1][r];
+    }
+    float4 ap[4][KQ], aa[4][KQ];
+    unsigned long long asv[4][KQ];
+    int arow[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      arow[j] = __builtin_amdgcn_readlane(sl, j);
+      if (arow[j] >= 0) {
+        const int r = arow[j] & (SLOT_BUF - 1), b = arow[j] >> 30;
+        load_pa<KQ>(a.F, b, r, d, ap[j], aa[j]);
+        load_sums_raw<KQ, E8>(a.F.sum[k1], r, d, asv[j]);
+      }
+    }
+    float4 rp[KQ];
+    if (sc) {
+      float4 ra[KQ];
+      int c;
+      rel_row<KQ, W32>(a.R, p, d, rd, ra_prev, rp, ra, c);
+    }
+    if (a.trace) tt[1] = now_10ns();
+    // where each scoring row lives, and which batch b-1 touched (lanes 0-3)
+    const int pw = (gp & 1) ? mt.y : mt.x;
+    const unsigned cur = (unsigned)mt.z;
+    const int bn = ((int)(cur >> 1) == g) ? (int)((cur & 1u) ^ 1u) : (int)(cur & 1u);
+    const uint64_t pend = sc ? (__ballot(l < 4 && pw == gp) & 0xfull) : 0ull;
+    const uint64_t inb1 = __ballot(l < 4 && bn == 1) & 0xfull;
+    float4 e[4][KQ];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) e[k][m] = ((inb1 >> k) & 1ull) ? x1[k][m] : x0[k][m];
+    // ---- round trip 3 (only rows batch b-1 touched): their state, sums, count ----
+    float4 pa[4][KQ];
+    unsigned long long psv[4][KQ];
+    int pc = 0;
+    if (pend) {
+      if (l < 4 && ((pend >> l) & 1ull)) pc = a.F.cnt[k1][sel4(l, s, o, n0r, n1r)];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!((pend >> k) & 1ull)) continue;
+        const int r = sel4(k, s, o, n0r, n1r), b = (int)((inb1 >> k) & 1ull);
+        if (ada) {
+          const float4* arow = reinterpret_cast<const float4*>(a.F.A[b] + (size_t)r * d);
+#pragma unroll
+          for (int m = 0; m < KQ; ++m) {
+            const int q = 64 * m + l;
+            pa[k][m] = arow[q < nq ? q : nq - 1];
+          }
+        }
+        load_sums_raw<KQ, E8>(a.F.sum[k1], r, d, psv[k]);
+      }
+    }
+    // ---- apply launch g-1's claimed rows (beside round trip 3): into the
+    // row's other buffer, then its meta word; nothing waits for them ----
+    const uint64_t wonm = __ballot(won != 0) & 0xfull;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!((wonm >> j) & 1ull)) continue;
+      const int c = __builtin_amdgcn_readlane(cl, j);
+      const int r = arow[j] & (SLOT_BUF - 1), b = arow[j] >> 30;
+      if (c > (E8 ? 127 : PACKED_MAX) && l == 0) atomicOr(a.err, ERR_PACKED);
+      float4 sm[KQ];
+      decode_sums<KQ, E8>(asv[j], d, sm);
+      row_update_s<KQ>(a.E.u, c, d, sm, ap[j], aa[j]);
+      store_row4<KQ>(a.F.P[b ^ 1], r, d, ap[j]);
+      if (ada) store_row4<KQ>(a.F.A[b ^ 1], r, d, aa[j]);
+      if (l == 0) a.F.meta[r].z = (g << 1) | (b ^ 1);
+      if (flush) zero_sums_row<KQ, E8>(a.F.sum[k1], a.F.cnt[k1], r, d);   // nobody reads them again
+      ++napp;
+    }
+    if (!sc) continue;
+    // ---- the pending rows' updates, computed here (the same bits as the
+    // applier's): the values batch b scores with ----
+    if (pend) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!((pend >> k) & 1ull)) continue;
+        const int c = __builtin_amdgcn_readlane(pc, k);
+        float4 sm[KQ], av[KQ];
+        decode_sums<KQ, E8>(psv[k], d, sm);
+#pragma unroll
+        for (int m = 0; m < KQ; ++m) av[m] = ada ? pa[k][m] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        row_update_s<KQ>(a.E.u, c, d, sm, e[k], av);
+      }
+    }
+    if (a.trace) tt[2] = now_10ns();
+    float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
+    float4 gp4[KQ], g0[KQ], g1[KQ];
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+#define SKGE_EL(X)                                                                    \
+  {                                                                                   \
+    const float vp = (e[0][m].X + rp[m].X) - e[1][m].X;   /* transe.py:32 */          \
+    const float v0 = (e[2][m].X + rp[m].X) - e[1][m].X;                               \
+    const float v1 = (e[0][m].X + rp[m].X) - e[3][m].X;                               \
+    ps += fabsf(vp);                                                                  \
+    n0 += fabsf(v0);                                                                  \
+    n1 += fabsf(v1);                                                                  \
+    gp4[m].X = signf_np(-((e[1][m].X - rp[m].X) - e[0][m].X)); /* transe.py:103,115 */ \
+    g0[m].X = signf_np((e[1][m].X - rp[m].X) - e[2][m].X);     /* transe.py:104,117 */ \
+    g1[m].X = signf_np((e[3][m].X - rp[m].X) - e[0][m].X);                            \
+  }
+      SKGE_EL(x)
+      SKGE_EL(y)
+      SKGE_EL(z)
+      SKGE_EL(w)
+#undef SKGE_EL
+    }
+    const float pscore = -wave_sum(ps);
+    const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
+    const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // strict >, transe.py:73
+    const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
+    if (a.trace) tt[3] = now_10ns();
+    unsigned long long* const racc = racc0 + (size_t)(w & rmask) * rrep;
+    {
+      // counts, slot records (with the buffer the row is in after this
+      // launch) and pending marks of batch b
+      const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
+      const int rE = sel4(l, s, o, neg0, neg1);
+      if (l < 4) {
+        const int bend = bn ^ (int)((pend >> l) & 1ull);
+        a.F.touched[k0][4 * w + l] = cE > 0 ? (rE | (bend << 30)) : -1;
+        if (cE > 0) {
+          atomicAdd(a.F.cnt[k0] + rE, cE);
+          reinterpret_cast<int*>(a.F.meta + rE)[g & 1] = g;
+        }
+      } else if (l == 4 && v0 + v1 > 0) {
+        atomicAdd(racc + (size_t)p * a.R.rw + rcw, (unsigned long long)(2 * (v0 + v1)));
+      }
+    }
+    if (v0 + v1 > 0) {
+      nv += v0 + v1;
+      const float fv0 = (float)v0, fv1 = (float)v1;
+      float4 cs[KQ], co[KQ], c0[KQ], c1[KQ], cr[KQ];
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) {
+#define SKGE_CO(X)                                                   \
+  cs[m].X = fv0 * gp4[m].X + fv1 * (gp4[m].X + g1[m].X);             \
+  co[m].X = -(fv0 * (gp4[m].X + g0[m].X) + fv1 * gp4[m].X);          \
+  c0[m].X = g0[m].X;                                                 \
+  c1[m].X = -g1[m].X;                                                \
+  cr[m].X = fv0 * (gp4[m].X + g0[m].X) + fv1 * (gp4[m].X + g1[m].X);
+        SKGE_CO(x)
+        SKGE_CO(y)
+        SKGE_CO(z)
+        SKGE_CO(w)
+#undef SKGE_CO
+      }
+      if (E8) {
+        unsigned int* es8 = reinterpret_cast<unsigned int*>(esum);
+        acc_row4_i8<KQ>(es8, s, cs, d);
+        acc_row4_i8<KQ>(es8, o, co, d);
+        if (v0) acc_row4_i8<KQ>(es8, neg0, c0, d);
+        if (v1) acc_row4_i8<KQ>(es8, neg1, c1, d);
+      } else {
+        Accum aE = {};
+        aE.sum = reinterpret_cast<float*>(esum);
+        acc_row4_i16<KQ>(aE, s, cs, d);
+        acc_row4_i16<KQ>(aE, o, co, d);
+        if (v0) acc_row4_i16<KQ>(aE, neg0, c0, d);
+        if (v1) acc_row4_i16<KQ>(aE, neg1, c1, d);
+      }
+      unsigned long long* rrow = racc + (size_t)p * a.R.rw;
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) {
+        const int q = 64 * m + l;
+        if (q < nq) {
+          if (W32) {
+            atomicAdd(rrow + 2 * q, pack_i32x2(cr[m].x, cr[m].y));
+            atomicAdd(rrow + 2 * q + 1, pack_i32x2(cr[m].z, cr[m].w));
+          } else {
+            atomicAdd(rrow + q, pack_i16x4(cr[m]));
+          }
+        }
+      }
+    }
+    if (a.trace && l == 0) {   // stamp after issue (no drain)
+      unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
+      tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
+      tr[5] = pend | ((unsigned long long)(v0 + v1 > 0) << 8);
+    }
+  }
+  if (l == 0) {
+    if (nv) {
+      atomicAdd(shard_of(a.nviol_shards), nv);
+      if (a.stats_viol) atomicAdd(shard_of(a.stats_viol), nv);
+    }
+    if (napp && a.E.claims) atomicAdd(shard_of(a.E.claims), napp);
+  }
+}
+
+// after a fused runner's epochs: rows whose current value is in buffer 1
+// copied into buffer 0 (the caller's tables); the meta words are then cleared
+// (hipMemsetAsync), so between runs every row lives in the caller's tables
+__global__ __launch_bounds__(256) void k_fused_fin(FusedTab F, int rows, int d) {
+  const int nq = d >> 2;
+  const long long n = (long long)rows * nq;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / nq), q = (int)(i - (long long)r * nq);
+    if (F.meta[r].z & 1) {
+      const size_t off = (size_t)r * nq + q;
+      reinterpret_cast<float4*>(F.P[0])[off] = reinterpret_cast<const float4*>(F.P[1])[off];
+      if (F.A[0]) reinterpret_cast<float4*>(F.A[0])[off] = reinterpret_cast<const float4*>(F.A[1])[off];
+    }
   }
 }
 
@@ -2541,6 +2963,8 @@ struct skge_pipe_runner {
   size_t lds = 0;                  // HolE: dynamic LDS per workgroup
   bool pair = false;               // HolE FFT, d = 200: two waves per positive (SKGE_HPIPE_PAIR)
   bool p2 = false;                 // TransE large batches: two positives per scoring wave (SKGE_PIPE_P2)
+  bool fused = false;              // TransE: k_pipe_fused (one kind of wave, no hand-offs)
+  int n_rows = 0, d = 0;           // fused: the entity table's geometry (k_fused_fin)
   int nlaunch() const { return (int)batch.size() + 2; }
 };
 
@@ -2562,6 +2986,18 @@ static void pipe_free(skge_pipe_runner* r) {
   if (r->st2) (void)hipStreamDestroy(r->st2);
   for (void* p : r->bufs) (void)hipFree(p);
   delete r;
+}
+
+template <int K>
+static void launch_fused(const skge_pipe_runner* r, dim3 gr, hipStream_t st, const PipeArgs& a) {
+  const dim3 bl(SKGE_PIPE_WG);
+  if (r->e8) {
+    if (r->w32) hipLaunchKernelGGL((k_pipe_fused<K, true, true>), gr, bl, 0, st, a);
+    else hipLaunchKernelGGL((k_pipe_fused<K, false, true>), gr, bl, 0, st, a);
+  } else {
+    if (r->w32) hipLaunchKernelGGL((k_pipe_fused<K, true, false>), gr, bl, 0, st, a);
+    else hipLaunchKernelGGL((k_pipe_fused<K, false, false>), gr, bl, 0, st, a);
+  }
 }
 
 // Enqueue one epoch: draw the negatives, nb1 batch launches, the flush, the
@@ -2676,6 +3112,9 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
         default: SKGE_HPIPE(4) break;
 #undef SKGE_HPIPE
       }
+    } else if (r->fused) {
+      if (r->kq <= 1) launch_fused<1>(r, dim3(r->grid[k]), st, a);
+      else launch_fused<2>(r, dim3(r->grid[k]), st, a);
     } else if (r->kq <= 1) SKGE_PB(1);
     else if (r->kq <= 2) SKGE_PB(2);
     else SKGE_PB(4);
@@ -2693,6 +3132,16 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
   }
   hipLaunchKernelGGL(k_pipe_advance, dim3(1), dim3(1), 0, st, r->epoch_key);
   if (ev) (void)hipEventRecord(ev[i + 1], st);
+}
+
+// fused runner: every row back into the caller's tables (buffer 0), meta cleared
+static void fused_finalize(const skge_pipe_runner* r, hipStream_t st) {
+  if (!r->fused) return;
+  const FusedTab& F = r->batch[0].F;
+  const long long n = (long long)r->n_rows * (r->d / 4);
+  const unsigned blocks = (unsigned)std::max(1ll, std::min((n + 255) / 256, 8192ll));
+  hipLaunchKernelGGL(k_fused_fin, dim3(blocks), dim3(256), 0, st, F, r->n_rows, r->d);
+  (void)hipMemsetAsync(F.meta, 0, (size_t)r->n_rows * sizeof(int4), st);
 }
 
 static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
@@ -2862,6 +3311,40 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
       return nullptr;
     }
   }
+  {
+    // fused runner (default at batches without owner marks, d <= 512;
+    // SKGE_PIPE_FUSED=0: k_pipe_batch): the second row buffer, the third
+    // accumulator copy and the per-row meta words
+    const char* fe = getenv("SKGE_PIPE_FUSED");
+    r->fused = !hole && !lazy && !r->owner && !r->split && !r->p2 && a.E.own[0] == nullptr &&
+               nq <= 128 && (long long)ent->rows < SLOT_BUF && !(fe && atoi(fe) == 0);
+    if (r->fused) {
+      FusedTab& F = a.F;
+      const int N = ent->rows;
+      const size_t sb = (size_t)N * nq * (r->e8 ? 4 : 8);
+      F.P[0] = ent->param;
+      F.P[1] = (float*)dalloc(r, (size_t)N * d * 4);
+      F.A[0] = ent->opt == SKGE_ADAGRAD ? ent->state : nullptr;
+      F.A[1] = F.A[0] ? (float*)dalloc(r, (size_t)N * d * 4) : nullptr;
+      F.sum[0] = ent->acc_sum;
+      F.cnt[0] = ent->acc_cnt;
+      F.touched[0] = ent->acc_touched;
+      for (int k = 1; k < 3; ++k) {
+        F.sum[k] = dalloc(r, sb);
+        F.cnt[k] = (int*)dalloc(r, (size_t)N * 4);
+        F.touched[k] = (int*)dalloc(r, (size_t)4 * bs * 4);
+      }
+      F.meta = (int4*)dalloc(r, (size_t)N * sizeof(int4));
+      r->n_rows = N;
+      r->d = d;
+      if (!F.P[1] || (F.A[0] && !F.A[1]) || !F.sum[1] || !F.sum[2] || !F.cnt[1] || !F.cnt[2] ||
+          !F.touched[1] || !F.touched[2] || !F.meta) {
+        set_error("pipelined runner: device allocation failed");
+        pipe_free(r);
+        return nullptr;
+      }
+    }
+  }
   r->rec = (int4*)dalloc(r, (size_t)T * sizeof(int4));
   r->rec_n1 = (int*)dalloc(r, (size_t)T * 4);
   r->err = (int*)dalloc(r, 4);
@@ -2999,6 +3482,20 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     const int b_items = p2_here ? (a.count + 1) / 2 : a.count;
     const int nBb = r->pair ? std::max(1, std::min(a.count, 2 * 16384))
                             : std::max(1, std::min((b_items + WPB - 1) / WPB, b_cap));
+    if (r->fused) {
+      // the epoch starts clean (the flush zeroes both copies it leaves), so a
+      // batch's first two launches have no pre-previous slots to zero
+      const int cprev = b >= 1 ? (int)batches[b - 1].second : 0;
+      const int cpp = b >= 2 ? (int)batches[b - 2].second : 0;
+      a.prev_slots = 4 * cprev;
+      a.pprev_slots = 4 * cpp;
+      a.nwork = std::max(a.count, std::max(cprev, cpp));
+      a.nA = 0;
+      r->batch.push_back(a);
+      r->grid.push_back(std::max(1, (rel->rows + a.nwork + WPB - 1) / WPB));
+      prev = a.count;
+      continue;
+    }
     r->batch.push_back(a);
     r->grid.push_back(a.nA + (a.count > 0 ? nBb : 0));
     prev = a.count;
@@ -3058,6 +3555,8 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
 extern "C" int skge_pipe_runner_run(skge_pipe_runner_t* r, void* stream, int nepochs) {
   SKGE_CHECK_ARG(r && r->exec, "bad runner");
   for (int i = 0; i < nepochs; ++i) SKGE_CHECK_HIP(hipGraphLaunch(r->exec, as_stream(stream)));
+  fused_finalize(r, as_stream(stream));
+  SKGE_CHECK_LAUNCH("pipelined runner finalize");
   return SKGE_OK;
 }
 
@@ -3094,6 +3593,7 @@ extern "C" int skge_pipe_runner_profile(skge_pipe_runner_t* r, void* stream, flo
   }
   if (rc == SKGE_OK) {
     enqueue_epoch(r, st, ev.data(), r->stats, trace_launch, dtrace);
+    fused_finalize(r, st);
     if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) rc = SKGE_EHIP;
   }
   if (rc == SKGE_OK) {

@@ -13,12 +13,16 @@ namespace skge {
 
 // error bits raised by apply kernels (read with skge_device_error):
 // 2 = a packed int16x4 row's count exceeded 32767 (its sums may have wrapped)
-// 4 = a deterministic fixed-point (ACC_FX64) sum reached half its range
-//     (|sum| >= 2^22 in gradient units; it wraps at 2^23)
+// 4 = a deterministic fixed-point (ACC_FX64) sum decoded at or past half its
+//     range (|sum| >= 2^22 in gradient units; it wraps at 2^23).  A PARTIAL
+//     guard: true sums of magnitude in [2^22, 3*2^22) decode to >= 2^22
+//     (wrapped or not) and are caught; a sum past 3*2^22 can wrap back below
+//     2^22 and pass.  The range is sized so the largest case measured (WN18
+//     RESCAL at nb = 2) stays orders of magnitude inside it (skge_device.h).
 __device__ int g_skge_dev_err = 0;
 
 // FX64 sums wrap silently past +-2^63 (2^23 in gradient units, FX_SCALE):
-// flag any decoded element at or past half of that range
+// flag any decoded element at or past half of that range (partial: see above)
 __device__ __forceinline__ void fx_check(long long x) {
   constexpr long long HALF = 1ll << 62;
   if (x >= HALF || x <= -HALF) atomicOr(&g_skge_dev_err, 4);

@@ -175,6 +175,8 @@ def check_device_error(stream_handle, what="device"):
         raise SkgeError("%s: a row's per-batch count exceeded 32767 (packed sums may have "
                         "wrapped); use force_f32=True" % what)
     if rc & 4:
-        raise SkgeError("%s: a deterministic fixed-point (FX64) sum reached 2^22 -- past 2^23 "
-                        "it wraps; use more batches or the default float sums" % what)
+        raise SkgeError("%s: a deterministic fixed-point (FX64) sum decoded at or past 2^22 "
+                        "(half of its 2^23 wrap-around range; this guard is partial: a sum past "
+                        "3*2^22 can wrap back below 2^22 unflagged); use more batches or the "
+                        "default float sums" % what)
     return rc
