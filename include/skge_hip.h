@@ -359,9 +359,16 @@ void skge_pair_runner_destroy(skge_pair_runner_t *r);
  * throughput path).  Same result, bit for bit, as skge_runner_create's loop
  * with the same tables and arguments: all negatives of an epoch are drawn in
  * one launch, then each mini-batch is ONE launch that scores batch b while
- * applying batch b-1's updates (accumulators double-buffered by batch parity;
- * a scoring wave that reads a row batch b-1 touched applies it first or waits
- * for its publisher).  Needs ent in SKGE_ACC_I16X4 mode, rel in
+ * applying batch b-1's updates.  Below 16k slot records per batch (d <= 512)
+ * every wave of a launch scores one positive, applies four slot records of
+ * the previous batch and zeroes four of the batch before (k_pipe_fused); a
+ * row the previous batch touched is updated by each of its readers itself,
+ * from its pre-update value, which stays readable because the applier
+ * writes the row's other buffer (the runner's second copy of E and its
+ * AdaGrad state; run() and profile() end by copying every row back into the
+ * caller's tables).  Larger batches: apply waves beside scoring waves that
+ * wait for a pending row's publisher (k_pipe_batch, owner marks).  Needs ent
+ * in SKGE_ACC_I16X4 mode (SKGE_ACC_I8X4: int8x4 sums, counts <= 127), rel in
  * SKGE_ACC_I16X4 or SKGE_ACC_I32X2 mode (the encoding of the relation sums
  * the runner keeps), d % 4 == 0, an entity table with slot records (capacity
  * >= 4 * batch), a dense single-copy relation table and no gates.  Any batch
@@ -369,8 +376,8 @@ void skge_pair_runner_destroy(skge_pair_runner_t *r);
  * <= 32767 (each occurrence adds a coefficient no larger than the count it
  * adds), and the apply reports a larger count through skge_pipe_runner_error
  * (bit 2); 32-bit relation sums are exact below 2^29 positives.  Allocates
- * the second accumulator copy and per-row batch marks itself (freed by
- * destroy).  *epoch_key must only advance (the runner advances it once per
+ * its extra accumulator copies, row buffers and per-row words itself (freed
+ * by destroy).  *epoch_key must only advance (the runner advances it once per
  * epoch).  Replaces the per-batch loop of skge/base.py:1268-1284.
  */
 typedef struct skge_pipe_runner skge_pipe_runner_t;
@@ -379,15 +386,8 @@ skge_pipe_runner_t *skge_pipe_runner_create(void *stream, const skge_table_t *en
                                             int64_t T, const void *set, int64_t set_capacity,
                                             int nbatches, uint64_t seed, uint64_t *epoch_key,
                                             float margin, int ntries, int *nviol_total);
-/* flags of skge_pipe_runner_create_ex */
-enum {
-  SKGE_PIPE_LAZY = 1   /* lazy apply: no entity apply waves; the first wave of a later batch
-                          to read a row applies its pending update (claimed with an atomicMax
-                          on a per-row launch id, published write-through), the epoch's flush
-                          launch applies the rest.  One entity accumulator copy (the caller's;
-                          no slot records needed), two int words per entity row.  Same
-                          parameters, bit for bit. */
-};
+/* skge_pipe_runner_create with a flags word; no flags are defined (round 5
+ * removed the lazy-apply variant, measured slower): flags must be 0. */
 skge_pipe_runner_t *skge_pipe_runner_create_ex(void *stream, const skge_table_t *ent,
                                                const skge_table_t *rel, int d, const int *trip,
                                                int64_t T, const void *set, int64_t set_capacity,

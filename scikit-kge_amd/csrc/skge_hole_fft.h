@@ -462,67 +462,6 @@ __device__ __forceinline__ const float* hole_fft_rows_pair(float* wbuf, const fl
   return reinterpret_cast<const float*>(z);
 }
 
-// SPEC form of hole_fft_rows (the pipelined runner's spectral entity sums,
-// SKGE_HPIPE_SPEC): the entity rows' pre-processed half spectra Z' -- the
-// inverse transform's input, linear in the row -- stay in b0 as signals 0
-// E[s], 1 E[o], then E[s'] (v0), E[o'] (v1), and only the relation row
-// (signal ne = 2 + v0 + v1) is inverse-transformed; the appliers transform
-// each entity row's summed Z' once.  Returns the relation row (float view,
-// row 0) and sets ne.
-__device__ __forceinline__ const float* hole_fft_rows_spec(float* wbuf, const float2* tw, int d,
-                                                           const HoleSpec& h, int v0, int v1,
-                                                           float gp, float g0, float g1, int& ne) {
-  const int M = d / 2;
-  float2* b0 = reinterpret_cast<float2*>(wbuf);
-  float2* b1 = b0 + 5 * M;
-  const float cE = (float)(v0 + v1) * gp, cF = v1 ? g1 : 0.0f;
-  const float cu = (float)(v0 + v1) * gp, cf = v0 ? g0 : 0.0f;
-  ne = 2 + v0 + v1;
-  __builtin_amdgcn_wave_barrier();   // every lane is done reading the forward buffers
-  if (h.on) {
-    float2 H[5][2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float2 r = h.r[j], eo = h.eo[j], fo = h.fo[j], es = h.es[j];
-      const float2 uh = cadd(cscale(cu, es), cscale(cf, h.fs[j]));
-      H[0][j] = cmulc(r, cadd(cscale(cE, eo), cscale(cF, fo)));          // E[s]
-      H[1][j] = cmul(r, uh);                                            // E[o]
-      H[2][j] = cadd(cmulc(uh, eo), cscale(cF, cmulc(es, fo)));         // R[p]
-      H[3][j] = cscale(g0, cmulc(r, eo));                               // E[s'] (v0)
-      H[4][j] = cscale(g1, cmul(r, es));                                // E[o'] (v1)
-    }
-    const int k = h.k;
-    fft_real_inv_pair(b0 + 0 * M, M, k, tw, H[0][0], H[0][1]);
-    fft_real_inv_pair(b0 + 1 * M, M, k, tw, H[1][0], H[1][1]);
-    int t = 2;
-    if (v0) fft_real_inv_pair(b0 + (t++) * M, M, k, tw, H[3][0], H[3][1]);
-    if (v1) fft_real_inv_pair(b0 + (t++) * M, M, k, tw, H[4][0], H[4][1]);
-    fft_real_inv_pair(b0 + t * M, M, k, tw, H[2][0], H[2][1]);
-  }
-  float2* z = M == 100 ? fft_run_c<100, 1, true>(b0 + ne * M, b1, tw)
-                       : fft_run<true>(b0 + ne * M, b1, M, 1, tw, d);
-  return reinterpret_cast<const float*>(z);
-}
-
-// An entity row's summed Z' (quad layout, scaled by 1/M when accumulated) ->
-// its spatial sums: one inverse transform in the wave's buffers.  Every
-// applier of a SPEC runner calls this one function, so a row's update has
-// the same bits whichever wave applies it.
-template <int KQ>
-__device__ __forceinline__ void spec_to_spatial(float* wbuf, const float2* tw, int d,
-                                                float4 (&sm)[KQ]) {
-  static_assert(KQ == 1, "spectral sums: d <= 256");
-  const int M = d / 2;
-  float2* b0 = reinterpret_cast<float2*>(wbuf);
-  float2* b1 = b0 + 5 * M;
-  __builtin_amdgcn_wave_barrier();
-  fft_put_row(b0, M, 0, sm[0], d);
-  const float2* z = M == 100 ? fft_run_c<100, 1, true>(b0, b1, tw)
-                             : fft_run<true>(b0, b1, M, 1, tw, d);
-  sm[0] = fft_get_row(z, M, 0, 1.0f, d);
-  __builtin_amdgcn_wave_barrier();   // the buffers are free again
-}
-
 // row t of hole_fft_rows' output, scaled by 1/M, added into accumulator row
 // `row`: lane l takes elements l + 64 k, so each float-atomic instruction
 // covers contiguous bytes (MI355X_MICROARCH.md "Global float atomics")

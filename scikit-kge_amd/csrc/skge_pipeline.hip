@@ -68,21 +68,10 @@ struct PipeTab {               // entity table
                                // (plain stores, one survives): the A role applies a row from
                                // that slot only, so duplicate slots cost no claim
   int* done;                   // [rows]: id of the launch whose update of the row was last applied
-                               // (lazy: whose first reader of the row has published it)
-  int* claim;                  // lazy only, [rows]: id of the last launch that claimed the row
   UpdParams u;
   int* claims;                 // profile only: rows applied in this launch (sharded)
   int* err;                    // ERR_* bits
-  unsigned long long* refs[2]; // owner mode, [rows] by batch parity: the batch's references to
-                               // the row, total (high word, fixed within the launch) and not
-                               // yet retired (low word) (k_own_batch)
-  int a4;                      // 1: one A-role wave per positive's 4 slots, one row per 16-lane
-                               // group (claim_and_apply4; d <= 256)
-  int agrp;                    // > 0: the A role's entity waves in groups of AGRP_WAVES, each
-                               // group over `agrp` slot records (one vector load), its waves
-                               // taking turns over the slots that name a row; 0: one wave per slot
 };
-constexpr int AGRP_WAVES = 4;
 
 struct RelTab {                // relation table
   float* P[2];                 // P[0]: the caller's parameters; P[1]: the other buffer
@@ -127,14 +116,11 @@ struct PipeArgs {
   const int* rec_n1;           // [T]: o'
   long long start;             // B role: this batch's positives [start, start + count)
   int count;
-  int count_next;              // owner mode: the next batch's positives (from start + count)
   int prev_slots;              // A role: entity slots of the previous batch
   int b, nb1;                  // batch index in the epoch (nb1: the flush), batches per epoch
   const uint64_t* epoch_key;
   int d, nA;                   // nA: workgroups of the A role
-  int n_ent;                   // entity rows (the lazy flush scans them all)
   int af;                      // HolE: activation (skge/actfun.py)
-  int b_first;                 // HolE: scoring workgroups dispatched first
   float margin;
   int* nviol_total;            // the caller's counter: += the epoch's violations, at the flush
   int* nviol_shards;           // [NSHARD][SHARD_STRIDE]: this epoch's violations so far
@@ -328,130 +314,6 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
   if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
 }
 
-// Four slot-recorded rows per A-role wave, in parallel: 16-lane group k holds
-// slot 4i + k's row, lane j of a group quads j, j + 16, j + 32, j + 48 (d <=
-// 256).  Claims (one atomic instruction), loads, updates, write-through stores
-// and the drain are one chain for all four rows -- a wave per positive instead
-// of a wave per slot, with the one-row wave's chain length.  row_update4 is
-// row_update's arithmetic element for element, and its squared-norm reduction
-// follows wave_sum's order exactly (register k of a group holds what lanes 16k
-// .. 16k + 15 hold in the one-row layout; the same four DPP steps per 16-lane
-// row, then (k0 + k1) + (k2 + k3)), so a row gets the same bits whichever
-// wave applies it (the scoring waves' claim_and_apply, or this).
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dpp_f<0xb1>(v);
-  v += dpp_f<0x4e>(v);
-  v += dpp_f<0x141>(v);
-  v += dpp_f<0x140>(v);
-  return v;   // every lane of the 16-lane row holds the row's total
-}
-
-__device__ __forceinline__ void row_update4(const UpdParams& t, int c, int d,
-                                            const unsigned long long (&sv)[4], float4 (&p)[4],
-                                            float4 (&a)[4]) {
-  const int gl = lane_id() & 15, nq = d >> 2;
-  const bool ada = t.opt == OPT_ADAGRAD;
-  const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
-  float ss[4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const bool in = 16 * m + gl < nq;
-    const float4 sm = unpack_i16x4(in ? sv[m] : 0ull);
-    ss[m] = 0.0f;
-#define SKGE_UP(X)                                                      \
-  {                                                                     \
-    const float g = (sm.X + t.rin * p[m].X) / div + t.rout * p[m].X;    \
-    float pv = p[m].X;                                                  \
-    if (ada) {                                                          \
-      a[m].X = a[m].X + g * g;                        /* param.py:147 */\
-      pv = pv - adagrad_step_fast(t.lr, g, a[m].X);   /* 152-155 */     \
-    } else {                                                            \
-      pv = pv - t.lr * g;                             /* param.py:130 */\
-    }                                                                   \
-    p[m].X = in ? pv : 0.0f;                                            \
-    ss[m] += p[m].X * p[m].X;                                           \
-  }
-    SKGE_UP(x)
-    SKGE_UP(y)
-    SKGE_UP(z)
-    SKGE_UP(w)
-#undef SKGE_UP
-  }
-  if (t.post != POST_NONE) {
-    const float tot = (row16_sum(ss[0]) + row16_sum(ss[1])) + (row16_sum(ss[2]) + row16_sum(ss[3]));
-    const float inv = proj_scale_fast(t.post, tot);   // param.py:165-166 / 171-173
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      p[m].x = p[m].x * inv;
-      p[m].y = p[m].y * inv;
-      p[m].z = p[m].z * inv;
-      p[m].w = p[m].w * inv;
-    }
-  }
-}
-
-template <bool E8>
-__device__ __forceinline__ void claim_and_apply4(const PipeTab& t, int pp, int slot0, int nslots,
-                                                 int d, int gp) {
-  const int l = lane_id(), grp = l >> 4, gl = l & 15, nq = d >> 2;
-  const int sl = slot0 + grp;
-  const int row = sl < nslots ? t.touched[pp][sl] : -1;   // lanes of a group: one address
-  if (!__ballot(row >= 0)) return;
-  int c = 0;
-  if (gl == 0 && row >= 0) c = atomicExch(t.cnt[pp] + row, 0);
-  const int rr = row >= 0 ? row : 0;   // (rows past the slots: a valid address, discarded)
-  unsigned long long sv[4];
-  float4 p[4], a[4];
-  const float4* prow = reinterpret_cast<const float4*>(t.P + (size_t)rr * d);
-  const float4* arow = reinterpret_cast<const float4*>(t.A + (size_t)rr * d);
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int q = 16 * m + gl, qc = q < nq ? q : nq - 1;
-    if (E8)
-      sv[m] = reinterpret_cast<const unsigned int*>(t.sum[pp])[(size_t)rr * nq + qc];
-    else
-      sv[m] = t.sum[pp][(size_t)rr * nq + qc];
-    p[m] = prow[qc];
-    a[m] = t.A ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  }
-  c = __builtin_amdgcn_ds_bpermute(grp << 6, c);   // the group's claim (lane 16 grp)
-  const bool mine = c != 0;
-  if (!__ballot(mine)) return;   // empty slots, or rows other waves own
-  if (mine && gl == 0 && c > (E8 ? 127 : PACKED_MAX)) atomicOr(t.err, ERR_PACKED);
-  if (E8) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) sv[m] = pack_i16x4(unpack_i8x4_sum((unsigned int)sv[m]));
-  }
-  row_update4(t.u, mine ? c : 1, d, sv, p, a);
-  // write-through 16-B stores through descriptors over the whole tables
-  // (per-lane offsets: the four groups' rows differ)
-  const __amdgpu_buffer_rsrc_t prs =
-      __builtin_amdgcn_make_buffer_rsrc(t.P, 0, 0x7FFFFFFF, 0x00020000);
-  const __amdgpu_buffer_rsrc_t ars =
-      __builtin_amdgcn_make_buffer_rsrc(t.A ? t.A : t.P, 0, 0x7FFFFFFF, 0x00020000);
-  if (mine) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int q = 16 * m + gl;
-      if (q < nq) {
-        if (E8)
-          reinterpret_cast<unsigned int*>(t.sum[pp])[(size_t)row * nq + q] = 0u;
-        else
-          t.sum[pp][(size_t)row * nq + q] = 0ull;
-        const int off = (row * d + 4 * q) * 4;
-        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&p[m]), prs, off,
-                                               0, AUX_SC1);
-        if (t.A)
-          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&a[m]), ars, off,
-                                                 0, AUX_SC1);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
-  if (mine && gl == 0) __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t.claims && l == 0) atomicAdd(shard_of(t.claims), __popcll(__ballot(mine && gl == 0)));
-}
-
 // Large batches: up to GRP_ROWS owner rows of a 64-slot group at once -- all
 // claims in one atomic instruction (lane j claims row j), all rows' loads in
 // one round trip, every claimed row updated and stored write-through, ONE
@@ -522,54 +384,6 @@ __device__ __forceinline__ void claim_and_apply_rows(const PipeTab& t, int pp, i
   }
 }
 
-// Two slot-recorded rows per A wave (SKGE_PIPE_ASLOTS 2): both claims (lanes 0
-// and 1 of one atomic instruction) and both rows' loads in one round trip, the
-// claimed rows applied and stored write-through, ONE drain, then both done
-// words.  Halves the A role's waves: the launch's waves then fit the chip's
-// residency (6 waves per SIMD here), so no scoring workgroup waits for an
-// apply workgroup to retire before it can start.
-template <int KQ>
-__device__ __forceinline__ void claim_and_apply2(const PipeTab& t, int pp, int r0, int r1, int d,
-                                                 int gp) {
-  const int l = lane_id(), nq = d >> 2;
-  int c = 0;
-  const int rl = l == 0 ? r0 : r1;
-  if (l < 2 && rl >= 0) c = atomicExch(t.cnt[pp] + rl, 0);
-  const int q0 = r0 >= 0 ? r0 : r1, q1 = r1 >= 0 ? r1 : r0;   // valid addresses for the loads
-  unsigned long long sv0[KQ], sv1[KQ];
-  float4 p0[KQ], a0[KQ], p1[KQ], a1[KQ];
-  load_upd_row<KQ>(t.P + (size_t)q0 * d, t.A ? t.A + (size_t)q0 * d : nullptr,
-                   t.sum[pp] + (size_t)q0 * nq, d, p0, a0, sv0);
-  load_upd_row<KQ>(t.P + (size_t)q1 * d, t.A ? t.A + (size_t)q1 * d : nullptr,
-                   t.sum[pp] + (size_t)q1 * nq, d, p1, a1, sv1);
-  const int c0 = __builtin_amdgcn_readlane(c, 0), c1 = __builtin_amdgcn_readlane(c, 1);
-  if (c0 == 0 && c1 == 0) return;   // other waves own the rows (or empty slots)
-  if (c0) {
-    if (c0 > PACKED_MAX && l == 0) atomicOr(t.err, ERR_PACKED);
-    row_update<KQ, false>(t.u, c0, d, sv0, sv0, p0, a0);
-    unsigned long long* srow = t.sum[pp] + (size_t)r0 * nq;
-#pragma unroll
-    for (int m = 0; m < KQ; ++m)
-      if (64 * m + l < nq) srow[64 * m + l] = 0ull;
-    store_row4_sc1<KQ>(t.P, r0, d, p0);
-    if (t.A) store_row4_sc1<KQ>(t.A, r0, d, a0);
-  }
-  if (c1) {
-    if (c1 > PACKED_MAX && l == 0) atomicOr(t.err, ERR_PACKED);
-    row_update<KQ, false>(t.u, c1, d, sv1, sv1, p1, a1);
-    unsigned long long* srow = t.sum[pp] + (size_t)r1 * nq;
-#pragma unroll
-    for (int m = 0; m < KQ; ++m)
-      if (64 * m + l < nq) srow[64 * m + l] = 0ull;
-    store_row4_sc1<KQ>(t.P, r1, d, p1);
-    if (t.A) store_row4_sc1<KQ>(t.A, r1, d, a1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
-  if (l < 2 && (l == 0 ? c0 : c1))
-    __hip_atomic_store(t.done + rl, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t.claims && l == 0) atomicAdd(shard_of(t.claims), (c0 != 0) + (c1 != 0));
-}
-
 // B role: make sure launch gp's update of entity `row` (pending at launch
 // start) has landed -- apply it if nobody has claimed it yet, else wait for
 // its publisher
@@ -625,13 +439,11 @@ __device__ __forceinline__ void rel_row(const RelTab& t, int row, int d, int rd,
   if (c) {
     row_update<KQ, W32>(t.u, c, d, sv, sw, p, a);   // (zeroes the lanes past the row)
   }
-#ifndef SKGE_PIPE_ABL_NO_RELZERO   // timing-only ablation
   else {
 #pragma unroll
     for (int m = 0; m < KQ; ++m)
       if (64 * m + l >= nq) p[m] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
-#endif
 }
 
 __device__ __forceinline__ unsigned long long now_10ns() { return __builtin_amdgcn_s_memrealtime(); }
@@ -679,37 +491,15 @@ __device__ __forceinline__ void rel_publish(const PipeArgs& a, int w, int rd, in
   if (!W32 && c > PACKED_MAX && l == 0) atomicOr(a.err, ERR_PACKED);
 }
 
-#ifdef SKGE_PIPE_WAVES_PER_EU
-#define SKGE_PIPE_OCC __attribute__((amdgpu_waves_per_eu(SKGE_PIPE_WAVES_PER_EU, 8)))
-#else
-#define SKGE_PIPE_OCC
-#endif
 #ifndef SKGE_PIPE_WG
 #define SKGE_PIPE_WG 256   // threads per workgroup
 #endif
-#ifndef SKGE_PIPE_ASLOTS
-#define SKGE_PIPE_ASLOTS 1   // entity slots per A-role wave (1 or 2)
-#endif
-constexpr int ASLOTS = SKGE_PIPE_ASLOTS;
-#ifndef SKGE_PIPE_A4_DEFAULT
-#define SKGE_PIPE_A4_DEFAULT 0   // A/B: SKGE_PIPE_A4
-#endif
-#ifndef SKGE_PIPE_AGRP_DEFAULT
-#define SKGE_PIPE_AGRP_DEFAULT 0   // A/B: SKGE_PIPE_AGRP
-#endif
-// ROLE 0: both roles in one grid (nA apply workgroups, then the scoring ones);
-// ROLE 1: apply role only (grid nA); ROLE 2: scoring role only (grid nB) --
-// the split form, two kernels on parallel branches of the epoch graph, each
-// with its own register budget (SKGE_PIPE_SPLIT)
-// P2 (round 4, large batches, SKGE_PIPE_P2): each scoring wave scores TWO
-// positives (2i, 2i + 1) side by side -- both records, both positives' rows
-// and marks in the same round trips, lanes 0-3 / 4-7 holding the two
-// positives' row roles -- so a wave's chain of dependent round trips covers
-// two positives and the batch's scoring waves run in half the rounds.  The
-// same per-positive arithmetic, slots and sums as the one-positive loop.
-template <int KQ, bool W32, bool E8, bool GRP = false, bool A4 = false, int ROLE = 0,
-          bool P2 = false>
-__global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeArgs a) {
+// k_pipe_batch (large batches: more than 16k slot records per batch; smaller
+// batches run k_pipe_fused below): nA apply workgroups (dispatched first: they
+// start the hand-offs the scoring waves may wait on), then the scoring ones.
+// GRP: owner marks, GRP_ROWS owner rows per apply round trip.
+template <int KQ, bool W32, bool E8, bool GRP = false>
+__global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
   const int d = a.d, nq = d >> 2;
@@ -719,21 +509,18 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
   const int rd = a.b & 1;                // relation buffer holding R_{b-1}
   const int rw = a.b < a.nb1 ? rd ^ 1 : 0;   // ... receiving R_b (the flush: the caller's)
   const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
-  const int nB = ROLE == 2 ? (int)gridDim.x : (int)gridDim.x - a.nA;
+  const int nB = (int)gridDim.x - a.nA;
   // apply workgroups first: they start the hand-offs the scoring waves may wait
   // on (measured: 6% faster than scoring first, 9% faster than interleaved)
-  // b_first (A/B, SKGE_PIPE_AFIRST=0): the scoring workgroups dispatched first
   const int blk = (int)blockIdx.x;
-  const bool is_a = ROLE == 1 || (ROLE == 0 && (a.b_first ? blk >= nB : blk < a.nA));
-  const int blk_a = ROLE == 1 ? blk : (a.b_first ? blk - nB : blk);
-  const int blk_b = ROLE == 2 ? blk : (a.b_first ? blk : blk - a.nA);
-  if (ROLE != 2 && is_a) {
+  const int blk_a = blk, blk_b = blk - a.nA;
+  if (blk < a.nA) {
     // ---- A role: write R_b, then apply the previous batch's entity rows ----
     const int nR = a.R.rows;
     // owner marks (large batches): items are groups of 64 slots, scanned
-    // lane-parallel; else one slot (ASLOTS) per item
+    // lane-parallel; else one slot per item
     const int* const ownp = a.E.own[pp];
-    const int total = nR + (ownp ? (a.prev_slots + 63) / 64 : (a.prev_slots + ASLOTS - 1) / ASLOTS);
+    const int total = nR + (ownp ? (a.prev_slots + 63) / 64 : a.prev_slots);
     const int wa = blk_a * wpb + (threadIdx.x >> 6);
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
     if (a.b == a.nb1 && wa == 0)   // the flush: fold the epoch's violation count
@@ -777,41 +564,9 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
             claim_and_apply<KQ, E8>(a.E, pp, row, d, gp);
           }
         }
-      } else if (A4) {
-        // one wave per positive: its 4 slots, one row per 16-lane group
-        if constexpr (A4 && KQ == 1) claim_and_apply4<E8>(a.E, pp, 4 * (w - nR), a.prev_slots, d, gp);
-      } else if (a.E.agrp) {
-        // a group of AGRP_WAVES waves over agrp slots: every wave loads the
-        // group's slot records (one vector load), and the k-th slot naming a
-        // row goes to wave k % AGRP_WAVES -- ~U apply waves are dispatched
-        // instead of one per slot (73% of slots name no row at nb = 100)
-        const int e = w - nR;
-        const int grp = e / AGRP_WAVES, sub = e % AGRP_WAVES;
-        const int i = grp * a.E.agrp + l;
-        const int r = (l < a.E.agrp && i < a.prev_slots) ? a.E.touched[pp][i] : -1;
-        uint64_t m = __ballot(r >= 0);
-        int k = 0;
-        while (m) {
-          const int j = __ffsll((unsigned long long)m) - 1;
-          m &= m - 1;
-          if ((k++ % AGRP_WAVES) == sub)
-            claim_and_apply<KQ, E8>(a.E, pp, __builtin_amdgcn_readlane(r, j), d, gp);
-        }
       } else {
-        if (ASLOTS == 2) {
-          const int i0 = 2 * (w - nR);
-          const int r0 = __builtin_amdgcn_readfirstlane(a.E.touched[pp][i0]);
-          const int r1 = i0 + 1 < a.prev_slots
-                             ? __builtin_amdgcn_readfirstlane(a.E.touched[pp][i0 + 1]) : -1;
-          if (r0 >= 0 || r1 >= 0) claim_and_apply2<KQ>(a.E, pp, r0, r1, d, gp);
-        } else {
-          const int row = __builtin_amdgcn_readfirstlane(a.E.touched[pp][w - nR]);
-#ifndef SKGE_PIPE_ABL_NOAPPLY_E   // timing-only ablation: entity rows never updated
-          if (row >= 0) claim_and_apply<KQ, E8>(a.E, pp, row, d, gp);
-#else
-          if (row >= 0 && l == 0) a.E.cnt[pp][row] = 0;
-#endif
-        }
+        const int row = __builtin_amdgcn_readfirstlane(a.E.touched[pp][w - nR]);
+        if (row >= 0) claim_and_apply<KQ, E8>(a.E, pp, row, d, gp);
       }
     }
     if (a.trace && l == 0) {
@@ -837,181 +592,6 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
   const __amdgpu_buffer_rsrc_t rec1_rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<int*>(a.rec_n1 + a.start), 0, a.count * 4, 0x00020000);
   int nv = 0;
-  if constexpr (P2) {
-    for (int i = blk_b * wpb + (threadIdx.x >> 6); 2 * i < a.count; i += nB * wpb) {
-      const int wv[2] = {2 * i, 2 * i + 1};
-      const bool has1 = wv[1] < a.count;
-      const int w1c = has1 ? wv[1] : wv[0];   // a valid record to load for an absent second
-      const u32x4 rx0 = __builtin_amdgcn_raw_buffer_load_b128(rec_rs, wv[0] * 16, 0, 0);
-      const u32x4 rx1 = __builtin_amdgcn_raw_buffer_load_b128(rec_rs, w1c * 16, 0, 0);
-      const int r10 = (int)__builtin_amdgcn_raw_buffer_load_b32(rec1_rs, wv[0] * 4, 0, 0);
-      const int r11 = (int)__builtin_amdgcn_raw_buffer_load_b32(rec1_rs, w1c * 4, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      int s[2], o[2], p[2], ng0[2], ng1[2], n0r[2], n1r[2];
-      s[0] = __builtin_amdgcn_readfirstlane((int)rx0.x);
-      o[0] = __builtin_amdgcn_readfirstlane((int)rx0.y);
-      p[0] = __builtin_amdgcn_readfirstlane((int)rx0.z);
-      ng0[0] = __builtin_amdgcn_readfirstlane((int)rx0.w);
-      ng1[0] = __builtin_amdgcn_readfirstlane(r10);
-      s[1] = __builtin_amdgcn_readfirstlane((int)rx1.x);
-      o[1] = __builtin_amdgcn_readfirstlane((int)rx1.y);
-      p[1] = __builtin_amdgcn_readfirstlane((int)rx1.z);
-      ng0[1] = __builtin_amdgcn_readfirstlane((int)rx1.w);
-      ng1[1] = __builtin_amdgcn_readfirstlane(r11);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        n0r[u] = ng0[u] >= 0 ? ng0[u] : s[u];
-        n1r[u] = ng1[u] >= 0 ? ng1[u] : o[u];
-      }
-      float4 es[2][KQ], eo[2][KQ], rp[2][KQ], fs[2][KQ], fo[2][KQ];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        load_row4<KQ>(a.E.P, s[u], d, es[u]);
-        load_row4<KQ>(a.E.P, o[u], d, eo[u]);
-        load_row4<KQ>(a.E.P, n0r[u], d, fs[u]);
-        load_row4<KQ>(a.E.P, n1r[u], d, fo[u]);
-      }
-      // lanes 0-3: the first positive's rows (s, o, s', o'), lanes 4-7 the second's
-      int mark = 0, dn = 0;
-      if (l < 8) {
-        const int k = l & 3;
-        const int rr = l < 4 ? sel4(k, s[0], o[0], n0r[0], n1r[0])
-                             : sel4(k, s[1], o[1], n0r[1], n1r[1]);
-        mark = a.E.pend[pp][rr];
-        dn = __hip_atomic_load(a.E.done + rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        float4 ra[KQ];
-        int c;
-        rel_row<KQ, W32>(a.R, p[u], d, rd, ra_prev, rp[u], ra, c);
-      }
-      const uint64_t pmask = has1 ? 0xffull : 0xfull;
-      const uint64_t pend = __ballot(mark == gp) & pmask;
-      const uint64_t unpub = pend & ~__ballot(dn == gp);
-      if (pend) {
-#pragma unroll 1
-        for (int k = 0; k < 8; ++k) {
-          if (!((unpub >> k) & 1ull)) continue;
-          const int row = k < 4 ? sel4(k & 3, s[0], o[0], n0r[0], n1r[0])
-                                : sel4(k & 3, s[1], o[1], n0r[1], n1r[1]);
-          ensure_applied<KQ, E8>(a.E, pp, row, d, gp, a.err);
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const uint64_t pu = pend >> (4 * u);
-          if (pu & 1ull) load_row4_sc1<KQ>(a.E.P, s[u], d, es[u]);
-          if (pu & 2ull) load_row4_sc1<KQ>(a.E.P, o[u], d, eo[u]);
-          if (pu & 4ull) load_row4_sc1<KQ>(a.E.P, n0r[u], d, fs[u]);
-          if (pu & 8ull) load_row4_sc1<KQ>(a.E.P, n1r[u], d, fo[u]);
-        }
-      }
-      int vv0[2], vv1[2];
-      float4 gp4[2][KQ], g0[2][KQ], g1[2][KQ];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
-#pragma unroll
-        for (int m = 0; m < KQ; ++m) {
-#define SKGE_EL(X)                                                                    \
-  {                                                                                   \
-    const float vp = (es[u][m].X + rp[u][m].X) - eo[u][m].X;   /* transe.py:32 */     \
-    const float v0 = (fs[u][m].X + rp[u][m].X) - eo[u][m].X;                          \
-    const float v1 = (es[u][m].X + rp[u][m].X) - fo[u][m].X;                          \
-    ps += fabsf(vp);                                                                  \
-    n0 += fabsf(v0);                                                                  \
-    n1 += fabsf(v1);                                                                  \
-    gp4[u][m].X = signf_np(-((eo[u][m].X - rp[u][m].X) - es[u][m].X));                \
-    g0[u][m].X = signf_np((eo[u][m].X - rp[u][m].X) - fs[u][m].X);                    \
-    g1[u][m].X = signf_np((fo[u][m].X - rp[u][m].X) - es[u][m].X);                    \
-  }
-          SKGE_EL(x)
-          SKGE_EL(y)
-          SKGE_EL(z)
-          SKGE_EL(w)
-#undef SKGE_EL
-        }
-        const float pscore = -wave_sum(ps);
-        const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
-        const bool live = u == 0 || has1;
-        vv0[u] = (live && ng0[u] >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // transe.py:73
-        vv1[u] = (live && ng1[u] >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
-      }
-      {   // counts, touched slots and pending marks of both positives (per-lane
-          // choices by selects: no dynamically indexed private arrays)
-        const bool second = (l & 4) != 0;
-        const int kk = l & 3;
-        const int v0 = second ? vv0[1] : vv0[0], v1 = second ? vv1[1] : vv1[0];
-        const int cE = sel4(kk, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
-        const int rE = second ? sel4(kk, s[1], o[1], ng0[1], ng1[1])
-                              : sel4(kk, s[0], o[0], ng0[0], ng1[0]);
-        const int slot = 4 * (second ? wv[1] : wv[0]) + kk;
-        const bool lr = l == 8 || (l == 9 && has1);   // the relation count lanes
-        const int ur = l == 9;
-        const int vr = ur ? vv0[1] + vv1[1] : vv0[0] + vv1[0];
-        if (l < 4 || (l < 8 && has1)) {
-          commit_slot(cnt_cp, tch_cp, rE, cE, slot);
-          if (cE > 0) {
-            pend_cp[rE] = g;
-            if (own_cp) own_cp[rE] = slot;
-          }
-        } else if (lr && vr > 0) {
-          const int wr = ur ? wv[1] : wv[0], pr = ur ? p[1] : p[0];
-          unsigned long long* const rac = racc0 + (size_t)(wr & rmask) * rrep;
-          atomicAdd(rac + (size_t)pr * a.R.rw + rcw, (unsigned long long)(2 * vr));
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int v0 = vv0[u], v1 = vv1[u];
-        if (v0 + v1 == 0) continue;
-        nv += v0 + v1;
-        const float fv0 = (float)v0, fv1 = (float)v1;
-        float4 cs[KQ], co[KQ], c0[KQ], c1[KQ], cr[KQ];
-#pragma unroll
-        for (int m = 0; m < KQ; ++m) {
-#define SKGE_CO(X)                                                            \
-  cs[m].X = fv0 * gp4[u][m].X + fv1 * (gp4[u][m].X + g1[u][m].X);             \
-  co[m].X = -(fv0 * (gp4[u][m].X + g0[u][m].X) + fv1 * gp4[u][m].X);          \
-  c0[m].X = g0[u][m].X;                                                       \
-  c1[m].X = -g1[u][m].X;                                                      \
-  cr[m].X = fv0 * (gp4[u][m].X + g0[u][m].X) + fv1 * (gp4[u][m].X + g1[u][m].X);
-          SKGE_CO(x)
-          SKGE_CO(y)
-          SKGE_CO(z)
-          SKGE_CO(w)
-#undef SKGE_CO
-        }
-        if (E8) {
-          unsigned int* es8 = reinterpret_cast<unsigned int*>(esum);
-          acc_row4_i8<KQ>(es8, s[u], cs, d);
-          acc_row4_i8<KQ>(es8, o[u], co, d);
-          if (v0) acc_row4_i8<KQ>(es8, ng0[u], c0, d);
-          if (v1) acc_row4_i8<KQ>(es8, ng1[u], c1, d);
-        } else {
-          Accum aE = {};
-          aE.sum = reinterpret_cast<float*>(esum);
-          acc_row4_i16<KQ>(aE, s[u], cs, d);
-          acc_row4_i16<KQ>(aE, o[u], co, d);
-          if (v0) acc_row4_i16<KQ>(aE, ng0[u], c0, d);
-          if (v1) acc_row4_i16<KQ>(aE, ng1[u], c1, d);
-        }
-        unsigned long long* rrow = racc0 + (size_t)(wv[u] & rmask) * rrep + (size_t)p[u] * a.R.rw;
-#pragma unroll
-        for (int m = 0; m < KQ; ++m) {
-          const int q = 64 * m + l;
-          if (q < nq) {
-            if (W32) {
-              atomicAdd(rrow + 2 * q, pack_i32x2(cr[m].x, cr[m].y));
-              atomicAdd(rrow + 2 * q + 1, pack_i32x2(cr[m].z, cr[m].w));
-            } else {
-              atomicAdd(rrow + q, pack_i16x4(cr[m]));
-            }
-          }
-        }
-      }
-    }
-  } else
   for (int w = blk_b * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
     // large batches: positive w adds its relation sums into replica w % reps
     // (k_rel_fold folds them after the launch), spreading the hot rows' atomics
@@ -1052,11 +632,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
       int c;
       rel_row<KQ, W32>(a.R, p, d, rd, ra_prev, rp, ra, c);
     }
-#ifdef SKGE_PIPE_ABL_NOENSURE   // timing-only ablation (tools/ablate.sh): ignore pending rows
-    const uint64_t pend = 0ull * __ballot(mark == gp);
-#else
     const uint64_t pend = __ballot(mark == gp) & 0xfull;
-#endif
     const uint64_t unpub = pend & ~__ballot(dn == gp);   // pending and not yet published
     if (a.trace) tt[1] = now_10ns();
     if (pend) {   // some entity rows have an update of batch b-1 outstanding
@@ -1131,7 +707,6 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
         SKGE_CO(w)
 #undef SKGE_CO
       }
-#ifndef SKGE_PIPE_ABL_NO_EATOM   // timing-only ablation (tools/ablate.sh): entity atomics dropped
       if (E8) {   // int8x4 sums: one 32-bit atomic per quad
         unsigned int* es8 = reinterpret_cast<unsigned int*>(esum);
         acc_row4_i8<KQ>(es8, s, cs, d);
@@ -1146,13 +721,9 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_pipe_batch(PipeA
         if (v0) acc_row4_i16<KQ>(aE, neg0, c0, d);
         if (v1) acc_row4_i16<KQ>(aE, neg1, c1, d);
       }
-#endif
       // relation sums: rows of rw words; int32x2 (two words per quad) when a
       // hot relation's batch total could pass 16 bits
       unsigned long long* rrow = racc + (size_t)p * a.R.rw;
-#ifdef SKGE_PIPE_ABL_NO_RATOM   // timing-only ablation: relation atomics dropped
-      if (rrow) continue;
-#endif
 #pragma unroll
       for (int m = 0; m < KQ; ++m) {
         const int q = 64 * m + l;
@@ -1563,602 +1134,6 @@ __global__ __launch_bounds__(256) void k_fused_fin(FusedTab F, int rows, int d) 
   }
 }
 
-// ---- lazy apply (skge_pipe_runner_create_ex with SKGE_PIPE_LAZY) ----
-//
-// Entity rows keep ONE accumulator (sum, cnt): the contributions of the last
-// batch that touched the row, not yet applied.  A launch has no entity apply
-// waves; instead the first scoring wave of batch b to read a row applies the
-// row's pending update before scoring with it: lane k of the wave claims its
-// row with atomicMax(claim[row], g) (old < g: first reader in this launch), in
-// the same memory round trip as the row's parameters, AdaGrad state, sums and
-// count; the claimer updates the row (row_update, the same code as every other
-// apply), writes it back write-through, zeroes the sums, drains and publishes
-// done[row] = g.  Other readers of the row in the same batch wait for that and
-// re-read it (sc1).  Rows nobody reads again are applied by the epoch's flush
-// launch.  Every batch's sums of a row are applied once, before any later read
-// of the row, by the same arithmetic: bitwise the two-launch loop's result.
-
-// 8-B write-through stores of zeros over a packed sum row (lanes past the row
-// fall outside the descriptor: dropped)
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-template <int KQ>
-__device__ __forceinline__ void zero_sum_row_sc1(unsigned long long* S, int row, int nq) {
-  row = __builtin_amdgcn_readfirstlane(row);
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(S + (size_t)row * nq, 0, nq * 8, 0x00020000);
-  const u32x2 z = {0u, 0u};
-#pragma unroll
-  for (int m = 0; m < KQ; ++m)
-    __builtin_amdgcn_raw_buffer_store_b64(z, rs, (64 * m + lane_id()) * 8, 0, AUX_SC1);
-}
-
-// parameters, AdaGrad state (P again when A is null: discarded) and packed sums
-// of one row, unconditional 16-B / 8-B loads; P and A zero past the row
-template <int KQ>
-__device__ __forceinline__ void load_lazy_row(const float* P, const float* A,
-                                              const unsigned long long* S, int row, int d,
-                                              float4 (&p)[KQ], float4 (&a)[KQ],
-                                              unsigned long long (&sv)[KQ]) {
-  const int l = lane_id(), nq = d >> 2;
-  const float4* prow = reinterpret_cast<const float4*>(P + (size_t)row * d);
-  const float4* arow = reinterpret_cast<const float4*>((A ? A : P) + (size_t)row * d);
-  const unsigned long long* srow = S + (size_t)row * nq;
-  const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll
-  for (int m = 0; m < KQ; ++m) {
-    const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
-    const float4 pv = prow[qc], av = arow[qc];
-    sv[m] = srow[qc];
-    p[m] = q < nq ? pv : z;
-    a[m] = q < nq && A ? av : z;
-  }
-}
-
-// the claimer's apply of one row: update, write back, zero the sums (not the
-// count: lane `lane` of the caller does that)
-template <int KQ>
-__device__ __forceinline__ void lazy_apply(const PipeTab& t, int row, int c, int d,
-                                           const unsigned long long (&sv)[KQ], float4 (&p)[KQ],
-                                           float4 (&a)[KQ]) {
-  row_update<KQ, false>(t.u, c, d, sv, sv, p, a);
-  store_row4_sc1<KQ>(t.P, row, d, p);
-  if (t.A) store_row4_sc1<KQ>(t.A, row, d, a);
-  zero_sum_row_sc1<KQ>(t.sum[0], row, d >> 2);
-}
-
-template <int KQ, bool W32>
-__global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_lazy_batch(PipeArgs a) {
-  const int wpb = blockDim.x >> 6;
-  const int l = lane_id();
-  const int d = a.d, nq = d >> 2;
-  const int rcw = W32 ? 2 * nq : nq;
-  const int g = launch_id(a);
-  const int rd = a.b & 1;
-  const int rw = a.b < a.nb1 ? rd ^ 1 : 0;
-  const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
-  const int nB = gridDim.x - a.nA;
-  if ((int)blockIdx.x < a.nA) {
-    // ---- A role: write R_b; at the flush also apply every pending entity row ----
-    const int nR = a.R.rows;
-    const bool flush = a.b == a.nb1;
-    const int nchunk = flush ? (a.n_ent + 63) / 64 : 0;
-    const int wa = (int)blockIdx.x * wpb + (threadIdx.x >> 6);
-    if (flush && wa == 0) fold_shards(a.nviol_shards, a.nviol_total);
-    for (int w = wa; w < nR + nchunk; w += a.nA * wpb) {
-      if (w < nR) {
-        rel_publish<KQ, W32>(a, w, rd, rw, ra_prev, ra_old);
-        continue;
-      }
-      const int r0 = (w - nR) * 64;
-      const int cv = r0 + l < a.n_ent ? a.E.cnt[0][r0 + l] : 0;
-      uint64_t mask = __ballot(cv != 0);
-      int napplied = 0;
-      while (mask) {
-        const int k = (int)__builtin_ctzll(mask);
-        mask &= mask - 1;
-        const int row = r0 + k;
-        const int c = __builtin_amdgcn_readlane(cv, k);
-        unsigned long long sv[KQ];
-        float4 p[KQ], av[KQ];
-        load_lazy_row<KQ>(a.E.P, a.E.A, a.E.sum[0], row, d, p, av, sv);
-        if (c > PACKED_MAX && l == 0) atomicOr(a.err, ERR_PACKED);
-        row_update<KQ, false>(a.E.u, c, d, sv, sv, p, av);
-        float4* prow = reinterpret_cast<float4*>(a.E.P + (size_t)row * d);
-        float4* arow = a.E.A ? reinterpret_cast<float4*>(a.E.A + (size_t)row * d) : nullptr;
-        unsigned long long* srow = a.E.sum[0] + (size_t)row * nq;
-#pragma unroll
-        for (int m = 0; m < KQ; ++m) {
-          const int q = 64 * m + l;
-          if (q < nq) {
-            prow[q] = p[m];
-            if (arow) arow[q] = av[m];
-            srow[q] = 0ull;
-          }
-        }
-        if (l == 0) a.E.cnt[0][row] = 0;
-        ++napplied;
-      }
-      if (a.E.claims && l == 0 && napplied) atomicAdd(shard_of(a.E.claims), napplied);
-    }
-    return;
-  }
-  // ---- B role: claim/apply/score/scatter batch b ----
-  unsigned long long* const esum = opaque_ptr(a.E.sum[0]);
-  int* const ecnt = opaque_ptr(a.E.cnt[0]);
-  int* const eclaim = opaque_ptr(a.E.claim);
-  int* const edone = opaque_ptr(a.E.done);
-  unsigned long long* const racc = opaque_ptr(a.R.acc[ra_cur]);
-  const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<int4*>(a.rec + a.start), 0, a.count * 16, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rec1_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<int*>(a.rec_n1 + a.start), 0, a.count * 4, 0x00020000);
-  int nv = 0, napplied = 0;
-  const int blk_b = (int)blockIdx.x - a.nA;
-  for (int w = blk_b * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
-    unsigned long long tt[4];
-    if (a.trace) tt[0] = now_10ns();
-    const u32x4 rx = __builtin_amdgcn_raw_buffer_load_b128(rec_rs, w * 16, 0, 0);
-    const int r1 = (int)__builtin_amdgcn_raw_buffer_load_b32(rec1_rs, w * 4, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    const int s = __builtin_amdgcn_readfirstlane((int)rx.x);
-    const int o = __builtin_amdgcn_readfirstlane((int)rx.y);
-    const int p = __builtin_amdgcn_readfirstlane((int)rx.z);
-    const int neg0 = __builtin_amdgcn_readfirstlane((int)rx.w);
-    const int neg1 = __builtin_amdgcn_readfirstlane(r1);
-    const int n0r = neg0 >= 0 ? neg0 : s, n1r = neg1 >= 0 ? neg1 : o;
-    // a row the wave reads twice is claimed / waited for by its first lane only
-    const int dupm = (o == s ? 2 : 0) | (n0r == s || n0r == o ? 4 : 0) |
-                     (n1r == s || n1r == o || n1r == n0r ? 8 : 0);
-    const int myrow = sel4(l, s, o, n0r, n1r);
-    const bool own = l < 4 && !((dupm >> l) & 1);
-    // one round trip: claims, counts, rows, AdaGrad states, sums, relation row
-    int old = g, cv = 0;
-    if (own) {
-      old = atomicMax(eclaim + myrow, g);
-      cv = ecnt[myrow];
-    }
-    float4 es[KQ], eo[KQ], fs[KQ], fo[KQ], as_[KQ], ao[KQ], a0[KQ], a1[KQ], rp[KQ];
-    unsigned long long ss[KQ], so[KQ], s0[KQ], s1[KQ];
-    load_lazy_row<KQ>(a.E.P, a.E.A, esum, s, d, es, as_, ss);
-    load_lazy_row<KQ>(a.E.P, a.E.A, esum, o, d, eo, ao, so);
-    load_lazy_row<KQ>(a.E.P, a.E.A, esum, n0r, d, fs, a0, s0);
-    load_lazy_row<KQ>(a.E.P, a.E.A, esum, n1r, d, fo, a1, s1);
-    {
-      float4 ra[KQ];
-      int c;
-      rel_row<KQ, W32>(a.R, p, d, rd, ra_prev, rp, ra, c);
-    }
-    const int clm = (int)(__ballot(own && old < g) & 0xfull);   // rows this wave claims
-    const int cnz = (int)(__ballot(own && old < g && cv != 0) & 0xfull);   // ... with sums
-    if (a.trace) tt[1] = now_10ns();
-    if (cnz) {
-      if (cnz & 1) lazy_apply<KQ>(a.E, s, __builtin_amdgcn_readlane(cv, 0), d, ss, es, as_);
-      if (cnz & 2) lazy_apply<KQ>(a.E, o, __builtin_amdgcn_readlane(cv, 1), d, so, eo, ao);
-      if (cnz & 4) lazy_apply<KQ>(a.E, n0r, __builtin_amdgcn_readlane(cv, 2), d, s0, fs, a0);
-      if (cnz & 8) lazy_apply<KQ>(a.E, n1r, __builtin_amdgcn_readlane(cv, 3), d, s1, fo, a1);
-      if (l < 4 && ((cnz >> l) & 1))
-        __hip_atomic_store(ecnt + myrow, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
-      napplied += __builtin_popcount(cnz);
-    }
-    if (l < 4 && ((clm >> l) & 1))
-      __hip_atomic_store(edone + myrow, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.trace) tt[2] = now_10ns();
-    // rows another wave of this batch claimed: wait for their publication, re-read
-    const int wt = (int)(__ballot(own && old >= g) & 0xfull);
-    if (wt) {
-      unsigned spins = 0;
-      for (;;) {
-        const bool ready = !(l < 4 && ((wt >> l) & 1)) ||
-                           __hip_atomic_load(edone + myrow, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT) == g;
-        if (__ballot(!ready) == 0ull) break;
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 22)) {   // ~0.5 s: never hang the GPU; report instead
-          if (l == 0) atomicOr(a.err, ERR_WAIT);
-          break;
-        }
-        if ((spins & 1023u) == 0 &&
-            __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-          break;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the re-reads below the poll
-      if (wt & 1) load_row4_sc1<KQ>(a.E.P, s, d, es);
-      if (wt & 2) load_row4_sc1<KQ>(a.E.P, o, d, eo);
-      if (wt & 4) load_row4_sc1<KQ>(a.E.P, n0r, d, fs);
-      if (wt & 8) load_row4_sc1<KQ>(a.E.P, n1r, d, fo);
-    }
-    if (dupm) {   // duplicates take the first equal row's (updated) values
-#pragma unroll
-      for (int m = 0; m < KQ; ++m) {
-        if (dupm & 2) eo[m] = es[m];
-        if (dupm & 4) fs[m] = n0r == s ? es[m] : eo[m];
-        if (dupm & 8) fo[m] = n1r == s ? es[m] : (n1r == o ? eo[m] : fs[m]);
-      }
-    }
-    float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
-    float4 gp4[KQ], g0[KQ], g1[KQ];
-#pragma unroll
-    for (int m = 0; m < KQ; ++m) {
-#define SKGE_EL(X)                                                                    \
-  {                                                                                   \
-    const float vp = (es[m].X + rp[m].X) - eo[m].X;   /* transe.py:32 */              \
-    const float v0 = (fs[m].X + rp[m].X) - eo[m].X;                                   \
-    const float v1 = (es[m].X + rp[m].X) - fo[m].X;                                   \
-    ps += fabsf(vp);                                                                  \
-    n0 += fabsf(v0);                                                                  \
-    n1 += fabsf(v1);                                                                  \
-    gp4[m].X = signf_np(-((eo[m].X - rp[m].X) - es[m].X)); /* transe.py:103,115 */    \
-    g0[m].X = signf_np((eo[m].X - rp[m].X) - fs[m].X);     /* transe.py:104,117 */    \
-    g1[m].X = signf_np((fo[m].X - rp[m].X) - es[m].X);                                \
-  }
-      SKGE_EL(x)
-      SKGE_EL(y)
-      SKGE_EL(z)
-      SKGE_EL(w)
-#undef SKGE_EL
-    }
-    const float pscore = -wave_sum(ps);
-    const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
-    const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // strict >, transe.py:73
-    const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
-    if (a.trace) tt[3] = now_10ns();
-    {
-      const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
-      const int rE = sel4(l, s, o, neg0, neg1);
-      if (l < 4) {
-        if (cE > 0) atomicAdd(ecnt + rE, cE);
-      } else if (l == 4 && v0 + v1 > 0) {
-        atomicAdd(racc + (size_t)p * a.R.rw + rcw, (unsigned long long)(2 * (v0 + v1)));
-      }
-    }
-    if (v0 + v1 > 0) {
-      nv += v0 + v1;
-      const float fv0 = (float)v0, fv1 = (float)v1;
-      float4 cs[KQ], co[KQ], c0[KQ], c1[KQ], cr[KQ];
-#pragma unroll
-      for (int m = 0; m < KQ; ++m) {
-#define SKGE_CO(X)                                                   \
-  cs[m].X = fv0 * gp4[m].X + fv1 * (gp4[m].X + g1[m].X);             \
-  co[m].X = -(fv0 * (gp4[m].X + g0[m].X) + fv1 * gp4[m].X);          \
-  c0[m].X = g0[m].X;                                                 \
-  c1[m].X = -g1[m].X;                                                \
-  cr[m].X = fv0 * (gp4[m].X + g0[m].X) + fv1 * (gp4[m].X + g1[m].X);
-        SKGE_CO(x)
-        SKGE_CO(y)
-        SKGE_CO(z)
-        SKGE_CO(w)
-#undef SKGE_CO
-      }
-      Accum aE = {};   // mode ACC_F32 (0), one copy
-      aE.sum = reinterpret_cast<float*>(esum);
-      acc_row4_i16<KQ>(aE, s, cs, d);
-      acc_row4_i16<KQ>(aE, o, co, d);
-      if (v0) acc_row4_i16<KQ>(aE, neg0, c0, d);
-      if (v1) acc_row4_i16<KQ>(aE, neg1, c1, d);
-      unsigned long long* rrow = racc + (size_t)p * a.R.rw;
-#pragma unroll
-      for (int m = 0; m < KQ; ++m) {
-        const int q = 64 * m + l;
-        if (q < nq) {
-          if (W32) {
-            atomicAdd(rrow + 2 * q, pack_i32x2(cr[m].x, cr[m].y));
-            atomicAdd(rrow + 2 * q + 1, pack_i32x2(cr[m].z, cr[m].w));
-          } else {
-            atomicAdd(rrow + q, pack_i16x4(cr[m]));
-          }
-        }
-      }
-    }
-    if (a.trace && l == 0) {   // stamp after issue (no drain)
-      unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
-      tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
-      tr[5] = (unsigned long long)(cnz | (wt << 4) | (clm << 12)) |
-              ((unsigned long long)(v0 + v1 > 0) << 8);
-    }
-  }
-  if (l == 0) {
-    if (nv) {
-      atomicAdd(shard_of(a.nviol_shards), nv);
-      if (a.stats_viol) atomicAdd(shard_of(a.stats_viol), nv);
-    }
-    if (napplied && a.E.claims) atomicAdd(shard_of(a.E.claims), napplied);
-  }
-}
-
-// ---- owner apply (SKGE_PIPE_OWNER): every entity row is updated inside the
-// launch that scores its batch, by the batch's LAST wave to reference it ----
-//
-// The batch's records are known before the launch, so the number of its
-// references to each entity row is counted ahead (refs[b & 1]: the previous
-// launch's scoring waves count the next batch's records; the epoch's first
-// batch, k_own_count) into one 64-bit word per row: the total in the high half,
-// which no wave of the launch changes until the row's last reference is
-// retired -- waves need not be resident together -- and the references not yet
-// retired in the low half.  A scoring wave loads its rows, their AdaGrad state
-// and their reference words with the record's rows (one round trip) and scores.
-//   * A row only this wave references (total 1; ~87% of references at
-//     WN18's batch) is updated from the wave's own contribution and count
-//     straight from registers -- the row's whole batch sum -- and stored; no
-//     atomics, no hand-off.
-//   * A shared row: the wave adds its exact packed contribution and count
-//     (memory-side atomics), waits for them to complete, then retires its
-//     reference (atomicSub with return).  The wave that retires the last one
-//     takes the row's sums and count with atomic exchanges (which also clear
-//     them: memory-side, so every wave's adds are seen) and updates the row
-//     from its registers: the row's parameters and state cannot have changed
-//     since the batch's waves loaded them, as each referencing wave had loaded
-//     them before retiring its reference.
-// After the launch every update of batch b has landed, so the next launch's
-// waves read plain rows: no pending marks, claims, waits or apply waves.
-// Relation rows keep the pipelined runner's scheme (double-buffered,
-// recomputed by every scoring wave, published by the A role's waves).  Every
-// row's update is row_update on its exact integer sums: bitwise the two-launch
-// runner's result.
-__global__ __launch_bounds__(256) void k_own_count(const int4* __restrict__ rec,
-                                                   const int* __restrict__ rec_n1, int count,
-                                                   unsigned long long* __restrict__ refs) {
-  constexpr unsigned long long ONE = 0x100000001ull;   // total + 1, live + 1
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < count; j += gridDim.x * blockDim.x) {
-    const int4 r = rec[j];
-    const int n1 = rec_n1[j];
-    atomicAdd(refs + r.x, ONE);
-    atomicAdd(refs + r.y, ONE);
-    if (r.w >= 0) atomicAdd(refs + r.w, ONE);
-    if (n1 >= 0) atomicAdd(refs + n1, ONE);
-  }
-}
-
-template <int KQ, bool W32>
-__global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_PIPE_OCC void k_own_batch(PipeArgs a) {
-  const int wpb = blockDim.x >> 6;
-  const int l = lane_id();
-  const int d = a.d, nq = d >> 2;
-  const int rcw = W32 ? 2 * nq : nq;
-  const int g = launch_id(a);
-  const int cp = a.b & 1;
-  const int rd = a.b & 1;
-  const int rw = a.b < a.nb1 ? rd ^ 1 : 0;
-  const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
-  const int nB = gridDim.x - a.nA;
-  if ((int)blockIdx.x < a.nA) {   // A role: the relation rows (R_b for the next launch)
-    const int wa = (int)blockIdx.x * wpb + (threadIdx.x >> 6);
-    const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
-    if (a.b == a.nb1 && wa == 0) fold_shards(a.nviol_shards, a.nviol_total);
-    for (int w = wa; w < a.R.rows; w += a.nA * wpb) rel_publish<KQ, W32>(a, w, rd, rw, ra_prev, ra_old);
-    if (a.trace && l == 0) {
-      unsigned long long* tr = a.trace + 2 + 6 * (size_t)a.count + 2 * (size_t)wa;
-      tr[0] = ta0;
-      tr[1] = now_10ns();
-    }
-    return;
-  }
-  unsigned long long* const refs = opaque_ptr(a.E.refs[cp]);
-  unsigned long long* const refs_next = opaque_ptr(a.E.refs[cp ^ 1]);
-  int* const cnt = opaque_ptr(a.E.cnt[0]);
-  unsigned long long* const esum = opaque_ptr(a.E.sum[0]);
-  unsigned long long* const racc = opaque_ptr(a.R.acc[ra_cur]);
-  float* const EP = opaque_ptr(a.E.P);
-  float* const EA = a.E.A ? opaque_ptr(a.E.A) : nullptr;
-  const __amdgpu_buffer_rsrc_t rec_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<int4*>(a.rec + a.start), 0, a.count * 16, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rec1_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<int*>(a.rec_n1 + a.start), 0, a.count * 4, 0x00020000);
-  // the next batch's records (counted here for the next launch)
-  const __amdgpu_buffer_rsrc_t nrec_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<int4*>(a.rec + a.start + a.count), 0, a.count_next * 16, 0x00020000);
-  const __amdgpu_buffer_rsrc_t nrec1_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<int*>(a.rec_n1 + a.start + a.count), 0, a.count_next * 4, 0x00020000);
-  int nv = 0;
-  for (int w = (int)(blockIdx.x - a.nA) * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
-    unsigned long long tt[4];
-    if (a.trace) tt[0] = now_10ns();
-    const u32x4 rx = __builtin_amdgcn_raw_buffer_load_b128(rec_rs, w * 16, 0, 0);
-    const int r1 = (int)__builtin_amdgcn_raw_buffer_load_b32(rec1_rs, w * 4, 0, 0);
-    // (lanes past the next batch read 0 through the descriptor: unused)
-    const u32x4 nx = __builtin_amdgcn_raw_buffer_load_b128(nrec_rs, w * 16, 0, 0);
-    const int nn1 = (int)__builtin_amdgcn_raw_buffer_load_b32(nrec1_rs, w * 4, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    const int s = __builtin_amdgcn_readfirstlane((int)rx.x);
-    const int o = __builtin_amdgcn_readfirstlane((int)rx.y);
-    const int p = __builtin_amdgcn_readfirstlane((int)rx.z);
-    const int neg0 = __builtin_amdgcn_readfirstlane((int)rx.w);
-    const int neg1 = __builtin_amdgcn_readfirstlane(r1);
-    const int n0r = neg0 >= 0 ? neg0 : s, n1r = neg1 >= 0 ? neg1 : o;
-    // this wave's references: lane k < 4 holds row k (s, o, s', o'; -1 if absent)
-    const int myrow = l < 4 ? sel4(l, s, o, neg0, neg1) : -1;
-    float4 es[KQ], eo[KQ], rp[KQ], fs[KQ], fo[KQ];
-    float4 as_[KQ], ao[KQ], af0[KQ], af1[KQ];
-    load_row4<KQ>(EP, s, d, es);
-    load_row4<KQ>(EP, o, d, eo);
-    load_row4<KQ>(EP, n0r, d, fs);
-    load_row4<KQ>(EP, n1r, d, fo);
-#ifdef SKGE_OWN_ABL_NOA   // timing-only ablations (tools/ablate.sh)
-    if (false) {
-#else
-    if (EA) {
-#endif
-      load_row4<KQ>(EA, s, d, as_);
-      load_row4<KQ>(EA, o, d, ao);
-      load_row4<KQ>(EA, n0r, d, af0);
-      load_row4<KQ>(EA, n1r, d, af1);
-    } else {
-#pragma unroll
-      for (int m = 0; m < KQ; ++m)
-        as_[m] = ao[m] = af0[m] = af1[m] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
-    const int rc = myrow >= 0 ? (int)(refs[myrow] >> 32) : 0;   // the batch's references
-    {
-      float4 ra[KQ];
-      int c;
-      rel_row<KQ, W32>(a.R, p, d, rd, ra_prev, rp, ra, c);
-    }
-    float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
-    float4 gp4[KQ], g0[KQ], g1[KQ];
-#pragma unroll
-    for (int m = 0; m < KQ; ++m) {
-#define SKGE_EL(X)                                                                    \
-  {                                                                                   \
-    const float vp = (es[m].X + rp[m].X) - eo[m].X;   /* transe.py:32 */              \
-    const float v0 = (fs[m].X + rp[m].X) - eo[m].X;                                   \
-    const float v1 = (es[m].X + rp[m].X) - fo[m].X;                                   \
-    ps += fabsf(vp);                                                                  \
-    n0 += fabsf(v0);                                                                  \
-    n1 += fabsf(v1);                                                                  \
-    gp4[m].X = signf_np(-((eo[m].X - rp[m].X) - es[m].X)); /* transe.py:103,115 */    \
-    g0[m].X = signf_np((eo[m].X - rp[m].X) - fs[m].X);     /* transe.py:104,117 */    \
-    g1[m].X = signf_np((fo[m].X - rp[m].X) - es[m].X);                                \
-  }
-      SKGE_EL(x)
-      SKGE_EL(y)
-      SKGE_EL(z)
-      SKGE_EL(w)
-#undef SKGE_EL
-    }
-    const float pscore = -wave_sum(ps);
-    const float ns0 = -wave_sum(n0), ns1 = -wave_sum(n1);
-    const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // strict >, transe.py:73
-    const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
-    nv += v0 + v1;
-    if (a.trace) tt[1] = now_10ns();
-    // per reference: its count, and whether this wave holds the row's only
-    // reference (refs == 1 and no other reference of this wave to the row)
-    const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
-    bool dup = false;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int rk = __builtin_amdgcn_readlane(myrow, k);
-      dup = dup || (k != l && rk == myrow);
-    }
-#ifdef SKGE_OWN_ABL_ALLSOLE
-    const bool sole = myrow >= 0 && rc >= 0;
-#else
-    const bool sole = myrow >= 0 && rc == 1 && !dup;
-#endif
-    const uint64_t sole_m = __ballot(sole) & 0xfull;
-    const uint64_t upd_m = __ballot(myrow >= 0 && cE > 0) & 0xfull;   // rows with contributions
-    const uint64_t shared_m = __ballot(myrow >= 0 && !sole) & 0xfull;
-    // the four rows' contributions (transe.py:122-160: s +gp, o -gp, s' +gn, o' -gn)
-    const float fv0 = (float)v0, fv1 = (float)v1;
-    // k: 0 = s, 1 = o, 2 = s', 3 = o'
-#define SKGE_CONTRIB(K, M, X)                                                            \
-  ((K) == 0 ? fv0 * gp4[M].X + fv1 * (gp4[M].X + g1[M].X)                               \
-   : (K) == 1 ? -(fv0 * (gp4[M].X + g0[M].X) + fv1 * gp4[M].X)                          \
-   : (K) == 2 ? g0[M].X : -g1[M].X)
-    Accum aE = {};   // mode ACC_F32 (0), one copy
-    aE.sum = reinterpret_cast<float*>(esum);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {   // shared rows with contributions: memory-side adds
-      if (!((shared_m >> k) & (upd_m >> k) & 1ull)) continue;
-      float4 c[KQ];
-#pragma unroll
-      for (int m = 0; m < KQ; ++m)
-        c[m] = make_float4(SKGE_CONTRIB(k, m, x), SKGE_CONTRIB(k, m, y), SKGE_CONTRIB(k, m, z),
-                           SKGE_CONTRIB(k, m, w));
-      acc_row4_i16<KQ>(aE, __builtin_amdgcn_readlane(myrow, k), c, d);
-    }
-    if (l < 4 && !sole && myrow >= 0 && cE > 0) atomicAdd(cnt + myrow, cE);
-    uint64_t last_m = 0;
-    if (shared_m) {   // retire the shared references once this wave's adds are done
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      unsigned long long old = 0;
-      if (l < 4 && !sole && myrow >= 0) old = atomicAdd(refs + myrow, ~0ull);   // live - 1
-      const bool lst = l < 4 && !sole && myrow >= 0 && (old & 0xffffffffull) == 1ull;
-      if (lst) refs[myrow] = 0ull;   // every other reference has read the total already
-      last_m = __ballot(lst) & 0xfull;
-    }
-    if (a.trace) tt[2] = now_10ns();
-    // update: sole rows with contributions, and the shared rows this wave retired last
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool own = (sole_m >> k) & (upd_m >> k) & 1ull;
-      const bool last = (last_m >> k) & 1ull;
-      if (!own && !last) continue;
-      const int row = __builtin_amdgcn_readlane(myrow, k);
-      unsigned long long sv[KQ];
-      int c;
-      if (own) {
-        c = __builtin_amdgcn_readlane(cE, k);
-#pragma unroll
-        for (int m = 0; m < KQ; ++m)
-          sv[m] = pack_i16x4(make_float4(SKGE_CONTRIB(k, m, x), SKGE_CONTRIB(k, m, y),
-                                         SKGE_CONTRIB(k, m, z), SKGE_CONTRIB(k, m, w)));
-      } else {   // the batch's sums and count, cleared in the same memory-side operation
-        int cx = 0;
-        if (l == 0) cx = atomicExch(cnt + row, 0);
-        unsigned long long* srow = esum + (size_t)row * nq;
-#pragma unroll
-        for (int m = 0; m < KQ; ++m) {
-          const int q = 64 * m + l;
-          sv[m] = q < nq ? atomicExch(srow + q, 0ull) : 0ull;
-        }
-        c = __builtin_amdgcn_readfirstlane(cx);
-        if (c == 0) continue;   // referenced, never violated
-        if (c > PACKED_MAX && l == 0) atomicOr(a.err, ERR_PACKED);
-      }
-      float4 pr[KQ], ar[KQ];
-#pragma unroll
-      for (int m = 0; m < KQ; ++m) {
-        pr[m] = k == 0 ? es[m] : k == 1 ? eo[m] : k == 2 ? fs[m] : fo[m];
-        ar[m] = k == 0 ? as_[m] : k == 1 ? ao[m] : k == 2 ? af0[m] : af1[m];
-      }
-      row_update<KQ, false>(a.E.u, c, d, sv, sv, pr, ar);
-      if (a.E.claims && l == 0) atomicAdd(shard_of(a.E.claims), 1);   // profile: rows updated
-      float4* prow = reinterpret_cast<float4*>(EP + (size_t)row * d);
-      float4* arow = EA ? reinterpret_cast<float4*>(EA + (size_t)row * d) : nullptr;
-#pragma unroll
-      for (int m = 0; m < KQ; ++m) {
-        const int q = 64 * m + l;
-        if (q < nq) {
-          prow[q] = pr[m];
-          if (arow) arow[q] = ar[m];
-        }
-      }
-    }
-    if (a.trace) tt[3] = now_10ns();
-    // no-return adds last: a wait for a later load or for the shared rows'
-    // adds would wait for them too (vmcnt counts in issue order)
-    if (l < 4 && sole) refs[myrow] = 0ull;   // retired (shared rows: by their last reference)
-    if (v0 + v1 > 0) {   // relation sums (int16x4 / int32x2), count word
-      const float fv0 = (float)v0, fv1 = (float)v1;
-      unsigned long long* rrow = racc + (size_t)p * a.R.rw;
-#pragma unroll
-      for (int m = 0; m < KQ; ++m) {
-        const int q = 64 * m + l;
-        float4 cr;
-        cr.x = fv0 * (gp4[m].x + g0[m].x) + fv1 * (gp4[m].x + g1[m].x);
-        cr.y = fv0 * (gp4[m].y + g0[m].y) + fv1 * (gp4[m].y + g1[m].y);
-        cr.z = fv0 * (gp4[m].z + g0[m].z) + fv1 * (gp4[m].z + g1[m].z);
-        cr.w = fv0 * (gp4[m].w + g0[m].w) + fv1 * (gp4[m].w + g1[m].w);
-        if (q < nq) {
-          if (W32) {
-            atomicAdd(rrow + 2 * q, pack_i32x2(cr.x, cr.y));
-            atomicAdd(rrow + 2 * q + 1, pack_i32x2(cr.z, cr.w));
-          } else {
-            atomicAdd(rrow + q, pack_i16x4(cr));
-          }
-        }
-      }
-      if (l == 0) atomicAdd(racc + (size_t)p * a.R.rw + rcw, (unsigned long long)(2 * (v0 + v1)));
-    }
-    if (w < a.count_next && l < 4) {   // the next batch's references
-      const int nr = sel4(l, (int)nx.x, (int)nx.y, (int)nx.w, nn1);
-      if (nr >= 0) atomicAdd(refs_next + nr, 0x100000001ull);
-    }
-    if (a.trace && l == 0) {
-      unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
-      tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
-      tr[5] = sole_m | (shared_m << 4) | ((unsigned long long)(v0 + v1 > 0) << 8) | (last_m << 12) |
-              (upd_m << 16);
-    }
-#undef SKGE_CONTRIB
-  }
-  if (l == 0 && nv) {
-    atomicAdd(shard_of(a.nviol_shards), nv);
-    if (a.stats_viol) atomicAdd(shard_of(a.stats_viol), nv);
-  }
-}
-
 // ======================== HolE pairwise, pipelined ========================
 //
 // The launch structure of k_pipe_batch for HolE (skge/hole.py:44-100, the
@@ -2241,12 +1216,9 @@ __device__ __forceinline__ void load_f32_row(const float* P, const float* A, con
   }
 }
 
-// SPEC (spectral entity sums): the summed Z' is inverse-transformed in the
-// wave's buffers (wb, tw) first
-template <int KQ, bool SPEC = false>
+template <int KQ>
 __device__ __forceinline__ void claim_and_apply_f(const PipeTab& t, int pp, int row, int d,
-                                                  int gp, float* wb = nullptr,
-                                                  const float2* tw = nullptr) {
+                                                  int gp) {
   const int l = lane_id(), nq = d >> 2;
   int c = 0;
   if (l == 0) c = atomicExch(t.cnt[pp] + row, 0);
@@ -2255,7 +1227,6 @@ __device__ __forceinline__ void claim_and_apply_f(const PipeTab& t, int pp, int 
   load_f32_row<KQ>(t.P, t.A, S, row, d, p, a, sm);
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row
-  if constexpr (SPEC) spec_to_spatial<KQ>(wb, tw, d, sm);
   row_update_f<KQ>(t.u, c, d, sm, p, a);
   float4* srow = reinterpret_cast<float4*>(S + (size_t)row * d);
 #pragma unroll
@@ -2268,62 +1239,14 @@ __device__ __forceinline__ void claim_and_apply_f(const PipeTab& t, int pp, int 
   if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
 }
 
-// The HolE launch's A role: its scoring waves hold ~180 VGPRs (2 waves per
-// SIMD), so the apply waves only get the residency the scoring waves leave
-// (~600 waves); each handles HGROUP slot-recorded rows at once -- the HGROUP
-// claims in one atomic instruction, every row's loads in flight together,
-// one drain, the done words in one store instruction.
-#ifndef SKGE_HPIPE_GROUP
-#define SKGE_HPIPE_GROUP 1   // A/B on WN18 d=200: 1 row 51.7M, 2: 51.4M, 4: 49.6M, 8: 48.0M
-#endif
-constexpr int HGROUP = SKGE_HPIPE_GROUP;
-#ifndef SKGE_HPIPE_SLOTS_PREFETCH
-#define SKGE_HPIPE_SLOTS_PREFETCH 1   // apply_slots_f (0: one slot group per iteration)
-#endif
-template <int KQ>
-__device__ __forceinline__ void claim_and_apply_group_f(const PipeTab& t, int pp, int s0, int ns,
-                                                        int d, int gp) {
-  const int l = lane_id(), nq = d >> 2;
-  int row = -1;
-  if (l < HGROUP && s0 + l < ns) row = t.touched[pp][s0 + l];
-  int c = 0;
-  if (row >= 0) c = atomicExch(t.cnt[pp] + row, 0);
-  float* S = reinterpret_cast<float*>(t.sum[pp]);
-  int rk[HGROUP];
-  float4 sm[HGROUP][KQ], p[HGROUP][KQ], a[HGROUP][KQ];
-#pragma unroll
-  for (int k = 0; k < HGROUP; ++k) {
-    rk[k] = __builtin_amdgcn_readlane(row, k);
-    load_f32_row<KQ>(t.P, t.A, S, rk[k] >= 0 ? rk[k] : 0, d, p[k], a[k], sm[k]);
-  }
-  const uint64_t won = __ballot(c != 0) & ((1ull << HGROUP) - 1);
-  if (!won) return;   // empty slots, or rows other waves own
-#pragma unroll
-  for (int k = 0; k < HGROUP; ++k) {
-    if (!((won >> k) & 1ull)) continue;
-    const int ck = __builtin_amdgcn_readlane(c, k);
-    row_update_f<KQ>(t.u, ck, d, sm[k], p[k], a[k]);
-    float4* srow = reinterpret_cast<float4*>(S + (size_t)rk[k] * d);
-#pragma unroll
-    for (int m = 0; m < KQ; ++m)
-      if (64 * m + l < nq) srow[64 * m + l] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    store_row4_sc1<KQ>(t.P, rk[k], d, p[k]);
-    if (t.A) store_row4_sc1<KQ>(t.A, rk[k], d, a[k]);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
-  if (c != 0) __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t.claims && l == 0) atomicAdd(shard_of(t.claims), (int)__builtin_popcountll(won));
-}
-
 // The HolE launch's A role over its share of the slot records: slots k0,
 // k0 + ks, ... < ns.  The slot ids come in one vector load per 64 slots (empty
 // slots cost nothing more), and each touched row's claim and loads are issued
 // while the previous row is updated and published, so a wave's rows overlap
 // instead of paying a dependent slot load + claim round trip each.
-template <int KQ, bool SPEC = false>
+template <int KQ>
 __device__ __forceinline__ void apply_slots_f(const PipeTab& t, int pp, int k0, int ks, int ns,
-                                              int d, int gp, float* wb = nullptr,
-                                              const float2* tw = nullptr) {
+                                              int d, int gp) {
   const int l = lane_id(), nq = d >> 2;
   float* S = reinterpret_cast<float*>(t.sum[pp]);
   for (int base = k0; base < ns; base += 64 * ks) {
@@ -2350,7 +1273,6 @@ __device__ __forceinline__ void apply_slots_f(const PipeTab& t, int pp, int k0, 
       }
       c = __builtin_amdgcn_readfirstlane(c);
       if (c != 0) {   // this wave owns the row
-        if constexpr (SPEC) spec_to_spatial<KQ>(wb, tw, d, sm);
         row_update_f<KQ>(t.u, c, d, sm, p, a);
         float4* srow = reinterpret_cast<float4*>(S + (size_t)r * d);
 #pragma unroll
@@ -2376,12 +1298,11 @@ __device__ __forceinline__ void apply_slots_f(const PipeTab& t, int pp, int k0, 
   }
 }
 
-template <int KQ, bool SPEC = false>
+template <int KQ>
 __device__ __forceinline__ void ensure_applied_f(const PipeTab& t, int pp, int row, int d, int gp,
-                                                 int* err, float* wb = nullptr,
-                                                 const float2* tw = nullptr) {
+                                                 int* err) {
   if (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gp) return;
-  claim_and_apply_f<KQ, SPEC>(t, pp, row, d, gp, wb, tw);
+  claim_and_apply_f<KQ>(t, pp, row, d, gp);
   unsigned spins = 0;
   while (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gp) {
     __builtin_amdgcn_s_sleep(2);
@@ -2464,16 +1385,9 @@ __device__ __forceinline__ void rel_publish_f(const PipeArgs& a, int w, int rd, 
   if (c && a.R.updated && l == 0) atomicAdd(shard_of(a.R.updated), 1);
 }
 
-#ifndef SKGE_HPIPE_OCC
-#define SKGE_HPIPE_OCC 2   // scoring waves per SIMD the apply-workgroup cap assumes
-#endif
-#if SKGE_HPIPE_OCC > 2
-#define SKGE_HPIPE_ATTR __attribute__((amdgpu_waves_per_eu(SKGE_HPIPE_OCC)))
-#else
-#define SKGE_HPIPE_ATTR
-#endif
+constexpr int HPIPE_OCC = 2;   // scoring waves per SIMD the apply-workgroup cap assumes (direct form)
 
-// PAIR (round 4, SKGE_HPIPE_PAIR; FFT at d = 200, no SPEC): 128-thread
+// PAIR (round 4, SKGE_HPIPE_PAIR; FFT at d = 200): 128-thread
 // workgroups, and a scoring workgroup's two waves score ONE positive together
 // -- each loads and settles two of its rows, the transforms' stage passes are
 // split between them (fft_run_c2: the same butterflies, the same bits), both
@@ -2490,19 +1404,9 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
   const int rd = a.b & 1;
   const int ra_prev = (g - 1) % 3, ra_cur = g % 3;
   float2* const tw = reinterpret_cast<float2*>(smem);
-  // the twiddle table into LDS before the loop.  (SKGE_HPIPE_TW_LATE, A/B:
-  // its global loads issued here and written to LDS just before the first
-  // barrier, overlapping the first record's round trip: 94.4 / 94.6 vs 94.9 M
-  // triples/s, no gain -- not on the critical path)
-  const int t0 = (int)threadIdx.x, t1 = t0 + 128;
-#ifdef SKGE_HPIPE_TW_LATE
-  const float2 twr0 = a.tw[t0 < d ? t0 : 0], twr1 = a.tw[t1 < d ? t1 : 0];
-  bool tw_pending = true;
-#else
-  const float2 twr0 = {}, twr1 = {};
+  // the twiddle table into LDS before the loop (its load overlapped with the
+  // first record's round trip measured no faster: not on the critical path)
   fft_twiddles(tw, a.tw, d);
-  bool tw_pending = false;
-#endif
   float* const wb = smem + 2 * d;   // the pair's two transform buffers
   float2* const b0 = reinterpret_cast<float2*>(wb);
   float2* const b1 = b0 + 5 * 100;
@@ -2545,11 +1449,6 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
       if (pend & 2ull) load_row4_sc1<1>(a.E.P, rb_row, d, xb);
     }
     if (a.trace) tt[2] = now_10ns();
-    if (tw_pending) {
-      if (t0 < d) tw[t0] = twr0;
-      if (t1 < d) tw[t1] = twr1;
-      tw_pending = false;
-    }
     __syncthreads();   // the previous positive's buffers are free, the twiddles in place
     if (hw == a.pair_r1) fft_put_row(b0, 100, 0, xr[0], d);
     if (hw == 0) {
@@ -2617,10 +1516,9 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
   }
 }
 
-template <int KM, bool FFT, bool SPEC = false, bool PAIR = false>
-__global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(PipeArgs a) {
-  static_assert(!SPEC || FFT, "spectral entity sums need the FFT form");
-  static_assert(!PAIR || (FFT && !SPEC), "the pair form is the FFT form's");
+template <int KM, bool FFT, bool PAIR = false>
+__global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
+  static_assert(!PAIR || FFT, "the pair form is the FFT form's");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6;
   const int l = lane_id();
@@ -2632,35 +1530,18 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
   const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
   const int nB = gridDim.x - a.nA;
   const int blk = (int)blockIdx.x;
-  const bool is_a = a.b_first ? blk >= nB : blk < a.nA;
-  if (is_a) {
+  if (blk < a.nA) {
     // ---- A role: write R_b, then apply the previous batch's entity rows ----
-    const int blk_a = a.b_first ? blk - nB : blk;
+    const int blk_a = blk;
     const int nR = a.R.rows;
     const int wa = blk_a * wpb + wave;
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
     if (a.b == a.nb1 && wa == 0) fold_shards(a.nviol_shards, a.nviol_total);
-    float2* const twA = reinterpret_cast<float2*>(smem);
-    float* const wbA = smem + 2 * d + wave * hole_fft_wave_floats(d);
-    if constexpr (SPEC) {   // the appliers' inverse transforms need the twiddles
-      fft_twiddles(twA, a.tw, d);
-      __syncthreads();
-    }
-#if SKGE_HPIPE_SLOTS_PREFETCH
     // items w = wa, wa + S, ...: relation rows w < nR, then entity slots w - nR
     const int S = a.nA * wpb;
     for (int w = wa; w < nR; w += S) rel_publish_f<1>(a, w, rd, rw, ra_prev, ra_old);
     const int k0 = wa >= nR ? wa - nR : wa - nR + ((nR - wa + S - 1) / S) * S;
-    apply_slots_f<1, SPEC>(a.E, pp, k0, S, a.prev_slots, d, gp, wbA, twA);
-#else
-    const int total = nR + (a.prev_slots + HGROUP - 1) / HGROUP;   // relation rows, slot groups
-    for (int w = wa; w < total; w += a.nA * wpb) {
-      if (w < nR)
-        rel_publish_f<1>(a, w, rd, rw, ra_prev, ra_old);
-      else
-        claim_and_apply_group_f<1>(a.E, pp, HGROUP * (w - nR), a.prev_slots, d, gp);
-    }
-#endif
+    apply_slots_f<1>(a.E, pp, k0, S, a.prev_slots, d, gp);
     if (a.trace && l == 0) {   // diagnostics (skge_pipe_runner_profile, tools/hole_trace.py)
       unsigned long long* tr = a.trace + 2 + 6 * (size_t)a.count + 2 * (size_t)wa;
       tr[0] = ta0;
@@ -2669,7 +1550,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     return;
   }
   // ---- B role: score batch b (k_hole_pos's arithmetic), scatter into cp / ra_cur ----
-  const int blk_b = a.b_first ? blk : blk - a.nA;
+  const int blk_b = blk - a.nA;
   if constexpr (PAIR) {
     hole_pipe_score_pair<KM>(a, smem, blk_b, nB);
     return;
@@ -2711,17 +1592,13 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
       int c;
       rel_row_f<1>(a.R, p, d, rd, ra_prev, rp, ra, c);
     }
-#ifndef SKGE_HPIPE_ABL_NO_PEND   // timing-only ablation: pending rows ignored
     const uint64_t pend = __ballot(mark == gp) & 0xfull;
-#else
-    const uint64_t pend = 0ull * __ballot(mark == gp);
-#endif
     if (a.trace) tt[1] = now_10ns();
     if (pend) {
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) {
         if (!((pend >> k) & 1ull)) continue;
-        ensure_applied_f<1, SPEC>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err, wb, tw);
+        ensure_applied_f<1>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err);
       }
       if (pend & 1ull) load_row4_sc1<1>(a.E.P, s, d, es);
       if (pend & 2ull) load_row4_sc1<1>(a.E.P, o, d, eo);
@@ -2777,21 +1654,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
     Accum aR = {};   // mode ACC_F32 (0), one copy
     aR.sum = racc + (size_t)p * rstride;
     aR.width = d;
-    if constexpr (SPEC) {
-      int ne;
-      const float* zr = hole_fft_rows_spec(wb, tw, d, hs, v0, v1, gpf, g0, g1, ne);
-      if (a.trace) {   // diagnostics: the inverse transform done (LDS results waited for)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        inv_dt = now_10ns() - tt[3];
-      }
-      const float* zs = wb;   // the entity rows' Z', signals 0 .. ne - 1
-      acc_fft_row<KM>(aR, 0, zr, 0, d);
-      acc_fft_row<KM>(aE, s, zs, 0, d);
-      acc_fft_row<KM>(aE, o, zs, 1, d);
-      if (v0) acc_fft_row<KM>(aE, neg0, zs, 2, d);
-      if (v1) acc_fft_row<KM>(aE, neg1, zs, 2 + v0, d);
-      (void)ne;
-    } else if constexpr (FFT) {
+    if constexpr (FFT) {    } else if constexpr (FFT) {
       const float* z = hole_fft_rows(wb, tw, d, hs, v0, v1, gpf, g0, g1);
       if (a.trace) {   // diagnostics: the inverse transforms done (LDS results waited for)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2804,9 +1667,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) SKGE_HPIPE_ATTR void k_hole_pipe(Pipe
       if (v1) acc_fft_row<KM>(aE, neg1, z, 3 + v0, d);
     } else {
       const HoleRows h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gpf, g0, g1);
-#ifndef SKGE_HPIPE_ABL_NO_RATOM   // timing-only ablation: relation sums dropped
       acc_q<KM>(aR, 0, h.cr, d, L.U);
-#endif
       acc_q<KM>(aE, s, h.cs, d, L.U);
       acc_q<KM>(aE, o, h.co, d, L.U);
       if (v0) acc_q<KM>(aE, neg0, h.c0, d, L.U);
@@ -2948,21 +1809,11 @@ struct skge_pipe_runner {
   std::vector<int> grid;
   bool w32 = false;                // int32x2 relation sums
   bool e8 = false;                 // int8x4 entity sums (SKGE_ACC_I8X4: per-batch counts <= 127)
-  bool grp = true;                 // owner marks: GRP_ROWS rows per apply round trip
-  bool lazy = false;               // SKGE_PIPE_LAZY: entity rows applied by their next reader
-  bool owner = false;              // SKGE_PIPE_OWNER: rows updated by their batch's last reference
   bool hole = false;               // HolE pairwise (k_hole_pipe, fp32 sums)
   bool fft = false;                // HolE: correlations in the frequency domain (skge_hole_fft.h)
   bool rfold = false;              // TransE: relation sums in replicas, k_rel_fold after each batch
-  bool spec = false;               // HolE FFT: entity sums as pre-processed half spectra
-                                   // (SKGE_HPIPE_SPEC; hole_fft_rows_spec / spec_to_spatial)
-  bool split = false;              // SKGE_PIPE_SPLIT: apply and scoring roles as two kernels on
-                                   // parallel branches (large batches: own register budgets)
-  hipStream_t st2 = nullptr;       // split: the scoring kernels' capture stream
-  hipEvent_t fork = nullptr, join = nullptr;
   size_t lds = 0;                  // HolE: dynamic LDS per workgroup
   bool pair = false;               // HolE FFT, d = 200: two waves per positive (SKGE_HPIPE_PAIR)
-  bool p2 = false;                 // TransE large batches: two positives per scoring wave (SKGE_PIPE_P2)
   bool fused = false;              // TransE: k_pipe_fused (one kind of wave, no hand-offs)
   int n_rows = 0, d = 0;           // fused: the entity table's geometry (k_fused_fin)
   int nlaunch() const { return (int)batch.size() + 2; }
@@ -2981,9 +1832,6 @@ static void pipe_free(skge_pipe_runner* r) {
   if (!r) return;
   if (r->exec) (void)hipGraphExecDestroy(r->exec);
   if (r->graph) (void)hipGraphDestroy(r->graph);
-  if (r->fork) (void)hipEventDestroy(r->fork);
-  if (r->join) (void)hipEventDestroy(r->join);
-  if (r->st2) (void)hipStreamDestroy(r->st2);
   for (void* p : r->bufs) (void)hipFree(p);
   delete r;
 }
@@ -3013,9 +1861,6 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
     hipLaunchKernelGGL(k_epoch_sample, dim3((unsigned)blocks), dim3(256), 0, st, r->trip, r->T,
                        r->half, r->seed, (const uint64_t*)r->epoch_key, r->set, r->n_ent,
                        r->ntries, r->rec, r->rec_n1);
-    if (r->owner)   // the epoch's first batch's references (k_own_batch counts the rest)
-      hipLaunchKernelGGL(k_own_count, dim3(std::max(1, std::min((r->batch[0].count + 255) / 256, 4096))),
-                         dim3(256), 0, st, r->rec, r->rec_n1, r->batch[0].count, r->batch[0].E.refs[0]);
   }
   ++i;
   if (ev) (void)hipEventRecord(ev[i], st);
@@ -3028,78 +1873,29 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
       a.stats_viol = stats + (3 * i + 2) * sh;
     }
     if (trace && i == trace_launch) a.trace = trace;
-#define SKGE_PB(K)                                                                               \
-  do {                                                                                           \
-    const dim3 gr(r->grid[k]), bl(SKGE_PIPE_WG);                                                 \
-    if (r->lazy) {                                                                               \
-      if (r->w32) hipLaunchKernelGGL((k_lazy_batch<K, true>), gr, bl, 0, st, a);                 \
-      else hipLaunchKernelGGL((k_lazy_batch<K, false>), gr, bl, 0, st, a);                       \
-    } else if (r->owner) {                                                                       \
-      if (r->w32) hipLaunchKernelGGL((k_own_batch<K, true>), gr, bl, 0, st, a);                  \
-      else hipLaunchKernelGGL((k_own_batch<K, false>), gr, bl, 0, st, a);                        \
-    } else if (a.E.own[0] && r->grp && r->split && a.count > 0) {                                \
-      /* large batches, split: the apply kernel here, the scoring kernel on st2 (forked and */   \
-      /* joined around the pair), each sized to its own role */                                  \
-      const dim3 ga(a.nA), gb(r->grid[k] - a.nA);                                                \
-      (void)hipEventRecord(r->fork, st);                                                        \
-      (void)hipStreamWaitEvent(r->st2, r->fork, 0);                                             \
-      if (r->e8) {                                                                               \
-        if (r->w32) {                                                                            \
-          hipLaunchKernelGGL((k_pipe_batch<K, true, true, true, false, 2>), gb, bl, 0, r->st2, a); \
-          hipLaunchKernelGGL((k_pipe_batch<K, true, true, true, false, 1>), ga, bl, 0, st, a);   \
-        } else {                                                                                 \
-          hipLaunchKernelGGL((k_pipe_batch<K, false, true, true, false, 2>), gb, bl, 0, r->st2, a); \
-          hipLaunchKernelGGL((k_pipe_batch<K, false, true, true, false, 1>), ga, bl, 0, st, a);  \
-        }                                                                                        \
-      } else {                                                                                   \
-        if (r->w32) {                                                                            \
-          hipLaunchKernelGGL((k_pipe_batch<K, true, false, true, false, 2>), gb, bl, 0, r->st2, a); \
-          hipLaunchKernelGGL((k_pipe_batch<K, true, false, true, false, 1>), ga, bl, 0, st, a);  \
-        } else {                                                                                 \
-          hipLaunchKernelGGL((k_pipe_batch<K, false, false, true, false, 2>), gb, bl, 0, r->st2, a); \
-          hipLaunchKernelGGL((k_pipe_batch<K, false, false, true, false, 1>), ga, bl, 0, st, a); \
-        }                                                                                        \
-      }                                                                                          \
-      (void)hipEventRecord(r->join, r->st2);                                                    \
-      (void)hipStreamWaitEvent(st, r->join, 0);                                                 \
-    } else if (a.E.own[0] && r->grp && r->p2) {   /* ... two positives per scoring wave */      \
-      if (r->e8) {                                                                               \
-        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, true, false, 0, true>), gr, bl, 0, st, a); \
-        else hipLaunchKernelGGL((k_pipe_batch<K, false, true, true, false, 0, true>), gr, bl, 0, st, a); \
-      } else {                                                                                   \
-        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true, false, 0, true>), gr, bl, 0, st, a); \
-        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true, false, 0, true>), gr, bl, 0, st, a); \
-      }                                                                                          \
-    } else if (a.E.own[0] && r->grp) {   /* large batches: grouped owner-row apply */             \
-      if (r->e8) {                                                                               \
-        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, true>), gr, bl, 0, st, a);   \
-        else hipLaunchKernelGGL((k_pipe_batch<K, false, true, true>), gr, bl, 0, st, a);         \
-      } else {                                                                                   \
-        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true>), gr, bl, 0, st, a);  \
-        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true>), gr, bl, 0, st, a);        \
-      }                                                                                          \
-    } else if (a.E.a4 && K == 1) {   /* one A-role wave per positive (claim_and_apply4) */       \
-      if (r->e8) {                                                                               \
-        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, false, true>), gr, bl, 0, st, a); \
-        else hipLaunchKernelGGL((k_pipe_batch<K, false, true, false, true>), gr, bl, 0, st, a);  \
-      } else {                                                                                   \
-        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, false, true>), gr, bl, 0, st, a); \
-        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, false, true>), gr, bl, 0, st, a); \
-      }                                                                                          \
-    } else if (r->e8) {                                                                          \
-      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true>), gr, bl, 0, st, a);           \
-      else hipLaunchKernelGGL((k_pipe_batch<K, false, true>), gr, bl, 0, st, a);                 \
-    } else {                                                                                     \
-      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false>), gr, bl, 0, st, a);          \
-      else hipLaunchKernelGGL((k_pipe_batch<K, false, false>), gr, bl, 0, st, a);                \
-    }                                                                                            \
+#define SKGE_PB(K)                                                                        \
+  do {                                                                                    \
+    const dim3 gr(r->grid[k]), bl(SKGE_PIPE_WG);                                          \
+    if (a.E.own[0]) {   /* large batches: owner marks, grouped owner-row apply */         \
+      if (r->e8) {                                                                        \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, true, true>), gr, bl, 0, st, a);  \
+      } else {                                                                            \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true>), gr, bl, 0, st, a); \
+      }                                                                                   \
+    } else if (r->e8) {                                                                   \
+      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true>), gr, bl, 0, st, a);    \
+      else hipLaunchKernelGGL((k_pipe_batch<K, false, true>), gr, bl, 0, st, a);          \
+    } else {                                                                              \
+      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false>), gr, bl, 0, st, a);   \
+      else hipLaunchKernelGGL((k_pipe_batch<K, false, false>), gr, bl, 0, st, a);         \
+    }                                                                                     \
   } while (0)
     if (r->hole) {
       const dim3 gr(r->grid[k]), bl(r->pair ? 128 : SKGE_PIPE_WG);
 #define SKGE_HPIPE(K)                                                          \
   if (r->pair)                                                                 \
-    hipLaunchKernelGGL((k_hole_pipe<K, true, false, true>), gr, bl, r->lds, st, a); \
-  else if (r->fft && r->spec)                                                  \
     hipLaunchKernelGGL((k_hole_pipe<K, true, true>), gr, bl, r->lds, st, a);   \
   else if (r->fft)                                                             \
     hipLaunchKernelGGL((k_hole_pipe<K, true>), gr, bl, r->lds, st, a);         \
@@ -3149,8 +1945,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
                                        const void* set, int64_t set_capacity, int nbatches,
                                        uint64_t seed, uint64_t* epoch_key, float margin,
                                        int ntries, int* nviol_total, int flags, bool hole, int af) {
-  const bool lazy = (flags & SKGE_PIPE_LAZY) != 0;
-  if ((flags & ~SKGE_PIPE_LAZY) || (hole && flags)) {
+  if (flags) {
     set_error("pipelined runner: unknown flags %d", flags);
     return nullptr;
   }
@@ -3173,9 +1968,9 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
                 "gates");
       return nullptr;
     }
-  } else if ((ent->acc_mode != SKGE_ACC_I16X4 && !(ent->acc_mode == SKGE_ACC_I8X4 && !lazy)) ||
+  } else if ((ent->acc_mode != SKGE_ACC_I16X4 && ent->acc_mode != SKGE_ACC_I8X4) ||
       (rel->acc_mode != SKGE_ACC_I16X4 && rel->acc_mode != SKGE_ACC_I32X2) || d % 4 || d > 1024 ||
-      ent->width != d || rel->width != d || (ent->acc_touched == nullptr && !lazy) ||
+      ent->width != d || rel->width != d || ent->acc_touched == nullptr ||
       rel->acc_touched != nullptr || rel->acc_replicas > 1 || ent->acc_replicas > 1 ||
       ent->gate || rel->gate) {
     set_error("pipelined runner: needs a packed (SKGE_ACC_I16X4) entity table with slot "
@@ -3190,7 +1985,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   }
   // batch geometry of StochasticTrainer._optim (skge/base.py:1246-1268)
   const int64_t bs = T / nbatches;
-  if ((!lazy && 4 * bs > ent->touched_cap) || 4 * bs > (1ll << 30)) {
+  if (4 * bs > ent->touched_cap || 4 * bs > (1ll << 30)) {
     set_error("pipelined runner: batch too large for the slot capacity");
     return nullptr;
   }
@@ -3198,29 +1993,19 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   for (int64_t s0 = 0; s0 < T; s0 += bs) batches.push_back({s0, (s0 + bs <= T) ? bs : T - s0});
   const int nb1 = (int)batches.size();
   skge_pipe_runner* r = new skge_pipe_runner();
-  r->lazy = lazy;
   r->hole = hole;
   r->e8 = !hole && ent->acc_mode == SKGE_ACC_I8X4;
-  {
-    const char* gr = getenv("SKGE_PIPE_GRP");   // A/B: 0 = one owner row per round trip
-    r->grp = !(gr && atoi(gr) == 0);
-  }
-  {
-    const char* sp = getenv("SKGE_PIPE_SPLIT");   // A/B: two kernels per large-batch launch
-    r->split = !hole && !lazy && sp && atoi(sp) != 0;
-    if (r->split && (hipStreamCreateWithFlags(&r->st2, hipStreamNonBlocking) != hipSuccess ||
-                     hipEventCreateWithFlags(&r->fork, hipEventDisableTiming) != hipSuccess ||
-                     hipEventCreateWithFlags(&r->join, hipEventDisableTiming) != hipSuccess)) {
-      set_error("pipelined runner: split-mode stream / event creation failed");
-      pipe_free(r);
-      return nullptr;
-    }
-  }
-  {
-    const char* ow = getenv("SKGE_PIPE_OWNER");   // A/B: entity rows by their last reference
-    r->owner = !hole && !lazy && !r->e8 && ow && atoi(ow) != 0;
-  }
   const int nq = d / 4;
+  const int N = ent->rows;
+  // large batches (more than 16k slot records): owner marks, k_pipe_batch's A
+  // role scans its slots 64 at a time
+  const bool grouped = !hole && 4 * bs > 4 * 4096;
+  // TransE below that: k_pipe_fused (d <= 512; SKGE_PIPE_FUSED=0: k_pipe_batch)
+  {
+    const char* fe = getenv("SKGE_PIPE_FUSED");
+    r->fused = !hole && !grouped && nq <= 128 && (long long)N < SLOT_BUF &&
+               !(fe && atoi(fe) == 0);
+  }
   PipeArgs a = {};
   auto upd = [](const skge_table_t* s) {
     UpdParams u;
@@ -3232,9 +2017,9 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     u.fdiv = s->fixed_div;
     return u;
   };
+  bool ok = true;
   {
     PipeTab& t = a.E;
-    const int N = ent->rows;
     t.P = ent->param;
     t.A = ent->opt == SKGE_ADAGRAD ? ent->state : nullptr;
     t.u = upd(ent);
@@ -3243,31 +2028,41 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     t.sum[0] = reinterpret_cast<unsigned long long*>(ent->acc_sum);
     t.cnt[0] = ent->acc_cnt;
     t.touched[0] = ent->acc_touched;
-    t.done = (int*)dalloc(r, (size_t)N * 4);
-    bool ok = t.done != nullptr;
-    if (lazy) {   // one accumulator copy (the caller's), claim words
-      t.claim = (int*)dalloc(r, (size_t)N * 4);
-      ok = ok && t.claim;
-    } else {      // a second accumulator copy, slot records and batch marks
+    if (r->fused) {
+      // the second row buffer, the other two accumulator copies, the meta words
+      FusedTab& F = a.F;
+      const size_t sb = (size_t)N * nq * (r->e8 ? 4 : 8);
+      F.P[0] = ent->param;
+      F.P[1] = (float*)dalloc(r, (size_t)N * d * 4);
+      F.A[0] = t.A;
+      F.A[1] = F.A[0] ? (float*)dalloc(r, (size_t)N * d * 4) : nullptr;
+      F.sum[0] = ent->acc_sum;
+      F.cnt[0] = ent->acc_cnt;
+      F.touched[0] = ent->acc_touched;
+      for (int k = 1; k < 3; ++k) {
+        F.sum[k] = dalloc(r, sb);
+        F.cnt[k] = (int*)dalloc(r, (size_t)N * 4);
+        F.touched[k] = (int*)dalloc(r, (size_t)4 * bs * 4);
+        ok = ok && F.sum[k] && F.cnt[k] && F.touched[k];
+      }
+      F.meta = (int4*)dalloc(r, (size_t)N * sizeof(int4));
+      ok = ok && F.P[1] && (!F.A[0] || F.A[1]) && F.meta;
+      r->n_rows = N;
+      r->d = d;
+    } else {
+      // a second accumulator copy, slot records, batch marks, done words
+      t.done = (int*)dalloc(r, (size_t)N * 4);
       t.sum[1] = (unsigned long long*)dalloc(r, (size_t)N * nq * (hole ? 16 : (r->e8 ? 4 : 8)));
       t.cnt[1] = (int*)dalloc(r, (size_t)N * 4);
       t.touched[1] = (int*)dalloc(r, (size_t)4 * bs * 4);
       t.pend[0] = (int*)dalloc(r, (size_t)N * 4);
       t.pend[1] = (int*)dalloc(r, (size_t)N * 4);
-      ok = ok && t.sum[1] && t.cnt[1] && t.touched[1] && t.pend[0] && t.pend[1];
-      // large batches (more than 16k slots): owner marks, the A role scans its
-      // slots 64 at a time (SKGE_PIPE_OWNMARK=0: one slot per item, as below)
-      const char* om = getenv("SKGE_PIPE_OWNMARK");
-      if (!hole && 4 * bs > 4 * 4096 && !(om && atoi(om) == 0)) {
+      ok = ok && t.done && t.sum[1] && t.cnt[1] && t.touched[1] && t.pend[0] && t.pend[1];
+      if (grouped) {
         t.own[0] = (int*)dalloc(r, (size_t)N * 4);
         t.own[1] = (int*)dalloc(r, (size_t)N * 4);
         ok = ok && t.own[0] && t.own[1];
       }
-    }
-    if (r->owner) {   // reference words by batch parity
-      t.refs[0] = (unsigned long long*)dalloc(r, (size_t)N * 8);
-      t.refs[1] = (unsigned long long*)dalloc(r, (size_t)N * 8);
-      ok = ok && t.refs[0] && t.refs[1];
     }
     RelTab& q = a.R;
     const int M = rel->rows;
@@ -3283,13 +2078,9 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     // TransE, large batches (the A role's owner-mark regime): the same spread,
     // one replica per ~256 expected adds into a row (bs / M), <= 16, folded by
     // k_rel_fold after every batch launch (WN18 nb = 2: 16; nb = 100: 1)
-    if (!hole && !lazy && !r->owner && 4 * bs > 4 * 4096) {
+    if (grouped) {
       const long long per_row = bs / std::max(1, M);
       while (q.reps < 16 && (long long)q.reps * 256 < per_row) q.reps *= 2;
-    }
-    if (!hole && !lazy && !r->owner && getenv("SKGE_PIPE_RREPS")) {   // A/B switch (power of 2)
-      q.reps = 1;
-      while (2 * q.reps <= std::min(64, atoi(getenv("SKGE_PIPE_RREPS")))) q.reps *= 2;
     }
     r->rfold = q.reps > 1;
     q.folded = r->rfold ? 1 : 0;
@@ -3305,52 +2096,14 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     q.A[1] = ada ? (float*)dalloc(r, (size_t)M * d * 4) : nullptr;
     for (int k = 0; k < 3; ++k)
       q.acc[k] = (unsigned long long*)dalloc(r, (size_t)q.reps * M * q.rw * 8);
-    if (!ok || !q.P[1] || (ada && !q.A[1]) || !q.acc[0] || !q.acc[1] || !q.acc[2]) {
-      set_error("pipelined runner: device allocation failed");
-      pipe_free(r);
-      return nullptr;
-    }
-  }
-  {
-    // fused runner (default at batches without owner marks, d <= 512;
-    // SKGE_PIPE_FUSED=0: k_pipe_batch): the second row buffer, the third
-    // accumulator copy and the per-row meta words
-    const char* fe = getenv("SKGE_PIPE_FUSED");
-    r->fused = !hole && !lazy && !r->owner && !r->split && !r->p2 && a.E.own[0] == nullptr &&
-               nq <= 128 && (long long)ent->rows < SLOT_BUF && !(fe && atoi(fe) == 0);
-    if (r->fused) {
-      FusedTab& F = a.F;
-      const int N = ent->rows;
-      const size_t sb = (size_t)N * nq * (r->e8 ? 4 : 8);
-      F.P[0] = ent->param;
-      F.P[1] = (float*)dalloc(r, (size_t)N * d * 4);
-      F.A[0] = ent->opt == SKGE_ADAGRAD ? ent->state : nullptr;
-      F.A[1] = F.A[0] ? (float*)dalloc(r, (size_t)N * d * 4) : nullptr;
-      F.sum[0] = ent->acc_sum;
-      F.cnt[0] = ent->acc_cnt;
-      F.touched[0] = ent->acc_touched;
-      for (int k = 1; k < 3; ++k) {
-        F.sum[k] = dalloc(r, sb);
-        F.cnt[k] = (int*)dalloc(r, (size_t)N * 4);
-        F.touched[k] = (int*)dalloc(r, (size_t)4 * bs * 4);
-      }
-      F.meta = (int4*)dalloc(r, (size_t)N * sizeof(int4));
-      r->n_rows = N;
-      r->d = d;
-      if (!F.P[1] || (F.A[0] && !F.A[1]) || !F.sum[1] || !F.sum[2] || !F.cnt[1] || !F.cnt[2] ||
-          !F.touched[1] || !F.touched[2] || !F.meta) {
-        set_error("pipelined runner: device allocation failed");
-        pipe_free(r);
-        return nullptr;
-      }
-    }
+    ok = ok && q.P[1] && (!ada || q.A[1]) && q.acc[0] && q.acc[1] && q.acc[2];
   }
   r->rec = (int4*)dalloc(r, (size_t)T * sizeof(int4));
   r->rec_n1 = (int*)dalloc(r, (size_t)T * 4);
   r->err = (int*)dalloc(r, 4);
   r->stats = (int*)dalloc(r, (size_t)(nb1 + 3) * 3 * NSHARD * SHARD_STRIDE * 4);
   int* vsh = (int*)dalloc(r, (size_t)NSHARD * SHARD_STRIDE * 4);
-  if (!r->rec || !r->rec_n1 || !r->err || !r->stats || !vsh) {
+  if (!ok || !r->rec || !r->rec_n1 || !r->err || !r->stats || !vsh) {
     set_error("pipelined runner: device allocation failed");
     pipe_free(r);
     return nullptr;
@@ -3358,7 +2111,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   r->trip = trip;
   r->T = T;
   r->half = perm_half(T);
-  r->n_ent = ent->rows;
+  r->n_ent = N;
   r->ntries = ntries;
   r->seed = seed;
   r->epoch_key = epoch_key;
@@ -3379,19 +2132,8 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   a.trace = nullptr;
   a.err = r->err;
   a.E.err = r->err;
-  a.n_ent = ent->rows;
   a.af = af;
-  {
-    const char* af_env = getenv("SKGE_HPIPE_AFIRST");   // A/B switch: 0 = scoring WGs first
-    a.b_first = hole && af_env && atoi(af_env) == 0 ? 1 : 0;   // default: apply WGs first
-    const char* paf = getenv("SKGE_PIPE_AFIRST");   // the same switch for TransE (A/B)
-    if (!hole && paf && atoi(paf) == 0) a.b_first = 1;
-  }
   r->fft = hole && hole_use_fft(d);
-  {
-    const char* sp = getenv("SKGE_HPIPE_SPEC");   // A/B: spectral entity sums
-    r->spec = r->fft && sp && atoi(sp) != 0;
-  }
   {
     // two waves per positive (default while the batch's 2 x B scoring waves fit
     // the chip's 4-wave-per-SIMD residency; SKGE_HPIPE_PAIR=0/1 forces).  WN18
@@ -3401,15 +2143,10 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     int64_t maxb = 0;
     for (const auto& bt : batches) maxb = std::max(maxb, bt.second);
     const bool fits = 2 * maxb <= 4 * 4 * 256;
-    r->pair = r->fft && !r->spec && d == 200 && (pe ? atoi(pe) != 0 : fits);
+    r->pair = r->fft && d == 200 && (pe ? atoi(pe) != 0 : fits);
     // the relation row's loads and update on wave 1 (3 rows each; same box,
-    // two rounds: 103.8 -> 104.6 M triples/s); SKGE_HPIPE_PAIR_R1=0: wave 0
-    const char* pr = getenv("SKGE_HPIPE_PAIR_R1");
-    a.pair_r1 = pr && atoi(pr) == 0 ? 0 : 1;
-  }
-  {
-    const char* p2e = getenv("SKGE_PIPE_P2");   // A/B: two positives per scoring wave
-    r->p2 = !hole && p2e && atoi(p2e) != 0;   // (owner mode, split roles: not combined)
+    // two rounds: 103.8 -> 104.6 M triples/s)
+    a.pair_r1 = 1;
   }
   a.tw = r->fft ? hole_fft_table(d) : nullptr;
   if (r->fft && !a.tw) {
@@ -3421,44 +2158,36 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
            : r->pair ? hole_fft_lds_bytes(d, 1)
            : r->fft ? hole_fft_lds_bytes(d, SKGE_PIPE_WG / 64)
                     : (size_t)(SKGE_PIPE_WG / 64) * hole_pos_lds_floats(d) * sizeof(float);
-  // A-role entity groups (SKGE_PIPE_AGRP: slots per group of AGRP_WAVES waves, <= 64)
-  int agrp = SKGE_PIPE_AGRP_DEFAULT;
-  if (getenv("SKGE_PIPE_AGRP")) agrp = std::max(0, std::min(64, atoi(getenv("SKGE_PIPE_AGRP"))));
-  // one A-role wave per positive, four rows in parallel (SKGE_PIPE_A4, d <= 256)
-  int a4 = SKGE_PIPE_A4_DEFAULT;
-  if (getenv("SKGE_PIPE_A4")) a4 = atoi(getenv("SKGE_PIPE_A4")) != 0;
-  int prev = 0;
-  for (int b = 0; b <= nb1; ++b) {   // b == nb1: flush of the last batch (A role only)
+  const int WPB = r->pair ? 2 : SKGE_PIPE_WG / 64;
+  for (int b = 0; b <= nb1; ++b) {   // b == nb1: flush of the last batch (no scoring)
     a.b = b;
     a.start = b < nb1 ? batches[b].first : 0;
     a.count = b < nb1 ? (int)batches[b].second : 0;
-    a.count_next = b + 1 < nb1 ? (int)batches[b + 1].second : 0;
-    a.prev_slots = 4 * prev;
-    // A role: every relation row, then the previous batch's entity slots (lazy:
-    // no entity rows, except the flush's sweep over all rows in 64-row chunks)
-    const bool grouped = a.E.own[0] != nullptr;   // owner marks: 64-slot groups
-    a.E.agrp = (!hole && !lazy && !r->owner && !grouped) ? agrp : 0;
-    a.E.a4 = (!hole && !lazy && !r->owner && !grouped && nq <= 64 &&
-              (long long)ent->rows * d * 4 < (1ll << 31)) ? a4 : 0;   // (table-wide descriptors)
-    const int a_items =
-        rel->rows + (hole ? (4 * prev + HGROUP - 1) / HGROUP
-                          : lazy ? (b == nb1 ? (ent->rows + 63) / 64 : 0)
-                                 : r->owner ? 0
-                                            : grouped ? (4 * prev + 63) / 64
-                                                      : a.E.a4 ? prev
-                                                      : a.E.agrp ? AGRP_WAVES * ((4 * prev + a.E.agrp - 1) / a.E.agrp)
-                                                                 : (4 * prev + ASLOTS - 1) / ASLOTS);
-    const int WPB = r->pair ? 2 : SKGE_PIPE_WG / 64;
+    const int cprev = b >= 1 ? (int)batches[b - 1].second : 0;
+    a.prev_slots = 4 * cprev;
+    if (r->fused) {
+      // one kind of wave: relation rows, then max(this, the previous and the
+      // pre-previous batch's positives) work items.  The epoch starts clean (the
+      // flush zeroes both copies it leaves), so the first two launches have no
+      // pre-previous slots to zero
+      const int cpp = b >= 2 ? (int)batches[b - 2].second : 0;
+      a.pprev_slots = 4 * cpp;
+      a.nwork = std::max(a.count, std::max(cprev, cpp));
+      a.nA = 0;
+      r->batch.push_back(a);
+      r->grid.push_back(std::max(1, (rel->rows + a.nwork + WPB - 1) / WPB));
+      continue;
+    }
+    // A role: every relation row, then the previous batch's entity slots
+    // (owner marks: 64-slot groups)
+    const int a_items = rel->rows + (hole ? 4 * cprev : grouped ? (4 * cprev + 63) / 64 : 4 * cprev);
     // HolE: the apply waves loop over their items within the residency the
-    // scoring waves leave (SKGE_HPIPE_OCC waves per SIMD: 2 at ~180 VGPRs; the
-    // flush has the chip to itself)
+    // scoring waves leave (direct form: 2 waves per SIMD at ~180 VGPRs; FFT: 4
+    // -- caps 150 / 250 / 400 / 600 / 800 / 1100 on WN18 d = 200: 74.7 / 77.6 /
+    // 80.5 / 81.7 / 75.4 / 70.5 M triples/s; the flush has the chip to itself)
     // (pair: two waves per positive, one positive per workgroup)
     auto nBwaves = [&](long long cnt) { return r->pair ? 2 * cnt : (cnt + WPB - 1) / WPB * WPB; };
-    // FFT variant (133 VGPRs, 3 waves per SIMD): the cap of a 4-wave residency,
-    // measured best on WN18 d = 200 (caps 150 / 250 / 400 / 600 / 800 / 1100:
-    // 74.7 / 77.6 / 80.5 / 81.7 / 75.4 / 70.5 M triples/s)
-    const int occ = r->pair ? std::max(4, SKGE_HPIPE_OCC)   // (pair: 114 VGPRs)
-                  : r->fft ? (r->spec ? 3 : 4) : SKGE_HPIPE_OCC;   // (spec: 149 VGPRs)
+    const int occ = r->pair ? std::max(4, HPIPE_OCC) : r->fft ? 4 : HPIPE_OCC;
     int a_cap = hole && b < nb1 ? std::max(1, (occ * 4 * 256 - (int)nBwaves(batches[b].second)) / WPB - 8) : 16384;
     // (large batches: more scoring waves than the chip holds -- they run in
     // rounds anyway -- so the apply waves get a fixed share instead of the
@@ -3466,39 +2195,11 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     // waves for 283k slot records, 42 ms per epoch)
     if (hole && b < nb1 && (long long)nBwaves(batches[b].second) > occ * 4 * 256)
       a_cap = std::max(a_cap, 256);
-    if (hole && b < nb1 && getenv("SKGE_HPIPE_ACAP")) a_cap = std::max(1, atoi(getenv("SKGE_HPIPE_ACAP")));
-    // TransE, large batches: the A role's waves loop over their slots within ~768
-    // workgroups instead of one wave per slot (the scoring waves then find the
-    // chip's residency free; nb = 2 on WN18: 284 -> 304-310 M triples/s, same run);
-    // at the reference's batch size one wave per slot is faster (148 vs 142 M)
-    if (!hole && !lazy && !grouped && b < nb1 && a_items > 4 * 4096) a_cap = 768;
-    if (!hole && !lazy && b < nb1 && getenv("SKGE_PIPE_ACAP"))   // A/B switch (TransE)
-      a_cap = std::max(1, atoi(getenv("SKGE_PIPE_ACAP")));
     a.nA = std::max(1, std::min((a_items + WPB - 1) / WPB, std::min(a_cap, 16384)));
-    int b_cap = 16384;
-    if (!hole && getenv("SKGE_PIPE_BCAP")) b_cap = std::max(1, atoi(getenv("SKGE_PIPE_BCAP")));   // A/B
-    // (P2 at large batches: one scoring wave per two positives)
-    const bool p2_here = !hole && r->p2 && grouped && r->grp && !r->split && !r->owner && !lazy;
-    const int b_items = p2_here ? (a.count + 1) / 2 : a.count;
     const int nBb = r->pair ? std::max(1, std::min(a.count, 2 * 16384))
-                            : std::max(1, std::min((b_items + WPB - 1) / WPB, b_cap));
-    if (r->fused) {
-      // the epoch starts clean (the flush zeroes both copies it leaves), so a
-      // batch's first two launches have no pre-previous slots to zero
-      const int cprev = b >= 1 ? (int)batches[b - 1].second : 0;
-      const int cpp = b >= 2 ? (int)batches[b - 2].second : 0;
-      a.prev_slots = 4 * cprev;
-      a.pprev_slots = 4 * cpp;
-      a.nwork = std::max(a.count, std::max(cprev, cpp));
-      a.nA = 0;
-      r->batch.push_back(a);
-      r->grid.push_back(std::max(1, (rel->rows + a.nwork + WPB - 1) / WPB));
-      prev = a.count;
-      continue;
-    }
+                            : std::max(1, std::min((a.count + WPB - 1) / WPB, 16384));
     r->batch.push_back(a);
     r->grid.push_back(a.nA + (a.count > 0 ? nBb : 0));
-    prev = a.count;
   }
   hipStream_t st = as_stream(stream);
   if (hipStreamSynchronize(st) != hipSuccess ||
