@@ -180,15 +180,11 @@ __global__ __launch_bounds__(256) void k_transe_sample_grad(SampleArgs a) {
       c1[k] = -g1[k];
       cr[k] = fv0 * (gp[k] + g0[k]) + fv1 * (gp[k] + g1[k]);
     }
-#ifndef SKGE_ABL_NO_EATOM   // timing-only ablation builds (tools/ablate.sh)
     acc_row<KM>(a.accE, s, cs, d);
     acc_row<KM>(a.accE, o, co, d);
     if (v0) acc_row<KM>(a.accE, neg0, c0, d);
     if (v1) acc_row<KM>(a.accE, neg1, c1, d);
-#endif
-#ifndef SKGE_ABL_NO_RATOM
     acc_row<KM>(replica(a.accR, j), p, cr, d);
-#endif
   }
   count_violations(a, nv);
 }
@@ -208,11 +204,7 @@ __device__ __forceinline__ PosL1 transe_l1_front(const SampleArgs& a, const Perm
                                                  float4 (&g0)[KQ], float4 (&g1)[KQ]) {
   const int l = lane_id();
   const int d = a.d;
-#ifndef SKGE_ABL_NO_PERM
   const long long t = (long long)perm_index((uint64_t)j, pm);
-#else
-  const long long t = j;
-#endif
   // first tries of both modes do not depend on the positive: their rows load
   // in the same memory round trip as the triple
   const int cand0 = draw(skey, j, 0, 0, a.n_ent), cand1 = draw(skey, j, 1, 0, a.n_ent);
@@ -229,9 +221,7 @@ __device__ __forceinline__ PosL1 transe_l1_front(const SampleArgs& a, const Perm
   load_row4<KQ>(a.E, o, d, eo);
   load_row4<KQ>(a.R, p, d, rp);
   bool ok = true;
-#ifndef SKGE_ABL_NO_FILTER
   if (l < 2) ok = l == 0 ? !set_contains(a.set, cand0, o, p) : !set_contains(a.set, s, cand1, p);
-#endif
   const uint64_t okm = __ballot(ok);
   int neg0 = (okm & 1ull) ? cand0 : -1;
   int neg1 = (okm & 2ull) ? cand1 : -1;
@@ -310,13 +300,11 @@ __device__ __forceinline__ void transe_l1_commit(const SampleArgs& a, long long 
     SKGE_CO(w)
 #undef SKGE_CO
   }
-#ifndef SKGE_ABL_NO_ATOM   // timing-only ablation builds (tools/ablate.sh)
   acc_row4_i16<KQ>(a.accE, r.s, cs, d);
   acc_row4_i16<KQ>(a.accE, r.o, co, d);
   if (v0) acc_row4_i16<KQ>(a.accE, r.neg0, c0, d);
   if (v1) acc_row4_i16<KQ>(a.accE, r.neg1, c1, d);
   acc_row4_i16<KQ>(replica(a.accR, j), r.p, cr, d);
-#endif
 }
 
 // TransE-L1 variant with exact packed int16x4 accumulation (ACC_I16X4) and the

@@ -383,32 +383,22 @@ __device__ __forceinline__ bool hole_pair_fast(const PairArgs& a, int i, float* 
   const float gp = -af_g_given_f(a.af, pf);  // hole.py:66
   const float gn = af_g_given_f(a.af, nf);   // hole.py:67
   float x[KM], y[KM], t[KM];
-#ifndef SKGE_ABL_HOLE_NO_GCORR
   // relation rows (pp, pn): (gp ccorr(E[sp],E[op]), gn ccorr(E[sn],E[on]))  hole.py:76-82
   corr_fast<KM>(sEs, sEo, sout, d, t);
   scale<KM>(x, t, gp);
   corr_fast<KM>(sFs, sFo, sout, d, t);
   scale<KM>(y, t, gn);
-#endif
-#ifndef SKGE_ABL_HOLE_NO_RATOM   // timing-only ablation builds (tools/ablate.sh)
   acc_two<KM>(replica(a.accR, i), pp, x, pn, y, d);
-#endif
   // entity rows (sp, sn): gp ccorr(R[pp],E[op]), gn ccorr(R[pn],E[on])   hole.py:93-94
   scale<KM>(x, ap, gp);
   scale<KM>(y, an, gn);
-#ifndef SKGE_ABL_HOLE_NO_EATOM
   acc_two<KM>(a.accE, sp, x, sn, y, d);
-#endif
-#ifndef SKGE_ABL_HOLE_NO_GCORR
   // entity rows (op, on): gp cconv(E[sp],R[pp]), gn cconv(E[sn],R[pn])    hole.py:95-96
   corr_fast<KM>(rEs, sRp, sout, d, t);
   scale<KM>(x, t, gp);
   corr_fast<KM>(rFs, sRn, sout, d, t);
   scale<KM>(y, t, gn);
-#endif
-#ifndef SKGE_ABL_HOLE_NO_EATOM
   acc_two<KM>(a.accE, op, x, on, y, d);
-#endif
   __builtin_amdgcn_wave_barrier();
   return true;
 }
@@ -731,14 +721,10 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
       q_lds_dbl(L.Q2, fo[0], d);
       __builtin_amdgcn_wave_barrier();
       float4 AB[2];
-#ifndef SKGE_ABL_HPOS_NO_CORR   // timing-only ablation builds (tools/ablate.sh)
       {
         const float* const b2[2] = {L.O2, L.Q2};
         corr_quad_b<2>(L.R2, b2, d, AB);
       }
-#else
-      AB[0] = AB[1] = eo[0];
-#endif
       A = AB[0];
       B = AB[1];
       praw = hole_score_q(es[0], A);
@@ -767,13 +753,11 @@ __global__ __launch_bounds__(256) void k_hole_pos(HolePosArgs a) {
       if (v1) acc_fft_row<KM>(a.accE, neg1, z, 3 + v0, d);
     } else {
       const HoleRows h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gp, g0, g1);
-#ifndef SKGE_ABL_HPOS_NO_ATOM
       acc_q<KM>(aR, p, h.cr, d, L.U);
       acc_q<KM>(a.accE, s, h.cs, d, L.U);
       acc_q<KM>(a.accE, o, h.co, d, L.U);
       if (v0) acc_q<KM>(a.accE, neg0, h.c0, d, L.U);
       if (v1) acc_q<KM>(a.accE, neg1, h.cq, d, L.U);
-#endif
     }
     __builtin_amdgcn_wave_barrier();
   }

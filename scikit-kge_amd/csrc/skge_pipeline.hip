@@ -846,7 +846,9 @@ __device__ __forceinline__ void store_row4(float* T, int row, int d, const float
     if (64 * m + l < nq) base[64 * m + l] = v[m];
 }
 
-template <int KQ, bool W32, bool E8>
+// MF (meta first): the scoring rows are loaded in a third round trip, from the
+// buffer their meta word names, instead of from both buffers in the second
+template <int KQ, bool W32, bool E8, bool MF>
 __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
@@ -913,11 +915,13 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
     float4 x0[4][KQ], x1[4][KQ];
     int4 mt = make_int4(0, 0, 0, 0);
     if (sc) {
+      if (!MF) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int r = sel4(k, s, o, n0r, n1r);
-        load_row4<KQ>(a.F.P[0], r, d, x0[k]);
-        load_row4<KQ>(a.F.P[1], r, d, x1[k]);
+        for (int k = 0; k < 4; ++k) {
+          const int r = sel4(k, s, o, n0r, n1r);
+          load_row4<KQ>(a.F.P[0], r, d, x0[k]);
+          load_row4<KQ>(a.F.P[1], r, d, x1[k]);
+        }
       }
       if (l < 4) mt = a.F.meta[sel4(l, s, o, n0r, n1r)];
     }
@@ -953,10 +957,18 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
     const uint64_t pend = sc ? (__ballot(l < 4 && pw == gp) & 0xfull) : 0ull;
     const uint64_t inb1 = __ballot(l < 4 && bn == 1) & 0xfull;
     float4 e[4][KQ];
+    if (MF) {   // round trip 3: the rows from the buffers their meta words name
+      if (sc) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < 4; ++k)
+          load_row4<KQ>(a.F.P[(inb1 >> k) & 1ull], sel4(k, s, o, n0r, n1r), d, e[k]);
+      }
+    } else {
 #pragma unroll
-      for (int m = 0; m < KQ; ++m) e[k][m] = ((inb1 >> k) & 1ull) ? x1[k][m] : x0[k][m];
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int m = 0; m < KQ; ++m) e[k][m] = ((inb1 >> k) & 1ull) ? x1[k][m] : x0[k][m];
+    }
     // ---- round trip 3 (only rows batch b-1 touched): their state, sums, count ----
     float4 pa[4][KQ];
     unsigned long long psv[4][KQ];
@@ -1814,7 +1826,7 @@ struct skge_pipe_runner {
   bool rfold = false;              // TransE: relation sums in replicas, k_rel_fold after each batch
   size_t lds = 0;                  // HolE: dynamic LDS per workgroup
   bool pair = false;               // HolE FFT, d = 200: two waves per positive (SKGE_HPIPE_PAIR)
-  bool fused = false;              // TransE: k_pipe_fused (one kind of wave, no hand-offs)
+  int fused = 0;                   // TransE: k_pipe_fused (one kind of wave, no hand-offs; 2: MF)
   int n_rows = 0, d = 0;           // fused: the entity table's geometry (k_fused_fin)
   int nlaunch() const { return (int)batch.size() + 2; }
 };
@@ -1836,16 +1848,21 @@ static void pipe_free(skge_pipe_runner* r) {
   delete r;
 }
 
-template <int K>
-static void launch_fused(const skge_pipe_runner* r, dim3 gr, hipStream_t st, const PipeArgs& a) {
+template <int K, bool MF>
+static void launch_fused_mf(const skge_pipe_runner* r, dim3 gr, hipStream_t st, const PipeArgs& a) {
   const dim3 bl(SKGE_PIPE_WG);
   if (r->e8) {
-    if (r->w32) hipLaunchKernelGGL((k_pipe_fused<K, true, true>), gr, bl, 0, st, a);
-    else hipLaunchKernelGGL((k_pipe_fused<K, false, true>), gr, bl, 0, st, a);
+    if (r->w32) hipLaunchKernelGGL((k_pipe_fused<K, true, true, MF>), gr, bl, 0, st, a);
+    else hipLaunchKernelGGL((k_pipe_fused<K, false, true, MF>), gr, bl, 0, st, a);
   } else {
-    if (r->w32) hipLaunchKernelGGL((k_pipe_fused<K, true, false>), gr, bl, 0, st, a);
-    else hipLaunchKernelGGL((k_pipe_fused<K, false, false>), gr, bl, 0, st, a);
+    if (r->w32) hipLaunchKernelGGL((k_pipe_fused<K, true, false, MF>), gr, bl, 0, st, a);
+    else hipLaunchKernelGGL((k_pipe_fused<K, false, false, MF>), gr, bl, 0, st, a);
   }
+}
+template <int K>
+static void launch_fused(const skge_pipe_runner* r, dim3 gr, hipStream_t st, const PipeArgs& a) {
+  if (r->fused == 2) launch_fused_mf<K, true>(r, gr, st, a);
+  else launch_fused_mf<K, false>(r, gr, st, a);
 }
 
 // Enqueue one epoch: draw the negatives, nb1 batch launches, the flush, the
@@ -2000,11 +2017,13 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   // large batches (more than 16k slot records): owner marks, k_pipe_batch's A
   // role scans its slots 64 at a time
   const bool grouped = !hole && 4 * bs > 4 * 4096;
-  // TransE below that: k_pipe_fused (d <= 512; SKGE_PIPE_FUSED=0: k_pipe_batch)
+  // TransE below that: k_pipe_batch; SKGE_PIPE_FUSED=1 / 2: k_pipe_fused
+  // (d <= 512; 2: meta first) -- A/B
   {
     const char* fe = getenv("SKGE_PIPE_FUSED");
-    r->fused = !hole && !grouped && nq <= 128 && (long long)N < SLOT_BUF &&
-               !(fe && atoi(fe) == 0);
+    const int fv = fe ? atoi(fe) : 0;
+    r->fused = (!hole && !grouped && nq <= 128 && (long long)N < SLOT_BUF && fv >= 1 && fv <= 2)
+                   ? fv : 0;
   }
   PipeArgs a = {};
   auto upd = [](const skge_table_t* s) {

@@ -721,11 +721,6 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
   // values are staged (a select right after a load would wait for it)
   auto load_step = [&](int ks) {
     const int k = ks * KS;
-#ifdef SKGE_ABL_GEMM_NOLOAD   // timing-only ablation (tools/ablate.sh): no operand loads
-#pragma unroll
-    for (int e = 0; e < SPT; ++e) ra[e] = rb[e] = (float)(k + e);
-    return;
-#endif
     const float* brow;
     int boff;
     if (prod == 0) {
@@ -798,17 +793,6 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
     store_step(buf, ks);
     __syncthreads();   // (also: every wave is done with buf's previous use, step ks - 2)
     if (ks + 1 < nk) load_step(ks + 1);   // in flight during this step's MFMAs
-#ifdef SKGE_ABL_RS_NOPAD   // timing-only upper bound of a d-exact tiling: the edge
-                           // column block (its 48 padding columns at d = 200) skips
-                           // its contraction entirely
-    if (c0 + GC > d) {
-      acc[0][0] += sA[buf][row][kq];
-      continue;
-    }
-#endif
-#ifdef SKGE_ABL_GEMM_NOMFMA   // timing-only ablation: no contraction
-    acc[0][0] += sA[buf][row][kq] + sB[buf][kq * (GC + 4) + (l & 15)];
-#else
     // B[k4 + kq][16 q + c]: product 0 at sB[(16 q + c)(KS + 4) + k4 + kq]
     // (banks 36 c + kq: distinct), product 1 at sB[(k4 + kq)(GC + 4) + 16 q + c]
     if (prod == 0) {
@@ -832,7 +816,6 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
                                                         0, 0);
       }
     }
-#endif
   }
   // epilogue: D[row 4g + reg][col] of accumulator q -> triple 16w + 4g + reg, column c0 + 16q + c
   float* out = (prod == 0 ? ws.WE : ws.EW) + (size_t)ksl * ws.part_stride;
@@ -1233,9 +1216,6 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
       __syncthreads();   // (also: every wave is done with buf's use two chunks ago)
       const int mm = min(WG_CH, cnt - b * WG_CH);   // items past mm are zero (coef 0)
       // A[row i][k = item] = coef Es[item][i], B[k = item][col j] = Eo[item][j]
-#ifdef SKGE_ABL_WG_NOMFMA   // timing-only ablation (tools/ablate.sh): no contraction
-      if (mm < 0)
-#endif
       for (int k0 = 0; k0 < mm; k0 += 4) {
         const int ik = k0 + (l >> 4);
         const float av_ = sEs[buf][ik][16 * wave + (l & 15)];
@@ -1254,14 +1234,6 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
       if (in[e]) accW.sum[os[e]] = acc[e >> 2][e & 3];
     return;
   }
-#ifdef SKGE_ABL_WG_NOAPPLY   // timing-only ablation: dW written, W not updated
-  if (os[0] != (size_t)-1) {
-#pragma unroll
-    for (int e = 0; e < 16; ++e)
-      if (in[e]) accW.sum[os[e]] = acc[e >> 2][e & 3];
-    return;
-  }
-#endif
   // same step as k_apply_wide (skge/param.py:115-155); every load of the
   // tile issued before any of it is used
   const float div = wa.fdiv > 0.0f ? wa.fdiv : (float)cnt;
@@ -1420,9 +1392,6 @@ __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__
       }
       __syncthreads();
       const int mm = min(WG_CH, cnt - b * WG_CH);
-#ifdef SKGE_ABL_RS_NOPAD   // (as above: edge dW tiles skip their contraction)
-      if (r0 + WG_T > d || c0 + WG_T > d) continue;
-#endif
       for (int k0 = 0; k0 < mm; k0 += 4) {
         const int ik = k0 + (l >> 4);
         const float av_ = sEs[ik][16 * wave + (l & 15)];
@@ -1517,12 +1486,6 @@ __global__ __launch_bounds__(256) void k_rescal_front_fused(const float* __restr
     if (bid - k * order == 0 && k < nwg) wid = k;
     gid = bid - min((bid + order - 1) / order, nwg);
   }
-#ifdef SKGE_ABL_FRONT_NODW   // timing-only ablations (tools/ablate.sh): one role only
-  if (wid >= 0) return;
-#endif
-#ifdef SKGE_ABL_FRONT_NOGEMM
-  if (wid < 0) return;
-#endif
   if (wid >= 0) {
     rescal_wgrad_part_body<VEC, COMB, IF>(E, d, ws, ws.ecoef, splits, wid,
                                 reinterpret_cast<float(*)[WG_T + 4]>(lds),

@@ -19,7 +19,6 @@ SKGE_AF_LINEAR, SKGE_AF_SIGMOID, SKGE_AF_TANH, SKGE_AF_RELU = 0, 1, 2, 3
 SKGE_SGD, SKGE_ADAGRAD = 0, 1
 SKGE_POST_NONE, SKGE_POST_NORMALIZE, SKGE_POST_NORMLESS1 = 0, 1, 2
 SKGE_ACC_F32, SKGE_ACC_I16X4, SKGE_ACC_I32X2, SKGE_ACC_FX64, SKGE_ACC_I8X4 = 0, 1, 2, 3, 4
-SKGE_PIPE_LAZY = 1
 
 c_p = ctypes.c_void_p
 c_i = ctypes.c_int

@@ -40,9 +40,6 @@ class DeviceKG(object):
 
 PACKED_MAX = 32767   # a 16-bit packed field's bound (csrc/skge_pipeline.hip PACKED_MAX)
 import os as _os
-# the pipelined runner's entity apply: lazy (by the row's next reader, SKGE_PIPE_LAZY) or
-# by apply waves of the next launch
-LAZY_DEFAULT = _os.environ.get("SKGE_LAZY", "0") == "1"
 
 
 def _bincount_max(col, n):
@@ -153,8 +150,7 @@ class EpochRunner(object):
     counters = False
 
     def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, stream=None,
-                 nviol_total=None, force_f32=False, replicas=1, pipelined=None, packed=None,
-                 lazy=None):
+                 nviol_total=None, force_f32=False, replicas=1, pipelined=None, packed=None):
         from .transe import TransE
         if not isinstance(model, TransE):
             raise NotImplementedError("device_loop supports TransE (the north-star path) only")
@@ -198,16 +194,14 @@ class EpochRunner(object):
         if pipelined and not can_pipe:
             raise ValueError("pipelined runner needs TransE-L1, d % 4 == 0, packed sums "
                              "and replicas == 1")
-        want_lazy = LAZY_DEFAULT if lazy is None else bool(lazy)
         if can_pipe and pipelined is None:
-            # the pipelined runner's scratch: the epoch's records and per-row
-            # words, plus (not lazy) a second entity accumulator copy (auto
-            # mode: only if it fits)
+            # the pipelined runner's scratch: the epoch's records, two more
+            # entity accumulator copies, per-row words and (k_pipe_fused) a
+            # second copy of E and its AdaGrad state (auto mode: only if it fits)
             torch.cuda.synchronize(dev)
             torch.cuda.empty_cache()
             acc = E.rows * (E.width * 2 + 4) + 4 * 4 * bs   # the entity accumulator itself
-            extra = acc + kg.T * 20 + (64 << 20) + (E.rows * 8 if want_lazy else
-                                                    E.rows * E.width * 2 + E.rows * 12)
+            extra = 3 * acc + kg.T * 20 + (64 << 20) + E.rows * (16 + 8 * E.width)
             can_pipe = extra < torch.cuda.mem_get_info(dev)[0] * 0.9
         torch.cuda.current_stream().synchronize()
         lib = L.lib()
@@ -216,18 +210,16 @@ class EpochRunner(object):
             # fits them (faster: half the atomics), else int32x2; entity sums in
             # 8-bit fields while every entity's per-batch count is <= 127 (half
             # the atomic bytes again; the apply checks every count)
-            e8 = (not want_lazy and packed_count_bound(kg, model.E.rows, bs, _tail8) <= 127 and
+            e8 = (packed_count_bound(kg, model.E.rows, bs, _tail8) <= 127 and
                   _os.environ.get("SKGE_PIPE_E8", "1") != "0")
             self._tables(model, updaters, packed, 1, rel_w32=rel_reps != 1, ent_i8=e8,
                          pad=self._pad)
             self.ent_i8 = e8
-            self.lazy = want_lazy
-            h = lib.skge_pipe_runner_create_ex(
+            h = lib.skge_pipe_runner_create(
                 L.stream_ptr(self.stream), self.te, self.tr,
                 self.d_pad if self._pad else model.d, L.ptr(kg.trip), kg.T,
                 L.ptr(kg.slots), kg.capacity, int(nbatches), int(seed) & (2 ** 64 - 1),
-                L.ptr(self.epoch_key), float(model.margin), int(ntries), L.ptr(self.nviol_total),
-                L.SKGE_PIPE_LAZY if self.lazy else 0)
+                L.ptr(self.epoch_key), float(model.margin), int(ntries), L.ptr(self.nviol_total))
             if h:
                 self.pipelined = True
                 self.handle = h
@@ -240,7 +232,6 @@ class EpochRunner(object):
             self.accE = self.accR = self.te = self.tr = None
             torch.cuda.empty_cache()
         self.pipelined = False
-        self.lazy = False
         if self._pad:   # the two-launch runner takes any d: no padded copies
             self._pad = False
             packed = packed and model.d % 4 == 0
@@ -414,7 +405,6 @@ class HolePipeRunner(object):
         self.kg = kg
         self.model = model
         self.nbatches = nbatches
-        self.lazy = False
         self.epoch_key = torch.zeros(1, dtype=torch.int64, device=dev)
         self.nviol_total = nviol_total if nviol_total is not None else \
             torch.zeros(1, dtype=torch.int32, device=dev)

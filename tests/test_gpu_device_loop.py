@@ -190,7 +190,7 @@ def test_runner_wn18_full_size_properties(l1):
         assert float(acc.sum.abs().sum().item()) == 0.0
 
 
-def _runner_result(n_ent, n_rel, T, d, nb, pipelined, epochs=2, seed=11, trip=None, lazy=False):
+def _runner_result(n_ent, n_rel, T, d, nb, pipelined, epochs=2, seed=11, trip=None):
     import skge_amd as S
     from skge_amd.device import DeviceKG, EpochRunner
     np.random.seed(seed)
@@ -200,8 +200,8 @@ def _runner_result(n_ent, n_rel, T, d, nb, pipelined, epochs=2, seed=11, trip=No
     if trip is None:
         trip, _ = make_kg(n_ent, n_rel, T)
     kg = DeviceKG(trip, m.device)
-    r = EpochRunner(m, upd, kg, nbatches=nb, seed=seed, pipelined=pipelined, lazy=lazy)
-    assert r.pipelined == pipelined and r.lazy == (lazy and pipelined)
+    r = EpochRunner(m, upd, kg, nbatches=nb, seed=seed, pipelined=pipelined)
+    assert r.pipelined == pipelined
     r.run(epochs)
     r.synchronize()
     for acc in (r.accE, r.accR):
@@ -225,15 +225,15 @@ def _runner_result(n_ent, n_rel, T, d, nb, pipelined, epochs=2, seed=11, trip=No
     (40943, 18, 141442, 200, 2),  # WN18 at nb = 2: relation sums in 16 replicas (k_rel_fold)
 ])
 def test_pipelined_runner_bitwise_equals_two_launch(n_ent, n_rel, T, d, nb, monkeypatch):
-    """The pipelined runner (one launch per batch, cross-workgroup hand-off of
-    the previous batch's updates) must reproduce the two-launch loop exactly --
-    with apply waves, with the lazy apply by the rows' next readers, and with
-    every row updated by its batch's last reference (SKGE_PIPE_OWNER)."""
+    """The pipelined runner (one launch per batch: k_pipe_batch's
+    cross-workgroup hand-off, and -- SKGE_PIPE_FUSED=1 / 2, below 16k slot
+    records and d <= 512 -- k_pipe_fused, where a pending row is updated by
+    its readers themselves) must reproduce the two-launch loop exactly."""
     a, trip = _runner_result(n_ent, n_rel, T, d, nb, pipelined=False)
-    for mode in ("apply", "lazy", "owner"):
-        monkeypatch.setenv("SKGE_PIPE_OWNER", "1" if mode == "owner" else "0")
-        b, _ = _runner_result(n_ent, n_rel, T, d, nb, pipelined=True, trip=trip,
-                              lazy=mode == "lazy")
+    for mode in ("hand-off", "fused", "fused-meta-first"):
+        monkeypatch.setenv("SKGE_PIPE_FUSED", {"hand-off": "0", "fused": "1",
+                                               "fused-meta-first": "2"}[mode])
+        b, _ = _runner_result(n_ent, n_rel, T, d, nb, pipelined=True, trip=trip)
         assert a["key"] == b["key"] == 2
         assert a["nviol"] == b["nviol"] > 0, mode
         for k in ("E", "R", "pE", "pR"):

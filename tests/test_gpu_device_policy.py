@@ -68,12 +68,11 @@ def test_dominant_relation_large_batch_exact(pipelined):
     np.testing.assert_allclose(E1, E2, atol=1e-5, rtol=1e-5)
 
 
-@pytest.mark.parametrize("lazy", [False, True])
-def test_dominant_relation_pipelined_equals_two_launch_bitwise(lazy):
+def test_dominant_relation_pipelined_equals_two_launch_bitwise():
     trip = _dominant_kg(3000, 7, 24000, 0.7, seed=4)
-    a = _train(trip, 3000, 7, 200, 2, epochs=2, pipelined=True, lazy=lazy)
+    a = _train(trip, 3000, 7, 200, 2, epochs=2, pipelined=True)
     b = _train(trip, 3000, 7, 200, 2, epochs=2, pipelined=False)
-    assert a[3].packed and b[3].packed and b[3].accR.replicas >= 2 and a[3].lazy == lazy
+    assert a[3].packed and b[3].packed and b[3].accR.replicas >= 2
     assert a[2] == b[2] > 0
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 

@@ -31,7 +31,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--d", type=int, default=200)
     ap.add_argument("--nb", type=int, default=100)
-    ap.add_argument("--lazy", type=int, default=0)
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -45,7 +44,7 @@ def main():
     m.add_hyperparam("margin", 2.0)
     upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
     kg = DeviceKG(trip, dev)
-    r = EpochRunner(m, upd, kg, nbatches=args.nb, seed=5, lazy=bool(args.lazy))
+    r = EpochRunner(m, upd, kg, nbatches=args.nb, seed=5)
     r.run(args.warmup)
     r.synchronize()
     for rep in range(2):
@@ -64,39 +63,10 @@ def main():
                   (np.array([bin(int(x)).count("1") for x in pend]) == 1).sum(),
                   (np.array([bin(int(x)).count("1") for x in pend]) >= 2).sum(), len(A),
                   stats[args.launch].tolist()))
-        if os.environ.get("SKGE_PIPE_OWNER", "0") != "0":   # owner-apply runner
-            sole, shared, lastm, updm = B[:, 5] & 0xf, (B[:, 5] >> 4) & 0xf, (B[:, 5] >> 12) & 0xf, (B[:, 5] >> 16) & 0xf
-            print("owner: waves with shared rows %d, retiring a row last %d, sole updates %d" % (
-                (shared != 0).sum(), (lastm != 0).sum(),
-                sum(bin(int(x & y)).count("1") for x, y in zip(sole, updm))))
-            print("percentiles (us)           p0     p10    p50    p90    p100")
-            print("B start                  ", pct(B[:, 0] - t0))
-            print("B record+rows+score      ", pct(B[:, 1] - B[:, 0]))
-            print("B shared adds+retire     ", pct((B[:, 2] - B[:, 1])[shared != 0]))
-            print("B update+stores          ", pct(B[:, 3] - B[:, 2]))
-            print("B tail adds              ", pct(B[:, 4] - B[:, 3]))
-            print("B end                    ", pct(B[:, 4] - t0))
-            if len(A):
-                print("A start / end            ", pct(A[:, 0] - t0), "/", pct(A[:, 1] - t0))
-            print("last end %.2f us" % ((max(B[:, 4].max(), A[:, 1].max() if len(A) else 0) - t0) / 100))
-            continue
-        if args.lazy:
-            cnz, wt, clm = B[:, 5] & 0xf, (B[:, 5] >> 4) & 0xf, (B[:, 5] >> 12) & 0xf
-            print("lazy: waves applying a row %d (rows %d), waiting %d, claiming %d" % (
-                (cnz != 0).sum(), sum(bin(int(x)).count("1") for x in cnz), (wt != 0).sum(),
-                (clm != 0).sum()))
-            print("percentiles (us)           p0     p10    p50    p90    p100")
-            print("B start                  ", pct(B[:, 0] - t0))
-            print("B record+claim+rows      ", pct(B[:, 1] - B[:, 0]))
-            print("B apply+drain (applying) ", pct((B[:, 2] - B[:, 1])[cnz != 0]))
-            print("B wait+score (waiting)   ", pct((B[:, 3] - B[:, 2])[wt != 0]))
-            print("B score (not waiting)    ", pct((B[:, 3] - B[:, 2])[wt == 0]))
-            print("B atomics issue (viol)   ", pct((B[:, 4] - B[:, 3])[viol == 1]))
-            print("B issue end              ", pct(B[:, 4] - t0))
-            print("last end %.2f us" % ((B[:, 4].max() - t0) / 100))
-            continue
         print("percentiles (us)           p0     p10    p50    p90    p100")
         print("B start                  ", pct(B[:, 0] - t0))
+        # (k_pipe_fused: "rows+marks" = record, rows, meta, the item's apply rows and
+        # the relation row; "settle" = the item's applies + the pending rows' updates)
         print("B rows+marks (ballot)    ", pct(B[:, 1] - B[:, 0]))
         print("B settle (pending)       ", pct((B[:, 2] - B[:, 1])[pend != 0]))
         print("B settle (none pending)  ", pct((B[:, 2] - B[:, 1])[pend == 0]))
