@@ -846,10 +846,51 @@ __device__ __forceinline__ void store_row4(float* T, int row, int d, const float
     if (64 * m + l < nq) base[64 * m + l] = v[m];
 }
 
-// MF (meta first): the scoring rows are loaded in a third round trip, from the
-// buffer their meta word names, instead of from both buffers in the second
-template <int KQ, bool W32, bool E8, bool MF>
+// the apply of one slot record of launch g-1 (i < prev_slots) into the row's
+// other buffer, and the zeroing of the row of launch g-2's slot record i
+template <int KQ, bool E8>
+__device__ __forceinline__ void fused_apply_slot(const PipeArgs& a, int i, int g, int k1, int k2,
+                                                 bool flush, int& napp) {
+  const int l = lane_id(), d = a.d;
+  const bool ada = a.F.A[0] != nullptr;
+  int v = -1;
+  if (l == 0 && i < a.prev_slots) v = a.F.touched[k1][i];
+  if (l == 1 && i < a.pprev_slots) v = a.F.touched[k2][i];
+  const int va = __builtin_amdgcn_readlane(v, 0), vz = __builtin_amdgcn_readlane(v, 1);
+  if (vz >= 0) zero_sums_row<KQ, E8>(a.F.sum[k2], a.F.cnt[k2], vz & (SLOT_BUF - 1), d);
+  if (va < 0) return;
+  const int r = va & (SLOT_BUF - 1), b = va >> 30;
+  int won = 0, c = 0;
+  if (l == 0) {
+    won = atomicExch(&a.F.meta[r].w, g) != g;
+    c = a.F.cnt[k1][r];
+  }
+  float4 p[KQ], av[KQ];
+  unsigned long long sv[KQ];
+  load_pa<KQ>(a.F, b, r, d, p, av);
+  load_sums_raw<KQ, E8>(a.F.sum[k1], r, d, sv);
+  won = __builtin_amdgcn_readfirstlane(won);
+  c = __builtin_amdgcn_readfirstlane(c);
+  if (!won) return;
+  if (c > (E8 ? 127 : PACKED_MAX) && l == 0) atomicOr(a.err, ERR_PACKED);
+  float4 sm[KQ];
+  decode_sums<KQ, E8>(sv, d, sm);
+  row_update_s<KQ>(a.E.u, c, d, sm, p, av);
+  store_row4<KQ>(a.F.P[b ^ 1], r, d, p);
+  if (ada) store_row4<KQ>(a.F.A[b ^ 1], r, d, av);
+  if (l == 0) a.F.meta[r].z = (g << 1) | (b ^ 1);
+  if (flush) zero_sums_row<KQ, E8>(a.F.sum[k1], a.F.cnt[k1], r, d);
+  ++napp;
+}
+
+// MODE 1: every item scores, applies and zeroes (rows from both buffers);
+// MODE 2: the same, the scoring rows loaded in a third round trip from the
+// buffer their meta word names (meta first); MODE 3: the scoring items (rows
+// from both buffers) first, then one item per slot record that applies and
+// zeroes -- the scoring waves never wait, so they go first
+template <int KQ, bool W32, bool E8, int MODE>
 __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
+  constexpr bool MF = MODE == 2, SPLIT = MODE == 3;
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
   const int d = a.d, nq = d >> 2;
@@ -879,6 +920,10 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
       rel_publish<KQ, W32>(a, item, rd, rw, ra_prev, ra_old);
       continue;
     }
+    if (SPLIT && item >= nR + a.count) {
+      fused_apply_slot<KQ, E8>(a, item - nR - a.count, g, k1, k2, flush, napp);
+      continue;
+    }
     const int w = item - nR;
     const bool sc = w < a.count;
     unsigned long long tt[4] = {0ull, 0ull, 0ull, 0ull};
@@ -892,7 +937,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
       r1v = (int)__builtin_amdgcn_raw_buffer_load_b32(rec1_rs, w * 4, 0, 0);
     }
     int sl = -1;
-    {
+    if (!SPLIT) {
       const int i = 4 * w + (l & 3);
       const bool lo = l < 4;
       if (lo ? i < a.prev_slots : (l < 8 && i < a.pprev_slots))
@@ -1848,7 +1893,7 @@ static void pipe_free(skge_pipe_runner* r) {
   delete r;
 }
 
-template <int K, bool MF>
+template <int K, int MF>
 static void launch_fused_mf(const skge_pipe_runner* r, dim3 gr, hipStream_t st, const PipeArgs& a) {
   const dim3 bl(SKGE_PIPE_WG);
   if (r->e8) {
@@ -1861,8 +1906,9 @@ static void launch_fused_mf(const skge_pipe_runner* r, dim3 gr, hipStream_t st, 
 }
 template <int K>
 static void launch_fused(const skge_pipe_runner* r, dim3 gr, hipStream_t st, const PipeArgs& a) {
-  if (r->fused == 2) launch_fused_mf<K, true>(r, gr, st, a);
-  else launch_fused_mf<K, false>(r, gr, st, a);
+  if (r->fused == 2) launch_fused_mf<K, 2>(r, gr, st, a);
+  else if (r->fused == 3) launch_fused_mf<K, 3>(r, gr, st, a);
+  else launch_fused_mf<K, 1>(r, gr, st, a);
 }
 
 // Enqueue one epoch: draw the negatives, nb1 batch launches, the flush, the
@@ -2022,7 +2068,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   {
     const char* fe = getenv("SKGE_PIPE_FUSED");
     const int fv = fe ? atoi(fe) : 0;
-    r->fused = (!hole && !grouped && nq <= 128 && (long long)N < SLOT_BUF && fv >= 1 && fv <= 2)
+    r->fused = (!hole && !grouped && nq <= 128 && (long long)N < SLOT_BUF && fv >= 1 && fv <= 3)
                    ? fv : 0;
   }
   PipeArgs a = {};
@@ -2191,7 +2237,8 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
       // pre-previous slots to zero
       const int cpp = b >= 2 ? (int)batches[b - 2].second : 0;
       a.pprev_slots = 4 * cpp;
-      a.nwork = std::max(a.count, std::max(cprev, cpp));
+      a.nwork = r->fused == 3 ? a.count + 4 * std::max(cprev, cpp)   // scoring, then slot items
+                              : std::max(a.count, std::max(cprev, cpp));
       a.nA = 0;
       r->batch.push_back(a);
       r->grid.push_back(std::max(1, (rel->rows + a.nwork + WPB - 1) / WPB));

@@ -230,9 +230,9 @@ def test_pipelined_runner_bitwise_equals_two_launch(n_ent, n_rel, T, d, nb, monk
     records and d <= 512 -- k_pipe_fused, where a pending row is updated by
     its readers themselves) must reproduce the two-launch loop exactly."""
     a, trip = _runner_result(n_ent, n_rel, T, d, nb, pipelined=False)
-    for mode in ("hand-off", "fused", "fused-meta-first"):
+    for mode in ("hand-off", "fused", "fused-meta-first", "split"):
         monkeypatch.setenv("SKGE_PIPE_FUSED", {"hand-off": "0", "fused": "1",
-                                               "fused-meta-first": "2"}[mode])
+                                               "fused-meta-first": "2", "split": "3"}[mode])
         b, _ = _runner_result(n_ent, n_rel, T, d, nb, pipelined=True, trip=trip)
         assert a["key"] == b["key"] == 2
         assert a["nviol"] == b["nviol"] > 0, mode
