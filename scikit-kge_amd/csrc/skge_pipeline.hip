@@ -1711,7 +1711,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
     Accum aR = {};   // mode ACC_F32 (0), one copy
     aR.sum = racc + (size_t)p * rstride;
     aR.width = d;
-    if constexpr (FFT) {    } else if constexpr (FFT) {
+    if constexpr (FFT) {
       const float* z = hole_fft_rows(wb, tw, d, hs, v0, v1, gpf, g0, g1);
       if (a.trace) {   // diagnostics: the inverse transforms done (LDS results waited for)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
