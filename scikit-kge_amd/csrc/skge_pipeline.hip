@@ -846,48 +846,11 @@ __device__ __forceinline__ void store_row4(float* T, int row, int d, const float
     if (64 * m + l < nq) base[64 * m + l] = v[m];
 }
 
-// the apply of one slot record of launch g-1 (i < prev_slots) into the row's
-// other buffer, and the zeroing of the row of launch g-2's slot record i
-template <int KQ, bool E8>
-__device__ __forceinline__ void fused_apply_slot(const PipeArgs& a, int i, int g, int k1, int k2,
-                                                 bool flush, int& napp) {
-  const int l = lane_id(), d = a.d;
-  const bool ada = a.F.A[0] != nullptr;
-  int v = -1;
-  if (l == 0 && i < a.prev_slots) v = a.F.touched[k1][i];
-  if (l == 1 && i < a.pprev_slots) v = a.F.touched[k2][i];
-  const int va = __builtin_amdgcn_readlane(v, 0), vz = __builtin_amdgcn_readlane(v, 1);
-  if (vz >= 0) zero_sums_row<KQ, E8>(a.F.sum[k2], a.F.cnt[k2], vz & (SLOT_BUF - 1), d);
-  if (va < 0) return;
-  const int r = va & (SLOT_BUF - 1), b = va >> 30;
-  int won = 0, c = 0;
-  if (l == 0) {
-    won = atomicExch(&a.F.meta[r].w, g) != g;
-    c = a.F.cnt[k1][r];
-  }
-  float4 p[KQ], av[KQ];
-  unsigned long long sv[KQ];
-  load_pa<KQ>(a.F, b, r, d, p, av);
-  load_sums_raw<KQ, E8>(a.F.sum[k1], r, d, sv);
-  won = __builtin_amdgcn_readfirstlane(won);
-  c = __builtin_amdgcn_readfirstlane(c);
-  if (!won) return;
-  if (c > (E8 ? 127 : PACKED_MAX) && l == 0) atomicOr(a.err, ERR_PACKED);
-  float4 sm[KQ];
-  decode_sums<KQ, E8>(sv, d, sm);
-  row_update_s<KQ>(a.E.u, c, d, sm, p, av);
-  store_row4<KQ>(a.F.P[b ^ 1], r, d, p);
-  if (ada) store_row4<KQ>(a.F.A[b ^ 1], r, d, av);
-  if (l == 0) a.F.meta[r].z = (g << 1) | (b ^ 1);
-  if (flush) zero_sums_row<KQ, E8>(a.F.sum[k1], a.F.cnt[k1], r, d);
-  ++napp;
-}
-
 // MODE 1: every item scores, applies and zeroes (rows from both buffers);
 // MODE 2: the same, the scoring rows loaded in a third round trip from the
 // buffer their meta word names (meta first); MODE 3: the scoring items (rows
-// from both buffers) first, then one item per slot record that applies and
-// zeroes -- the scoring waves never wait, so they go first
+// from both buffers) first, then one item per four slot records that applies
+// and zeroes them -- the scoring waves never wait, so they go first
 template <int KQ, bool W32, bool E8, int MODE>
 __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
   constexpr bool MF = MODE == 2, SPLIT = MODE == 3;
@@ -920,12 +883,12 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
       rel_publish<KQ, W32>(a, item, rd, rw, ra_prev, ra_old);
       continue;
     }
-    if (SPLIT && item >= nR + a.count) {
-      fused_apply_slot<KQ, E8>(a, item - nR - a.count, g, k1, k2, flush, napp);
-      continue;
-    }
-    const int w = item - nR;
-    const bool sc = w < a.count;
+    // the item's positive (scoring) and slot group (4 slot records applied,
+    // 4 zeroed): both the same w in the one-role modes; SPLIT: the scoring
+    // items first, then the slot groups
+    const int w = SPLIT ? (item - nR < a.count ? item - nR : -1) : item - nR;
+    const int wa = SPLIT ? (item - nR < a.count ? -1 : item - nR - a.count) : item - nR;
+    const bool sc = w >= 0 && w < a.count;
     unsigned long long tt[4] = {0ull, 0ull, 0ull, 0ull};
     if (a.trace) tt[0] = now_10ns();
     // ---- round trip 1: the record; slot records 4w..4w+3 of launch g-1 (lanes
@@ -937,8 +900,8 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
       r1v = (int)__builtin_amdgcn_raw_buffer_load_b32(rec1_rs, w * 4, 0, 0);
     }
     int sl = -1;
-    if (!SPLIT) {
-      const int i = 4 * w + (l & 3);
+    if (wa >= 0) {
+      const int i = 4 * wa + (l & 3);
       const bool lo = l < 4;
       if (lo ? i < a.prev_slots : (l < 8 && i < a.pprev_slots))
         sl = (lo ? a.F.touched[k1] : a.F.touched[k2])[i];
@@ -1466,7 +1429,7 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
   fft_twiddles(tw, a.tw, d);
   float* const wb = smem + 2 * d;   // the pair's two transform buffers
   float2* const b0 = reinterpret_cast<float2*>(wb);
-  float2* const b1 = b0 + 5 * 100;
+  float2* const b1 = b0 + LayPair::BUF;   // (the pair form's LDS layout, skge_hole_fft.h)
   Accum aE = {};
   aE.sum = reinterpret_cast<float*>(a.E.sum[cp]);
   aE.width = d;
@@ -1507,18 +1470,18 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
     }
     if (a.trace) tt[2] = now_10ns();
     __syncthreads();   // the previous positive's buffers are free, the twiddles in place
-    if (hw == a.pair_r1) fft_put_row(b0, 100, 0, xr[0], d);
+    if (hw == a.pair_r1) fft_put_row<LayPair>(b0, 100, 0, xr[0], d);
     if (hw == 0) {
-      fft_put_row(b0, 100, 1, xa[0], d);
-      fft_put_row(b0, 100, 2, xb[0], d);
+      fft_put_row<LayPair>(b0, 100, 1, xa[0], d);
+      fft_put_row<LayPair>(b0, 100, 2, xb[0], d);
     } else {
-      fft_put_row(b0, 100, 3, xa[0], d);
-      fft_put_row(b0, 100, 4, xb[0], d);
+      fft_put_row<LayPair>(b0, 100, 3, xa[0], d);
+      fft_put_row<LayPair>(b0, 100, 4, xb[0], d);
     }
     __syncthreads();
-    const float2* Z = fft_run_c2<100, 5, false>(b0, b1, tw, hw);
+    const float2* Z = fft_run_c2<100, 5, false, LayPair>(b0, b1, tw, hw);
     float praw, raw0, raw1;
-    const HoleSpec hs = hole_fft_spectra(Z, tw, d, praw, raw0, raw1);
+    const HoleSpec hs = hole_fft_spectra<LayPair, 3>(Z, tw, d, praw, raw0, raw1);
     const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
     const int v0 = uni((neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0);   // hole.py:56
     const int v1 = uni((neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0);
@@ -1556,12 +1519,12 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
       Accum aR = {};
       aR.sum = racc + (size_t)p * rstride;
       aR.width = d;
-      acc_fft_row<KM>(aR, 0, z, 2, d);
-      acc_fft_row<KM>(aE, s, z, 0, d);
+      acc_fft_row<KM, LayPair>(aR, 0, z, 2, d);
+      acc_fft_row<KM, LayPair>(aE, s, z, 0, d);
     } else {
-      acc_fft_row<KM>(aE, o, z, 1, d);
-      if (v0) acc_fft_row<KM>(aE, neg0, z, 3, d);
-      if (v1) acc_fft_row<KM>(aE, neg1, z, 3 + v0, d);
+      acc_fft_row<KM, LayPair>(aE, o, z, 1, d);
+      if (v0) acc_fft_row<KM, LayPair>(aE, neg0, z, 3, d);
+      if (v1) acc_fft_row<KM, LayPair>(aE, neg1, z, 3 + v0, d);
     }
     __builtin_amdgcn_wave_barrier();
     stamp(pend | (1ull << 8) | ((unsigned long long)v0 << 9) | ((unsigned long long)v1 << 10) |
@@ -2220,7 +2183,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     return nullptr;
   }
   r->lds = !hole ? 0
-           : r->pair ? hole_fft_lds_bytes(d, 1)
+           : r->pair ? (size_t)(2 * d + 4 * LayPair::BUF) * sizeof(float)
            : r->fft ? hole_fft_lds_bytes(d, SKGE_PIPE_WG / 64)
                     : (size_t)(SKGE_PIPE_WG / 64) * hole_pos_lds_floats(d) * sizeof(float);
   const int WPB = r->pair ? 2 : SKGE_PIPE_WG / 64;
@@ -2237,7 +2200,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
       // pre-previous slots to zero
       const int cpp = b >= 2 ? (int)batches[b - 2].second : 0;
       a.pprev_slots = 4 * cpp;
-      a.nwork = r->fused == 3 ? a.count + 4 * std::max(cprev, cpp)   // scoring, then slot items
+      a.nwork = r->fused == 3 ? a.count + std::max(cprev, cpp)   // scoring, then slot groups
                               : std::max(a.count, std::max(cprev, cpp));
       a.nA = 0;
       r->batch.push_back(a);
