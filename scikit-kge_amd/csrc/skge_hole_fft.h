@@ -49,31 +49,6 @@ __host__ __device__ __forceinline__ size_t hole_fft_lds_bytes(int d, int waves) 
 // the runners call it at creation)
 const float2* hole_fft_table(int d);
 
-// LDS layouts of the transform buffers: LY::at<S, INV>(M, t, j) is the float2
-// index of element j of signal t at stage boundary S (0: a transform's input,
-// s + 1: stage s's output; INV: the inverse transform's buffers).
-struct LayN {   // natural: signals at stride M (every kernel but the pair form)
-  template <int S, bool INV>
-  __device__ __forceinline__ static int at(int M, int t, int j) { return t * M + j; }
-};
-// The pair form's layout (M = 100; radix 4, 5, 5; round 5): a butterfly pass
-// serves 32 lanes per LDS cycle (64 banks, 8 B per lane), and at stride M the
-// passes' 32-lane groups hit the same banks -- the radix-4 stage writes its 4
-// outputs at stride 4 (4-way), and two signals in one group overlap at stride
-// 100 (100 mod 32 = 4).  Strides 122 / 121 / 116 and an XOR of the low two
-// bits by the 32-element block in the radix-4 stage's output cut the modelled
-// LDS cycles of the transforms from 391 to 257 (ideal 204; tools/lds_banks.py).
-// The forward input keeps an even stride (rows enter as 16-B stores).
-struct LayPair {
-  static constexpr int BUF = 600;   // float2 per buffer (5 signals, the widest stride)
-  template <int S, bool INV>
-  __device__ __forceinline__ static int at(int, int t, int j) {
-    if (S == 0) return t * (INV ? 121 : 122) + j;
-    if (S == 1) return t * 116 + (j ^ ((j >> 5) & 3));
-    return t * 116 + j;
-  }
-};
-
 __device__ __forceinline__ float2 cmul(const float2& a, const float2& b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
@@ -258,7 +233,7 @@ __device__ __forceinline__ float2* fft_run_c(float2* x, float2* y, const float2*
 // buffers -- wave h takes the stage passes j = h, h + 2, ... of
 // fft_stage_c, so each butterfly is the same arithmetic on the same inputs
 // (the same bits as fft_run_c) and a stage boundary is a workgroup barrier.
-template <int R, bool INV, int M, int NT, int P, class LY, int SI>
+template <int R, bool INV, int M, int NT, int P>
 __device__ __forceinline__ void fft_stage_c2(const float2* x, float2* y, const float2* tw, int h) {
   constexpr int T = M / R, n = NT * T, stw = 2 * M / (P * R), NP = (n + 63) / 64;
   int l = lane_id();
@@ -269,9 +244,10 @@ __device__ __forceinline__ void fft_stage_c2(const float2* x, float2* y, const f
     if (b < n) {
       const int tr = b / T, i = b - tr * T;
       const int ip = i / P, k = i - ip * P;
+      const float2* xs = x + tr * M + i;
       float2 u[R], v[R];
 #pragma unroll
-      for (int q = 0; q < R; ++q) u[q] = x[LY::template at<SI, INV>(M, tr, i + q * T)];
+      for (int q = 0; q < R; ++q) u[q] = xs[q * T];
       if (P > 1) {
 #pragma unroll
         for (int q = 1; q < R; ++q) {
@@ -281,43 +257,39 @@ __device__ __forceinline__ void fft_stage_c2(const float2* x, float2* y, const f
         }
       }
       fft_dft<R, INV>(u, v);
+      float2* ys = y + tr * M + ip * P * R + k;
 #pragma unroll
-      for (int t = 0; t < R; ++t) y[LY::template at<SI + 1, INV>(M, tr, ip * P * R + k + t * P)] = v[t];
+      for (int t = 0; t < R; ++t) ys[t * P] = v[t];
     }
   }
 }
 
 // fft_run_c over the pair (entered after a barrier that published the
 // inputs; returns after the barrier that publishes the output)
-template <int M, int NT, bool INV, class LY = LayN, int P = 1, int MR = M, int SI = 0>
+template <int M, int NT, bool INV, int P = 1, int MR = M>
 __device__ __forceinline__ float2* fft_run_c2(float2* x, float2* y, const float2* tw, int h) {
   if constexpr (MR == 1) {
     return x;
   } else {
     constexpr int R = MR % 4 == 0 ? 4 : (MR % 2 == 0 ? 2 : (MR % 3 == 0 ? 3 : 5));
     static_assert(MR % R == 0, "the transform length must factor into 2, 3 and 5");
-    fft_stage_c2<R, INV, M, NT, P, LY, SI>(x, y, tw, h);
+    fft_stage_c2<R, INV, M, NT, P>(x, y, tw, h);
     __syncthreads();
-    return fft_run_c2<M, NT, INV, LY, P * R, MR / R, SI + 1>(y, x, tw, h);
+    return fft_run_c2<M, NT, INV, P * R, MR / R>(y, x, tw, h);
   }
 }
 
 // quad-layout real row -> complex signal t of buffer b (z[2l], z[2l+1])
-template <class LY = LayN>
 __device__ __forceinline__ void fft_put_row(float2* b, int M, int t, const float4& v, int d) {
   const int l = lane_id();
-  if (4 * l < d) *reinterpret_cast<float4*>(b + LY::template at<0, false>(M, t, 2 * l)) = v;
+  if (4 * l < d) *reinterpret_cast<float4*>(b + t * M + 2 * l) = v;
 }
 
 // the spectrum at k and M - k of real row t from its complex transform Z:
 // X_k = (Z_k + conj Z_{M-k}) / 2 - i W^k (Z_k - conj Z_{M-k}) / 2  (Z_M = Z_0)
-// (LY, S: element j of signal t at LY::at<S, false>(M, t, j); LayN with t = 0
-// is the row pointer form Z + t M of the one-wave kernels)
-template <class LY = LayN, int S = 0>
 __device__ __forceinline__ void fft_real_pair(const float2* Z, int M, int k, const float2* tw,
-                                              float2& xk, float2& xmk, int t = 0) {
-  const float2 a = Z[LY::template at<S, false>(M, t, k)];
-  const float2 b = Z[LY::template at<S, false>(M, t, k == 0 ? 0 : M - k)];
+                                              float2& xk, float2& xmk) {
+  const float2 a = Z[k], b = Z[k == 0 ? 0 : M - k];
   {
     const float2 e = cadd(a, cconj(b)), f = csub(a, cconj(b));
     const float2 wf = cmul(tw[k], f);
@@ -333,18 +305,17 @@ __device__ __forceinline__ void fft_real_pair(const float2* Z, int M, int k, con
 // inverse pre-processing of a Hermitian half-spectrum (H at k and M - k):
 // Z'_k = ((H_k + conj H_{M-k}) + i conj(W^k) (H_k - conj H_{M-k})) / 2, written
 // at k (< M) and at M - k (when 0 < k and M - k != k)
-template <class LY = LayN>
 __device__ __forceinline__ void fft_real_inv_pair(float2* Z, int M, int k, const float2* tw,
-                                                  const float2& hk, const float2& hmk, int t = 0) {
+                                                  const float2& hk, const float2& hmk) {
   {
     const float2 e = cadd(hk, cconj(hmk)), f = csub(hk, cconj(hmk));
     const float2 wf = cmulc(tw[k], f);   // conj(W^k) f
-    Z[LY::template at<0, true>(M, t, k)] = make_float2(0.5f * (e.x - wf.y), 0.5f * (e.y + wf.x));
+    Z[k] = make_float2(0.5f * (e.x - wf.y), 0.5f * (e.y + wf.x));
   }
   if (k > 0 && M - k != k) {
     const float2 e = cadd(hmk, cconj(hk)), f = csub(hmk, cconj(hk));
     const float2 wf = cmulc(tw[M - k], f);
-    Z[LY::template at<0, true>(M, t, M - k)] = make_float2(0.5f * (e.x - wf.y), 0.5f * (e.y + wf.x));
+    Z[M - k] = make_float2(0.5f * (e.x - wf.y), 0.5f * (e.y + wf.x));
   }
 }
 
@@ -373,7 +344,6 @@ struct HoleSpec {
 // the spectra at (k, M - k) of the five transformed rows in Z and the three
 // raw scores (hole_fft_forward's second half; the pair form calls it in both
 // waves, which then hold the same values)
-template <class LY = LayN, int S = 0>
 __device__ __forceinline__ HoleSpec hole_fft_spectra(const float2* Z, const float2* tw, int d,
                                                      float& praw, float& raw0, float& raw1) {
   const int M = d / 2;
@@ -383,11 +353,11 @@ __device__ __forceinline__ HoleSpec hole_fft_spectra(const float2* Z, const floa
   float ps = 0.0f, p0 = 0.0f, p1 = 0.0f;
   if (h.on) {
     const int k = h.k;
-    fft_real_pair<LY, S>(Z, M, k, tw, h.r[0], h.r[1], 0);
-    fft_real_pair<LY, S>(Z, M, k, tw, h.es[0], h.es[1], 1);
-    fft_real_pair<LY, S>(Z, M, k, tw, h.fs[0], h.fs[1], 2);
-    fft_real_pair<LY, S>(Z, M, k, tw, h.eo[0], h.eo[1], 3);
-    fft_real_pair<LY, S>(Z, M, k, tw, h.fo[0], h.fo[1], 4);
+    fft_real_pair(Z + 0 * M, M, k, tw, h.r[0], h.r[1]);
+    fft_real_pair(Z + 1 * M, M, k, tw, h.es[0], h.es[1]);
+    fft_real_pair(Z + 2 * M, M, k, tw, h.fs[0], h.fs[1]);
+    fft_real_pair(Z + 3 * M, M, k, tw, h.eo[0], h.eo[1]);
+    fft_real_pair(Z + 4 * M, M, k, tw, h.fo[0], h.fo[1]);
     // weights: k and M - k each count twice unless 0 or M; the middle pair once
     const float wk = k == 0 ? 1.0f : 2.0f, wm = k == 0 ? 1.0f : (M - k == k ? 0.0f : 2.0f);
     ps = wk * fft_score_term(h.es[0], h.r[0], h.eo[0]) + wm * fft_score_term(h.es[1], h.r[1], h.eo[1]);
@@ -427,7 +397,6 @@ __device__ __forceinline__ HoleSpec hole_fft_forward(float* wbuf, const float2* 
 // the inverse transforms' inputs (pre-processed half spectra) of the
 // contribution rows t in [lo, hi): 0 E[s], 1 E[o], 2 R[p], then E[s'] (v0),
 // E[o'] (v1)
-template <class LY = LayN>
 __device__ __forceinline__ void hole_inv_inputs(float2* b0, int M, const float2* tw,
                                                 const HoleSpec& h, int v0, int v1, float gp,
                                                 float g0, float g1, int lo, int hi) {
@@ -446,15 +415,15 @@ __device__ __forceinline__ void hole_inv_inputs(float2* b0, int M, const float2*
     H[4][j] = cscale(g1, cmul(r, es));                                // E[o'] (v1)
   }
   const int k = h.k;
-  if (lo <= 0 && 0 < hi) fft_real_inv_pair<LY>(b0, M, k, tw, H[0][0], H[0][1], 0);
-  if (lo <= 1 && 1 < hi) fft_real_inv_pair<LY>(b0, M, k, tw, H[1][0], H[1][1], 1);
-  if (lo <= 2 && 2 < hi) fft_real_inv_pair<LY>(b0, M, k, tw, H[2][0], H[2][1], 2);
+  if (lo <= 0 && 0 < hi) fft_real_inv_pair(b0 + 0 * M, M, k, tw, H[0][0], H[0][1]);
+  if (lo <= 1 && 1 < hi) fft_real_inv_pair(b0 + 1 * M, M, k, tw, H[1][0], H[1][1]);
+  if (lo <= 2 && 2 < hi) fft_real_inv_pair(b0 + 2 * M, M, k, tw, H[2][0], H[2][1]);
   int t = 3;
   if (v0) {
-    if (lo <= t && t < hi) fft_real_inv_pair<LY>(b0, M, k, tw, H[3][0], H[3][1], t);
+    if (lo <= t && t < hi) fft_real_inv_pair(b0 + t * M, M, k, tw, H[3][0], H[3][1]);
     ++t;
   }
-  if (v1 && lo <= t && t < hi) fft_real_inv_pair<LY>(b0, M, k, tw, H[4][0], H[4][1], t);
+  if (v1 && lo <= t && t < hi) fft_real_inv_pair(b0 + t * M, M, k, tw, H[4][0], H[4][1]);
 }
 
 __device__ __forceinline__ const float* hole_fft_rows(float* wbuf, const float2* tw, int d,
@@ -476,29 +445,27 @@ __device__ __forceinline__ const float* hole_fft_rows(float* wbuf, const float2*
   return reinterpret_cast<const float*>(z);
 }
 
-// Pair form of hole_fft_rows (M = 100, LayPair buffers): both waves hold the
-// spectra h; wave hw writes its share of the inverse inputs (0: rows 0-2, 1:
-// the negatives' rows), then the pair runs the transforms.  Same bits as
-// hole_fft_rows (the same butterflies; only the LDS addresses differ).  The
-// output (boundary 3) is read with acc_fft_row<KM, LayPair>.
+// Pair form of hole_fft_rows (M = 100): both waves hold the spectra h; wave hw
+// writes its share of the inverse inputs (0: rows 0-2, 1: the negatives'
+// rows), then the pair runs the transforms.  Same bits as hole_fft_rows.
 __device__ __forceinline__ const float* hole_fft_rows_pair(float* wbuf, const float2* tw,
                                                            const HoleSpec& h, int v0, int v1,
                                                            float gp, float g0, float g1, int hw) {
   constexpr int M = 100;
   float2* b0 = reinterpret_cast<float2*>(wbuf);
-  float2* b1 = b0 + LayPair::BUF;
+  float2* b1 = b0 + 5 * M;
   __syncthreads();   // both waves are done reading the forward buffers
-  hole_inv_inputs<LayPair>(b0, M, tw, h, v0, v1, gp, g0, g1, hw ? 3 : 0, hw ? 5 : 3);
+  hole_inv_inputs(b0, M, tw, h, v0, v1, gp, g0, g1, hw ? 3 : 0, hw ? 5 : 3);
   __syncthreads();
-  float2* z = v0 + v1 == 2 ? fft_run_c2<M, 5, true, LayPair>(b0, b1, tw, hw)
-                           : fft_run_c2<M, 4, true, LayPair>(b0, b1, tw, hw);
+  float2* z = v0 + v1 == 2 ? fft_run_c2<M, 5, true>(b0, b1, tw, hw)
+                           : fft_run_c2<M, 4, true>(b0, b1, tw, hw);
   return reinterpret_cast<const float*>(z);
 }
 
 // row t of hole_fft_rows' output, scaled by 1/M, added into accumulator row
 // `row`: lane l takes elements l + 64 k, so each float-atomic instruction
 // covers contiguous bytes (MI355X_MICROARCH.md "Global float atomics")
-template <int KM, class LY = LayN>
+template <int KM>
 __device__ __forceinline__ void acc_fft_row(const Accum& acc, int row, const float* z, int t,
                                             int d) {
   const float s = 2.0f / (float)d;   // 1/M
@@ -506,8 +473,8 @@ __device__ __forceinline__ void acc_fft_row(const Accum& acc, int row, const flo
   const int l = lane_id();
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
-    const int e = l + 64 * k;   // float e of row t: element e / 2 of the complex signal
-    x[k] = e < d ? s * z[2 * LY::template at<3, true>(d / 2, t, e >> 1) + (e & 1)] : 0.0f;
+    const int e = l + 64 * k;
+    x[k] = e < d ? s * z[t * d + e] : 0.0f;
   }
   acc_row<KM>(acc, row, x, d);
 }

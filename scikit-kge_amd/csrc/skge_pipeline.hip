@@ -751,34 +751,37 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
   }
 }
 
-// ---- fused runner (round 5): one kind of wave, no hand-offs ----
+// ---- fused runner (round 5): nothing waits ----
 //
-// k_pipe_batch gives each launch two roles: apply waves for batch b-1's rows
-// (dispatched first) and scoring waves that WAIT for any row batch b-1
-// touched (claim / done word / write-through re-read).  Its per-wave traces
-// put the scoring waves' start at ~3.2 us (p50) behind ~1.4k apply
-// workgroups, with ~30% of them settling a pending row.  k_pipe_fused has one
-// kind of wave and nothing waits:
+// k_pipe_batch gives each launch apply waves for batch b-1's rows (dispatched
+// first) and scoring waves that WAIT for any row batch b-1 touched (claim /
+// done word / write-through re-read); its per-wave traces put the scoring
+// waves' start at ~3.2 us (p50) behind ~1.4k apply workgroups, with ~30% of
+// them settling a pending row.  In k_pipe_fused no wave waits:
 //
-//   * work item w scores positive w of batch b, applies launch g-1's slot
-//     records 4w..4w+3 (claimed through the row's meta word) and zeroes the
-//     rows of launch g-2's slot records 4w..4w+3 (the accumulator copy launch
-//     g+1 adds into) -- one workgroup per four positives instead of one per
-//     positive plus one per slot record;
 //   * a scoring wave that reads a row batch b-1 touched computes that row's
 //     update itself from its pre-update value, state, sums and count
-//     (row_update_s, the applier's arithmetic: the same bits) instead of
-//     waiting for its publication.  The pre-update value stays readable all
-//     launch because the applier writes the row's OTHER buffer (FusedTab);
-//   * the buffer holding a row is its meta word z (launch id and buffer of the
-//     last write), loaded with its pending mark in the round trip that loads
-//     the row -- from both buffers, two 16-B loads per lane instead of a
-//     dependent third round trip.
+//     (row_update_s, the applier's arithmetic: the same bits) -- the
+//     pre-update value stays readable all launch because the applier writes
+//     the row's OTHER buffer (FusedTab); the buffer holding a row is its meta
+//     word z (launch id and buffer of the last write), loaded with its pending
+//     mark in the round trip that loads the row from both buffers;
+//   * so the scoring items go first (one per positive), then one item per
+//     four slot records of launch g-1 (claimed through the row's meta word,
+//     applied into the other buffer) that also zeroes the rows of launch g-2's
+//     four slot records (the accumulator copy launch g+1 adds into).
 //
 // Relation rows as in k_pipe_batch (double-buffered and recomputed by every
 // scoring wave; items 0..nR-1 publish them for the next launch).  After a
 // runner's epochs k_fused_fin copies rows living in buffer 1 back into the
 // caller's tables and clears the meta words.
+//
+// Measured (WN18, same box): d = 50 on its 64-wide padded tables 10.52 ->
+// 10.08 us per launch; d = 200 9.78 vs 8.48 us for k_pipe_batch, which stays
+// the default there -- at 800-B rows the second buffer's loads and the
+// rotating copies cost more than the waits save (the one-role form, every item
+// scoring, applying and zeroing, measured 11.45 us; loading the rows after
+// their meta words instead of from both buffers, 10.61 us).
 
 template <int KQ, bool E8>
 __device__ __forceinline__ void load_sums_raw(const void* S, int row, int d,
@@ -846,14 +849,8 @@ __device__ __forceinline__ void store_row4(float* T, int row, int d, const float
     if (64 * m + l < nq) base[64 * m + l] = v[m];
 }
 
-// MODE 1: every item scores, applies and zeroes (rows from both buffers);
-// MODE 2: the same, the scoring rows loaded in a third round trip from the
-// buffer their meta word names (meta first); MODE 3: the scoring items (rows
-// from both buffers) first, then one item per four slot records that applies
-// and zeroes them -- the scoring waves never wait, so they go first
-template <int KQ, bool W32, bool E8, int MODE>
+template <int KQ, bool W32, bool E8>
 __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
-  constexpr bool MF = MODE == 2, SPLIT = MODE == 3;
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
   const int d = a.d, nq = d >> 2;
@@ -883,11 +880,11 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
       rel_publish<KQ, W32>(a, item, rd, rw, ra_prev, ra_old);
       continue;
     }
-    // the item's positive (scoring) and slot group (4 slot records applied,
-    // 4 zeroed): both the same w in the one-role modes; SPLIT: the scoring
-    // items first, then the slot groups
-    const int w = SPLIT ? (item - nR < a.count ? item - nR : -1) : item - nR;
-    const int wa = SPLIT ? (item - nR < a.count ? -1 : item - nR - a.count) : item - nR;
+    // the item's positive (the scoring items first: nothing waits for the
+    // others, so they need not start early) or slot group (four slot records
+    // applied, four zeroed)
+    const int w = item - nR < a.count ? item - nR : -1;
+    const int wa = item - nR < a.count ? -1 : item - nR - a.count;
     const bool sc = w >= 0 && w < a.count;
     unsigned long long tt[4] = {0ull, 0ull, 0ull, 0ull};
     if (a.trace) tt[0] = now_10ns();
@@ -923,13 +920,11 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
     float4 x0[4][KQ], x1[4][KQ];
     int4 mt = make_int4(0, 0, 0, 0);
     if (sc) {
-      if (!MF) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int r = sel4(k, s, o, n0r, n1r);
-          load_row4<KQ>(a.F.P[0], r, d, x0[k]);
-          load_row4<KQ>(a.F.P[1], r, d, x1[k]);
-        }
+      for (int k = 0; k < 4; ++k) {
+        const int r = sel4(k, s, o, n0r, n1r);
+        load_row4<KQ>(a.F.P[0], r, d, x0[k]);
+        load_row4<KQ>(a.F.P[1], r, d, x1[k]);
       }
       if (l < 4) mt = a.F.meta[sel4(l, s, o, n0r, n1r)];
     }
@@ -965,18 +960,10 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_fused(PipeArgs a) {
     const uint64_t pend = sc ? (__ballot(l < 4 && pw == gp) & 0xfull) : 0ull;
     const uint64_t inb1 = __ballot(l < 4 && bn == 1) & 0xfull;
     float4 e[4][KQ];
-    if (MF) {   // round trip 3: the rows from the buffers their meta words name
-      if (sc) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          load_row4<KQ>(a.F.P[(inb1 >> k) & 1ull], sel4(k, s, o, n0r, n1r), d, e[k]);
-      }
-    } else {
+    for (int k = 0; k < 4; ++k)
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int m = 0; m < KQ; ++m) e[k][m] = ((inb1 >> k) & 1ull) ? x1[k][m] : x0[k][m];
-    }
+      for (int m = 0; m < KQ; ++m) e[k][m] = ((inb1 >> k) & 1ull) ? x1[k][m] : x0[k][m];
     // ---- round trip 3 (only rows batch b-1 touched): their state, sums, count ----
     float4 pa[4][KQ];
     unsigned long long psv[4][KQ];
@@ -1429,7 +1416,7 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
   fft_twiddles(tw, a.tw, d);
   float* const wb = smem + 2 * d;   // the pair's two transform buffers
   float2* const b0 = reinterpret_cast<float2*>(wb);
-  float2* const b1 = b0 + LayPair::BUF;   // (the pair form's LDS layout, skge_hole_fft.h)
+  float2* const b1 = b0 + 5 * 100;
   Accum aE = {};
   aE.sum = reinterpret_cast<float*>(a.E.sum[cp]);
   aE.width = d;
@@ -1470,18 +1457,18 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
     }
     if (a.trace) tt[2] = now_10ns();
     __syncthreads();   // the previous positive's buffers are free, the twiddles in place
-    if (hw == a.pair_r1) fft_put_row<LayPair>(b0, 100, 0, xr[0], d);
+    if (hw == a.pair_r1) fft_put_row(b0, 100, 0, xr[0], d);
     if (hw == 0) {
-      fft_put_row<LayPair>(b0, 100, 1, xa[0], d);
-      fft_put_row<LayPair>(b0, 100, 2, xb[0], d);
+      fft_put_row(b0, 100, 1, xa[0], d);
+      fft_put_row(b0, 100, 2, xb[0], d);
     } else {
-      fft_put_row<LayPair>(b0, 100, 3, xa[0], d);
-      fft_put_row<LayPair>(b0, 100, 4, xb[0], d);
+      fft_put_row(b0, 100, 3, xa[0], d);
+      fft_put_row(b0, 100, 4, xb[0], d);
     }
     __syncthreads();
-    const float2* Z = fft_run_c2<100, 5, false, LayPair>(b0, b1, tw, hw);
+    const float2* Z = fft_run_c2<100, 5, false>(b0, b1, tw, hw);
     float praw, raw0, raw1;
-    const HoleSpec hs = hole_fft_spectra<LayPair, 3>(Z, tw, d, praw, raw0, raw1);
+    const HoleSpec hs = hole_fft_spectra(Z, tw, d, praw, raw0, raw1);
     const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
     const int v0 = uni((neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0);   // hole.py:56
     const int v1 = uni((neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0);
@@ -1519,12 +1506,12 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
       Accum aR = {};
       aR.sum = racc + (size_t)p * rstride;
       aR.width = d;
-      acc_fft_row<KM, LayPair>(aR, 0, z, 2, d);
-      acc_fft_row<KM, LayPair>(aE, s, z, 0, d);
+      acc_fft_row<KM>(aR, 0, z, 2, d);
+      acc_fft_row<KM>(aE, s, z, 0, d);
     } else {
-      acc_fft_row<KM, LayPair>(aE, o, z, 1, d);
-      if (v0) acc_fft_row<KM, LayPair>(aE, neg0, z, 3, d);
-      if (v1) acc_fft_row<KM, LayPair>(aE, neg1, z, 3 + v0, d);
+      acc_fft_row<KM>(aE, o, z, 1, d);
+      if (v0) acc_fft_row<KM>(aE, neg0, z, 3, d);
+      if (v1) acc_fft_row<KM>(aE, neg1, z, 3 + v0, d);
     }
     __builtin_amdgcn_wave_barrier();
     stamp(pend | (1ull << 8) | ((unsigned long long)v0 << 9) | ((unsigned long long)v1 << 10) |
@@ -1834,7 +1821,7 @@ struct skge_pipe_runner {
   bool rfold = false;              // TransE: relation sums in replicas, k_rel_fold after each batch
   size_t lds = 0;                  // HolE: dynamic LDS per workgroup
   bool pair = false;               // HolE FFT, d = 200: two waves per positive (SKGE_HPIPE_PAIR)
-  int fused = 0;                   // TransE: k_pipe_fused (one kind of wave, no hand-offs; 2: MF)
+  bool fused = false;              // TransE: k_pipe_fused (nothing waits; d <= 64 by default)
   int n_rows = 0, d = 0;           // fused: the entity table's geometry (k_fused_fin)
   int nlaunch() const { return (int)batch.size() + 2; }
 };
@@ -1856,22 +1843,15 @@ static void pipe_free(skge_pipe_runner* r) {
   delete r;
 }
 
-template <int K, int MF>
-static void launch_fused_mf(const skge_pipe_runner* r, dim3 gr, hipStream_t st, const PipeArgs& a) {
+static void launch_fused(const skge_pipe_runner* r, dim3 gr, hipStream_t st, const PipeArgs& a) {
   const dim3 bl(SKGE_PIPE_WG);
   if (r->e8) {
-    if (r->w32) hipLaunchKernelGGL((k_pipe_fused<K, true, true, MF>), gr, bl, 0, st, a);
-    else hipLaunchKernelGGL((k_pipe_fused<K, false, true, MF>), gr, bl, 0, st, a);
+    if (r->w32) hipLaunchKernelGGL((k_pipe_fused<1, true, true>), gr, bl, 0, st, a);
+    else hipLaunchKernelGGL((k_pipe_fused<1, false, true>), gr, bl, 0, st, a);
   } else {
-    if (r->w32) hipLaunchKernelGGL((k_pipe_fused<K, true, false, MF>), gr, bl, 0, st, a);
-    else hipLaunchKernelGGL((k_pipe_fused<K, false, false, MF>), gr, bl, 0, st, a);
+    if (r->w32) hipLaunchKernelGGL((k_pipe_fused<1, true, false>), gr, bl, 0, st, a);
+    else hipLaunchKernelGGL((k_pipe_fused<1, false, false>), gr, bl, 0, st, a);
   }
-}
-template <int K>
-static void launch_fused(const skge_pipe_runner* r, dim3 gr, hipStream_t st, const PipeArgs& a) {
-  if (r->fused == 2) launch_fused_mf<K, 2>(r, gr, st, a);
-  else if (r->fused == 3) launch_fused_mf<K, 3>(r, gr, st, a);
-  else launch_fused_mf<K, 1>(r, gr, st, a);
 }
 
 // Enqueue one epoch: draw the negatives, nb1 batch launches, the flush, the
@@ -1935,8 +1915,7 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
 #undef SKGE_HPIPE
       }
     } else if (r->fused) {
-      if (r->kq <= 1) launch_fused<1>(r, dim3(r->grid[k]), st, a);
-      else launch_fused<2>(r, dim3(r->grid[k]), st, a);
+      launch_fused(r, dim3(r->grid[k]), st, a);
     } else if (r->kq <= 1) SKGE_PB(1);
     else if (r->kq <= 2) SKGE_PB(2);
     else SKGE_PB(4);
@@ -2026,13 +2005,15 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   // large batches (more than 16k slot records): owner marks, k_pipe_batch's A
   // role scans its slots 64 at a time
   const bool grouped = !hole && 4 * bs > 4 * 4096;
-  // TransE below that: k_pipe_batch; SKGE_PIPE_FUSED=1 / 2: k_pipe_fused
-  // (d <= 512; 2: meta first) -- A/B
+  // TransE below that: k_pipe_fused for rows of up to 64 floats (WN18 d = 50
+  // on its 64-wide padded tables: 10.52 -> 10.08 us per launch, same box),
+  // k_pipe_batch above (d = 200: 8.48 vs 9.78 us -- at 800-B rows the fused
+  // kernel's second-buffer loads and rotating copies cost more than its
+  // waits save).  SKGE_PIPE_FUSED=0 / 1 forces either (d <= 256).
   {
     const char* fe = getenv("SKGE_PIPE_FUSED");
-    const int fv = fe ? atoi(fe) : 0;
-    r->fused = (!hole && !grouped && nq <= 128 && (long long)N < SLOT_BUF && fv >= 1 && fv <= 3)
-                   ? fv : 0;
+    const bool ok = !hole && !grouped && nq <= 64 && (long long)N < SLOT_BUF;
+    r->fused = ok && (fe ? atoi(fe) != 0 : nq <= 16);
   }
   PipeArgs a = {};
   auto upd = [](const skge_table_t* s) {
@@ -2183,7 +2164,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     return nullptr;
   }
   r->lds = !hole ? 0
-           : r->pair ? (size_t)(2 * d + 4 * LayPair::BUF) * sizeof(float)
+           : r->pair ? hole_fft_lds_bytes(d, 1)
            : r->fft ? hole_fft_lds_bytes(d, SKGE_PIPE_WG / 64)
                     : (size_t)(SKGE_PIPE_WG / 64) * hole_pos_lds_floats(d) * sizeof(float);
   const int WPB = r->pair ? 2 : SKGE_PIPE_WG / 64;
@@ -2200,8 +2181,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
       // pre-previous slots to zero
       const int cpp = b >= 2 ? (int)batches[b - 2].second : 0;
       a.pprev_slots = 4 * cpp;
-      a.nwork = r->fused == 3 ? a.count + std::max(cprev, cpp)   // scoring, then slot groups
-                              : std::max(a.count, std::max(cprev, cpp));
+      a.nwork = a.count + std::max(cprev, cpp);   // scoring items, then slot groups
       a.nA = 0;
       r->batch.push_back(a);
       r->grid.push_back(std::max(1, (rel->rows + a.nwork + WPB - 1) / WPB));

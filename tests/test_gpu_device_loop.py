@@ -226,13 +226,13 @@ def _runner_result(n_ent, n_rel, T, d, nb, pipelined, epochs=2, seed=11, trip=No
 ])
 def test_pipelined_runner_bitwise_equals_two_launch(n_ent, n_rel, T, d, nb, monkeypatch):
     """The pipelined runner (one launch per batch: k_pipe_batch's
-    cross-workgroup hand-off, and -- SKGE_PIPE_FUSED=1 / 2, below 16k slot
-    records and d <= 512 -- k_pipe_fused, where a pending row is updated by
-    its readers themselves) must reproduce the two-launch loop exactly."""
+    cross-workgroup hand-off, and -- forced with SKGE_PIPE_FUSED=1 wherever it
+    applies, below 16k slot records and d <= 256 -- k_pipe_fused, where a
+    pending row is updated by its readers themselves) must reproduce the
+    two-launch loop exactly."""
     a, trip = _runner_result(n_ent, n_rel, T, d, nb, pipelined=False)
-    for mode in ("hand-off", "fused", "fused-meta-first", "split"):
-        monkeypatch.setenv("SKGE_PIPE_FUSED", {"hand-off": "0", "fused": "1",
-                                               "fused-meta-first": "2", "split": "3"}[mode])
+    for mode in ("hand-off", "fused"):
+        monkeypatch.setenv("SKGE_PIPE_FUSED", {"hand-off": "0", "fused": "1"}[mode])
         b, _ = _runner_result(n_ent, n_rel, T, d, nb, pipelined=True, trip=trip)
         assert a["key"] == b["key"] == 2
         assert a["nviol"] == b["nviol"] > 0, mode
