@@ -31,14 +31,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--d", type=int, default=200)
     ap.add_argument("--nb", type=int, default=100)
+    ap.add_argument("--skew", choices=("none", "zipf"), default="none")
     args = ap.parse_args()
     import numpy as np
     import torch
     import skge_amd as S
     from skge_amd.device import DeviceKG, EpochRunner
-    from bench import make_wn18_kg, N_ENT, N_REL
+    from bench import make_wn18_kg, make_zipf_kg, N_ENT, N_REL
     dev = torch.device("cuda", 0)
-    trip = make_wn18_kg()
+    trip = make_zipf_kg() if args.skew == "zipf" else make_wn18_kg()
     np.random.seed(42)
     m = S.TransE((N_ENT, N_ENT, N_REL), args.d)
     m.add_hyperparam("margin", 2.0)
