@@ -363,6 +363,8 @@ def main():
                          "|R|=10k d=512, B=131072 per GPU (BASELINE.json configs[4])")
     ap.add_argument("--c5-scale", type=float, default=1.0,
                     help="config 5 only: scale |E| and T (quick rehearsals)")
+    ap.add_argument("--c5-no-counter-split", action="store_true",
+                    help="config 5 only: skip the K extra epochs without update counters")
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the measured gather roofline (skge_roofline_gather)")
     ap.add_argument("--runner", default="auto", choices=["auto", "pairs", "hole_pipe"],
@@ -1187,6 +1189,23 @@ def run_config5(args):
     if world > 1:
         dist.barrier()
     elapsed = max_over_ranks(elapsed, world, dev)
+    counter_cost = None
+    if prof is not None and not args.c5_no_counter_split:
+        # the next K epochs without the update counters: the counters' price
+        # (these are later epochs -- fewer margin violations -- so the split is
+        # an upper bound on what the counters cost, not an exact A/B)
+        e_off, p_off = eager_epochs(runner, kg, nb, d, args.steps, counters=False)
+        counter_cost = {
+            "timed_epochs_ms": round(1000.0 * elapsed / args.steps, 3),
+            "next_epochs_no_counters_ms": round(1000.0 * e_off / args.steps, 3),
+            "apply_us": round(prof["kernels"]["accum_apply"]["avg_us"], 3),
+            "apply_us_no_counters": round(p_off["kernels"]["accum_apply"]["avg_us"], 3),
+            "sample_grad_us": round(prof["kernels"]["transe_sample_grad"]["avg_us"], 3),
+            "sample_grad_us_no_counters":
+                round(p_off["kernels"]["transe_sample_grad"]["avg_us"], 3),
+            "note": "value/frac come from the timed epochs W+1..W+K with the per-row "
+                    "update counters on (they give U for k_apply's 8(d) bytes); epochs "
+                    "W+K+1..W+2K ran without them"}
     value = replica_value(T * args.steps, world, elapsed)
     if prof is None:
         prof = pipe_profile(runner, kg, nb, d)
@@ -1221,6 +1240,12 @@ def run_config5(args):
             "cpu_baseline": None if (args.no_cpu or world > 1) else
                             cpu_baseline_config5(args.cpu_seconds),   # N = 1 only
             "detail": {"runner": "pipelined" if runner.pipelined else "two-launch",
+                       "timed_epochs": "epochs %d..%d (after %d warm-up epochs as replays "
+                                       "of the epoch graph), launched eagerly with HIP "
+                                       "events between the kernels"
+                                       % (args.warmup + 1, args.warmup + args.steps,
+                                          args.warmup),
+                       "counter_cost": counter_cost,
                        "accumulator": {"entity": acc_label(runner.accE),
                                        "relation": acc_label(runner.accR)},
                        "build_s": round(t_build, 1),
@@ -1240,7 +1265,7 @@ def run_config5(args):
         dist.destroy_process_group()
 
 
-def eager_epochs(runner, kg, nb, d, epochs, opt_k=12):
+def eager_epochs(runner, kg, nb, d, epochs, opt_k=12, counters=True):
     """`epochs` epochs of the two-launch runner's graph (skge_epoch.hip
     skge_runner_create: per batch k_transe_*_sample_grad then k_apply, then
     the epoch-key advance) launched eagerly on the runner's stream, HIP events
@@ -1249,7 +1274,9 @@ def eager_epochs(runner, kg, nb, d, epochs, opt_k=12):
     the rows the applies updated.  Returns (wall seconds, profile): per kernel
     the mean device time over these launches and the SURVEY 8(d) bytes --
     sample_grad 4d(3B + P) + 20B per batch, k_apply k d U with U the counted
-    rows -- so frac and ms_per_step come from the same epochs."""
+    rows -- so frac and ms_per_step come from the same epochs.  counters=False
+    runs the same sequence without the counters (U is then unknown: None),
+    which prices the counter atomics."""
     import torch
     from skge_amd import _lib as L
     lib = L.lib()
@@ -1258,9 +1285,12 @@ def eager_epochs(runner, kg, nb, d, epochs, opt_k=12):
     dev = runner.model.device
     te = L.SkgeTable.from_buffer_copy(runner.te)
     tr = L.SkgeTable.from_buffer_copy(runner.tr)
-    ucE = torch.zeros(te.rows, dtype=torch.int32, device=dev)
-    ucR = torch.zeros(tr.rows, dtype=torch.int32, device=dev)
-    te.upd_count, tr.upd_count = L.ptr(ucE), L.ptr(ucR)
+    if counters:
+        ucE = torch.zeros(te.rows, dtype=torch.int32, device=dev)
+        ucR = torch.zeros(tr.rows, dtype=torch.int32, device=dev)
+        te.upd_count, tr.upd_count = L.ptr(ucE), L.ptr(ucR)
+    else:
+        te.upd_count = tr.upd_count = None
     tabs = (L.SkgeTable * 2)(te, tr)
     nviol = torch.zeros(1, dtype=torch.int32, device=dev)
     T = kg.T
@@ -1293,9 +1323,9 @@ def eager_epochs(runner, kg, nb, d, epochs, opt_k=12):
     n = len(ev)
     t_s = sum(e[0].elapsed_time(e[1]) for e in ev) * 1e3 / n
     t_a = sum(e[1].elapsed_time(e[2]) for e in ev) * 1e3 / n
-    U = (int(ucE.sum().item()) + int(ucR.sum().item())) / n
+    U = (int(ucE.sum().item()) + int(ucR.sum().item())) / n if counters else None
     b_s = sum(algorithmic_bytes(d, c, 2 * c, 0, 0) for _, c in batches) / len(batches)
-    b_a = float(opt_k) * d * U
+    b_a = float(opt_k) * d * U if counters else 0.0
     kern = {"transe_sample_grad": {"name": "transe_sample_grad", "avg_us": t_s, "launches": n,
                                    "bytes_per_launch": b_s,
                                    "achieved_gbs": b_s / (t_s * 1e-6) / 1e9},

@@ -378,15 +378,19 @@ __device__ __forceinline__ float2 unpack_i32x2(unsigned long long u) {
 }
 
 template <int KQ>
-__device__ __forceinline__ void acc_row4_i16(const Accum& a, int row, const float4 (&c)[KQ],
+__device__ __forceinline__ void add_row4_i16(unsigned long long* base, const float4 (&c)[KQ],
                                              int d) {
-  unsigned long long* base = reinterpret_cast<unsigned long long*>(a.sum) + (size_t)row * (d >> 2);
   const int l = lane_id(), nq = d >> 2;
 #pragma unroll
   for (int m = 0; m < KQ; ++m) {
     const int q = 64 * m + l;
     if (q < nq) atomicAdd(base + q, pack_i16x4(c[m]));
   }
+}
+template <int KQ>
+__device__ __forceinline__ void acc_row4_i16(const Accum& a, int row, const float4 (&c)[KQ],
+                                             int d) {
+  add_row4_i16<KQ>(reinterpret_cast<unsigned long long*>(a.sum) + (size_t)row * (d >> 2), c, d);
 }
 
 // 64-bit mixing (splitmix64 finaliser) for counter-based random numbers and

@@ -26,479 +26,31 @@
 //     buffer W(b)), accumulators triple-buffered by launch id.  Every B wave
 //     recomputes R_b[p] from R_{b-1}[p] and batch b-1's sum itself (a few
 //     hundred bytes of L2-hot reads); one A wave per row writes R_b[p] for the
-//     next launch and clears the accumulator copy two launches old.
+//     next launch and clears the accumulator copy two launches old;
+//   * hot entity rows (skewed KGs, skge_pipe.h PipeTab::hot): a hub's sums and
+//     count go to one of HOT_REPS replicas per positive and a dedicated apply
+//     item folds them, so its ~hundreds of adds per batch do not serialise on
+//     one row's addresses.
 //
 // Every row update depends only on that row's own (exact integer) sums, count,
 // parameters and AdaGrad state, computed by the same code (row_update), so the
 // result is bitwise identical to the two-launch loop (tested).
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
 #include "skge_hole.h"
 #include "skge_hole_fft.h"
-#include "skge_host.h"
+#include "skge_pipe.h"
 #include "skge_sampler.h"
 
 namespace skge {
 
-// Packed int16x4 entity sums are exact while every field's total stays within
-// +-32767.  Each occurrence adds a coefficient no larger in magnitude than the
-// count it adds (s: |v0 gp + v1 (gp + g1)| <= v0 + 2 v1, ...), so a row whose
-// count c is <= 32767 cannot have wrapped; the apply flags any larger count
-// (the host picks packed sums only when its bound keeps counts below that,
-// skge_amd/device.py packed_count_bound).  Relation rows use int32x2 sums
-// (|v0 (gp + g0) + v1 (gp + g1)| <= 2 (v0 + v1) per positive): exact for any
-// batch size this runner accepts.
-constexpr int PACKED_MAX = 32767;
-enum : int { ERR_WAIT = 1, ERR_PACKED = 2 };
-
-struct UpdParams {
-  int opt, post;
-  float lr, rin, rout, fdiv;   // g = (sum + rin*P)/div + rout*P, div = fdiv > 0 ? fdiv : count
-};
-
-struct PipeTab {               // entity table
-  float* P;
-  float* A;                    // AdaGrad state or nullptr (SGD)
-  unsigned long long* sum[2];  // exact int16x4 sums, by batch parity
-  int* cnt[2];
-  int* touched[2];             // slot records of the batch
-  int* pend[2];                // [rows]: id of the launch that last accumulated into the row
-  int* own[2];                 // large batches, [rows] by batch parity: a slot naming the row
-                               // (plain stores, one survives): the A role applies a row from
-                               // that slot only, so duplicate slots cost no claim
-  int* done;                   // [rows]: id of the launch whose update of the row was last applied
-  UpdParams u;
-  int* claims;                 // profile only: rows applied in this launch (sharded)
-  int* err;                    // ERR_* bits
-};
-
-struct RelTab {                // relation table
-  float* P[2];                 // P[0]: the caller's parameters; P[1]: the other buffer
-  float* A[2];                 // AdaGrad state, likewise (nullptr: SGD)
-  unsigned long long* acc[3];  // [rows][rw]: int16x4 sums in words [0, d/4), count in word d/4
-                               // (w32: int32x2 sums in words [0, d/2), count in word d/2)
-  int rows, rw;
-  int folded;                  // replicas folded into replica 0 after each batch (k_rel_fold*)
-  int reps;                    // HolE: accumulator replicas per copy (row p of replica k at
-                               // k * rows + p); positive w adds into replica w % reps
-  UpdParams u;
-  int* updated;                // profile only: rows with a nonzero count (sharded)
-};
-
-// The fused TransE runner's entity table (k_pipe_fused, round 5).  Rows live
-// in one of two buffers; a row updated in launch g is written to the buffer
-// its previous value is NOT in, so the pre-update value stays readable for
-// the whole launch.  Sums, counts and slot records rotate over three copies
-// by launch id: launch g adds into copy g % 3, reads and applies copy
-// (g - 1) % 3 and zeroes copy (g - 2) % 3 (the copy launch g + 1 adds into).
-struct FusedTab {
-  float* P[2];        // P[0]: the caller's parameters; P[1]: the runner's second buffer
-  float* A[2];        // AdaGrad state, likewise (nullptr: SGD)
-  void* sum[3];       // exact packed sums (int8x4 / int16x4) by launch id % 3
-  int* cnt[3];
-  int* touched[3];    // slot records by launch id % 3: row | buffer << 30 (the buffer
-                      // holding the row after that launch), -1: no row
-  int4* meta;         // [rows]: x / y: id of the last even / odd launch that accumulated
-                      // into the row; z: (id of the launch that last wrote the row << 1) |
-                      // the buffer it wrote; w: id of the last launch that claimed its apply
-};
-constexpr int SLOT_BUF = 1 << 30;
-
-struct PipeArgs {
-  PipeTab E;
-  RelTab R;
-  FusedTab F;                  // fused runner (k_pipe_fused) only
-  int pprev_slots;             // fused: slots of the launch before the previous one (zeroed)
-  int nwork;                   // fused: work items (max of this, the previous and the
-                               // pre-previous launch's positives)
-  const int4* rec;             // [T]: (s, o, p, s') of the epoch's positive j
-  const int* rec_n1;           // [T]: o'
-  long long start;             // B role: this batch's positives [start, start + count)
-  int count;
-  int prev_slots;              // A role: entity slots of the previous batch
-  int b, nb1;                  // batch index in the epoch (nb1: the flush), batches per epoch
-  const uint64_t* epoch_key;
-  int d, nA;                   // nA: workgroups of the A role
-  int af;                      // HolE: activation (skge/actfun.py)
-  float margin;
-  int* nviol_total;            // the caller's counter: += the epoch's violations, at the flush
-  int* nviol_shards;           // [NSHARD][SHARD_STRIDE]: this epoch's violations so far
-  int* stats_viol;             // profile only: violating pairs of this launch (sharded)
-  unsigned long long* trace;   // diagnostics only: per-wave timestamps of one launch
-  const float2* tw;            // HolE FFT form: the twiddle table (hole_fft_table)
-  int* err;                    // set when a bounded wait gives up
-  int pair_r1;                 // HolE pair form: the wave (0 / 1) that loads and updates R[p]
-};
-
-// Launch id: consecutive within an epoch (batches 0..nb1-1, then the flush)
-// and across epochs (epoch e+1's batch 0 follows epoch e's flush); >= 2, so
-// zero-initialised marks never look pending.
-__device__ __forceinline__ int launch_id(const PipeArgs& a) {
-  return (int)(*a.epoch_key * (uint64_t)(a.nb1 + 1)) + a.b + 2;
-}
-
-// 16-B write-through (sc1) row accesses through a buffer descriptor over one
-// row (MI355X_MICROARCH.md: 4-B sc1 stores are ~6x the 16-B time per byte).
-// Lanes past the row fall outside the descriptor: loads return 0, stores drop.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-constexpr int AUX_SC1 = 16;
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const float* T, int row, int d) {
-  row = __builtin_amdgcn_readfirstlane(row);
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(T) + (size_t)row * d, 0, d * 4,
-                                           0x00020000);
-}
-
-template <int KQ>
-__device__ __forceinline__ void load_row4_sc1(const float* T, int row, int d, float4 (&v)[KQ]) {
-  const __amdgpu_buffer_rsrc_t rs = row_rsrc(T, row, d);
-  const int l = lane_id();
-#pragma unroll
-  for (int m = 0; m < KQ; ++m) {
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, (64 * m + l) * 16, 0, AUX_SC1);
-    v[m] = *reinterpret_cast<const float4*>(&x);
-  }
-}
-
-template <int KQ>
-__device__ __forceinline__ void store_row4_sc1(float* T, int row, int d, const float4 (&v)[KQ]) {
-  const __amdgpu_buffer_rsrc_t rs = row_rsrc(T, row, d);
-  const int l = lane_id();
-#pragma unroll
-  for (int m = 0; m < KQ; ++m)
-    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&v[m]), rs,
-                                           (64 * m + l) * 16, 0, AUX_SC1);
-}
-
-// load a quad-layout row of P, A (optional) and packed sums (clamped,
-// unconditional loads; lanes past the row read the last quad)
-template <int KQ>
-__device__ __forceinline__ void load_upd_row(const float* P, const float* A,
-                                             const unsigned long long* S, int d, float4 (&p)[KQ],
-                                             float4 (&a)[KQ], unsigned long long (&sv)[KQ]) {
-  const int l = lane_id(), nq = d >> 2;
-  const float4* prow = reinterpret_cast<const float4*>(P);
-  const float4* arow = reinterpret_cast<const float4*>(A);
-#pragma unroll
-  for (int m = 0; m < KQ; ++m) {
-    const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
-    sv[m] = S[qc];
-    p[m] = prow[qc];
-    a[m] = A ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  }
-}
-
-// One row's update from its exact packed sums (W32: int32x2 in sv / sw, else
-// int16x4 in sv) and occurrence count c > 0: segment
-// mean + AdaGrad / SGD + projection; the same arithmetic as apply_row_i16
-// (skge_update.hip) and the reference (skge/param.py:130, 147-155;
-// skge/transe.py normalize).  Lanes past the row end with zeros.
-// (row_update_s: the same from the sums already decoded to floats, zero past
-// the row -- the fused runner's form; every packed apply shares this code, so
-// a row's update has the same bits whichever kernel computes it)
-template <int KQ>
-__device__ __forceinline__ void row_update_s(const UpdParams& t, int c, int d,
-                                             const float4 (&sms)[KQ], float4 (&p)[KQ],
-                                             float4 (&a)[KQ]) {
-  const int l = lane_id(), nq = d >> 2;
-  const bool ada = t.opt == OPT_ADAGRAD;
-  const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
-  float ss = 0.0f;
-#pragma unroll
-  for (int m = 0; m < KQ; ++m) {
-    const bool in = 64 * m + l < nq;
-    const float4 sm = sms[m];
-#define SKGE_UP(X)                                                      \
-  {                                                                     \
-    const float g = (sm.X + t.rin * p[m].X) / div + t.rout * p[m].X;    \
-    float pv = p[m].X;                                                  \
-    if (ada) {                                                          \
-      a[m].X = a[m].X + g * g;                        /* param.py:147 */\
-      pv = pv - adagrad_step_fast(t.lr, g, a[m].X);   /* 152-155 */     \
-    } else {                                                            \
-      pv = pv - t.lr * g;                             /* param.py:130 */\
-    }                                                                   \
-    p[m].X = in ? pv : 0.0f;                                            \
-    ss += p[m].X * p[m].X;                                              \
-  }
-    SKGE_UP(x)
-    SKGE_UP(y)
-    SKGE_UP(z)
-    SKGE_UP(w)
-#undef SKGE_UP
-  }
-  if (t.post != POST_NONE) {
-    ss = wave_sum(ss);
-    const float inv = proj_scale_fast(t.post, ss);   // param.py:165-166 / 171-173
-#pragma unroll
-    for (int m = 0; m < KQ; ++m) {
-      p[m].x = p[m].x * inv;
-      p[m].y = p[m].y * inv;
-      p[m].z = p[m].z * inv;
-      p[m].w = p[m].w * inv;
-    }
-  }
-}
-
-template <int KQ, bool W32>
-__device__ __forceinline__ void row_update(const UpdParams& t, int c, int d,
-                                           const unsigned long long (&sv)[KQ],
-                                           const unsigned long long (&sw)[KQ], float4 (&p)[KQ],
-                                           float4 (&a)[KQ]) {
-  const int l = lane_id(), nq = d >> 2;
-  float4 sm[KQ];
-#pragma unroll
-  for (int m = 0; m < KQ; ++m) {
-    const bool in = 64 * m + l < nq;
-    if (W32) {   // int32x2 sums: quad q in words sv (elements 0, 1) and sw (2, 3)
-      const float2 lo = unpack_i32x2(in ? sv[m] : 0ull), hi = unpack_i32x2(in ? sw[m] : 0ull);
-      sm[m] = make_float4(lo.x, lo.y, hi.x, hi.y);
-    } else {     // int16x4 sums
-      sm[m] = unpack_i16x4(in ? sv[m] : 0ull);
-    }
-  }
-  row_update_s<KQ>(t, c, d, sm, p, a);
-}
-
-// Claim a pending entity row's update (the first wave to swap its count out
-// applies it) and, if claimed, apply it from accumulator copy `pp` and publish
-// it as launch `gp` (write-through stores, drain, done word).  The row's sums,
-// parameters and state are loaded in the same memory round trip as the claim:
-// nobody writes them before the claim is won, and a loser discards them.
-template <int KQ, bool E8 = false>
-__device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int row, int d, int gp) {
-  const int l = lane_id(), nq = d >> 2;
-  int c = 0;
-  if (l == 0) c = atomicExch(t.cnt[pp] + row, 0);
-  unsigned long long* srow = t.sum[pp] + (size_t)row * nq;
-  unsigned int* srow8 = reinterpret_cast<unsigned int*>(t.sum[pp]) + (size_t)row * nq;
-  unsigned long long sv[KQ];
-  float4 p[KQ], a[KQ];
-  if (E8) {   // int8x4 sums: one dword per quad, re-packed as int16x4 for row_update
-    unsigned int s8[KQ];
-    const float4* prow = reinterpret_cast<const float4*>(t.P + (size_t)row * d);
-    const float4* arow = reinterpret_cast<const float4*>(t.A + (size_t)row * d);
-#pragma unroll
-    for (int m = 0; m < KQ; ++m) {
-      const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
-      s8[m] = srow8[qc];
-      p[m] = prow[qc];
-      a[m] = t.A ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
-#pragma unroll
-    for (int m = 0; m < KQ; ++m) sv[m] = pack_i16x4(unpack_i8x4_sum(s8[m]));
-  } else {
-    load_upd_row<KQ>(t.P + (size_t)row * d, t.A ? t.A + (size_t)row * d : nullptr, srow, d, p, a,
-                     sv);
-  }
-  c = __builtin_amdgcn_readfirstlane(c);
-  if (c == 0) return;   // another wave owns the row
-  // a field may have wrapped: 16-bit fields past 32767, 8-bit fields past 127
-  if (c > (E8 ? 127 : PACKED_MAX) && l == 0) atomicOr(t.err, ERR_PACKED);
-  row_update<KQ, false>(t.u, c, d, sv, sv, p, a);
-#pragma unroll
-  for (int m = 0; m < KQ; ++m) {
-    const int q = 64 * m + l;
-    if (q < nq) {
-      if (E8)
-        srow8[q] = 0u;
-      else
-        srow[q] = 0ull;
-    }
-  }
-  store_row4_sc1<KQ>(t.P, row, d, p);
-  if (t.A) store_row4_sc1<KQ>(t.A, row, d, a);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
-  if (l == 0) __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
-}
-
-// Large batches: up to GRP_ROWS owner rows of a 64-slot group at once -- all
-// claims in one atomic instruction (lane j claims row j), all rows' loads in
-// one round trip, every claimed row updated and stored write-through, ONE
-// drain, then the done words -- instead of a claim / load / store / drain
-// chain per row.
-#ifndef SKGE_PIPE_GRP_ROWS
-#define SKGE_PIPE_GRP_ROWS 4   // WN18 nb = 2, same box: 8 rows 467 M, 4 rows 482-488 M (124 -> 85 VGPRs)
-#endif
-constexpr int GRP_ROWS = SKGE_PIPE_GRP_ROWS;
-template <int KQ, bool E8>
-__device__ __forceinline__ void claim_and_apply_rows(const PipeTab& t, int pp, int rl, int n,
-                                                     int d, int gp) {
-  const int l = lane_id(), nq = d >> 2;
-  int c = 0;
-  if (l < n) c = atomicExch(t.cnt[pp] + rl, 0);   // lane j holds row j (j < n)
-  float4 p[GRP_ROWS][KQ], a[GRP_ROWS][KQ];
-  unsigned long long sv[GRP_ROWS][KQ];
-  int row[GRP_ROWS];
-#pragma unroll
-  for (int j = 0; j < GRP_ROWS; ++j) {
-    row[j] = __builtin_amdgcn_readlane(rl, j < n ? j : 0);
-    const float4* prow = reinterpret_cast<const float4*>(t.P + (size_t)row[j] * d);
-    const float4* arow = reinterpret_cast<const float4*>(t.A + (size_t)row[j] * d);
-#pragma unroll
-    for (int m = 0; m < KQ; ++m) {
-      const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
-      if (E8)
-        sv[j][m] = reinterpret_cast<const unsigned int*>(t.sum[pp])[(size_t)row[j] * nq + qc];
-      else
-        sv[j][m] = t.sum[pp][(size_t)row[j] * nq + qc];
-      p[j][m] = prow[qc];
-      a[j][m] = t.A ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
-  }
-  int any = 0;
-#pragma unroll
-  for (int j = 0; j < GRP_ROWS; ++j) {
-    const int cj = __builtin_amdgcn_readlane(c, j);
-    if (j >= n || cj == 0) continue;   // past the rows, or another wave owns the row
-    any = 1;
-    if (cj > (E8 ? 127 : PACKED_MAX) && l == 0) atomicOr(t.err, ERR_PACKED);
-    if (E8) {
-#pragma unroll
-      for (int m = 0; m < KQ; ++m) sv[j][m] = pack_i16x4(unpack_i8x4_sum((unsigned int)sv[j][m]));
-    }
-    row_update<KQ, false>(t.u, cj, d, sv[j], sv[j], p[j], a[j]);
-#pragma unroll
-    for (int m = 0; m < KQ; ++m) {
-      const int q = 64 * m + l;
-      if (q < nq) {
-        if (E8)
-          reinterpret_cast<unsigned int*>(t.sum[pp])[(size_t)row[j] * nq + q] = 0u;
-        else
-          t.sum[pp][(size_t)row[j] * nq + q] = 0ull;
-      }
-    }
-    store_row4_sc1<KQ>(t.P, row[j], d, p[j]);
-    if (t.A) store_row4_sc1<KQ>(t.A, row[j], d, a[j]);
-  }
-  if (!any) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
-  if (l < n && c != 0) __hip_atomic_store(t.done + rl, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t.claims && l == 0) {
-    int k = 0;
-#pragma unroll
-    for (int j = 0; j < GRP_ROWS; ++j) k += (j < n && __builtin_amdgcn_readlane(c, j) != 0);
-    atomicAdd(shard_of(t.claims), k);
-  }
-}
-
-// B role: make sure launch gp's update of entity `row` (pending at launch
-// start) has landed -- apply it if nobody has claimed it yet, else wait for
-// its publisher
-template <int KQ, bool E8 = false>
-__device__ __forceinline__ void ensure_applied(const PipeTab& t, int pp, int row, int d, int gp,
-                                               int* err) {
-  if (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gp) return;
-  claim_and_apply<KQ, E8>(t, pp, row, d, gp);
-  unsigned spins = 0;
-  while (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gp) {
-    __builtin_amdgcn_s_sleep(2);
-    if (++spins > (1u << 22)) {   // ~0.5 s: never hang the GPU; report instead
-      if (lane_id() == 0) atomicOr(err, ERR_WAIT);
-      break;
-    }
-    if ((spins & 1023u) == 0 &&   // once one wait has given up, the rest stop too
-        __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      break;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the re-read below the poll
-}
-
-// relation row R_b[row] (the value batch b scores with): R_{b-1}[row] from
-// buffer rd updated with batch b-1's sums (accumulator copy ra).  W32: int32x2
-// sums, words 2q, 2q+1 hold quad q and word 2 nq the count; else int16x4
-// sums, word q holds quad q and word nq the count.  Every load is issued
-// before the count is read (kept in load_upd_row's shape: hipcc would sink
-// loads used only under `if (c)` below the count's wait).  Lanes past the row
-// end with zeros whether or not the row was updated (they enter the scores).
-template <int KQ, bool W32>
-__device__ __forceinline__ void rel_row(const RelTab& t, int row, int d, int rd, int ra,
-                                        float4 (&p)[KQ], float4 (&a)[KQ], int& c) {
-  const int l = lane_id(), nq = d >> 2;
-  const unsigned long long* acc = t.acc[ra] + (size_t)row * t.rw;
-  unsigned long long sv[KQ], sw[KQ];
-  if (W32) {
-    const float4* prow = reinterpret_cast<const float4*>(t.P[rd] + (size_t)row * d);
-    const float4* arow = reinterpret_cast<const float4*>(t.A[rd] + (size_t)row * d);
-#pragma unroll
-    for (int m = 0; m < KQ; ++m) {
-      const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
-      const ulonglong2 w = reinterpret_cast<const ulonglong2*>(acc)[qc];
-      sv[m] = w.x;
-      sw[m] = w.y;
-      p[m] = prow[qc];
-      a[m] = t.A[rd] ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
-  } else {
-    load_upd_row<KQ>(t.P[rd] + (size_t)row * d, t.A[rd] ? t.A[rd] + (size_t)row * d : nullptr,
-                     acc, d, p, a, sv);
-  }
-  c = __builtin_amdgcn_readfirstlane((int)acc[W32 ? 2 * nq : nq]);
-  if (c) {
-    row_update<KQ, W32>(t.u, c, d, sv, sw, p, a);   // (zeroes the lanes past the row)
-  }
-  else {
-#pragma unroll
-    for (int m = 0; m < KQ; ++m)
-      if (64 * m + l >= nq) p[m] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  }
-}
-
-__device__ __forceinline__ unsigned long long now_10ns() { return __builtin_amdgcn_s_memrealtime(); }
-
-// A kernel argument made opaque to the compiler (kept in SGPRs, or spilled to
-// VGPR lanes): under SGPR pressure hipcc otherwise re-loads argument fields
-// from the kernarg segment where they are used, and the scoring wave's
-// scatter section paid one dependent scalar-memory round trip per pointer.
-template <typename T>
-__device__ __forceinline__ T* opaque_ptr(T* p) {
-  unsigned long long v = reinterpret_cast<unsigned long long>(p);
-  asm volatile("" : "+s"(v));
-  return reinterpret_cast<T*>(v);
-}
-
-// A role, relation row w: write R_b[w] (from R_{b-1} and batch b-1's sums) to
-// buffer rw for the next launch, clear the accumulator copy two launches old
-// (at the flush also the previous one: no scoring wave reads it any more)
-template <int KQ, bool W32>
-__device__ __forceinline__ void rel_publish(const PipeArgs& a, int w, int rd, int rw, int ra_prev,
-                                            int ra_old) {
-  const int l = lane_id(), d = a.d, nq = d >> 2;
-  const int rcw = W32 ? 2 * nq : nq;
-  float4 p[KQ], av[KQ];
-  int c;
-  rel_row<KQ, W32>(a.R, w, d, rd, ra_prev, p, av, c);
-  float4* prow = reinterpret_cast<float4*>(a.R.P[rw] + (size_t)w * d);
-  float4* arow = a.R.A[rw] ? reinterpret_cast<float4*>(a.R.A[rw] + (size_t)w * d) : nullptr;
-  unsigned long long* old = a.R.acc[ra_old] + (size_t)w * a.R.rw;
-  unsigned long long* prev = a.R.acc[ra_prev] + (size_t)w * a.R.rw;
-  const bool flush = a.b == a.nb1;
-#pragma unroll
-  for (int m = 0; m < KQ; ++m) {
-    const int q = 64 * m + l;
-    if (q < nq) {
-      prow[q] = p[m];
-      if (arow) arow[q] = av[m];
-    }
-  }
-  for (int q = l; q <= rcw; q += 64) {
-    old[q] = 0ull;
-    if (flush) prev[q] = 0ull;
-  }
-  if (c && a.R.updated && l == 0) atomicAdd(shard_of(a.R.updated), 1);
-  if (!W32 && c > PACKED_MAX && l == 0) atomicOr(a.err, ERR_PACKED);
-}
-
-#ifndef SKGE_PIPE_WG
-#define SKGE_PIPE_WG 256   // threads per workgroup
-#endif
 // k_pipe_batch (large batches: more than 16k slot records per batch; smaller
 // batches run k_pipe_fused below): nA apply workgroups (dispatched first: they
 // start the hand-offs the scoring waves may wait on), then the scoring ones.
 // GRP: owner marks, GRP_ROWS owner rows per apply round trip.
-template <int KQ, bool W32, bool E8, bool GRP = false>
+template <int KQ, bool W32, bool E8, bool GRP = false, bool HOT = false>
 __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
@@ -520,7 +72,8 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
     // owner marks (large batches): items are groups of 64 slots, scanned
     // lane-parallel; else one slot per item
     const int* const ownp = a.E.own[pp];
-    const int total = nR + (ownp ? (a.prev_slots + 63) / 64 : a.prev_slots);
+    const int nH = a.E.nhot, nRH = nR + nH;   // then one item per hot row
+    const int total = nRH + (ownp ? (a.prev_slots + 63) / 64 : a.prev_slots);
     const int wa = blk_a * wpb + (threadIdx.x >> 6);
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
     if (a.b == a.nb1 && wa == 0)   // the flush: fold the epoch's violation count
@@ -528,10 +81,12 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
     for (int w = wa; w < total; w += a.nA * wpb) {
       if (w < nR) {
         rel_publish<KQ, W32>(a, w, rd, rw, ra_prev, ra_old);
+      } else if (w < nRH) {
+        claim_and_apply<KQ, E8, HOT>(a.E, pp, a.E.hot_rows[w - nR], d, gp);
       } else if (ownp) {
         // 64 slots: their rows and owner marks in two vector loads; only the
         // slot each row's owner mark names applies it (no claim on duplicates)
-        const int i = 64 * (w - nR) + l;
+        const int i = 64 * (w - nRH) + l;
         const int r = i < a.prev_slots ? a.E.touched[pp][i] : -1;
         const bool mine = r >= 0 && ownp[r] == i;
         uint64_t m = __ballot(mine);
@@ -561,12 +116,12 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
             const int k = __ffsll((unsigned long long)m) - 1;
             m &= m - 1;
             const int row = __builtin_amdgcn_readlane(r, k);
-            claim_and_apply<KQ, E8>(a.E, pp, row, d, gp);
+            claim_and_apply<KQ, E8, HOT>(a.E, pp, row, d, gp);
           }
         }
       } else {
-        const int row = __builtin_amdgcn_readfirstlane(a.E.touched[pp][w - nR]);
-        if (row >= 0) claim_and_apply<KQ, E8>(a.E, pp, row, d, gp);
+        const int row = __builtin_amdgcn_readfirstlane(a.E.touched[pp][w - nRH]);
+        if (row >= 0) claim_and_apply<KQ, E8, HOT>(a.E, pp, row, d, gp);
       }
     }
     if (a.trace && l == 0) {
@@ -621,11 +176,12 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
     // row whose update is already published needs only the re-read below (at
     // nb = 2 every row is pending; one done check per row in sequence had cost
     // ~1.9 us per wave)
-    int mark = 0, dn = 0;
+    int mark = 0, dn = 0, hx = -1;
     if (l < 4) {
       const int rr = sel4(l, s, o, n0r, n1r);
       mark = a.E.pend[pp][rr];
       dn = __hip_atomic_load(a.E.done + rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (HOT) hx = a.E.hot[rr];
     }
     {
       float4 ra[KQ];
@@ -640,7 +196,8 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) {
         if (!((unpub >> k) & 1ull)) continue;
-        ensure_applied<KQ, E8>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err);
+        ensure_applied<KQ, E8>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err,
+                               HOT && __builtin_amdgcn_readlane(hx, k) >= 0);
       }
       if (pend & 1ull) load_row4_sc1<KQ>(a.E.P, s, d, es);
       if (pend & 2ull) load_row4_sc1<KQ>(a.E.P, o, d, eo);
@@ -679,7 +236,14 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
       // counts, touched slots and pending marks of this batch
       const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
       const int rE = sel4(l, s, o, neg0, neg1);
-      if (l < 4) {
+      if (HOT && l < 4 && hx >= 0) {   // hot row: count into its replica, marker, no slot record
+        if (cE > 0) {
+          atomicAdd(a.E.hcnt[cp] + hx * HOT_REPS + (w & (HOT_REPS - 1)), cE);
+          cnt_cp[rE] = 1;
+          pend_cp[rE] = g;
+        }
+        tch_cp[4 * w + l] = -1;
+      } else if (l < 4) {
         commit_slot(cnt_cp, tch_cp, rE, cE, 4 * w + l);
         if (cE > 0) {
           pend_cp[rE] = g;
@@ -714,12 +278,16 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
         if (v0) acc_row4_i8<KQ>(es8, neg0, c0, d);
         if (v1) acc_row4_i8<KQ>(es8, neg1, c1, d);
       } else {
-        Accum aE = {};   // mode ACC_F32 (0), one copy
-        aE.sum = reinterpret_cast<float*>(esum);
-        acc_row4_i16<KQ>(aE, s, cs, d);
-        acc_row4_i16<KQ>(aE, o, co, d);
-        if (v0) acc_row4_i16<KQ>(aE, neg0, c0, d);
-        if (v1) acc_row4_i16<KQ>(aE, neg1, c1, d);
+        // a hot row's sums go to replica w % HOT_REPS
+        auto base = [&](int k, int row) {
+          const int h = HOT ? __builtin_amdgcn_readlane(hx, k) : -1;
+          return h >= 0 ? a.E.hsum[cp] + ((size_t)h * HOT_REPS + (w & (HOT_REPS - 1))) * a.E.hw
+                        : esum + (size_t)row * nq;
+        };
+        add_row4_i16<KQ>(base(0, s), cs, d);
+        add_row4_i16<KQ>(base(1, o), co, d);
+        if (v0) add_row4_i16<KQ>(base(2, neg0), c0, d);
+        if (v1) add_row4_i16<KQ>(base(3, neg1), c1, d);
       }
       // relation sums: rows of rw words; int32x2 (two words per quad) when a
       // hot relation's batch total could pass 16 bits
@@ -1141,591 +709,7 @@ __global__ __launch_bounds__(256) void k_fused_fin(FusedTab F, int rows, int d) 
   }
 }
 
-// ======================== HolE pairwise, pipelined ========================
-//
-// The launch structure of k_pipe_batch for HolE (skge/hole.py:44-100, the
-// pairwise gradients, E post normless1): launch g scores batch b -- one wave
-// per positive, both of its pairs, k_hole_pos's seven correlations and exact
-// arithmetic -- while other workgroups apply batch b-1's rows (claim,
-// write-through publish, done word; a scoring wave reading a row batch b-1
-// touched applies it itself or waits).  Sums are fp32 (HolE contributions are
-// not small integers): entity sums [rows][d] double-buffered by batch parity,
-// relation sums [rows][rw words] (floats 0..d-1, count as an int at float d)
-// triple-buffered by launch id, one copy (every scoring wave recomputes
-// R_b[p] from R_{b-1}[p] and batch b-1's sums, as k_pipe_batch does).  Float
-// atomics add in any order, so the result equals the two-launch HolE loop to
-// fp32 rounding, not bit for bit.  Scoring workgroups are dispatched first
-// (their correlations are the launch's long pole): the apply waves then run
-// beside them.
-
-// One row's update from fp32 sums (zero past the row); row_update's arithmetic
-template <int KQ>
-__device__ __forceinline__ void row_update_f(const UpdParams& t, int c, int d,
-                                             const float4 (&sm)[KQ], float4 (&p)[KQ],
-                                             float4 (&a)[KQ]) {
-  const int l = lane_id(), nq = d >> 2;
-  const bool ada = t.opt == OPT_ADAGRAD;
-  const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
-  float ss = 0.0f;
-#pragma unroll
-  for (int m = 0; m < KQ; ++m) {
-    const bool in = 64 * m + l < nq;
-#define SKGE_UP(X)                                                      \
-  {                                                                     \
-    const float g = (sm[m].X + t.rin * p[m].X) / div + t.rout * p[m].X; \
-    float pv = p[m].X;                                                  \
-    if (ada) {                                                          \
-      a[m].X = a[m].X + g * g;                        /* param.py:147 */\
-      pv = pv - (t.lr * g) / fmaxf(sqrtf(a[m].X), 1e-7f); /* 152-155 */ \
-    } else {                                                            \
-      pv = pv - t.lr * g;                             /* param.py:130 */\
-    }                                                                   \
-    p[m].X = in ? pv : 0.0f;                                            \
-    ss += p[m].X * p[m].X;                                              \
-  }
-    SKGE_UP(x)
-    SKGE_UP(y)
-    SKGE_UP(z)
-    SKGE_UP(w)
-#undef SKGE_UP
-  }
-  if (t.post != POST_NONE) {
-    ss = wave_sum(ss);
-    const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss) : (ss < 1.0f ? 1.0f : ss);
-#pragma unroll
-    for (int m = 0; m < KQ; ++m) {
-      p[m].x = p[m].x / nrm;
-      p[m].y = p[m].y / nrm;
-      p[m].z = p[m].z / nrm;
-      p[m].w = p[m].w / nrm;
-    }
-  }
-}
-
-// P, A (P again when A is null: discarded) and fp32 sums of one quad-layout
-// row, unconditional 16-B loads; sums zero past the row
-template <int KQ>
-__device__ __forceinline__ void load_f32_row(const float* P, const float* A, const float* S,
-                                             int row, int d, float4 (&p)[KQ], float4 (&a)[KQ],
-                                             float4 (&sm)[KQ]) {
-  const int l = lane_id(), nq = d >> 2;
-  const float4* prow = reinterpret_cast<const float4*>(P + (size_t)row * d);
-  const float4* arow = reinterpret_cast<const float4*>((A ? A : P) + (size_t)row * d);
-  const float4* srow = reinterpret_cast<const float4*>(S + (size_t)row * d);
-  const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll
-  for (int m = 0; m < KQ; ++m) {
-    const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
-    const float4 sv = srow[qc];
-    p[m] = prow[qc];
-    a[m] = arow[qc];
-    sm[m] = q < nq ? sv : z;
-  }
-}
-
-template <int KQ>
-__device__ __forceinline__ void claim_and_apply_f(const PipeTab& t, int pp, int row, int d,
-                                                  int gp) {
-  const int l = lane_id(), nq = d >> 2;
-  int c = 0;
-  if (l == 0) c = atomicExch(t.cnt[pp] + row, 0);
-  float* S = reinterpret_cast<float*>(t.sum[pp]);
-  float4 sm[KQ], p[KQ], a[KQ];
-  load_f32_row<KQ>(t.P, t.A, S, row, d, p, a, sm);
-  c = __builtin_amdgcn_readfirstlane(c);
-  if (c == 0) return;   // another wave owns the row
-  row_update_f<KQ>(t.u, c, d, sm, p, a);
-  float4* srow = reinterpret_cast<float4*>(S + (size_t)row * d);
-#pragma unroll
-  for (int m = 0; m < KQ; ++m)
-    if (64 * m + l < nq) srow[64 * m + l] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  store_row4_sc1<KQ>(t.P, row, d, p);
-  if (t.A) store_row4_sc1<KQ>(t.A, row, d, a);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
-  if (l == 0) __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
-}
-
-// The HolE launch's A role over its share of the slot records: slots k0,
-// k0 + ks, ... < ns.  The slot ids come in one vector load per 64 slots (empty
-// slots cost nothing more), and each touched row's claim and loads are issued
-// while the previous row is updated and published, so a wave's rows overlap
-// instead of paying a dependent slot load + claim round trip each.
-template <int KQ>
-__device__ __forceinline__ void apply_slots_f(const PipeTab& t, int pp, int k0, int ks, int ns,
-                                              int d, int gp) {
-  const int l = lane_id(), nq = d >> 2;
-  float* S = reinterpret_cast<float*>(t.sum[pp]);
-  for (int base = k0; base < ns; base += 64 * ks) {
-    const int k = base + l * ks;
-    const int rowl = k < ns ? t.touched[pp][k] : -1;
-    uint64_t m = __ballot(rowl >= 0);
-    if (!m) continue;
-    int i = __builtin_ctzll(m);
-    m &= m - 1;
-    int r = __builtin_amdgcn_readlane(rowl, i), c = 0;
-    float4 sm[KQ], p[KQ], a[KQ];
-    if (l == 0) c = atomicExch(t.cnt[pp] + r, 0);
-    load_f32_row<KQ>(t.P, t.A, S, r, d, p, a, sm);
-    int nclaim = 0;
-    while (true) {
-      int rn = -1, cn = 0;
-      float4 smn[KQ], pn[KQ], an[KQ];
-      if (m) {   // the next row's claim and loads in flight behind this row
-        i = __builtin_ctzll(m);
-        m &= m - 1;
-        rn = __builtin_amdgcn_readlane(rowl, i);
-        if (l == 0) cn = atomicExch(t.cnt[pp] + rn, 0);
-        load_f32_row<KQ>(t.P, t.A, S, rn, d, pn, an, smn);
-      }
-      c = __builtin_amdgcn_readfirstlane(c);
-      if (c != 0) {   // this wave owns the row
-        row_update_f<KQ>(t.u, c, d, sm, p, a);
-        float4* srow = reinterpret_cast<float4*>(S + (size_t)r * d);
-#pragma unroll
-        for (int q = 0; q < KQ; ++q)
-          if (64 * q + l < nq) srow[64 * q + l] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        store_row4_sc1<KQ>(t.P, r, d, p);
-        if (t.A) store_row4_sc1<KQ>(t.A, r, d, a);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
-        if (l == 0) __hip_atomic_store(t.done + r, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ++nclaim;
-      }
-      if (rn < 0) break;
-      r = rn;
-      c = cn;
-#pragma unroll
-      for (int q = 0; q < KQ; ++q) {
-        sm[q] = smn[q];
-        p[q] = pn[q];
-        a[q] = an[q];
-      }
-    }
-    if (t.claims && l == 0 && nclaim) atomicAdd(shard_of(t.claims), nclaim);
-  }
-}
-
-template <int KQ>
-__device__ __forceinline__ void ensure_applied_f(const PipeTab& t, int pp, int row, int d, int gp,
-                                                 int* err) {
-  if (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gp) return;
-  claim_and_apply_f<KQ>(t, pp, row, d, gp);
-  unsigned spins = 0;
-  while (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gp) {
-    __builtin_amdgcn_s_sleep(2);
-    if (++spins > (1u << 22)) {   // ~0.5 s: never hang the GPU; report instead
-      if (lane_id() == 0) atomicOr(err, ERR_WAIT);
-      break;
-    }
-    if ((spins & 1023u) == 0 &&
-        __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      break;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the re-read below the poll
-}
-
-// relation row R_b[row] from R_{b-1} (buffer rd) and batch b-1's fp32 sums
-// (copy ra: floats [0, d), count at float d); zero past the row
-template <int KQ>
-__device__ __forceinline__ void rel_row_f(const RelTab& t, int row, int d, int rd, int ra,
-                                          float4 (&p)[KQ], float4 (&a)[KQ], int& c) {
-  const int l = lane_id(), nq = d >> 2;
-  const float* acc = reinterpret_cast<const float*>(t.acc[ra] + (size_t)row * t.rw);
-  float4 sm[KQ];
-  load_f32_row<KQ>(t.P[rd] + (size_t)row * d, t.A[rd] ? t.A[rd] + (size_t)row * d : nullptr,
-                   acc, 0, d, p, a, sm);
-  c = __builtin_amdgcn_readfirstlane(__float_as_int(acc[d]));
-  const int nrep = t.folded ? 1 : t.reps;   // folded: replica 0 holds the sum
-  for (int k = 1; k < nrep; ++k) {   // large batches: the replicas, in a fixed order
-    const float* ak = reinterpret_cast<const float*>(t.acc[ra] +
-                                                     ((size_t)k * t.rows + row) * t.rw);
-    const float4* ak4 = reinterpret_cast<const float4*>(ak);
-#pragma unroll
-    for (int m = 0; m < KQ; ++m) {
-      const int q = 64 * m + l;
-      const float4 v = ak4[q < nq ? q : nq - 1];
-      if (q < nq) {
-        sm[m].x += v.x;
-        sm[m].y += v.y;
-        sm[m].z += v.z;
-        sm[m].w += v.w;
-      }
-    }
-    c += __builtin_amdgcn_readfirstlane(__float_as_int(ak[d]));
-  }
-  if (c) {
-    row_update_f<KQ>(t.u, c, d, sm, p, a);
-  } else {
-#pragma unroll
-    for (int m = 0; m < KQ; ++m)
-      if (64 * m + l >= nq) p[m] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  }
-}
-
-template <int KQ>
-__device__ __forceinline__ void rel_publish_f(const PipeArgs& a, int w, int rd, int rw,
-                                              int ra_prev, int ra_old) {
-  const int l = lane_id(), d = a.d, nq = d >> 2;
-  float4 p[KQ], av[KQ];
-  int c;
-  rel_row_f<KQ>(a.R, w, d, rd, ra_prev, p, av, c);
-  float4* prow = reinterpret_cast<float4*>(a.R.P[rw] + (size_t)w * d);
-  float4* arow = a.R.A[rw] ? reinterpret_cast<float4*>(a.R.A[rw] + (size_t)w * d) : nullptr;
-  unsigned long long* old = a.R.acc[ra_old] + (size_t)w * a.R.rw;
-  unsigned long long* prev = a.R.acc[ra_prev] + (size_t)w * a.R.rw;
-  const bool flush = a.b == a.nb1;
-#pragma unroll
-  for (int m = 0; m < KQ; ++m) {
-    const int q = 64 * m + l;
-    if (q < nq) {
-      prow[q] = p[m];
-      if (arow) arow[q] = av[m];
-    }
-  }
-  for (int k = 0; k < a.R.reps; ++k) {   // rw 8-B words: the sums and the count
-    const size_t ko = (size_t)k * a.R.rows * a.R.rw;
-    for (int q = l; q < a.R.rw; q += 64) {
-      old[ko + q] = 0ull;
-      if (flush) prev[ko + q] = 0ull;
-    }
-  }
-  if (c && a.R.updated && l == 0) atomicAdd(shard_of(a.R.updated), 1);
-}
-
-constexpr int HPIPE_OCC = 2;   // scoring waves per SIMD the apply-workgroup cap assumes (direct form)
-
-// PAIR (round 4, SKGE_HPIPE_PAIR; FFT at d = 200): 128-thread
-// workgroups, and a scoring workgroup's two waves score ONE positive together
-// -- each loads and settles two of its rows, the transforms' stage passes are
-// split between them (fft_run_c2: the same butterflies, the same bits), both
-// compute the spectra and scores (identical values), and each issues half of
-// the contribution rows' atomics -- so a positive's serial chain is shorter.
-template <int KM>
-__device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* smem, int blk_b,
-                                                     int nB) {
-  const int hw = (int)(threadIdx.x >> 6);   // the wave's half of the pair
-  const int l = lane_id();
-  const int d = a.d;
-  const int g = launch_id(a), gp = g - 1;
-  const int cp = a.b & 1, pp = cp ^ 1;
-  const int rd = a.b & 1;
-  const int ra_prev = (g - 1) % 3, ra_cur = g % 3;
-  float2* const tw = reinterpret_cast<float2*>(smem);
-  // the twiddle table into LDS before the loop (its load overlapped with the
-  // first record's round trip measured no faster: not on the critical path)
-  fft_twiddles(tw, a.tw, d);
-  float* const wb = smem + 2 * d;   // the pair's two transform buffers
-  float2* const b0 = reinterpret_cast<float2*>(wb);
-  float2* const b1 = b0 + 5 * 100;
-  Accum aE = {};
-  aE.sum = reinterpret_cast<float*>(a.E.sum[cp]);
-  aE.width = d;
-  const int rstride = 2 * a.R.rw;
-  int nv = 0;
-  for (int w = blk_b; w < a.count; w += nB) {
-    float* const racc = reinterpret_cast<float*>(a.R.acc[ra_cur]) +
-                        (size_t)(w % a.R.reps) * a.R.rows * rstride;
-    unsigned long long tt[4] = {0ull, 0ull, 0ull, 0ull};   // diagnostics: wave 0's phases
-    if (a.trace) tt[0] = now_10ns();
-    const long long j = a.start + w;
-    const int4 r4 = a.rec[j];
-    const int r1 = a.rec_n1[j];
-    __builtin_amdgcn_sched_barrier(0);
-    const int s = uni(r4.x), o = uni(r4.y), p = uni(r4.z), neg0 = uni(r4.w);
-    const int neg1 = uni(r1);
-    const int n0r = neg0 >= 0 ? neg0 : s, n1r = neg1 >= 0 ? neg1 : o;
-    // wave 0: E[s], E[s'] (signals 1, 2); wave 1: E[o], E[o'] (3, 4); R[p] (0)
-    // on wave pair_r1
-    const int ra_row = hw ? o : s, rb_row = hw ? n1r : n0r;
-    float4 xa[1], xb[1], xr[1] = {};
-    load_row4<1>(a.E.P, ra_row, d, xa);
-    load_row4<1>(a.E.P, rb_row, d, xb);
-    int mark = 0;
-    if (l < 2) mark = a.E.pend[pp][l ? rb_row : ra_row];
-    if (hw == a.pair_r1) {
-      float4 rav[1];
-      int c;
-      rel_row_f<1>(a.R, p, d, rd, ra_prev, xr, rav, c);
-    }
-    const uint64_t pend = __ballot(mark == gp) & 0x3ull;
-    if (a.trace) tt[1] = now_10ns();
-    if (pend) {
-      if (pend & 1ull) ensure_applied_f<1>(a.E, pp, ra_row, d, gp, a.err);
-      if (pend & 2ull) ensure_applied_f<1>(a.E, pp, rb_row, d, gp, a.err);
-      if (pend & 1ull) load_row4_sc1<1>(a.E.P, ra_row, d, xa);
-      if (pend & 2ull) load_row4_sc1<1>(a.E.P, rb_row, d, xb);
-    }
-    if (a.trace) tt[2] = now_10ns();
-    __syncthreads();   // the previous positive's buffers are free, the twiddles in place
-    if (hw == a.pair_r1) fft_put_row(b0, 100, 0, xr[0], d);
-    if (hw == 0) {
-      fft_put_row(b0, 100, 1, xa[0], d);
-      fft_put_row(b0, 100, 2, xb[0], d);
-    } else {
-      fft_put_row(b0, 100, 3, xa[0], d);
-      fft_put_row(b0, 100, 4, xb[0], d);
-    }
-    __syncthreads();
-    const float2* Z = fft_run_c2<100, 5, false>(b0, b1, tw, hw);
-    float praw, raw0, raw1;
-    const HoleSpec hs = hole_fft_spectra(Z, tw, d, praw, raw0, raw1);
-    const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
-    const int v0 = uni((neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0);   // hole.py:56
-    const int v1 = uni((neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0);
-    if (a.trace) tt[3] = now_10ns();
-    // trace record of positive w (wave 0, lane 0): stamps, then the flags word
-    // (bits 0-1: wave 0's pending rows s, s'; 8 violating; 9 v0; 10 v1; 16+:
-    // the inverse phase in 10 ns ticks)
-    auto stamp = [&](unsigned long long flags) {
-      if (a.trace && hw == 0 && l == 0) {
-        unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
-        tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
-        tr[5] = flags;
-      }
-    };
-    if (hw == 0) {
-      const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
-      const int rE = sel4(l, s, o, neg0, neg1);
-      if (l < 4) {
-        commit_slot(a.E.cnt[cp], a.E.touched[cp], rE, cE, 4 * w + l);
-        if (cE > 0) a.E.pend[cp][rE] = g;
-      } else if (l == 4 && v0 + v1 > 0) {
-        atomicAdd(reinterpret_cast<int*>(racc + (size_t)p * rstride + d), 2 * (v0 + v1));
-      }
-      nv += v0 + v1;
-    }
-    if (v0 + v1 == 0) {   // (the same in both waves)
-      stamp(pend);
-      continue;
-    }
-    const float gpf = -af_g_given_f(a.af, pf);   // hole.py:66
-    const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
-    const float* z = hole_fft_rows_pair(wb, tw, hs, v0, v1, gpf, g0, g1, hw);
-    const unsigned long long inv_dt = a.trace ? now_10ns() - tt[3] : 0ull;
-    if (hw == 0) {
-      Accum aR = {};
-      aR.sum = racc + (size_t)p * rstride;
-      aR.width = d;
-      acc_fft_row<KM>(aR, 0, z, 2, d);
-      acc_fft_row<KM>(aE, s, z, 0, d);
-    } else {
-      acc_fft_row<KM>(aE, o, z, 1, d);
-      if (v0) acc_fft_row<KM>(aE, neg0, z, 3, d);
-      if (v1) acc_fft_row<KM>(aE, neg1, z, 3 + v0, d);
-    }
-    __builtin_amdgcn_wave_barrier();
-    stamp(pend | (1ull << 8) | ((unsigned long long)v0 << 9) | ((unsigned long long)v1 << 10) |
-          (inv_dt << 16));
-  }
-  if (l == 0 && nv) {
-    atomicAdd(shard_of(a.nviol_shards), nv);
-    if (a.stats_viol) atomicAdd(shard_of(a.stats_viol), nv);
-  }
-}
-
-template <int KM, bool FFT, bool PAIR = false>
-__global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
-  static_assert(!PAIR || FFT, "the pair form is the FFT form's");
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6;
-  const int l = lane_id();
-  const int d = a.d;
-  const int g = launch_id(a), gp = g - 1;
-  const int cp = a.b & 1, pp = cp ^ 1;
-  const int rd = a.b & 1;
-  const int rw = a.b < a.nb1 ? rd ^ 1 : 0;
-  const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
-  const int nB = gridDim.x - a.nA;
-  const int blk = (int)blockIdx.x;
-  if (blk < a.nA) {
-    // ---- A role: write R_b, then apply the previous batch's entity rows ----
-    const int blk_a = blk;
-    const int nR = a.R.rows;
-    const int wa = blk_a * wpb + wave;
-    const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
-    if (a.b == a.nb1 && wa == 0) fold_shards(a.nviol_shards, a.nviol_total);
-    // items w = wa, wa + S, ...: relation rows w < nR, then entity slots w - nR
-    const int S = a.nA * wpb;
-    for (int w = wa; w < nR; w += S) rel_publish_f<1>(a, w, rd, rw, ra_prev, ra_old);
-    const int k0 = wa >= nR ? wa - nR : wa - nR + ((nR - wa + S - 1) / S) * S;
-    apply_slots_f<1>(a.E, pp, k0, S, a.prev_slots, d, gp);
-    if (a.trace && l == 0) {   // diagnostics (skge_pipe_runner_profile, tools/hole_trace.py)
-      unsigned long long* tr = a.trace + 2 + 6 * (size_t)a.count + 2 * (size_t)wa;
-      tr[0] = ta0;
-      tr[1] = now_10ns();
-    }
-    return;
-  }
-  // ---- B role: score batch b (k_hole_pos's arithmetic), scatter into cp / ra_cur ----
-  const int blk_b = blk - a.nA;
-  if constexpr (PAIR) {
-    hole_pipe_score_pair<KM>(a, smem, blk_b, nB);
-    return;
-  }
-  // FFT: the workgroup's twiddle table, then per wave two transform buffers
-  float2* const tw = reinterpret_cast<float2*>(smem);
-  if constexpr (FFT) {
-    fft_twiddles(tw, a.tw, d);
-    __syncthreads();
-  }
-  float* const wb = FFT ? smem + 2 * d + wave * hole_fft_wave_floats(d) : nullptr;
-  const HolePosLds L(FFT ? smem : smem + wave * hole_pos_lds_floats(d), d);
-  Accum aE = {};   // mode ACC_F32 (0), one copy
-  aE.sum = reinterpret_cast<float*>(a.E.sum[cp]);
-  aE.width = d;
-  const int rstride = 2 * a.R.rw;   // floats per relation accumulator row
-  int nv = 0;
-  for (int w = blk_b * wpb + wave; w < a.count; w += nB * wpb) {
-    float* const racc = reinterpret_cast<float*>(a.R.acc[ra_cur]) +
-                        (size_t)(w % a.R.reps) * a.R.rows * rstride;
-    unsigned long long tt[4] = {0ull, 0ull, 0ull, 0ull};
-    if (a.trace) tt[0] = now_10ns();
-    const long long j = a.start + w;
-    const int4 r4 = a.rec[j];
-    const int r1 = a.rec_n1[j];
-    __builtin_amdgcn_sched_barrier(0);
-    const int s = uni(r4.x), o = uni(r4.y), p = uni(r4.z), neg0 = uni(r4.w);
-    const int neg1 = uni(r1);
-    const int n0r = neg0 >= 0 ? neg0 : s, n1r = neg1 >= 0 ? neg1 : o;
-    float4 es[1], eo[1], rp[1], fs[1], fo[1];
-    load_row4<1>(a.E.P, s, d, es);
-    load_row4<1>(a.E.P, o, d, eo);
-    load_row4<1>(a.E.P, n0r, d, fs);
-    load_row4<1>(a.E.P, n1r, d, fo);
-    int mark = 0;
-    if (l < 4) mark = a.E.pend[pp][sel4(l, s, o, n0r, n1r)];
-    {
-      float4 ra[1];
-      int c;
-      rel_row_f<1>(a.R, p, d, rd, ra_prev, rp, ra, c);
-    }
-    const uint64_t pend = __ballot(mark == gp) & 0xfull;
-    if (a.trace) tt[1] = now_10ns();
-    if (pend) {
-#pragma unroll 1
-      for (int k = 0; k < 4; ++k) {
-        if (!((pend >> k) & 1ull)) continue;
-        ensure_applied_f<1>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err);
-      }
-      if (pend & 1ull) load_row4_sc1<1>(a.E.P, s, d, es);
-      if (pend & 2ull) load_row4_sc1<1>(a.E.P, o, d, eo);
-      if (pend & 4ull) load_row4_sc1<1>(a.E.P, n0r, d, fs);
-      if (pend & 8ull) load_row4_sc1<1>(a.E.P, n1r, d, fo);
-    }
-    if (a.trace) tt[2] = now_10ns();
-    float praw, raw0, raw1;
-    float4 A = {}, B = {};
-    HoleSpec hs;
-    if constexpr (FFT) {
-      hs = hole_fft_forward(wb, tw, d, rp[0], es[0], fs[0], eo[0], fo[0], praw, raw0, raw1);
-    } else {
-      q_lds_dbl(L.R2, rp[0], d);
-      q_lds_dbl(L.O2, eo[0], d);
-      q_lds_dbl(L.Q2, fo[0], d);
-      __builtin_amdgcn_wave_barrier();
-      float4 AB[2];
-      {
-        const float* const b2[2] = {L.O2, L.Q2};
-        corr_quad_b<2>(L.R2, b2, d, AB);
-      }
-      A = AB[0];
-      B = AB[1];
-      praw = hole_score_q(es[0], A);
-      raw0 = hole_score_q(fs[0], A);
-      raw1 = hole_score_q(es[0], B);
-    }
-    const float pf = af_f(a.af, praw), f0 = af_f(a.af, raw0), f1 = af_f(a.af, raw1);
-    const int v0 = uni((neg0 >= 0 && f0 + a.margin > pf) ? 1 : 0);   // hole.py:56
-    const int v1 = uni((neg1 >= 0 && f1 + a.margin > pf) ? 1 : 0);
-    if (a.trace) tt[3] = now_10ns();
-    {
-      const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
-      const int rE = sel4(l, s, o, neg0, neg1);
-      if (l < 4) {
-        commit_slot(a.E.cnt[cp], a.E.touched[cp], rE, cE, 4 * w + l);
-        if (cE > 0) a.E.pend[cp][rE] = g;
-      } else if (l == 4 && v0 + v1 > 0) {
-        atomicAdd(reinterpret_cast<int*>(racc + (size_t)p * rstride + d), 2 * (v0 + v1));
-      }
-    }
-    if (a.trace && l == 0 && v0 + v1 == 0) {
-      unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
-      tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
-      tr[5] = pend;
-    }
-    if (v0 + v1 == 0) continue;
-    nv += v0 + v1;
-    unsigned long long inv_dt = 0ull;            // diagnostics: the inverse-transform phase
-    const float gpf = -af_g_given_f(a.af, pf);   // hole.py:66
-    const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
-    Accum aR = {};   // mode ACC_F32 (0), one copy
-    aR.sum = racc + (size_t)p * rstride;
-    aR.width = d;
-    if constexpr (FFT) {
-      const float* z = hole_fft_rows(wb, tw, d, hs, v0, v1, gpf, g0, g1);
-      if (a.trace) {   // diagnostics: the inverse transforms done (LDS results waited for)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        inv_dt = now_10ns() - tt[3];   // (reported in the flags word's high bits)
-      }
-      acc_fft_row<KM>(aR, 0, z, 2, d);
-      acc_fft_row<KM>(aE, s, z, 0, d);
-      acc_fft_row<KM>(aE, o, z, 1, d);
-      if (v0) acc_fft_row<KM>(aE, neg0, z, 3, d);
-      if (v1) acc_fft_row<KM>(aE, neg1, z, 3 + v0, d);
-    } else {
-      const HoleRows h = hole_pos_rows(L, d, es[0], fs[0], A, B, v0, v1, gpf, g0, g1);
-      acc_q<KM>(aR, 0, h.cr, d, L.U);
-      acc_q<KM>(aE, s, h.cs, d, L.U);
-      acc_q<KM>(aE, o, h.co, d, L.U);
-      if (v0) acc_q<KM>(aE, neg0, h.c0, d, L.U);
-      if (v1) acc_q<KM>(aE, neg1, h.cq, d, L.U);
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (a.trace && l == 0) {   // stamp after issue (no drain)
-      unsigned long long* tr = a.trace + 2 + 6 * (size_t)w;
-      tr[0] = tt[0]; tr[1] = tt[1]; tr[2] = tt[2]; tr[3] = tt[3]; tr[4] = now_10ns();
-      tr[5] = pend | (1ull << 8) | ((unsigned long long)v0 << 9) | ((unsigned long long)v1 << 10) |
-              (inv_dt << 16);
-    }
-  }
-  if (l == 0 && nv) {
-    atomicAdd(shard_of(a.nviol_shards), nv);
-    if (a.stats_viol) atomicAdd(shard_of(a.stats_viol), nv);
-  }
-}
-
 __global__ void k_pipe_advance(uint64_t* ek) { *ek += 1; }
-
-// HolE, large batches: the fp32 form of k_rel_fold -- float e of row p summed
-// over the replicas in index order (the order rel_row_f's readers used, so the
-// same bits), the count word (float index d of the row) as an int; replicas
-// 1..reps-1 zeroed.  The readers then load replica 0 alone instead of every
-// replica (nb = 2: 16-32 replicas of 800 B per scoring wave).
-__global__ __launch_bounds__(256) void k_rel_fold_f(PipeArgs a) {
-  const int g = launch_id(a);
-  float* acc = reinterpret_cast<float*>(a.R.acc[g % 3]);
-  const int rstride = 2 * a.R.rw, d = a.d;
-  const size_t rrep = (size_t)a.R.rows * rstride;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < rrep;
-       i += (size_t)gridDim.x * blockDim.x) {
-    if ((int)(i % rstride) == d) {   // the count
-      int* ai = reinterpret_cast<int*>(acc);
-      int c = ai[i];
-      for (int k = 1; k < a.R.reps; ++k) {
-        c += ai[k * rrep + i];
-        ai[k * rrep + i] = 0;
-      }
-      ai[i] = c;
-    } else {
-      float v = acc[i];
-      for (int k = 1; k < a.R.reps; ++k) {
-        v += acc[k * rrep + i];
-        acc[k * rrep + i] = 0.0f;
-      }
-      acc[i] = v;
-    }
-  }
-}
 
 // Large TransE batches (RelTab::reps > 1): after batch launch g, fold the
 // relation accumulator copy g % 3's replicas 1..reps-1 into replica 0 (the
@@ -1882,38 +866,35 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
 #define SKGE_PB(K)                                                                        \
   do {                                                                                    \
     const dim3 gr(r->grid[k]), bl(SKGE_PIPE_WG);                                          \
-    if (a.E.own[0]) {   /* large batches: owner marks, grouped owner-row apply */         \
-      if (r->e8) {                                                                        \
+    /* own marks: large batches (grouped owner-row apply); nhot: hot-row replicas */     \
+    const bool gp_ = a.E.own[0] != nullptr, hot_ = a.E.nhot > 0;                          \
+    if (r->e8) {                                                                          \
+      if (gp_) {                                                                          \
         if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, true>), gr, bl, 0, st, a); \
         else hipLaunchKernelGGL((k_pipe_batch<K, false, true, true>), gr, bl, 0, st, a);  \
       } else {                                                                            \
-        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true>), gr, bl, 0, st, a); \
-        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true>), gr, bl, 0, st, a); \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true>), gr, bl, 0, st, a);  \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, true>), gr, bl, 0, st, a);        \
       }                                                                                   \
-    } else if (r->e8) {                                                                   \
-      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true>), gr, bl, 0, st, a);    \
-      else hipLaunchKernelGGL((k_pipe_batch<K, false, true>), gr, bl, 0, st, a);          \
+    } else if (hot_) {                                                                    \
+      if (gp_) {                                                                          \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true, true>), gr, bl, 0, st, a); \
+      } else {                                                                            \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, false, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, false, true>), gr, bl, 0, st, a); \
+      }                                                                                   \
+    } else if (gp_) {                                                                     \
+      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true>), gr, bl, 0, st, a); \
+      else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true>), gr, bl, 0, st, a);   \
     } else {                                                                              \
       if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false>), gr, bl, 0, st, a);   \
       else hipLaunchKernelGGL((k_pipe_batch<K, false, false>), gr, bl, 0, st, a);         \
     }                                                                                     \
   } while (0)
     if (r->hole) {
-      const dim3 gr(r->grid[k]), bl(r->pair ? 128 : SKGE_PIPE_WG);
-#define SKGE_HPIPE(K)                                                          \
-  if (r->pair)                                                                 \
-    hipLaunchKernelGGL((k_hole_pipe<K, true, true>), gr, bl, r->lds, st, a);   \
-  else if (r->fft)                                                             \
-    hipLaunchKernelGGL((k_hole_pipe<K, true>), gr, bl, r->lds, st, a);         \
-  else                                                                         \
-    hipLaunchKernelGGL((k_hole_pipe<K, false>), gr, bl, r->lds, st, a);
-      switch (km_for(a.d)) {
-        case 1: SKGE_HPIPE(1) break;
-        case 2: SKGE_HPIPE(2) break;
-        case 3: SKGE_HPIPE(3) break;
-        default: SKGE_HPIPE(4) break;
-#undef SKGE_HPIPE
-      }
+      launch_hole_pipe(km_for(a.d), r->pair, r->fft, dim3(r->grid[k]),
+                       dim3(r->pair ? 128 : SKGE_PIPE_WG), r->lds, st, a);
     } else if (r->fused) {
       launch_fused(r, dim3(r->grid[k]), st, a);
     } else if (r->kq <= 1) SKGE_PB(1);
@@ -1923,8 +904,7 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
     if (r->rfold && a.count > 0) {
       const size_t words = (size_t)a.R.rows * a.R.rw;
       if (r->hole)   // fp32 sums + an int count per row
-        hipLaunchKernelGGL(k_rel_fold_f, dim3((unsigned)std::min<size_t>((2 * words + 255) / 256, 4096)),
-                           dim3(256), 0, st, a);
+        launch_rel_fold_f(dim3((unsigned)std::min<size_t>((2 * words + 255) / 256, 4096)), st, a);
       else
         hipLaunchKernelGGL(k_rel_fold, dim3((unsigned)std::min<size_t>((words + 255) / 256, 4096)),
                            dim3(256), 0, st, a);
@@ -1943,6 +923,64 @@ static void fused_finalize(const skge_pipe_runner* r, hipStream_t st) {
   const unsigned blocks = (unsigned)std::max(1ll, std::min((n + 255) / 256, 8192ll));
   hipLaunchKernelGGL(k_fused_fin, dim3(blocks), dim3(256), 0, st, F, r->n_rows, r->d);
   (void)hipMemsetAsync(F.meta, 0, (size_t)r->n_rows * sizeof(int4), st);
+}
+
+// Hot rows (PipeTab::hot): entities whose subject / object occurrences in the
+// KG put them in >= HOT_MIN slots of an average batch -- the hubs of a skewed
+// KG, whose per-batch atomics otherwise serialise on one row.  The HOT_MAX
+// most frequent get replicated sums.  Returns false on an allocation failure.
+__global__ void k_ent_occ(const int* __restrict__ trip, long long T, int* occ) {
+  for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < T;
+       j += (long long)gridDim.x * blockDim.x) {
+    atomicAdd(occ + trip[3 * j], 1);
+    atomicAdd(occ + trip[3 * j + 1], 1);
+  }
+}
+
+static bool find_hot_rows(skge_pipe_runner* r, hipStream_t st, PipeTab& t, const int* trip,
+                          long long T, int nb1, int N, int nq) {
+  t.hot = t.hot_rows = nullptr;
+  t.nhot = 0;
+  int* occ = nullptr;
+  if (hipMalloc(&occ, (size_t)N * 4) != hipSuccess) return false;
+  std::vector<int> h(N);
+  const unsigned blocks = (unsigned)std::max(1ll, std::min((T + 255) / 256, 4096ll));
+  bool ok = hipMemsetAsync(occ, 0, (size_t)N * 4, st) == hipSuccess;
+  hipLaunchKernelGGL(k_ent_occ, dim3(blocks), dim3(256), 0, st, trip, T, occ);
+  ok = ok && hipMemcpyAsync(h.data(), occ, (size_t)N * 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+       hipStreamSynchronize(st) == hipSuccess;
+  (void)hipFree(occ);
+  if (!ok) return false;
+  std::vector<std::pair<int, int>> cand;   // (occurrences, row)
+  for (int i = 0; i < N; ++i)
+    if ((long long)h[i] >= (long long)HOT_MIN * nb1) cand.push_back({h[i], i});
+  if (cand.empty()) return true;
+  std::sort(cand.begin(), cand.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
+    return x.first != y.first ? x.first > y.first : x.second < y.second;
+  });
+  if ((int)cand.size() > HOT_MAX) cand.resize(HOT_MAX);
+  const int nh = (int)cand.size();
+  std::fill(h.begin(), h.end(), -1);
+  std::vector<int> rows(nh);
+  for (int j = 0; j < nh; ++j) {
+    rows[j] = cand[j].second;
+    h[rows[j]] = j;
+  }
+  t.hw = (nq + 15) / 16 * 16;
+  int* dh = (int*)dalloc(r, (size_t)N * 4);
+  int* dr = (int*)dalloc(r, (size_t)nh * 4);
+  for (int k = 0; k < 2; ++k) {
+    t.hsum[k] = (unsigned long long*)dalloc(r, (size_t)nh * HOT_REPS * t.hw * 8);
+    t.hcnt[k] = (int*)dalloc(r, (size_t)nh * HOT_REPS * 4);
+  }
+  if (!dh || !dr || !t.hsum[0] || !t.hsum[1] || !t.hcnt[0] || !t.hcnt[1] ||
+      hipMemcpy(dh, h.data(), (size_t)N * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(dr, rows.data(), (size_t)nh * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return false;
+  t.hot = dh;
+  t.hot_rows = dr;
+  t.nhot = nh;
+  return true;
 }
 
 static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
@@ -2072,6 +1110,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
         t.own[1] = (int*)dalloc(r, (size_t)N * 4);
         ok = ok && t.own[0] && t.own[1];
       }
+      if (ok && !hole && !r->e8) ok = find_hot_rows(r, as_stream(stream), t, trip, T, nb1, N, nq);
     }
     RelTab& q = a.R;
     const int M = rel->rows;
@@ -2189,7 +1228,8 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     }
     // A role: every relation row, then the previous batch's entity slots
     // (owner marks: 64-slot groups)
-    const int a_items = rel->rows + (hole ? 4 * cprev : grouped ? (4 * cprev + 63) / 64 : 4 * cprev);
+    const int a_items = rel->rows + a.E.nhot +
+                        (hole ? 4 * cprev : grouped ? (4 * cprev + 63) / 64 : 4 * cprev);
     // HolE: the apply waves loop over their items within the residency the
     // scoring waves leave (direct form: 2 waves per SIMD at ~180 VGPRs; FFT: 4
     // -- caps 150 / 250 / 400 / 600 / 800 / 1100 on WN18 d = 200: 74.7 / 77.6 /
@@ -2344,6 +1384,10 @@ extern "C" int skge_pipe_runner_error(skge_pipe_runner_t* r, void* stream) {
 
 extern "C" int skge_pipe_runner_nlaunches(const skge_pipe_runner_t* r) {
   return r ? r->nlaunch() : -1;
+}
+
+extern "C" int skge_pipe_runner_hot_rows(const skge_pipe_runner_t* r) {
+  return r ? (r->batch.empty() ? 0 : r->batch[0].E.nhot) : -1;
 }
 
 extern "C" void skge_pipe_runner_destroy(skge_pipe_runner_t* r) { pipe_free(r); }

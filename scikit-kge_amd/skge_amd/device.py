@@ -165,6 +165,7 @@ class EpochRunner(object):
         bs = kg.T // nbatches
         self.nbatches = nbatches
         self._auto = pipelined is None
+        self.hot_rows = 0   # pipelined TransE: entity rows with replicated sums (skewed KGs)
         # d % 4 != 0 (e.g. the reference's d = 50): the packed / pipelined
         # runners work on quads, so they run on zero-padded copies of the
         # tables (width rounded up to 4), copied in and out around every run().
@@ -224,6 +225,7 @@ class EpochRunner(object):
                 self.pipelined = True
                 self.handle = h
                 self.nlaunches = lib.skge_pipe_runner_nlaunches(h)
+                self.hot_rows = lib.skge_pipe_runner_hot_rows(h)
                 return
             err = lib.skge_last_error().decode()
             if not (self._auto and "allocation" in err):
