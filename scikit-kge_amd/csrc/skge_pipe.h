@@ -150,6 +150,34 @@ __device__ __forceinline__ void store_row4_sc1(float* T, int row, int d, const f
                                            (64 * m + l) * 16, 0, AUX_SC1);
 }
 
+// plain 16-B row stores (lanes past the row skipped)
+template <int KQ>
+__device__ __forceinline__ void store_row4(float* T, int row, int d, const float4 (&v)[KQ]) {
+  float4* r = reinterpret_cast<float4*>(T + (size_t)row * d);
+  const int l = lane_id(), nq = d >> 2;
+#pragma unroll
+  for (int m = 0; m < KQ; ++m)
+    if (64 * m + l < nq) r[64 * m + l] = v[m];
+}
+
+// A claimed row's new value and state: while scoring waves of the launch may
+// read it (wt), write-through stores, a drain, then the done word; at the
+// flush (no scoring waves; the next launch sees plain stores) plain stores
+template <int KQ>
+__device__ __forceinline__ void publish_row(const PipeTab& t, int row, int d, const float4 (&p)[KQ],
+                                            const float4 (&a)[KQ], int gp, bool wt) {
+  if (!wt) {
+    store_row4<KQ>(t.P, row, d, p);
+    if (t.A) store_row4<KQ>(t.A, row, d, a);
+    return;
+  }
+  store_row4_sc1<KQ>(t.P, row, d, p);
+  if (t.A) store_row4_sc1<KQ>(t.A, row, d, a);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+  if (lane_id() == 0)
+    __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // load a quad-layout row of P, A (optional) and packed sums (clamped,
 // unconditional loads; lanes past the row read the last quad)
 template <int KQ>
@@ -240,48 +268,14 @@ __device__ __forceinline__ void row_update(const UpdParams& t, int c, int d,
   row_update_s<KQ>(t, c, d, sm, p, a);
 }
 
-// A claimed hot row: add its HOT_REPS replica rows into the packed sums sv
-// (64-bit integer adds: the same words one row would have accumulated), zero
-// the replicas, return the row's count (the sum of the replica counts)
-template <int KQ>
-__device__ __forceinline__ int hot_fold(const PipeTab& t, int pp, int h, int d,
-                                        unsigned long long (&sv)[KQ]) {
-  const int l = lane_id(), nq = d >> 2;
-  unsigned long long* hrow = t.hsum[pp] + (size_t)h * HOT_REPS * t.hw;
-  int* hc = t.hcnt[pp] + h * HOT_REPS;
-  const int c = wave_sum_int(l < HOT_REPS ? hc[l] : 0);
-  // four replicas per round trip (a deeper batch would raise the whole
-  // kernel's register count, and with it cut every launch's residency)
-#pragma unroll 1
-  for (int k0 = 0; k0 < HOT_REPS; k0 += 4) {
-    unsigned long long x[4][KQ];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int m = 0; m < KQ; ++m) {
-        const int q = 64 * m + l;
-        x[k][m] = q < nq ? hrow[(size_t)(k0 + k) * t.hw + q] : 0ull;
-      }
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int m = 0; m < KQ; ++m) {
-        const int q = 64 * m + l;
-        sv[m] += x[k][m];
-        if (q < nq) hrow[(size_t)(k0 + k) * t.hw + q] = 0ull;
-      }
-  }
-  if (l < HOT_REPS) hc[l] = 0;
-  return c;
-}
-
 // Claim a pending entity row's update (the first wave to swap its count out
 // applies it) and, if claimed, apply it from accumulator copy `pp` and publish
 // it as launch `gp` (write-through stores, drain, done word).  The row's sums,
 // parameters and state are loaded in the same memory round trip as the claim:
 // nobody writes them before the claim is won, and a loser discards them.
-template <int KQ, bool E8 = false, bool HOT = false>
-__device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int row, int d, int gp) {
+template <int KQ, bool E8 = false>
+__device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int row, int d, int gp,
+                                                bool wt = true) {
   const int l = lane_id(), nq = d >> 2;
   int c = 0;
   if (l == 0) c = atomicExch(t.cnt[pp] + row, 0);
@@ -308,10 +302,6 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
   }
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row
-  if (HOT) {
-    const int h = t.hot[row];
-    if (h >= 0) c = hot_fold<KQ>(t, pp, h, d, sv);
-  }
   // a field may have wrapped: 16-bit fields past 32767, 8-bit fields past 127
   if (c > (E8 ? 127 : PACKED_MAX) && l == 0) atomicOr(t.err, ERR_PACKED);
   row_update<KQ, false>(t.u, c, d, sv, sv, p, a);
@@ -325,10 +315,67 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
         srow[q] = 0ull;
     }
   }
-  store_row4_sc1<KQ>(t.P, row, d, p);
-  if (t.A) store_row4_sc1<KQ>(t.A, row, d, a);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
-  if (l == 0) __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  publish_row<KQ>(t, row, d, p, a, gp, wt);
+  if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
+}
+
+// Hot row h (PipeTab::hot; applied only by its dedicated A-role item): the
+// claim, the row's parameters and state, the replica counts and all replica
+// sums in ONE round trip (the row's own sums stay zero: every contribution
+// went to a replica), the replicas added as 64-bit words -- the words one row
+// would have accumulated -- and zeroed, then claim_and_apply's update and
+// write-through publish.  Scoring waves reading a pending hot row wait for it.
+template <int KQ>
+__device__ __forceinline__ void claim_and_apply_hot(const PipeTab& t, int pp, int h, int d,
+                                                    int gp, bool wt) {
+  const int l = lane_id(), nq = d >> 2;
+  const int row = __builtin_amdgcn_readfirstlane(t.hot_rows[h]);
+  int c = 0;
+  if (l == 0) c = atomicExch(t.cnt[pp] + row, 0);
+  unsigned long long* hrow = t.hsum[pp] + (size_t)h * HOT_REPS * t.hw;
+  int* hc = t.hcnt[pp] + h * HOT_REPS;
+  const int cl = l < HOT_REPS ? hc[l] : 0;
+  float4 p[KQ], a[KQ];
+  const float4* prow = reinterpret_cast<const float4*>(t.P + (size_t)row * d);
+  const float4* arow = reinterpret_cast<const float4*>(t.A + (size_t)row * d);
+  // replicas per round trip: all of them at one quad per lane (a few dozen
+  // VGPRs: the A role's registers stay under the scoring role's)
+  constexpr int G = KQ == 1 ? HOT_REPS : 4;
+  unsigned long long sv[KQ], x[G][KQ];
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
+    sv[m] = 0ull;
+    p[m] = prow[qc];
+    a[m] = t.A ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+#pragma unroll 1
+  for (int k0 = 0; k0 < HOT_REPS; k0 += G) {
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) {
+        const int q = 64 * m + l;
+        x[k][m] = q < nq ? hrow[(size_t)(k0 + k) * t.hw + q] : 0ull;
+      }
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+#pragma unroll
+      for (int m = 0; m < KQ; ++m) sv[m] += x[k][m];
+  }
+  if (__builtin_amdgcn_readfirstlane(c) == 0) return;   // the row has no update this batch
+  c = wave_sum_int(cl);
+#pragma unroll
+  for (int k = 0; k < HOT_REPS; ++k)
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+      const int q = 64 * m + l;
+      if (q < nq) hrow[(size_t)k * t.hw + q] = 0ull;
+    }
+  if (l < HOT_REPS) hc[l] = 0;
+  if (c > PACKED_MAX && l == 0) atomicOr(t.err, ERR_PACKED);
+  row_update<KQ, false>(t.u, c, d, sv, sv, p, a);
+  publish_row<KQ>(t, row, d, p, a, gp, wt);
   if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
 }
 
@@ -338,12 +385,15 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
 // drain, then the done words -- instead of a claim / load / store / drain
 // chain per row.
 #ifndef SKGE_PIPE_GRP_ROWS
-#define SKGE_PIPE_GRP_ROWS 4   // WN18 nb = 2, same box: 8 rows 467 M, 4 rows 482-488 M (124 -> 85 VGPRs)
+// WN18 nb = 2, same box: 8 rows 467 M, 4 rows 482-488 M (124 -> 85 VGPRs);
+// round 5 (with the flush's plain stores; 4 -> 2 rows: 90 -> 77 VGPRs, 5 -> 6
+// waves per SIMD): 4 rows 521-523 M, 2 rows 530 M, 1 row 503 M
+#define SKGE_PIPE_GRP_ROWS 2
 #endif
 constexpr int GRP_ROWS = SKGE_PIPE_GRP_ROWS;
 template <int KQ, bool E8>
 __device__ __forceinline__ void claim_and_apply_rows(const PipeTab& t, int pp, int rl, int n,
-                                                     int d, int gp) {
+                                                     int d, int gp, bool wt) {
   const int l = lane_id(), nq = d >> 2;
   int c = 0;
   if (l < n) c = atomicExch(t.cnt[pp] + rl, 0);   // lane j holds row j (j < n)
@@ -388,12 +438,20 @@ __device__ __forceinline__ void claim_and_apply_rows(const PipeTab& t, int pp, i
           t.sum[pp][(size_t)row[j] * nq + q] = 0ull;
       }
     }
-    store_row4_sc1<KQ>(t.P, row[j], d, p[j]);
-    if (t.A) store_row4_sc1<KQ>(t.A, row[j], d, a[j]);
+    if (wt) {
+      store_row4_sc1<KQ>(t.P, row[j], d, p[j]);
+      if (t.A) store_row4_sc1<KQ>(t.A, row[j], d, a[j]);
+    } else {   // the flush: no reader in this launch
+      store_row4<KQ>(t.P, row[j], d, p[j]);
+      if (t.A) store_row4<KQ>(t.A, row[j], d, a[j]);
+    }
   }
   if (!any) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
-  if (l < n && c != 0) __hip_atomic_store(t.done + rl, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (wt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+    if (l < n && c != 0)
+      __hip_atomic_store(t.done + rl, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (t.claims && l == 0) {
     int k = 0;
 #pragma unroll

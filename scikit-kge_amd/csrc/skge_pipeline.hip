@@ -76,13 +76,14 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
     const int total = nRH + (ownp ? (a.prev_slots + 63) / 64 : a.prev_slots);
     const int wa = blk_a * wpb + (threadIdx.x >> 6);
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
+    const bool wt = a.b < a.nb1;   // the flush scores nothing: plain stores
     if (a.b == a.nb1 && wa == 0)   // the flush: fold the epoch's violation count
       fold_shards(a.nviol_shards, a.nviol_total);
     for (int w = wa; w < total; w += a.nA * wpb) {
       if (w < nR) {
         rel_publish<KQ, W32>(a, w, rd, rw, ra_prev, ra_old);
       } else if (w < nRH) {
-        claim_and_apply<KQ, E8, HOT>(a.E, pp, a.E.hot_rows[w - nR], d, gp);
+        if (HOT) claim_and_apply_hot<KQ>(a.E, pp, w - nR, d, gp, wt);
       } else if (ownp) {
         // 64 slots: their rows and owner marks in two vector loads; only the
         // slot each row's owner mark names applies it (no claim on duplicates)
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
               }
             }
             const int rl = __builtin_amdgcn_ds_bpermute(src << 2, r);
-            claim_and_apply_rows<KQ, E8>(a.E, pp, rl, n, d, gp);
+            claim_and_apply_rows<KQ, E8>(a.E, pp, rl, n, d, gp, wt);
             m &= ~tk;
           }
         } else {
@@ -116,12 +117,12 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
             const int k = __ffsll((unsigned long long)m) - 1;
             m &= m - 1;
             const int row = __builtin_amdgcn_readlane(r, k);
-            claim_and_apply<KQ, E8, HOT>(a.E, pp, row, d, gp);
+            claim_and_apply<KQ, E8>(a.E, pp, row, d, gp, wt);
           }
         }
       } else {
         const int row = __builtin_amdgcn_readfirstlane(a.E.touched[pp][w - nRH]);
-        if (row >= 0) claim_and_apply<KQ, E8, HOT>(a.E, pp, row, d, gp);
+        if (row >= 0) claim_and_apply<KQ, E8>(a.E, pp, row, d, gp, wt);
       }
     }
     if (a.trace && l == 0) {
@@ -406,15 +407,6 @@ __device__ __forceinline__ void zero_sums_row(void* S, int* cnt, int row, int d)
     }
   }
   if (l == 0) cnt[row] = 0;
-}
-
-template <int KQ>
-__device__ __forceinline__ void store_row4(float* T, int row, int d, const float4 (&v)[KQ]) {
-  const int l = lane_id(), nq = d >> 2;
-  float4* base = reinterpret_cast<float4*>(T + (size_t)row * d);
-#pragma unroll
-  for (int m = 0; m < KQ; ++m)
-    if (64 * m + l < nq) base[64 * m + l] = v[m];
 }
 
 template <int KQ, bool W32, bool E8>
