@@ -549,6 +549,7 @@ def main():
         del r2
 
     pipelined, nlaunches = runner.pipelined, runner.nlaunches
+    hot_rows = getattr(runner, "hot_rows", 0)
     acc_names = {"entity": acc_label(runner.accE), "relation": acc_label(runner.accR)}
     launch_us_max = max_over_ranks(prof["dominant"]["avg_us"], world, dev)
     line = None
@@ -625,6 +626,7 @@ def main():
                 "launches_per_step": nlaunches,
                 "runner": "pipelined (1 launch/batch)" if pipelined else "two-launch",
                 "accumulator": acc_names,
+                "hot_rows": hot_rows,   # entity rows with replicated sums (skewed KGs)
                 "per_replica_value": round(rank_value, 1),
                 "large_batch": large,
                 "rank_setup": info,

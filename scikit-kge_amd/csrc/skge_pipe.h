@@ -20,7 +20,13 @@ constexpr int PACKED_MAX = 32767;
 enum : int { ERR_WAIT = 1, ERR_PACKED = 2 };
 // hot rows (PipeTab::hot): replicas per row, the expected slots per batch
 // that make a row hot, at most this many hot rows
-constexpr int HOT_REPS = 16, HOT_MIN = 16, HOT_MAX = 64;
+#ifndef SKGE_HOT_REPS
+#define SKGE_HOT_REPS 4
+#endif
+#ifndef SKGE_HOT_MIN
+#define SKGE_HOT_MIN 16
+#endif
+constexpr int HOT_REPS = SKGE_HOT_REPS, HOT_MIN = SKGE_HOT_MIN, HOT_MAX = 256;
 
 struct UpdParams {
   int opt, post;
@@ -40,13 +46,15 @@ struct PipeTab {               // entity table
   int* done;                   // [rows]: id of the launch whose update of the row was last applied
   // hot rows (skewed KGs): rows expected in >= HOT_MIN slots per batch add
   // their sums and counts into HOT_REPS replicas (positive w into replica
-  // w % HOT_REPS) instead of one row, record no slot, and are applied by a
-  // dedicated A-role item; their count word holds a nonzero marker
+  // w % HOT_REPS) instead of one row and record no slot or mark; their values
+  // live in hP / hA during a run (hot_value), and readers never wait for them
   const int* hot;              // [rows]: hot index h, or -1 (nullptr: no hot rows)
   const int* hot_rows;         // [nhot]: the hot rows
   int nhot, hw;                // hw: 8-B words per replica row (sums, whole 128-B lines)
-  unsigned long long* hsum[2]; // [nhot][HOT_REPS][hw] by batch parity
-  int* hcnt[2];                // [nhot][HOT_REPS]
+  unsigned long long* hsum[3]; // [nhot][HOT_REPS][hw] by launch id % 3
+  int* hcnt[3];                // [nhot][HOT_REPS] by launch id % 3
+  float* hP[2];                // [nhot][d]: the value after launch g in hP[g & 1]
+  float* hA[2];                // AdaGrad state likewise (nullptr: SGD)
   UpdParams u;
   int* claims;                 // profile only: rows applied in this launch (sharded)
   int* err;                    // ERR_* bits
@@ -319,27 +327,27 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
   if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
 }
 
-// Hot row h (PipeTab::hot; applied only by its dedicated A-role item): the
-// claim, the row's parameters and state, the replica counts and all replica
-// sums in ONE round trip (the row's own sums stay zero: every contribution
-// went to a replica), the replicas added as 64-bit words -- the words one row
-// would have accumulated -- and zeroed, then claim_and_apply's update and
-// write-through publish.  Scoring waves reading a pending hot row wait for it.
+// Hot rows (PipeTab::hot): nobody waits for them.  Their values live in two
+// buffers by launch-id parity -- hP[g & 1] holds the value after launch g's
+// update -- and their sums / counts in three replica copies by launch id % 3
+// (launch g adds into copy g % 3, consumes (g-1) % 3, zeroes (g-2) % 3).  The
+// value a launch-g reader needs is the one after batch b-1's update: the
+// previous value hP[(g-1) & 1] updated with copy (g-1) % 3 -- inputs nobody
+// writes during launch g -- so every reader computes it itself, with the
+// applier's code (the same bits), in one round trip: the row, its state, the
+// replica counts and all replica sums (added as 64-bit words: the words one
+// row would have accumulated).  Returns the count (0: no update; p, a = the
+// previous value and state).  Lanes past the row end with zeros.
 template <int KQ>
-__device__ __forceinline__ void claim_and_apply_hot(const PipeTab& t, int pp, int h, int d,
-                                                    int gp, bool wt) {
+__device__ __forceinline__ int hot_value(const PipeTab& t, int h, int g, int d, float4 (&p)[KQ],
+                                         float4 (&a)[KQ]) {
   const int l = lane_id(), nq = d >> 2;
-  const int row = __builtin_amdgcn_readfirstlane(t.hot_rows[h]);
-  int c = 0;
-  if (l == 0) c = atomicExch(t.cnt[pp] + row, 0);
-  unsigned long long* hrow = t.hsum[pp] + (size_t)h * HOT_REPS * t.hw;
-  int* hc = t.hcnt[pp] + h * HOT_REPS;
-  const int cl = l < HOT_REPS ? hc[l] : 0;
-  float4 p[KQ], a[KQ];
-  const float4* prow = reinterpret_cast<const float4*>(t.P + (size_t)row * d);
-  const float4* arow = reinterpret_cast<const float4*>(t.A + (size_t)row * d);
-  // replicas per round trip: all of them at one quad per lane (a few dozen
-  // VGPRs: the A role's registers stay under the scoring role's)
+  const int src = (g - 1) & 1, cp = (g - 1) % 3;
+  const float4* prow = reinterpret_cast<const float4*>(t.hP[src] + (size_t)h * d);
+  const float4* arow = reinterpret_cast<const float4*>(t.hA[src] + (size_t)h * d);
+  const unsigned long long* hrow = t.hsum[cp] + (size_t)h * HOT_REPS * t.hw;
+  const int cl = l < HOT_REPS ? t.hcnt[cp][h * HOT_REPS + l] : 0;
+  // replicas per round trip
   constexpr int G = KQ == 1 ? HOT_REPS : 4;
   unsigned long long sv[KQ], x[G][KQ];
 #pragma unroll
@@ -347,7 +355,7 @@ __device__ __forceinline__ void claim_and_apply_hot(const PipeTab& t, int pp, in
     const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
     sv[m] = 0ull;
     p[m] = prow[qc];
-    a[m] = t.A ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    a[m] = t.hA[src] ? arow[qc] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
 #pragma unroll 1
   for (int k0 = 0; k0 < HOT_REPS; k0 += G) {
@@ -363,8 +371,29 @@ __device__ __forceinline__ void claim_and_apply_hot(const PipeTab& t, int pp, in
 #pragma unroll
       for (int m = 0; m < KQ; ++m) sv[m] += x[k][m];
   }
-  if (__builtin_amdgcn_readfirstlane(c) == 0) return;   // the row has no update this batch
-  c = wave_sum_int(cl);
+  const int c = wave_sum_int(cl);
+  if (c) {
+    row_update<KQ, false>(t.u, c, d, sv, sv, p, a);   // (zeroes the lanes past the row)
+  } else {
+#pragma unroll
+    for (int m = 0; m < KQ; ++m)
+      if (64 * m + l >= nq) p[m] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  return c;
+}
+
+// Launch g's item for hot row h: its value after the launch into hP[g & 1]
+// (plain stores: read only by later launches), the replica copy two launches
+// old zeroed (launch g + 1 adds into it)
+template <int KQ>
+__device__ __forceinline__ void apply_hot(const PipeTab& t, int h, int g, int d) {
+  const int l = lane_id(), nq = d >> 2;
+  float4 p[KQ], a[KQ];
+  const int c = hot_value<KQ>(t, h, g, d, p, a);
+  store_row4<KQ>(t.hP[g & 1], h, d, p);
+  if (t.hA[0]) store_row4<KQ>(t.hA[g & 1], h, d, a);
+  const int old = (g - 2) % 3;
+  unsigned long long* hrow = t.hsum[old] + (size_t)h * HOT_REPS * t.hw;
 #pragma unroll
   for (int k = 0; k < HOT_REPS; ++k)
 #pragma unroll
@@ -372,11 +401,9 @@ __device__ __forceinline__ void claim_and_apply_hot(const PipeTab& t, int pp, in
       const int q = 64 * m + l;
       if (q < nq) hrow[(size_t)k * t.hw + q] = 0ull;
     }
-  if (l < HOT_REPS) hc[l] = 0;
+  if (l < HOT_REPS) t.hcnt[old][h * HOT_REPS + l] = 0;
   if (c > PACKED_MAX && l == 0) atomicOr(t.err, ERR_PACKED);
-  row_update<KQ, false>(t.u, c, d, sv, sv, p, a);
-  publish_row<KQ>(t, row, d, p, a, gp, wt);
-  if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
+  if (c && t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
 }
 
 // Large batches: up to GRP_ROWS owner rows of a 64-slot group at once -- all
@@ -463,14 +490,11 @@ __device__ __forceinline__ void claim_and_apply_rows(const PipeTab& t, int pp, i
 // B role: make sure launch gp's update of entity `row` (pending at launch
 // start) has landed -- apply it if nobody has claimed it yet, else wait for
 // its publisher
-// (a hot row is only waited for: its dedicated A-role item, dispatched ahead
-// of the slots, applies it, and the replica fold stays out of the B role's
-// registers)
 template <int KQ, bool E8 = false>
 __device__ __forceinline__ void ensure_applied(const PipeTab& t, int pp, int row, int d, int gp,
-                                               int* err, bool hot = false) {
+                                               int* err) {
   if (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gp) return;
-  if (!hot) claim_and_apply<KQ, E8>(t, pp, row, d, gp);
+  claim_and_apply<KQ, E8>(t, pp, row, d, gp);
   unsigned spins = 0;
   while (__hip_atomic_load(t.done + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gp) {
     __builtin_amdgcn_s_sleep(2);

@@ -76,14 +76,17 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
     const int total = nRH + (ownp ? (a.prev_slots + 63) / 64 : a.prev_slots);
     const int wa = blk_a * wpb + (threadIdx.x >> 6);
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
-    const bool wt = a.b < a.nb1;   // the flush scores nothing: plain stores
+#ifndef SKGE_PIPE_FLUSH_PLAIN
+#define SKGE_PIPE_FLUSH_PLAIN 1
+#endif
+    const bool wt = !SKGE_PIPE_FLUSH_PLAIN || a.b < a.nb1;   // the flush scores nothing: plain stores
     if (a.b == a.nb1 && wa == 0)   // the flush: fold the epoch's violation count
       fold_shards(a.nviol_shards, a.nviol_total);
     for (int w = wa; w < total; w += a.nA * wpb) {
       if (w < nR) {
         rel_publish<KQ, W32>(a, w, rd, rw, ra_prev, ra_old);
       } else if (w < nRH) {
-        if (HOT) claim_and_apply_hot<KQ>(a.E, pp, w - nR, d, gp, wt);
+        if (HOT) apply_hot<KQ>(a.E, w - nR, g, d);
       } else if (ownp) {
         // 64 slots: their rows and owner marks in two vector loads; only the
         // slot each row's owner mark names applies it (no claim on duplicates)
@@ -197,13 +200,28 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
 #pragma unroll 1
       for (int k = 0; k < 4; ++k) {
         if (!((unpub >> k) & 1ull)) continue;
-        ensure_applied<KQ, E8>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err,
-                               HOT && __builtin_amdgcn_readlane(hx, k) >= 0);
+        ensure_applied<KQ, E8>(a.E, pp, sel4(k, s, o, n0r, n1r), d, gp, a.err);
       }
       if (pend & 1ull) load_row4_sc1<KQ>(a.E.P, s, d, es);
       if (pend & 2ull) load_row4_sc1<KQ>(a.E.P, o, d, eo);
       if (pend & 4ull) load_row4_sc1<KQ>(a.E.P, n0r, d, fs);
       if (pend & 8ull) load_row4_sc1<KQ>(a.E.P, n1r, d, fo);
+    }
+    if (HOT) {   // hot rows: the value after batch b-1's update, computed here
+      const uint64_t hm = __ballot(hx >= 0) & 0xfull;
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) {
+        if (!((hm >> k) & 1ull)) continue;
+        float4 hv[KQ], ha[KQ];
+        hot_value<KQ>(a.E, __builtin_amdgcn_readlane(hx, k), g, d, hv, ha);
+#pragma unroll
+        for (int m = 0; m < KQ; ++m) {
+          if (k == 0) es[m] = hv[m];
+          if (k == 1) eo[m] = hv[m];
+          if (k == 2) fs[m] = hv[m];
+          if (k == 3) fo[m] = hv[m];
+        }
+      }
     }
     if (a.trace) tt[2] = now_10ns();
     float ps = 0.0f, n0 = 0.0f, n1 = 0.0f;
@@ -237,12 +255,8 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
       // counts, touched slots and pending marks of this batch
       const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
       const int rE = sel4(l, s, o, neg0, neg1);
-      if (HOT && l < 4 && hx >= 0) {   // hot row: count into its replica, marker, no slot record
-        if (cE > 0) {
-          atomicAdd(a.E.hcnt[cp] + hx * HOT_REPS + (w & (HOT_REPS - 1)), cE);
-          cnt_cp[rE] = 1;
-          pend_cp[rE] = g;
-        }
+      if (HOT && l < 4 && hx >= 0) {   // hot row: count into its replica, no slot record
+        if (cE > 0) atomicAdd(a.E.hcnt[g % 3] + hx * HOT_REPS + (w & (HOT_REPS - 1)), cE);
         tch_cp[4 * w + l] = -1;
       } else if (l < 4) {
         commit_slot(cnt_cp, tch_cp, rE, cE, 4 * w + l);
@@ -282,7 +296,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
         // a hot row's sums go to replica w % HOT_REPS
         auto base = [&](int k, int row) {
           const int h = HOT ? __builtin_amdgcn_readlane(hx, k) : -1;
-          return h >= 0 ? a.E.hsum[cp] + ((size_t)h * HOT_REPS + (w & (HOT_REPS - 1))) * a.E.hw
+          return h >= 0 ? a.E.hsum[g % 3] + ((size_t)h * HOT_REPS + (w & (HOT_REPS - 1))) * a.E.hw
                         : esum + (size_t)row * nq;
         };
         add_row4_i16<KQ>(base(0, s), cs, d);
@@ -907,6 +921,45 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
   if (ev) (void)hipEventRecord(ev[i + 1], st);
 }
 
+// Hot rows around a run: before the first launch g0 (from the epoch key) the
+// caller's rows into hP / hA[(g0 - 1) & 1]; after the last (the flush, id
+// g0 - 1 of the next epoch key) hP / hA[that & 1] back into the caller's
+// tables and every replica copy cleared, so a run may start at any key.
+__global__ __launch_bounds__(256) void k_hot_io(PipeTab t, int nb1, const uint64_t* ek, int d,
+                                                int back) {
+  const int g0 = (int)(*ek * (uint64_t)(nb1 + 1)) + 2;   // launch_id of batch 0
+  const int b = (g0 - 1) & 1;
+  const long long n = (long long)t.nhot * d;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int h = (int)(i / d), e = (int)(i - (long long)h * d);
+    const size_t off = (size_t)t.hot_rows[h] * d + e;
+    if (back) {
+      t.P[off] = t.hP[b][i];
+      if (t.A) t.A[off] = t.hA[b][i];
+    } else {
+      t.hP[b][i] = t.P[off];
+      if (t.A) t.hA[b][i] = t.A[off];
+    }
+  }
+  if (back) {
+    const long long nw = (long long)t.nhot * HOT_REPS * t.hw, nc = (long long)t.nhot * HOT_REPS;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nw;
+         i += (long long)gridDim.x * blockDim.x) {
+      for (int k = 0; k < 3; ++k) t.hsum[k][i] = 0ull;
+      if (i < nc)
+        for (int k = 0; k < 3; ++k) t.hcnt[k][i] = 0;
+    }
+  }
+}
+
+static void hot_io(const skge_pipe_runner* r, hipStream_t st, bool back) {
+  if (r->batch.empty() || r->batch[0].E.nhot == 0) return;
+  const PipeArgs& a = r->batch[0];
+  hipLaunchKernelGGL(k_hot_io, dim3(64), dim3(256), 0, st, a.E, a.nb1, a.epoch_key, a.d,
+                     back ? 1 : 0);
+}
+
 // fused runner: every row back into the caller's tables (buffer 0), meta cleared
 static void fused_finalize(const skge_pipe_runner* r, hipStream_t st) {
   if (!r->fused) return;
@@ -930,7 +983,8 @@ __global__ void k_ent_occ(const int* __restrict__ trip, long long T, int* occ) {
 }
 
 static bool find_hot_rows(skge_pipe_runner* r, hipStream_t st, PipeTab& t, const int* trip,
-                          long long T, int nb1, int N, int nq) {
+                          long long T, int nb1, int N, int d) {
+  const int nq = d / 4;
   t.hot = t.hot_rows = nullptr;
   t.nhot = 0;
   int* occ = nullptr;
@@ -961,11 +1015,18 @@ static bool find_hot_rows(skge_pipe_runner* r, hipStream_t st, PipeTab& t, const
   t.hw = (nq + 15) / 16 * 16;
   int* dh = (int*)dalloc(r, (size_t)N * 4);
   int* dr = (int*)dalloc(r, (size_t)nh * 4);
-  for (int k = 0; k < 2; ++k) {
+  bool got = dh && dr;
+  for (int k = 0; k < 3; ++k) {
     t.hsum[k] = (unsigned long long*)dalloc(r, (size_t)nh * HOT_REPS * t.hw * 8);
     t.hcnt[k] = (int*)dalloc(r, (size_t)nh * HOT_REPS * 4);
+    got = got && t.hsum[k] && t.hcnt[k];
   }
-  if (!dh || !dr || !t.hsum[0] || !t.hsum[1] || !t.hcnt[0] || !t.hcnt[1] ||
+  for (int k = 0; k < 2; ++k) {
+    t.hP[k] = (float*)dalloc(r, (size_t)nh * d * 4);
+    t.hA[k] = t.A ? (float*)dalloc(r, (size_t)nh * d * 4) : nullptr;
+    got = got && t.hP[k] && (!t.A || t.hA[k]);
+  }
+  if (!got ||
       hipMemcpy(dh, h.data(), (size_t)N * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(dr, rows.data(), (size_t)nh * 4, hipMemcpyHostToDevice) != hipSuccess)
     return false;
@@ -1102,7 +1163,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
         t.own[1] = (int*)dalloc(r, (size_t)N * 4);
         ok = ok && t.own[0] && t.own[1];
       }
-      if (ok && !hole && !r->e8) ok = find_hot_rows(r, as_stream(stream), t, trip, T, nb1, N, nq);
+      if (ok && !hole && !r->e8) ok = find_hot_rows(r, as_stream(stream), t, trip, T, nb1, N, d);
     }
     RelTab& q = a.R;
     const int M = rel->rows;
@@ -1296,7 +1357,9 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
 
 extern "C" int skge_pipe_runner_run(skge_pipe_runner_t* r, void* stream, int nepochs) {
   SKGE_CHECK_ARG(r && r->exec, "bad runner");
+  hot_io(r, as_stream(stream), false);
   for (int i = 0; i < nepochs; ++i) SKGE_CHECK_HIP(hipGraphLaunch(r->exec, as_stream(stream)));
+  hot_io(r, as_stream(stream), true);
   fused_finalize(r, as_stream(stream));
   SKGE_CHECK_LAUNCH("pipelined runner finalize");
   return SKGE_OK;
@@ -1334,7 +1397,9 @@ extern "C" int skge_pipe_runner_profile(skge_pipe_runner_t* r, void* stream, flo
     }
   }
   if (rc == SKGE_OK) {
+    hot_io(r, st, false);
     enqueue_epoch(r, st, ev.data(), r->stats, trace_launch, dtrace);
+    hot_io(r, st, true);
     fused_finalize(r, st);
     if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) rc = SKGE_EHIP;
   }

@@ -241,24 +241,6 @@ def test_pipelined_runner_bitwise_equals_two_launch(n_ent, n_rel, T, d, nb, monk
             assert np.array_equal(a[k], b[k]), (k, mode)
 
 
-@pytest.mark.parametrize("nb", [100, 10])
-def test_pipelined_hot_rows_bitwise_on_skewed_kg(nb):
-    """A Zipf(1.1)-skewed WN18-sized KG (bench.py --skew zipf): its hub
-    entities' sums and counts go to 16 replicas each (k_pipe_batch's hot
-    rows, folded by the row's apply); the result must still equal the
-    two-launch loop bit for bit.  (At nb = 2 the hub's per-batch count passes
-    the packed sums' 32767, so neither runner takes packed sums there.)"""
-    from bench import make_zipf_kg
-    trip = make_zipf_kg()
-    a, _ = _runner_result(40943, 18, len(trip), 200, nb, pipelined=False, trip=trip)
-    b, _ = _runner_result(40943, 18, len(trip), 200, nb, pipelined=True, trip=trip)
-    assert b["hot"] > 0
-    assert a["key"] == b["key"] == 2
-    assert a["nviol"] == b["nviol"] > 0
-    for k in ("E", "R", "pE", "pR"):
-        assert np.array_equal(a[k], b[k]), k
-
-
 def test_trainer_device_loop_fit():
     import skge_amd as S
     np.random.seed(42)

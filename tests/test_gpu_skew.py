@@ -17,24 +17,63 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n_ent,n_rel,T,d,nb", [
-    (2000, 11, 12000, 64, 10),        # hot rows in every batch
-    (40943, 18, 141442, 200, 100),    # WN18 geometry, skewed
-    (40943, 18, 141442, 200, 10),     # WN18 skewed at nb = 10: 14k positives per batch, packed
-                                      # sums from the per-batch (binomial) count bound
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb,fused", [
+    (2000, 11, 12000, 64, 10, "1"),       # hot rows in every batch (k_pipe_fused: no replicas)
+    (2000, 11, 12000, 64, 10, "0"),       # the same on k_pipe_batch: hot-row replicas
+    (40943, 18, 141442, 200, 100, None),  # WN18 geometry, skewed (hot-row replicas)
+    (40943, 18, 141442, 200, 10, None),   # WN18 skewed at nb = 10: 14k positives per batch,
+                                          # packed sums from the per-batch (binomial) count bound
 ])
-def test_pipelined_transe_bitwise_equals_two_launch_on_zipf(n_ent, n_rel, T, d, nb):
+def test_pipelined_transe_bitwise_equals_two_launch_on_zipf(n_ent, n_rel, T, d, nb, fused,
+                                                            monkeypatch):
+    """k_pipe_batch gives the hub rows 16 replicas of their sums and counts,
+    and every scoring wave that reads a hub computes its value itself
+    (hot_value, the applier's code): still the two-launch loop bit for bit."""
     from bench import make_zipf_kg
     from test_gpu_device_loop import _runner_result
+    if fused is not None:
+        monkeypatch.setenv("SKGE_PIPE_FUSED", fused)
     trip = make_zipf_kg(n_ent, n_rel, T, seed=3)
     top = np.bincount(np.concatenate([trip[:, 0], trip[:, 1]])).max()
     assert top > 10 * 2 * T / n_ent   # the KG is skewed: the hottest row is far above average
     a, _ = _runner_result(n_ent, n_rel, T, d, nb, pipelined=False, trip=trip)
     b, _ = _runner_result(n_ent, n_rel, T, d, nb, pipelined=True, trip=trip)
+    assert (b["hot"] > 0) == (fused != "1"), b["hot"]
     assert a["key"] == b["key"] == 2
     assert a["nviol"] == b["nviol"] > 0
     for k in ("E", "R", "pE", "pR"):
         assert np.array_equal(a[k], b[k]), k
+
+
+def test_pipelined_hot_rows_across_runs():
+    """Hot rows live in the runner's own buffers during a run (copied in
+    before the first launch, back after the flush): two run(1) calls must
+    equal one run(2) bit for bit, and the tables between runs must hold the
+    trained values."""
+    import skge_amd as S
+    from bench import make_zipf_kg
+    from skge_amd.device import DeviceKG, EpochRunner
+
+    def train(calls):
+        np.random.seed(5)
+        m = S.TransE((2000, 2000, 11), 200)
+        m.add_hyperparam("margin", 2.0)
+        upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
+        kg = DeviceKG(make_zipf_kg(2000, 11, 12000, seed=3), m.device)
+        r = EpochRunner(m, upd, kg, nbatches=10, seed=7, pipelined=True)
+        assert r.hot_rows > 0
+        mid = None
+        for k, n in enumerate(calls):
+            r.run(n)
+            r.synchronize()
+            if k == 0:
+                mid = m.E.data.cpu().numpy().copy()
+        return m.E.data.cpu().numpy().copy(), upd["E"].p2.cpu().numpy().copy(), mid
+    e2, a2, _ = train([2])
+    e11, a11, mid = train([1, 1])
+    e1, _, _ = train([1])
+    assert np.array_equal(mid, e1)
+    assert np.array_equal(e2, e11) and np.array_equal(a2, a11)
 
 
 @pytest.mark.parametrize("n_ent,n_rel,T,d,nb,epochs,opt", [
