@@ -20,13 +20,14 @@ constexpr int PACKED_MAX = 32767;
 enum : int { ERR_WAIT = 1, ERR_PACKED = 2 };
 // hot rows (PipeTab::hot): replicas per row, the expected slots per batch
 // that make a row hot, at most this many hot rows
-#ifndef SKGE_HOT_REPS
-#define SKGE_HOT_REPS 4
-#endif
-#ifndef SKGE_HOT_MIN
-#define SKGE_HOT_MIN 16
-#endif
-constexpr int HOT_REPS = SKGE_HOT_REPS, HOT_MIN = SKGE_HOT_MIN, HOT_MAX = 256;
+// hot rows (PipeTab::hot): replicas per row; a row is hot when its expected
+// slots per batch are >= HOT_MIN and >= HOT_REL x the average row's; at most
+// HOT_MAX rows.  WN18 Zipf(1.1), nb = 100, same box: HOT_MIN 16 / 8 / 4 ->
+// 110.6 / 116.1 / 117.4 M triples/s (4 replicas); 16 replicas 108.2 M (the
+// readers' fold: 97 VGPRs, 4 waves per SIMD; 4 replicas: 74 VGPRs, 6).  The
+// relative bar keeps a uniform KG's rows at large batches out (WN18 nb = 2:
+// ~3.5 slots per row and batch; hot rows there cost 531 / 519 vs 540 M).
+constexpr int HOT_REPS = 4, HOT_MIN = 4, HOT_REL = 8, HOT_MAX = 256;
 
 struct UpdParams {
   int opt, post;

@@ -76,10 +76,8 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
     const int total = nRH + (ownp ? (a.prev_slots + 63) / 64 : a.prev_slots);
     const int wa = blk_a * wpb + (threadIdx.x >> 6);
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
-#ifndef SKGE_PIPE_FLUSH_PLAIN
-#define SKGE_PIPE_FLUSH_PLAIN 1
-#endif
-    const bool wt = !SKGE_PIPE_FLUSH_PLAIN || a.b < a.nb1;   // the flush scores nothing: plain stores
+    // the flush scores nothing: plain stores (WN18 nb = 2, same box: 496 -> 539 M)
+    const bool wt = a.b < a.nb1;
     if (a.b == a.nb1 && wa == 0)   // the flush: fold the epoch's violation count
       fold_shards(a.nviol_shards, a.nviol_total);
     for (int w = wa; w < total; w += a.nA * wpb) {
@@ -971,9 +969,10 @@ static void fused_finalize(const skge_pipe_runner* r, hipStream_t st) {
 }
 
 // Hot rows (PipeTab::hot): entities whose subject / object occurrences in the
-// KG put them in >= HOT_MIN slots of an average batch -- the hubs of a skewed
-// KG, whose per-batch atomics otherwise serialise on one row.  The HOT_MAX
-// most frequent get replicated sums.  Returns false on an allocation failure.
+// KG put them in >= HOT_MIN slots of an average batch and >= HOT_REL times the
+// average row's -- the hubs of a skewed KG, pending for most scoring waves and
+// whose per-batch atomics otherwise serialise on one row.  The HOT_MAX most
+// frequent get replicated sums.  Returns false on an allocation failure.
 __global__ void k_ent_occ(const int* __restrict__ trip, long long T, int* occ) {
   for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < T;
        j += (long long)gridDim.x * blockDim.x) {
@@ -997,9 +996,11 @@ static bool find_hot_rows(skge_pipe_runner* r, hipStream_t st, PipeTab& t, const
        hipStreamSynchronize(st) == hipSuccess;
   (void)hipFree(occ);
   if (!ok) return false;
+  // expected slots per batch = occurrences / nb1; the average row's: 2T / N / nb1
+  const double bar = std::max((double)HOT_MIN * nb1, (double)HOT_REL * 2.0 * (double)T / N);
   std::vector<std::pair<int, int>> cand;   // (occurrences, row)
   for (int i = 0; i < N; ++i)
-    if ((long long)h[i] >= (long long)HOT_MIN * nb1) cand.push_back({h[i], i});
+    if ((double)h[i] >= bar) cand.push_back({h[i], i});
   if (cand.empty()) return true;
   std::sort(cand.begin(), cand.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
     return x.first != y.first ? x.first > y.first : x.second < y.second;
