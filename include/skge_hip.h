@@ -417,11 +417,13 @@ int skge_pipe_runner_run(skge_pipe_runner_t *r, void *stream, int nepochs);
 int skge_pipe_runner_error(skge_pipe_runner_t *r, void *stream);
 int skge_pipe_runner_nlaunches(const skge_pipe_runner_t *r);
 /* Hot entity rows of a TransE pipelined runner (hand-off kernel, int16x4
- * sums): rows whose subject/object occurrences put them in >= 16 slots of an
- * average batch (the hubs of a skewed KG), at most 64.  Their per-batch sums
- * and counts are spread over 16 replicas (positive w into replica w % 16)
- * and folded exactly by the row's apply, so a hub's atomics do not serialise
- * on one row; bitwise the same result.  Returns their number (0: none). */
+ * sums): rows whose subject/object occurrences put them in >= 4 slots of an
+ * average batch and >= 8x the average row's (the hubs of a skewed KG), at
+ * most 256.  Their per-batch sums and counts are spread over 4 replicas
+ * (positive w into replica w % 4), and every scoring wave that reads a hub
+ * computes its updated value itself from the replicas (exact integer sums:
+ * bitwise the same result), so nothing waits on a hub and its atomics do not
+ * serialise on one row.  Returns their number (0: none). */
 int skge_pipe_runner_hot_rows(const skge_pipe_runner_t *r);
 /* One epoch launched eagerly (trains like run(1)) with HIP events around every
  * launch: us_out[i] = launch i's duration (i = 0: negative draws, 1..nb1:
