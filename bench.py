@@ -364,7 +364,7 @@ def main():
     ap.add_argument("--c5-scale", type=float, default=1.0,
                     help="config 5 only: scale |E| and T (quick rehearsals)")
     ap.add_argument("--c5-no-counter-split", action="store_true",
-                    help="config 5 only: skip the K extra epochs without update counters")
+                    help="config 5 only: skip the extra epoch that prices the update counters")
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the measured gather roofline (skge_roofline_gather)")
     ap.add_argument("--runner", default="auto", choices=["auto", "pairs", "hole_pipe"],
@@ -1200,21 +1200,16 @@ def run_config5(args):
     elapsed = max_over_ranks(elapsed, world, dev)
     counter_cost = None
     if prof is not None and not args.c5_no_counter_split:
-        # the next K epochs without the update counters: the counters' price
-        # (these are later epochs -- fewer margin violations -- so the split is
-        # an upper bound on what the counters cost, not an exact A/B)
-        e_off, p_off = eager_epochs(runner, kg, nb, d, args.steps, counters=False)
+        # the counters' price at the same epochs: the next epoch's even batches
+        # count their rows, the odd ones do not
+        _, alt = eager_epochs(runner, kg, nb, d, 1, counters="alt")
         counter_cost = {
-            "timed_epochs_ms": round(1000.0 * elapsed / args.steps, 3),
-            "next_epochs_no_counters_ms": round(1000.0 * e_off / args.steps, 3),
-            "apply_us": round(prof["kernels"]["accum_apply"]["avg_us"], 3),
-            "apply_us_no_counters": round(p_off["kernels"]["accum_apply"]["avg_us"], 3),
-            "sample_grad_us": round(prof["kernels"]["transe_sample_grad"]["avg_us"], 3),
-            "sample_grad_us_no_counters":
-                round(p_off["kernels"]["transe_sample_grad"]["avg_us"], 3),
-            "note": "value/frac come from the timed epochs W+1..W+K with the per-row "
-                    "update counters on (they give U for k_apply's 8(d) bytes); epochs "
-                    "W+K+1..W+2K ran without them"}
+            "apply_us_counters": round(alt["apply_us_counters"], 3),
+            "apply_us_no_counters": round(alt["apply_us_no_counters"], 3),
+            "note": "epoch W+K+1, even batches with the per-row update counters "
+                    "(skge/param.py:149-150, AdaGrad's updateCounts -- work the reference "
+                    "does, so the timed epochs keep them; they also give U for k_apply's "
+                    "8(d) bytes), odd batches without"}
     value = replica_value(T * args.steps, world, elapsed)
     if prof is None:
         prof = pipe_profile(runner, kg, nb, d)
@@ -1284,8 +1279,9 @@ def eager_epochs(runner, kg, nb, d, epochs, opt_k=12, counters=True):
     the mean device time over these launches and the SURVEY 8(d) bytes --
     sample_grad 4d(3B + P) + 20B per batch, k_apply k d U with U the counted
     rows -- so frac and ms_per_step come from the same epochs.  counters=False
-    runs the same sequence without the counters (U is then unknown: None),
-    which prices the counter atomics."""
+    "alt" counts on even batches only and returns the mean k_apply time of
+    the counting and the non-counting batches of the same epochs (the
+    counters' price; neighbouring batches apply about as many rows)."""
     import torch
     from skge_amd import _lib as L
     lib = L.lib()
@@ -1294,13 +1290,17 @@ def eager_epochs(runner, kg, nb, d, epochs, opt_k=12, counters=True):
     dev = runner.model.device
     te = L.SkgeTable.from_buffer_copy(runner.te)
     tr = L.SkgeTable.from_buffer_copy(runner.tr)
-    if counters:
-        ucE = torch.zeros(te.rows, dtype=torch.int32, device=dev)
-        ucR = torch.zeros(tr.rows, dtype=torch.int32, device=dev)
-        te.upd_count, tr.upd_count = L.ptr(ucE), L.ptr(ucR)
-    else:
-        te.upd_count = tr.upd_count = None
+    ucE = torch.zeros(te.rows, dtype=torch.int32, device=dev)
+    ucR = torch.zeros(tr.rows, dtype=torch.int32, device=dev)
+    te.upd_count, tr.upd_count = L.ptr(ucE), L.ptr(ucR)
     tabs = (L.SkgeTable * 2)(te, tr)
+    te0 = L.SkgeTable.from_buffer_copy(te)
+    tr0 = L.SkgeTable.from_buffer_copy(tr)
+    te0.upd_count = tr0.upd_count = None
+    tabs0 = (L.SkgeTable * 2)(te0, tr0)
+    # counters: True -> every apply counts its rows; "alt" -> even batches
+    # count, odd ones do not (the counters' price at the same epochs)
+    on = (lambda i: True) if counters is True else (lambda i: i % 2 == 0)
     nviol = torch.zeros(1, dtype=torch.int32, device=dev)
     T = kg.T
     bs = T // nb
@@ -1323,7 +1323,8 @@ def eager_epochs(runner, kg, nb, d, epochs, opt_k=12, counters=True):
                                                     float(runner.model.margin), runner.ntries,
                                                     L.ptr(nviol), None, None), "sample_grad")
                 e[1].record(st)
-                L.check(lib.skge_accum_apply(sp, tabs, 2, L.int_array(4 * cnt, cnt)), "apply")
+                L.check(lib.skge_accum_apply(sp, tabs if on(i - 1) else tabs0, 2,
+                                             L.int_array(4 * cnt, cnt)), "apply")
                 e[2].record(st)
             L.check(lib.skge_epoch_advance(sp, L.ptr(runner.epoch_key)), "advance")
     st.synchronize()
@@ -1332,9 +1333,14 @@ def eager_epochs(runner, kg, nb, d, epochs, opt_k=12, counters=True):
     n = len(ev)
     t_s = sum(e[0].elapsed_time(e[1]) for e in ev) * 1e3 / n
     t_a = sum(e[1].elapsed_time(e[2]) for e in ev) * 1e3 / n
-    U = (int(ucE.sum().item()) + int(ucR.sum().item())) / n if counters else None
+    n_on = sum(1 for i in range(n) if on(i))
+    U = (int(ucE.sum().item()) + int(ucR.sum().item())) / n_on
     b_s = sum(algorithmic_bytes(d, c, 2 * c, 0, 0) for _, c in batches) / len(batches)
-    b_a = float(opt_k) * d * U if counters else 0.0
+    b_a = float(opt_k) * d * U
+    if counters == "alt":
+        t_on = sum(e[1].elapsed_time(e[2]) for i, e in enumerate(ev) if on(i)) * 1e3 / n_on
+        t_off = sum(e[1].elapsed_time(e[2]) for i, e in enumerate(ev) if not on(i)) * 1e3 / (n - n_on)
+        return elapsed, {"apply_us_counters": t_on, "apply_us_no_counters": t_off, "U": U}
     kern = {"transe_sample_grad": {"name": "transe_sample_grad", "avg_us": t_s, "launches": n,
                                    "bytes_per_launch": b_s,
                                    "achieved_gbs": b_s / (t_s * 1e-6) / 1e9},

@@ -1127,7 +1127,7 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_mfma(const float* __restri
   const bool upd = gv != 0;
   if (APPLY && !upd) return;   // the model returned None: no update
   if (APPLY && rem == 0 && tid == 0 && wa.opt == OPT_ADAGRAD && wa.ucnt)
-    wa.ucnt[p] += 1;   // updateCounts, skge/param.py:149-150
+    atomicAdd(wa.ucnt + (p), 1);   // updateCounts, skge/param.py:149-150
   __shared__ float sEs[2][WG_CH][WG_T + 4];
   __shared__ float sEo[2][WG_CH][WG_T + 4];
   const int r0 = rt * WG_T, c0 = ct * WG_T;
@@ -1524,7 +1524,7 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_fin(int d, RescalWs ws, Ac
   const bool upd = gv != 0;
   if (APPLY && !upd) return;   // the model returned None: no update
   if (APPLY && rem == 0 && tid == 0 && wa.opt == OPT_ADAGRAD && wa.ucnt)
-    wa.ucnt[p] += 1;   // updateCounts, skge/param.py:149-150
+    atomicAdd(wa.ucnt + (p), 1);   // updateCounts, skge/param.py:149-150
   const int nch = (cnt + WG_CH - 1) / WG_CH, ngr = (nch + WG_PF - 1) / WG_PF;
   const int nsp = min(splits, ngr);
   const float* part = ws.wpart + (size_t)blk * splits * (WG_T * WG_T);

@@ -66,7 +66,7 @@ __device__ __forceinline__ void update_row(const TableDev& t, int row, const flo
   float* arow = t.A ? t.A + (size_t)row * w : nullptr;
   const bool ada = t.opt == OPT_ADAGRAD;
   float p[KM], a[KM];
-  if (ada && t.ucnt && l == 0) t.ucnt[row] += 1;   // updateCounts[i] += 1  param.py:149-150
+  if (ada && t.ucnt && l == 0) atomicAdd(t.ucnt + (row), 1);   // updateCounts[i] += 1  param.py:149-150
 #pragma unroll
   for (int k = 0; k < KM; ++k) {   // unconditional loads (see load_row)
     const int e = l + 64 * k;
@@ -173,7 +173,7 @@ __device__ __forceinline__ void apply_row(const TableDev& t, int row, bool upd) 
     for (int k = 0; k < KM; ++k)
       if (l + 64 * k < w) fx_check(xrow[l + 64 * k]);
   }
-  if (upd && ada && t.ucnt && l == 0) t.ucnt[row] += 1;   // param.py:149-150
+  if (upd && ada && t.ucnt && l == 0) atomicAdd(t.ucnt + (row), 1);   // param.py:149-150
   const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
   float ss = 0.0f;
 #pragma unroll
@@ -255,7 +255,7 @@ __device__ __forceinline__ void i16_finish(const TableDev& t, int row, bool upd,
   const bool ada = t.opt == OPT_ADAGRAD;
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row, or a stale slot
-  if (upd && ada && t.ucnt && l == 0) t.ucnt[row] += 1;   // param.py:149-150
+  if (upd && ada && t.ucnt && l == 0) atomicAdd(t.ucnt + (row), 1);   // param.py:149-150
   // each occurrence adds a coefficient no larger than its count: c <= 32767
   // means no 16-bit field can have wrapped
   if (c > 32767 && l == 0) atomicOr(&g_skge_dev_err, 2);
@@ -466,7 +466,7 @@ __device__ __forceinline__ void apply_row_rep_block(const TableDev& t, int row, 
         for (int k = 0; k < KR; ++k) p[k] = p[k] / nrm;
       }
     }
-    if (upd && ada && t.ucnt && l == 0) t.ucnt[row] += 1;   // param.py:149-150
+    if (upd && ada && t.ucnt && l == 0) atomicAdd(t.ucnt + (row), 1);   // param.py:149-150
     if (upd) {
 #pragma unroll
       for (int k = 0; k < KR; ++k) {
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(256) void k_apply_wide(TableDev t, int nslots) {
     const float g = (t.acc.sum[off] + t.rin * pv) / div + t.rout * pv;
     t.acc.sum[off] = 0.0f;
     if (gate) {
-      if (e == 0 && t.opt == OPT_ADAGRAD && t.ucnt) t.ucnt[row] += 1;   // param.py:149-150
+      if (e == 0 && t.opt == OPT_ADAGRAD && t.ucnt) atomicAdd(t.ucnt + (row), 1);   // param.py:149-150
       if (t.opt == OPT_ADAGRAD) {
         const float av = t.A[off] + g * g;
         t.A[off] = av;
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(256) void k_update_rows_wide(TableDev t, const floa
     const long long e = q - i * w;
     const size_t off = (size_t)idx[i] * w + e;
     const float gv = g[q];
-    if (e == 0 && t.opt == OPT_ADAGRAD && t.ucnt) t.ucnt[idx[i]] += 1;   // param.py:149-150
+    if (e == 0 && t.opt == OPT_ADAGRAD && t.ucnt) atomicAdd(t.ucnt + (idx[i]), 1);   // param.py:149-150
     if (t.opt == OPT_ADAGRAD) {
       const float av = t.A[off] + gv * gv;
       t.A[off] = av;
@@ -791,7 +791,7 @@ __device__ __forceinline__ void wstep_quad(const WStep& w, long long q) {
   const int rt = tile / nt, ct = tile - rt * nt;
   const int r = rt * WS_T + e / WS_T, c = ct * WS_T + e % WS_T;
   if (r >= w.d || c >= w.d) return;
-  if (tile == 0 && e == 0 && w.opt == OPT_ADAGRAD && w.ucnt) w.ucnt[p] += 1;   // param.py:149-150
+  if (tile == 0 && e == 0 && w.opt == OPT_ADAGRAD && w.ucnt) atomicAdd(w.ucnt + (p), 1);   // param.py:149-150
   // split-K groups of 128 of the relation's dW items (skge_rescal.hip
   // WS_GROUP): splits past its groups wrote nothing
   const int nit = w.dwcnt ? w.dwcnt[p] : cnt;
@@ -838,7 +838,7 @@ __global__ __launch_bounds__(256) void k_apply_wstep(TableDev t0, int n0, WStep 
         *w.cur ^= 1;
         if (w.opt == OPT_ADAGRAD && w.ucnt)   // updateCounts, skge/param.py:149-150
           for (int p = 0; p < w.M; ++p)
-            if (w.rel_off[p + 1] > w.rel_off[p]) w.ucnt[p] += 1;
+            if (w.rel_off[p + 1] > w.rel_off[p]) atomicAdd(w.ucnt + (p), 1);
       }
       return;
     }
