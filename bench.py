@@ -124,6 +124,23 @@ def pmc_traffic(kernel_substr, fname="pmc.json"):
     return None, None
 
 
+def pmc_traffic_epochs(kernel_substr, fname, first, count):
+    """Config 5: a kernel's per-launch traffic averaged over the SAME epochs
+    the line times (first .. first+count-1; epoch 0 = the warm-up), from the
+    newest committed per-epoch PMC summary (tools/pmc_epochs.py)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", fname)))
+    for f in reversed(files):
+        data = json.load(open(f))
+        for name, eps in data.items():
+            if kernel_substr in name:
+                sel = [e for e in eps if first <= e["epoch"] < first + count]
+                if len(sel) == count:
+                    return (sum(e["traffic_bytes_per_launch"] for e in sel) / count,
+                            "%s epochs %d..%d" % (os.path.relpath(f, ROOT), first, first + count - 1))
+    return None, None
+
+
 def dist_env():
     """(world, rank, local_rank) from the torchrun environment (1, 0, 0 alone)."""
     return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
@@ -1215,7 +1232,10 @@ def run_config5(args):
         prof = pipe_profile(runner, kg, nb, d)
     k = prof["dominant"]
     if rank == 0:
-        traffic, traffic_src = pmc_traffic(PMC_KERNEL.get(k["name"], k["name"]), "pmc_c5.json")
+        traffic, traffic_src = pmc_traffic_epochs(PMC_KERNEL.get(k["name"], k["name"]),
+                                                  "pmc_c5_epochs.json", args.warmup, args.steps)
+        if traffic is None:
+            traffic, traffic_src = pmc_traffic(PMC_KERNEL.get(k["name"], k["name"]), "pmc_c5.json")
         line = {
             "metric": "triples/sec (score+grad+update), synthetic TransE |E|=50M |R|=10k d=512, "
                       "B=131072 per GPU (BASELINE configs[4])" +
