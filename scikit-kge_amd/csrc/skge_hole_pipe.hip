@@ -101,13 +101,14 @@ __device__ __forceinline__ void claim_and_apply_f(const PipeTab& t, int pp, int 
   c = __builtin_amdgcn_readfirstlane(c);
   if (c == 0) return;   // another wave owns the row
   row_update_f<KQ>(t.u, c, d, sm, p, a);
-  // only P is read by this launch's scoring waves: it alone is written
-  // through and drained before the done word (skge_pipe.h publish_row)
-  publish_row<KQ>(t, row, d, p, a, gp, true);
   float4* srow = reinterpret_cast<float4*>(S + (size_t)row * d);
 #pragma unroll
   for (int m = 0; m < KQ; ++m)
     if (64 * m + l < nq) srow[64 * m + l] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  store_row4_sc1<KQ>(t.P, row, d, p);
+  if (t.A) store_row4_sc1<KQ>(t.A, row, d, a);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+  if (l == 0) __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
 }
 
@@ -146,11 +147,14 @@ __device__ __forceinline__ void apply_slots_f(const PipeTab& t, int pp, int k0, 
       c = __builtin_amdgcn_readfirstlane(c);
       if (c != 0) {   // this wave owns the row
         row_update_f<KQ>(t.u, c, d, sm, p, a);
-        publish_row<KQ>(t, r, d, p, a, gp, true);
         float4* srow = reinterpret_cast<float4*>(S + (size_t)r * d);
 #pragma unroll
         for (int q = 0; q < KQ; ++q)
           if (64 * q + l < nq) srow[64 * q + l] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        store_row4_sc1<KQ>(t.P, r, d, p);
+        if (t.A) store_row4_sc1<KQ>(t.A, r, d, a);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+        if (l == 0) __hip_atomic_store(t.done + r, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ++nclaim;
       }
       if (rn < 0) break;
