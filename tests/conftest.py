@@ -30,5 +30,7 @@ def pytest_sessionfinish(session, exitstatus):
                    "min_headroom": recs[0][1] if recs else None,
                    "worst": [{"what": w, "headroom": h, "max_abs_err": e, "n": n}
                              for w, h, e, n in recs[:40]],
-                   "all": [[w, h, e, n] for w, h, e, n in recs]}, f, indent=1,
-                  default=lambda x: str(x))
+                   "all": [[w, h, e, n] for w, h, e, n in recs],
+                   # check_step: rows that needed the sign-flip allowance
+                   "flip_rows": [[w, k, n, a] for w, k, n, a in parity_util.FLIPS]},
+                  f, indent=1, default=lambda x: str(x))
