@@ -138,9 +138,14 @@ def check_step(got, want, before, grads, p2_after, lr, what, post=None, opt="ada
         bad = np.abs(got - want) > tol / min_headroom
         raise AssertionError("%s: %d of %d elements past tol/%g, headroom %.3g, max |err| %.3g"
                              % (what, int(bad.sum()), got.size, min_headroom, h, emax))
+    # rows along the last axis: E / R rows, or the d rows of each of RESCAL's
+    # W_p matrices (an element's flip touches its row; a projection moves it)
     plain = np.abs(got - want) > ATOL + RTOL * np.abs(want)
-    nflip = int(plain.reshape(want.shape[0], -1).any(axis=1).sum())
-    nrows = len(np.unique(np.asarray(grads[1]))) if grads is not None else want.shape[0]
+    flat = plain.reshape(-1, want.shape[-1])
+    nflip = int(flat.any(axis=1).sum())
+    per = flat.shape[0] // want.shape[0]      # last-axis rows per first-axis index
+    nrows = (len(np.unique(np.asarray(grads[1]))) * per if grads is not None
+             else flat.shape[0])
     allowed = max(FLIP_ROWS_MIN, int(np.ceil(FLIP_ROWS_FRAC * nrows)))
     FLIPS.append((what, nflip, nrows, allowed))
     if nflip > allowed:
