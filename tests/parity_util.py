@@ -30,8 +30,10 @@ FLIPS = []     # (what, rows past the plain bar, rows checked, allowed)
 # differently.  A real bug that flips signs would do so in many rows, so the
 # rows that need the allowance -- any element past the plain ATOL + RTOL
 # |want| bar -- may be at most FLIP_ROWS_FRAC of the checked rows (at least
-# FLIP_ROWS_MIN).
-FLIP_ROWS_FRAC = 0.02
+# FLIP_ROWS_MIN).  Measured on the full GPU suite: at most 2.6% (RESCAL's W
+# after a runner epoch, every element updated every batch), 1.3% (HolE E);
+# a sign error in the path would put about half of the rows past the bar.
+FLIP_ROWS_FRAC = 0.05
 FLIP_ROWS_MIN = 3
 
 
