@@ -20,6 +20,8 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("n_ent,n_rel,T,d,nb,fused", [
     (2000, 11, 12000, 64, 10, "1"),       # hot rows in every batch (k_pipe_fused: no replicas)
     (2000, 11, 12000, 64, 10, "0"),       # the same on k_pipe_batch: hot-row replicas
+    (2000, 11, 12000, 512, 10, None),     # two quads per lane (hot rows at KQ = 2)
+    (1000, 5, 6000, 1024, 6, None),       # the widest packed row (KQ = 4)
     (40943, 18, 141442, 200, 100, None),  # WN18 geometry, skewed (hot-row replicas)
     (40943, 18, 141442, 200, 10, None),   # WN18 skewed at nb = 10: 14k positives per batch,
                                           # packed sums from the per-batch (binomial) count bound
