@@ -669,11 +669,12 @@ def mark_failure(line, key, msg):
     value (set to null), else detail[key]."""
     if line is None:
         return
+    err = msg if isinstance(msg, dict) else {"error": msg}
     if key is None:
         line["value"] = None
-        line["error"] = msg
+        line.update(err)
     else:
-        line.setdefault("detail", {})[key] = {"error": msg}
+        line.setdefault("detail", {})[key] = err
 
 
 def run_with_watchdog(fn, line, limit, key=None):
@@ -703,7 +704,11 @@ def run_with_watchdog(fn, line, limit, key=None):
     try:
         out = fn()
     except Exception as e:
-        out = {"error": "%s: %s" % (type(e).__name__, e)}
+        import traceback
+        where = traceback.extract_tb(e.__traceback__)[-3:]
+        out = {"error": "%s: %s" % (type(e).__name__, e),
+               "where": ["%s:%d %s" % (os.path.basename(f.filename), f.lineno, f.name)
+                         for f in where]}
     with lock:
         done.set()
         if state["printed"]:
@@ -910,7 +915,7 @@ def run_dp(args):
     m = run_with_watchdog(lambda: measure_dp(args, dev, nb, args.warmup, args.steps), skel, limit)
     if failed(m):
         if rank == 0:
-            mark_failure(skel, None, m["error"])
+            mark_failure(skel, None, m)
             print(json.dumps(skel), flush=True)
         os._exit(WATCHDOG_EXIT)     # ranks may be out of step in a failed collective
     line = dp_line(args, world, m, m.get("phases"), nb=nb, info=info) if rank == 0 else None
@@ -939,7 +944,7 @@ def run_dp(args):
     det = run_with_watchdog(details, line, limit, key="details")
     if rank == 0:
         if failed(det):
-            mark_failure(line, "details", det["error"])
+            mark_failure(line, "details", det)
         else:
             line["detail"].update(det)
         print(json.dumps(line), flush=True)
