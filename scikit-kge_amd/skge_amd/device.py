@@ -215,6 +215,10 @@ class EpochRunner(object):
                   _os.environ.get("SKGE_PIPE_E8", "1") != "0")
             self._tables(model, updaters, packed, 1, rel_w32=rel_reps != 1, ent_i8=e8,
                          pad=self._pad)
+            # the tables' zero-filled accumulators were made on the current
+            # stream; the runner works on its own (a reused allocation could
+            # otherwise hold a freed runner's counts when the first launch runs)
+            torch.cuda.current_stream().synchronize()
             self.ent_i8 = e8
             h = lib.skge_pipe_runner_create(
                 L.stream_ptr(self.stream), self.te, self.tr,
@@ -244,6 +248,7 @@ class EpochRunner(object):
                                  "accumulator copies hold; use packed=None or force_f32=True")
             packed = False
         self._tables(model, updaters, packed, max(int(replicas), rel_reps) if packed else replicas)
+        torch.cuda.current_stream().synchronize()   # (as above)
         h = lib.skge_runner_create(L.stream_ptr(self.stream), int(bool(model.l1)),
                                    self.te, self.tr,
                                    model.d, L.ptr(kg.trip), kg.T, L.ptr(kg.slots), kg.capacity,
@@ -327,11 +332,15 @@ class EpochRunner(object):
         torch.cuda.current_stream().wait_stream(self.stream)
 
     def run(self, nepochs=1):
+        """nepochs epochs on the runner's stream, ordered after the caller's
+        stream (parameters it wrote) and before its later work."""
         lib = L.lib()
         fn = lib.skge_pipe_runner_run if self.pipelined else lib.skge_runner_run
+        self.stream.wait_stream(torch.cuda.current_stream())
         self._pad_in()
         L.check(fn(self.handle, L.stream_ptr(self.stream), int(nepochs)), "runner run")
         self._pad_out()
+        torch.cuda.current_stream().wait_stream(self.stream)
 
     def profile(self, trace_launch=None):
         """Pipelined runner only: one eager epoch with HIP events around every
@@ -347,6 +356,7 @@ class EpochRunner(object):
         stats = np.zeros((n, 3), dtype=np.int32)
         tr = np.zeros(2 + 6 * self.kg.T + 8 * self.kg.T + 64, dtype=np.uint64) \
             if trace_launch else None
+        self.stream.wait_stream(torch.cuda.current_stream())
         EpochRunner._pad_in(self)   # (also HolePipeRunner.profile: no padded tables there)
         L.check(L.lib().skge_pipe_runner_profile(
             self.handle, L.stream_ptr(self.stream), us.ctypes.data, stats.ctypes.data, n,
@@ -438,8 +448,10 @@ class HolePipeRunner(object):
         return isinstance(model, HolE) and d % 4 == 0 and 4 <= d <= 256
 
     def run(self, nepochs=1):
+        self.stream.wait_stream(torch.cuda.current_stream())
         L.check(L.lib().skge_pipe_runner_run(self.handle, L.stream_ptr(self.stream),
                                              int(nepochs)), "hole runner run")
+        torch.cuda.current_stream().wait_stream(self.stream)
 
     profile = EpochRunner.profile
 
@@ -514,8 +526,10 @@ class PairLoopRunner(object):
         self.nlaunches = lib.skge_pair_runner_nlaunches(h)
 
     def run(self, nepochs=1):
+        self.stream.wait_stream(torch.cuda.current_stream())
         L.check(L.lib().skge_pair_runner_run(self.handle, L.stream_ptr(self.stream),
                                              int(nepochs)), "pair runner run")
+        torch.cuda.current_stream().wait_stream(self.stream)
 
     def synchronize(self):
         self.stream.synchronize()

@@ -253,9 +253,13 @@ class DataParallelRunner(object):
         torch.cuda.current_stream().wait_stream(self.stream)
 
     def run(self, nepochs=1):
+        # ordered after the caller's stream (parameters it wrote), and its later
+        # work after the epochs
+        self.stream.wait_stream(torch.cuda.current_stream())
         self._pad_in()
         self._run(nepochs)
         self._pad_out()
+        torch.cuda.current_stream().wait_stream(self.stream)
 
     def _run(self, nepochs):
         with torch.cuda.stream(self.stream):

@@ -307,7 +307,9 @@ class ShardedRunner(object):
         """nepochs epochs.  With capture (the "nccl" backend, or one process)
         the first epoch runs eagerly and is then captured -- kernels and RCCL
         collectives -- into one CUDA graph that later epochs replay: no host
-        read or host-side size anywhere in an epoch."""
+        read or host-side size anywhere in an epoch.  Ordered after the
+        caller's stream, and its later work after the epochs."""
+        self.stream.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.stream):
             for _ in range(int(nepochs)):
                 if not self.capture:
@@ -321,6 +323,7 @@ class ShardedRunner(object):
                     self.graph = g
                 else:
                     self.graph.replay()
+        torch.cuda.current_stream().wait_stream(self.stream)
 
     def synchronize(self):
         self.stream.synchronize()
