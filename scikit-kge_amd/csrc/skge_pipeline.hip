@@ -68,9 +68,6 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
   const int blk_a = blk, blk_b = blk - a.nA;
   if (blk < a.nA) {
     // ---- A role: write R_b, then apply the previous batch's entity rows ----
-#ifdef SKGE_PIPE_APRIO
-    __builtin_amdgcn_s_setprio(SKGE_PIPE_APRIO);   // experiment: appliers first at issue
-#endif
     const int nR = a.R.rows;
     // owner marks (large batches): items are groups of 64 slots, scanned
     // lane-parallel; else one slot per item
