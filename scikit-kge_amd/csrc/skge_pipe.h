@@ -178,9 +178,6 @@ __device__ __forceinline__ void store_row4(float* T, int row, int d, const float
 // write-through and drained before the done word; the state and the zeroed
 // packed sums follow as plain stores after it (the kernel boundary publishes
 // them), keeping them out of the drain the waiters wait on.
-#ifndef SKGE_PIPE_PUB_P
-#define SKGE_PIPE_PUB_P 1
-#endif
 template <int KQ>
 __device__ __forceinline__ void publish_row(const PipeTab& t, int row, int d, const float4 (&p)[KQ],
                                             const float4 (&a)[KQ], int gp, bool wt) {
@@ -190,11 +187,10 @@ __device__ __forceinline__ void publish_row(const PipeTab& t, int row, int d, co
     return;
   }
   store_row4_sc1<KQ>(t.P, row, d, p);
-  if (!SKGE_PIPE_PUB_P && t.A) store_row4_sc1<KQ>(t.A, row, d, a);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
   if (lane_id() == 0)
     __hip_atomic_store(t.done + row, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (SKGE_PIPE_PUB_P && t.A) store_row4<KQ>(t.A, row, d, a);
+  if (t.A) store_row4<KQ>(t.A, row, d, a);
 }
 
 // load a quad-layout row of P, A (optional) and packed sums (clamped,
@@ -324,21 +320,18 @@ __device__ __forceinline__ void claim_and_apply(const PipeTab& t, int pp, int ro
   // a field may have wrapped: 16-bit fields past 32767, 8-bit fields past 127
   if (c > (E8 ? 127 : PACKED_MAX) && l == 0) atomicOr(t.err, ERR_PACKED);
   row_update<KQ, false>(t.u, c, d, sv, sv, p, a);
-  auto zero_sums = [&]() {
-#pragma unroll
-    for (int m = 0; m < KQ; ++m) {
-      const int q = 64 * m + l;
-      if (q < nq) {
-        if (E8)
-          srow8[q] = 0u;
-        else
-          srow[q] = 0ull;
-      }
-    }
-  };
-  if (!SKGE_PIPE_PUB_P) zero_sums();
   publish_row<KQ>(t, row, d, p, a, gp, wt);
-  if (SKGE_PIPE_PUB_P) zero_sums();
+  // the consumed sums zeroed after the publish (publish_row)
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l;
+    if (q < nq) {
+      if (E8)
+        srow8[q] = 0u;
+      else
+        srow[q] = 0ull;
+    }
+  }
   if (t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
 }
 
@@ -472,7 +465,6 @@ __device__ __forceinline__ void claim_and_apply_rows(const PipeTab& t, int pp, i
     row_update<KQ, false>(t.u, cj, d, sv[j], sv[j], p[j], a[j]);
     if (wt) {
       store_row4_sc1<KQ>(t.P, row[j], d, p[j]);
-      if (!SKGE_PIPE_PUB_P && t.A) store_row4_sc1<KQ>(t.A, row[j], d, a[j]);
     } else {   // the flush: no reader in this launch
       store_row4<KQ>(t.P, row[j], d, p[j]);
     }
@@ -483,12 +475,12 @@ __device__ __forceinline__ void claim_and_apply_rows(const PipeTab& t, int pp, i
     if (l < n && c != 0)
       __hip_atomic_store(t.done + rl, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // the state (unless already written through) and the zeroed sums: plain
-  // stores after the done words (publish_row)
+  // the state and the zeroed sums: plain stores after the done words
+  // (publish_row)
 #pragma unroll
   for (int j = 0; j < GRP_ROWS; ++j) {
     if (j >= n || __builtin_amdgcn_readlane(c, j) == 0) continue;
-    if ((!wt || SKGE_PIPE_PUB_P) && t.A) store_row4<KQ>(t.A, row[j], d, a[j]);
+    if (t.A) store_row4<KQ>(t.A, row[j], d, a[j]);
 #pragma unroll
     for (int m = 0; m < KQ; ++m) {
       const int q = 64 * m + l;
