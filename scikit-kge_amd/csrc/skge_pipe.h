@@ -27,13 +27,8 @@ enum : int { ERR_WAIT = 1, ERR_PACKED = 2 };
 // readers' fold: 97 VGPRs, 4 waves per SIMD; 4 replicas: 74 VGPRs, 6).  The
 // relative bar keeps a uniform KG's rows at large batches out (WN18 nb = 2:
 // ~3.5 slots per row and batch; hot rows there cost 531 / 519 vs 540 M).
-#ifndef SKGE_HOT_MIN
-#define SKGE_HOT_MIN 4
-#endif
-#ifndef SKGE_HOT_REL
-#define SKGE_HOT_REL 8
-#endif
-constexpr int HOT_REPS = 4, HOT_MIN = SKGE_HOT_MIN, HOT_REL = SKGE_HOT_REL, HOT_MAX = 256;
+// (HOT_MIN 2 / 3, HOT_REL 4: within noise of these, same box)
+constexpr int HOT_REPS = 4, HOT_MIN = 4, HOT_REL = 8, HOT_MAX = 256;
 
 struct UpdParams {
   int opt, post;
