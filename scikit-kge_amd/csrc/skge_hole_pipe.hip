@@ -388,11 +388,7 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
   }
 }
 
-// ROLE: 0 = both roles in one launch (workgroups < nA apply); 1 = the apply
-// role alone (grid nA); 2 = the scoring role alone (grid nB) -- the split form
-// runs 1 and 2 on parallel branches of the epoch graph, so the apply waves
-// get their own (small) register budget
-template <int KM, bool FFT, bool PAIR = false, int ROLE = 0>
+template <int KM, bool FFT, bool PAIR = false>
 __global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
   static_assert(!PAIR || FFT, "the pair form is the FFT form's");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -404,9 +400,9 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
   const int rd = a.b & 1;
   const int rw = a.b < a.nb1 ? rd ^ 1 : 0;
   const int ra_prev = (g - 1) % 3, ra_cur = g % 3, ra_old = (g - 2) % 3;
-  const int nB = ROLE == 2 ? (int)gridDim.x : (int)gridDim.x - a.nA;
-  const int blk = (int)blockIdx.x + (ROLE == 2 ? a.nA : 0);
-  if (ROLE == 1 || (ROLE == 0 && blk < a.nA)) {
+  const int nB = gridDim.x - a.nA;
+  const int blk = (int)blockIdx.x;
+  if (blk < a.nA) {
     // ---- A role: write R_b, then apply the previous batch's entity rows ----
     const int blk_a = blk;
     const int nR = a.R.rows;
@@ -596,22 +592,14 @@ __global__ __launch_bounds__(256) void k_rel_fold_f(PipeArgs a) {
 }
 
 void launch_hole_pipe(int km, bool pair, bool fft, dim3 gr, dim3 bl, size_t lds, hipStream_t st,
-                      const PipeArgs& a, int role) {
-#define SKGE_HPIPE_R(K, R)                                                     \
-  if (pair)                                                                    \
-    hipLaunchKernelGGL((k_hole_pipe<K, true, true, R>), gr, bl, lds, st, a);   \
-  else if (fft)                                                                \
-    hipLaunchKernelGGL((k_hole_pipe<K, true, false, R>), gr, bl, lds, st, a);  \
-  else                                                                         \
-    hipLaunchKernelGGL((k_hole_pipe<K, false, false, R>), gr, bl, lds, st, a);
+                      const PipeArgs& a) {
 #define SKGE_HPIPE(K)                                                          \
-  if (role == 1) {                                                             \
-    SKGE_HPIPE_R(K, 1)                                                         \
-  } else if (role == 2) {                                                      \
-    SKGE_HPIPE_R(K, 2)                                                         \
-  } else {                                                                     \
-    SKGE_HPIPE_R(K, 0)                                                         \
-  }
+  if (pair)                                                                    \
+    hipLaunchKernelGGL((k_hole_pipe<K, true, true>), gr, bl, lds, st, a);      \
+  else if (fft)                                                                \
+    hipLaunchKernelGGL((k_hole_pipe<K, true>), gr, bl, lds, st, a);            \
+  else                                                                         \
+    hipLaunchKernelGGL((k_hole_pipe<K, false>), gr, bl, lds, st, a);
   switch (km) {
     case 1: SKGE_HPIPE(1) break;
     case 2: SKGE_HPIPE(2) break;
@@ -619,7 +607,6 @@ void launch_hole_pipe(int km, bool pair, bool fft, dim3 gr, dim3 bl, size_t lds,
     default: SKGE_HPIPE(4) break;
   }
 #undef SKGE_HPIPE
-#undef SKGE_HPIPE_R
 }
 
 void launch_rel_fold_f(dim3 gr, hipStream_t st, const PipeArgs& a) {

@@ -616,7 +616,7 @@ constexpr int HPIPE_OCC = 2;   // HolE: scoring waves per SIMD the apply-workgro
 
 // skge_hole_pipe.hip's launchers (host side)
 void launch_hole_pipe(int km, bool pair, bool fft, dim3 gr, dim3 bl, size_t lds, hipStream_t st,
-                      const PipeArgs& a, int role = 0);
+                      const PipeArgs& a);
 void launch_rel_fold_f(dim3 gr, hipStream_t st, const PipeArgs& a);
 
 }  // namespace skge

@@ -810,9 +810,6 @@ struct skge_pipe_runner {
   size_t lds = 0;                  // HolE: dynamic LDS per workgroup
   bool pair = false;               // HolE FFT, d = 200: two waves per positive (SKGE_HPIPE_PAIR)
   bool fused = false;              // TransE: k_pipe_fused (nothing waits; d <= 64 by default)
-  bool hsplit = false;             // HolE: the two roles as two kernels (SKGE_HPIPE_SPLIT=1)
-  hipStream_t st2 = nullptr;       // hsplit: the apply branch's stream
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int n_rows = 0, d = 0;           // fused: the entity table's geometry (k_fused_fin)
   int nlaunch() const { return (int)batch.size() + 2; }
 };
@@ -828,9 +825,6 @@ static void* dalloc(skge_pipe_runner* r, size_t bytes) {
 static void pipe_free(skge_pipe_runner* r) {
   (void)hipGetLastError();   // a failed allocation must not poison later launch checks
   if (!r) return;
-  if (r->ev_fork) (void)hipEventDestroy(r->ev_fork);
-  if (r->ev_join) (void)hipEventDestroy(r->ev_join);
-  if (r->st2) (void)hipStreamDestroy(r->st2);
   if (r->exec) (void)hipGraphExecDestroy(r->exec);
   if (r->graph) (void)hipGraphDestroy(r->graph);
   for (void* p : r->bufs) (void)hipFree(p);
@@ -902,18 +896,7 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
       else hipLaunchKernelGGL((k_pipe_batch<K, false, false>), gr, bl, 0, st, a);         \
     }                                                                                     \
   } while (0)
-    if (r->hole && r->hsplit && a.count > 0) {
-      // split form: the apply role on a parallel branch (its own kernel, its
-      // own register budget), the scoring role here; joined before the next
-      const dim3 bl(r->pair ? 128 : SKGE_PIPE_WG);
-      (void)hipEventRecord(r->ev_fork, st);
-      (void)hipStreamWaitEvent(r->st2, r->ev_fork, 0);
-      launch_hole_pipe(km_for(a.d), r->pair, r->fft, dim3(a.nA), bl, 0, r->st2, a, 1);
-      launch_hole_pipe(km_for(a.d), r->pair, r->fft, dim3(r->grid[k] - a.nA), bl, r->lds, st,
-                       a, 2);
-      (void)hipEventRecord(r->ev_join, r->st2);
-      (void)hipStreamWaitEvent(st, r->ev_join, 0);
-    } else if (r->hole) {
+    if (r->hole) {
       launch_hole_pipe(km_for(a.d), r->pair, r->fft, dim3(r->grid[k]),
                        dim3(r->pair ? 128 : SKGE_PIPE_WG), r->lds, st, a);
     } else if (r->fused) {
@@ -1322,17 +1305,6 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     r->grid.push_back(a.nA + (a.count > 0 ? nBb : 0));
   }
   hipStream_t st = as_stream(stream);
-  if (hole) {
-    const char* hs = getenv("SKGE_HPIPE_SPLIT");
-    r->hsplit = hs && atoi(hs) != 0;
-    if (r->hsplit && (hipStreamCreateWithFlags(&r->st2, hipStreamNonBlocking) != hipSuccess ||
-                      hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming) != hipSuccess ||
-                      hipEventCreateWithFlags(&r->ev_join, hipEventDisableTiming) != hipSuccess)) {
-      set_error("pipelined runner: stream / event creation failed");
-      pipe_free(r);
-      return nullptr;
-    }
-  }
   if (hipStreamSynchronize(st) != hipSuccess ||
       hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
     set_error("hipStreamBeginCapture failed");
