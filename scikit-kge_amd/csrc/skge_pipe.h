@@ -608,6 +608,10 @@ __device__ __forceinline__ void rel_publish(const PipeArgs& a, int w, int rd, in
   if (!W32 && c > PACKED_MAX && l == 0) atomicOr(a.err, ERR_PACKED);
 }
 
+// large batches (owner marks, k_pipe_batch's GRP instances): 3-wave
+// workgroups (WN18 nb = 2, same box: 508-510 -> 520 M triples/s; 128: 517 M;
+// nb = 100 unchanged by either, so it keeps SKGE_PIPE_WG)
+constexpr int PIPE_WG_GRP = 192;
 #ifndef SKGE_PIPE_WG
 #define SKGE_PIPE_WG 256   // threads per workgroup
 #endif

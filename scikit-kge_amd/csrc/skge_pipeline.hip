@@ -51,7 +51,7 @@ namespace skge {
 // start the hand-offs the scoring waves may wait on), then the scoring ones.
 // GRP: owner marks, GRP_ROWS owner rows per apply round trip.
 template <int KQ, bool W32, bool E8, bool GRP = false, bool HOT = false>
-__global__ __launch_bounds__(SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
+__global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
   const int d = a.d, nq = d >> 2;
@@ -869,9 +869,9 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
     if (trace && i == trace_launch) a.trace = trace;
 #define SKGE_PB(K)                                                                        \
   do {                                                                                    \
-    const dim3 gr(r->grid[k]), bl(SKGE_PIPE_WG);                                          \
     /* own marks: large batches (grouped owner-row apply); nhot: hot-row replicas */     \
     const bool gp_ = a.E.own[0] != nullptr, hot_ = a.E.nhot > 0;                          \
+    const dim3 gr(r->grid[k]), bl(gp_ ? PIPE_WG_GRP : SKGE_PIPE_WG);                      \
     if (r->e8) {                                                                          \
       if (gp_) {                                                                          \
         if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, true>), gr, bl, 0, st, a); \
@@ -1260,7 +1260,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
            : r->pair ? hole_fft_lds_bytes(d, 1)
            : r->fft ? hole_fft_lds_bytes(d, SKGE_PIPE_WG / 64)
                     : (size_t)(SKGE_PIPE_WG / 64) * hole_pos_lds_floats(d) * sizeof(float);
-  const int WPB = r->pair ? 2 : SKGE_PIPE_WG / 64;
+  const int WPB = r->pair ? 2 : (grouped ? PIPE_WG_GRP : SKGE_PIPE_WG) / 64;
   for (int b = 0; b <= nb1; ++b) {   // b == nb1: flush of the last batch (no scoring)
     a.b = b;
     a.start = b < nb1 ? batches[b].first : 0;
