@@ -103,15 +103,24 @@ def kg_label(args, seed_txt):
     return "synthetic WN18-shaped KG (|E|=40943 |R|=18 T=141442 uniform, %s)" % seed_txt
 
 
+# The round whose committed PMC summaries a line may quote: only the same
+# round's (a line never cites an older kernel's traffic; without this round's
+# summary, traffic is null)
+PMC_ROUND = "r06"
+
+
+def _round_files(fname):
+    f = os.path.join(ROOT, "profiles", PMC_ROUND, fname)
+    return [f] if os.path.exists(f) else []
+
+
 def pmc_traffic(kernel_substr, fname="pmc.json"):
-    """Per-launch HBM-side traffic of a kernel from the newest committed rocprofv3
-    PMC summary (profiles/<round>/<fname>, made by `tools/gpu_run.sh pmc` +
-    tools/pmc_summary.py; pmc.json for the default line, pmc_c<k>.json for
-    config k): 2*FETCH_SIZE + WRITE_SIZE per the gfx950 correction in
-    MI355X_MICROARCH.md "HBM"."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", fname)))
-    for f in reversed(files):
+    """Per-launch HBM-side traffic of a kernel from this round's committed
+    rocprofv3 PMC summary (profiles/<PMC_ROUND>/<fname>, made by
+    `tools/gpu_run.sh pmc` + tools/pmc_summary.py; pmc.json for the default
+    line, pmc_c<k>.json for config k): 2*FETCH_SIZE + WRITE_SIZE per the
+    gfx950 correction in MI355X_MICROARCH.md "HBM"."""
+    for f in _round_files(fname):
         data = json.load(open(f))
         for name, e in data.items():
             if kernel_substr in name and "traffic_bytes_per_launch" in e:
@@ -127,10 +136,8 @@ def pmc_traffic(kernel_substr, fname="pmc.json"):
 def pmc_traffic_epochs(kernel_substr, fname, first, count):
     """Config 5: a kernel's per-launch traffic averaged over the SAME epochs
     the line times (first .. first+count-1; epoch 0 = the warm-up), from the
-    newest committed per-epoch PMC summary (tools/pmc_epochs.py)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", fname)))
-    for f in reversed(files):
+    round's committed per-epoch PMC summary (tools/pmc_epochs.py)."""
+    for f in _round_files(fname):
         data = json.load(open(f))
         for name, eps in data.items():
             if kernel_substr in name:
@@ -297,9 +304,66 @@ def replica_value(positives_per_rank, world, elapsed_max):
     return world * positives_per_rank / elapsed_max
 
 
+def handoff_probe(dev, rounds=2000, reps=3):
+    """skge_handoff_probe: the pipelined runner's publish / wait hand-off (16-B
+    write-through payload, drain, write-through flag; sc1 poll + re-read)
+    ping-ponged between two workgroups.  Reported in the line's detail so a
+    slow box's hand-off chain is visible in the record itself (the headline
+    launch is a chain of such hops).  Best of `reps` runs, us per hop."""
+    import torch
+    from skge_amd import _lib as L
+    lib = L.lib()
+    buf = torch.zeros(256, dtype=torch.int32, device=dev)
+    out = torch.zeros(3, dtype=torch.int64, device=dev)
+    best, bad, gave_up = None, 0, 0
+    for _ in range(reps):
+        L.check(lib.skge_handoff_probe(L.stream_ptr(), L.ptr(buf), rounds, L.ptr(out)),
+                "handoff probe")
+        torch.cuda.synchronize()
+        ticks, b, g = (int(x) for x in out.tolist())
+        us_hop = ticks * 0.01 / (2 * rounds)
+        best = us_hop if best is None else min(best, us_hop)
+        bad += b
+        gave_up |= g
+    return {"us_per_hop": round(best, 4), "us_per_round_trip": round(2 * best, 4),
+            "rounds": rounds, "payload_mismatches": bad, "wait_gave_up": bool(gave_up),
+            "form": "16-B sc1 payload + vmcnt(0) + sc1 flag; sc1 poll + s_sleep(2), sc1 re-read; "
+                    "blocks 0/1 (round-robin: different XCDs), idle chip, best of %d" % reps}
+
+
 def algorithmic_bytes(d, B, P, U_E, U_R, opt_k=12):
     """BYTES(batch) = 4d(3B + P) + k d (U_E + U_R) + 20B."""
     return 4 * d * (3 * B + P) + opt_k * d * (U_E + U_R) + 20 * B
+
+
+# The reference's own pure-NumPy path, measured in the survey container
+# (BASELINE.md table "CPU reference, measured in the survey container":
+# positive triples/s, 8-vCPU Xeon, effectively one thread); it cannot travel to
+# the GPU box, so lines carry it beside their own timed oracle sample
+REFERENCE_CPU = {
+    ("transe", 200, "adagrad"): (21600.0, "score+grad+update only (BASELINE.md config 2)"),
+    ("transe", 50, "sgd"): (44300.0, "end-to-end incl. the Python sampler; no score-only "
+                                     "figure (BASELINE.md config 1)"),
+    ("transe", 50, "adagrad"): (36500.0, "end-to-end incl. the Python sampler (BASELINE.md "
+                                         "config 1')"),
+    ("hole", 200, "adagrad"): (6300.0, "score+grad+update only (BASELINE.md config 3)"),
+    ("rescal", 200, "adagrad"): (6490.0, "score+grad+update only, 5 batches (BASELINE.md "
+                                         "config 4)"),
+    ("transe", 512, "adagrad"): (5600.0, "score+grad+update only, |E|=1M scaled-down table "
+                                         "(BASELINE.md config 5)"),
+}
+
+
+def reference_cpu(model, d, opt):
+    """The reference's own figure for this workload (None if the survey did
+    not measure one)."""
+    v = REFERENCE_CPU.get((model, d, opt))
+    if v is None:
+        return None
+    return {"value": v[0], "unit": "triples/s", "cores": 1, "kind": "reference",
+            "measured": "survey container (8-vCPU Xeon, numpy 2.2.6), not this box: the "
+                        "reference cannot travel to the GPU box",
+            "what": v[1], "source": "BASELINE.md"}
 
 
 def cpu_baseline(trip, d, nb, seconds=12.0, model="transe", margin=2.0, opt="adagrad"):
@@ -350,7 +414,8 @@ def cpu_baseline(trip, d, nb, seconds=12.0, model="transe", margin=2.0, opt="ada
                       % (nb_done, nb, npos, {"transe": "TransE-L1", "hole": "HolE",
                                              "rescal": "RESCAL"}[model], d,
                          {"adagrad": "AdaGrad", "sgd": "SGD"}[opt], margin),
-            "e2e_value": npos / t_all}
+            "e2e_value": npos / t_all,
+            "reference": reference_cpu(model, d, opt)}
 
 
 def main():
@@ -516,9 +581,11 @@ def main():
                                int(round(geo["applied_rows"]))),
                 "avg_launch_us": round(m_us, 3), "bytes_per_launch": round(m_b),
                 "GB_s": round(m_gbs, 1),
-                "frac": round(prof["dominant"].get("impl_gbs", prof["dominant"]["achieved_gbs"])
-                              / m_gbs, 4),
-                "frac_note": "implementation bytes / the same bytes moved without dependencies",
+                "frac_of_same_geometry_kernel":
+                    round(prof["dominant"].get("impl_gbs", prof["dominant"]["achieved_gbs"])
+                          / m_gbs, 4),
+                "frac_note": "implementation bytes / the same bytes moved by a same-geometry "
+                             "kernel without dependencies (itself latency-bound: not a roofline)",
                 "streaming_gather_GB_s": {"wn18_table_33MB": round(s_gbs, 1),
                                           "table_4GB": round(h_gbs, 1)}}
 
@@ -572,6 +639,7 @@ def main():
                  "runner": "pipelined" if r2.pipelined else "two-launch"}
         del r2
 
+    probe = handoff_probe(dev) if runner.pipelined else None
     pipelined, nlaunches = runner.pipelined, runner.nlaunches
     hot_rows = getattr(runner, "hot_rows", 0)
     acc_names = {"entity": acc_label(runner.accE), "relation": acc_label(runner.accR)}
@@ -651,6 +719,7 @@ def main():
                 "runner": "pipelined (1 launch/batch)" if pipelined else "two-launch",
                 "accumulator": acc_names,
                 "hot_rows": hot_rows,   # entity rows with replicated sums (skewed KGs)
+                "handoff_probe": probe,
                 "per_replica_value": round(rank_value, 1),
                 "large_batch": large,
                 "rank_setup": info,
@@ -1148,7 +1217,8 @@ def cpu_baseline_config5(seconds=10.0, n_ent=1_000_000, n_rel=10_000, d=512, bat
                       "SURVEY 6 scaled-down config-5 shape (|E|=%d |R|=%d; the 50M-row fp64 "
                       "table and state do not make a CPU sample); oracle/skge_oracle.py fp64 "
                       "NumPy, 1 thread; score+grad+update only (host sampler untimed)"
-                      % (nbat, batch, d, n_ent, n_rel)}
+                      % (nbat, batch, d, n_ent, n_rel),
+            "reference": reference_cpu("transe", 512, "adagrad")}
 
 
 def make_config5_kg(n_ent, n_rel, n_triples, dev, seed):

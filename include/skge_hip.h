@@ -359,15 +359,18 @@ void skge_pair_runner_destroy(skge_pair_runner_t *r);
  * throughput path).  Same result, bit for bit, as skge_runner_create's loop
  * with the same tables and arguments: all negatives of an epoch are drawn in
  * one launch, then each mini-batch is ONE launch that scores batch b while
- * applying batch b-1's updates.  Below 16k slot records per batch (d <= 512)
- * every wave of a launch scores one positive, applies four slot records of
- * the previous batch and zeroes four of the batch before (k_pipe_fused); a
- * row the previous batch touched is updated by each of its readers itself,
- * from its pre-update value, which stays readable because the applier
- * writes the row's other buffer (the runner's second copy of E and its
- * AdaGrad state; run() and profile() end by copying every row back into the
- * caller's tables).  Larger batches: apply waves beside scoring waves that
- * wait for a pending row's publisher (k_pipe_batch, owner marks).  Needs ent
+ * applying batch b-1's updates.  Below 16k slot records per batch with d <= 64
+ * (the default there; SKGE_PIPE_FUSED=1 forces it up to d <= 256): k_pipe_fused,
+ * whose work items are first one scoring item per positive, then one item per
+ * four slot records of the previous batch (applied) and four of the batch
+ * before (zeroed); a row the previous batch touched is updated by each of its
+ * readers itself, from its pre-update value, which stays readable because the
+ * applier writes the row's other buffer (the runner's second copy of E and
+ * its AdaGrad state; run() and profile() end by copying every row back into
+ * the caller's tables).  Otherwise k_pipe_batch: apply waves beside scoring
+ * waves that wait for a pending row's publisher (below 16k slot records the
+ * apply items walk a touched-row bitmap, 32 rows each; above, owner marks over
+ * the slot records).  Needs ent
  * in SKGE_ACC_I16X4 mode (SKGE_ACC_I8X4: int8x4 sums, counts <= 127), rel in
  * SKGE_ACC_I16X4 or SKGE_ACC_I32X2 mode (the encoding of the relation sums
  * the runner keeps), d % 4 == 0, an entity table with slot records (capacity
@@ -508,6 +511,14 @@ int skge_shard_fold_violations(void *stream, int *vshards, int *nviol_total);
 int skge_roofline_gather(void *stream, float *P, float *A, void *S, int rows, int d, int n_gather,
                          int rows_per_wave, int atom_rows_per_wave, int n_rmw, uint32_t salt,
                          float *out);
+/* Hand-off latency probe: the pipelined runner's publish / wait form (16-B
+ * write-through payload, drain, write-through flag; the waiter polls the flag
+ * and re-reads the payload with write-through loads) ping-ponged `rounds`
+ * times between two workgroups.  buf: >= 1024 device bytes (zeroed here);
+ * out [3] (device u64): out[0] = 10-ns ticks for all rounds (two hops each),
+ * out[1] = payload mismatches (0 expected), out[2] = 1 if a bounded wait gave
+ * up.  Lets a bench line say how slow this box's hand-offs are. */
+int skge_handoff_probe(void *stream, void *buf, int rounds, uint64_t *out);
 
 /* ---------------- evaluation ---------------- */
 

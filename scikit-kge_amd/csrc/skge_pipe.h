@@ -18,8 +18,6 @@ namespace skge {
 // batch size this runner accepts.
 constexpr int PACKED_MAX = 32767;
 enum : int { ERR_WAIT = 1, ERR_PACKED = 2 };
-// hot rows (PipeTab::hot): replicas per row, the expected slots per batch
-// that make a row hot, at most this many hot rows
 // hot rows (PipeTab::hot): replicas per row; a row is hot when its expected
 // slots per batch are >= HOT_MIN and >= HOT_REL x the average row's; at most
 // HOT_MAX rows.  WN18 Zipf(1.1), nb = 100, same box: HOT_MIN 16 / 8 / 4 ->
@@ -46,6 +44,13 @@ struct PipeTab {               // entity table
                                // (plain stores, one survives): the A role applies a row from
                                // that slot only, so duplicate slots cost no claim
   int* done;                   // [rows]: id of the launch whose update of the row was last applied
+  // touched-row bitmaps (k_pipe_batch below 16k slot records): bit r of
+  // bm[parity] set by every scoring lane that records row r; the next launch's
+  // A role gives one item to each 2^bm_shift rows and applies only the set
+  // bits' rows (cleared as it reads them), so the apply waves number
+  // rows / 2^bm_shift instead of one per slot record (nullptr: slot records)
+  unsigned* bm[2];
+  int bm_shift;
   // hot rows (skewed KGs): rows expected in >= HOT_MIN slots per batch add
   // their sums and counts into HOT_REPS replicas (positive w into replica
   // w % HOT_REPS) instead of one row and record no slot or mark; their values
@@ -106,6 +111,7 @@ struct PipeArgs {
   long long start;             // B role: this batch's positives [start, start + count)
   int count;
   int prev_slots;              // A role: entity slots of the previous batch
+  int bm_items;                // A role, bitmap mode: items over the previous batch's bitmap
   int b, nb1;                  // batch index in the epoch (nb1: the flush), batches per epoch
   const uint64_t* epoch_key;
   int d, nA;                   // nA: workgroups of the A role

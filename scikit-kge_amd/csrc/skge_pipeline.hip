@@ -46,6 +46,14 @@
 
 namespace skge {
 
+// touched-row bitmaps below 16k slot records (PipeTab::bm), rows per apply item
+#ifndef SKGE_PIPE_BITMAP
+#define SKGE_PIPE_BITMAP 0
+#endif
+#ifndef SKGE_PIPE_BM_SHIFT
+#define SKGE_PIPE_BM_SHIFT 5
+#endif
+
 // k_pipe_batch (large batches: more than 16k slot records per batch; smaller
 // batches run k_pipe_fused below): nA apply workgroups (dispatched first: they
 // start the hand-offs the scoring waves may wait on), then the scoring ones.
@@ -72,8 +80,9 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
     // owner marks (large batches): items are groups of 64 slots, scanned
     // lane-parallel; else one slot per item
     const int* const ownp = a.E.own[pp];
+    unsigned* const bmp = a.E.bm[pp];
     const int nH = a.E.nhot, nRH = nR + nH;   // then one item per hot row
-    const int total = nRH + (ownp ? (a.prev_slots + 63) / 64 : a.prev_slots);
+    const int total = nRH + (bmp ? a.bm_items : ownp ? (a.prev_slots + 63) / 64 : a.prev_slots);
     const int wa = blk_a * wpb + (threadIdx.x >> 6);
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
     // the flush scores nothing: plain stores (WN18 nb = 2, same box: 496 -> 539 M)
@@ -85,6 +94,28 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
         rel_publish<KQ, W32>(a, w, rd, rw, ra_prev, ra_old);
       } else if (w < nRH) {
         if (HOT) apply_hot<KQ>(a.E, w - nR, g, d);
+      } else if (bmp) {
+        // rows [i << sh, (i + 1) << sh) of the bitmap: the set bits' rows,
+        // GRP_ROWS per claim / load / drain round trip; the bits cleared
+        // (launch g + 1's scoring waves set them again)
+        const int sh = a.E.bm_shift, i = w - nRH;
+        const int r0 = i << sh, wi = r0 >> 5, b0 = r0 & 31;
+        const unsigned msk = sh >= 5 ? 0xffffffffu : ((1u << (1 << sh)) - 1u) << b0;
+        unsigned m = (unsigned)__builtin_amdgcn_readfirstlane((int)bmp[wi]) & msk;
+        if (m && l == 0) atomicAnd(bmp + wi, ~msk);
+        while (m) {
+          // lanes j < n: the rows of m's next n set bits
+          int rl = 0, n = 0;
+#pragma unroll
+          for (int j = 0; j < GRP_ROWS; ++j) {
+            if (!m) break;
+            const int k = __ffs(m) - 1;
+            m &= m - 1u;
+            if (l == j) rl = 32 * wi + k;
+            ++n;
+          }
+          claim_and_apply_rows<KQ, E8>(a.E, pp, rl, n, d, gp, wt);
+        }
       } else if (ownp) {
         // 64 slots: their rows and owner marks in two vector loads; only the
         // slot each row's owner mark names applies it (no claim on duplicates)
@@ -138,6 +169,7 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
   int* const tch_cp = opaque_ptr(a.E.touched[cp]);
   int* const pend_cp = opaque_ptr(a.E.pend[cp]);
   int* const own_cp = a.E.own[cp];
+  unsigned* const bm_cp = a.E.bm[cp];
   unsigned long long* const racc0 = opaque_ptr(a.R.acc[ra_cur]);
   const size_t rrep = (size_t)a.R.rows * a.R.rw;   // words per relation replica
   const int rmask = a.R.reps - 1;                  // reps: a power of two (k_rel_fold)
@@ -257,7 +289,14 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
         if (cE > 0) atomicAdd(a.E.hcnt[g % 3] + hx * HOT_REPS + (w & (HOT_REPS - 1)), cE);
         tch_cp[4 * w + l] = -1;
       } else if (l < 4) {
-        commit_slot(cnt_cp, tch_cp, rE, cE, 4 * w + l);
+        if (bm_cp) {   // touched-row bitmap instead of slot records
+          if (cE > 0) {
+            atomicAdd(cnt_cp + rE, cE);
+            atomicOr(bm_cp + (rE >> 5), 1u << (rE & 31));
+          }
+        } else {
+          commit_slot(cnt_cp, tch_cp, rE, cE, 4 * w + l);
+        }
         if (cE > 0) {
           pend_cp[rE] = g;
           if (own_cp) own_cp[rE] = 4 * w + l;   // large batches: this slot may own the row
@@ -738,11 +777,17 @@ __global__ __launch_bounds__(256) void k_rel_fold(PipeArgs a) {
 }
 
 // draw every negative of the epoch: one thread per positive, the same draws and
-// first-accepted-try rule as k_transe_sample_grad (skge/sample.py:41-46)
+// first-accepted-try rule as k_transe_sample_grad (skge/sample.py:41-46).
+// err (pipelined runners; nullptr elsewhere): once a launch has set an error
+// bit (a wrapped packed sum, a wait that gave up) every later epoch draws no
+// negatives -- no pair, no contribution, no row update -- so the tables are
+// left as the failing epoch left them and the runner refuses further run()s
+// once the error has been read (skge_pipe_runner_error)
 __global__ void k_epoch_sample(const int* __restrict__ trip, long long T, int half, uint64_t seed,
                                const uint64_t* ekp, TripleSet set, int n_ent, int ntries,
-                               int4* rec, int* rec_n1) {
+                               int4* rec, int* rec_n1, const int* err) {
   const uint64_t ek = *ekp;
+  if (err && *err) ntries = 0;
   const Perm pm = {(uint64_t)T, half, epoch_perm_key(seed, ek)};
   const uint64_t skey = epoch_sample_key(seed, ek);
   for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < T;
@@ -775,7 +820,7 @@ int launch_epoch_sample(hipStream_t st, const int* trip, long long T, uint64_t s
   long long blocks = (T + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(k_epoch_sample, dim3((unsigned)blocks), dim3(256), 0, st, trip, T,
-                     perm_half(T), seed, epoch_key, set, n_ent, ntries, rec, rec_n1);
+                     perm_half(T), seed, epoch_key, set, n_ent, ntries, rec, rec_n1, nullptr);
   SKGE_CHECK_LAUNCH("epoch sample");
   return SKGE_OK;
 }
@@ -808,8 +853,9 @@ struct skge_pipe_runner {
   bool fft = false;                // HolE: correlations in the frequency domain (skge_hole_fft.h)
   bool rfold = false;              // TransE: relation sums in replicas, k_rel_fold after each batch
   size_t lds = 0;                  // HolE: dynamic LDS per workgroup
-  bool pair = false;               // HolE FFT, d = 200: two waves per positive (SKGE_HPIPE_PAIR)
+  bool pair = false;               // HolE FFT, d = 200: two waves per positive (while 2 x B waves fit the chip)
   bool fused = false;              // TransE: k_pipe_fused (nothing waits; d <= 64 by default)
+  bool invalid = false;            // an error bit was read or a launch failed: run() refuses
   int n_rows = 0, d = 0;           // fused: the entity table's geometry (k_fused_fin)
   int nlaunch() const { return (int)batch.size() + 2; }
 };
@@ -854,7 +900,7 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(k_epoch_sample, dim3((unsigned)blocks), dim3(256), 0, st, r->trip, r->T,
                        r->half, r->seed, (const uint64_t*)r->epoch_key, r->set, r->n_ent,
-                       r->ntries, r->rec, r->rec_n1);
+                       r->ntries, r->rec, r->rec_n1, (const int*)r->err);
   }
   ++i;
   if (ev) (void)hipEventRecord(ev[i], st);
@@ -1163,6 +1209,13 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
         t.own[0] = (int*)dalloc(r, (size_t)N * 4);
         t.own[1] = (int*)dalloc(r, (size_t)N * 4);
         ok = ok && t.own[0] && t.own[1];
+      } else if (!hole && SKGE_PIPE_BITMAP && ((long long)N >> SKGE_PIPE_BM_SHIFT) < 4 * bs) {
+        // touched-row bitmaps: fewer apply items than slot records
+        t.bm_shift = SKGE_PIPE_BM_SHIFT;
+        for (int k = 0; k < 2; ++k) {
+          t.bm[k] = (unsigned*)dalloc(r, (size_t)((N + 31) / 32) * 4);
+          ok = ok && t.bm[k];
+        }
       }
       if (ok && !hole && !r->e8) ok = find_hot_rows(r, as_stream(stream), t, trip, T, nb1, N, d);
     }
@@ -1237,15 +1290,14 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   a.af = af;
   r->fft = hole && hole_use_fft(d);
   {
-    // two waves per positive (default while the batch's 2 x B scoring waves fit
-    // the chip's 4-wave-per-SIMD residency; SKGE_HPIPE_PAIR=0/1 forces).  WN18
+    // two waves per positive (while the batch's 2 x B scoring waves fit the
+    // chip's 4-wave-per-SIMD residency).  WN18
     // d = 200, same box: nb = 100 93.7 -> 106.7 M triples/s (14.6 -> 12.8 us per
     // launch); nb = 2 (70k positives per launch) 157 -> 142 M, so off there
-    const char* pe = getenv("SKGE_HPIPE_PAIR");
     int64_t maxb = 0;
     for (const auto& bt : batches) maxb = std::max(maxb, bt.second);
     const bool fits = 2 * maxb <= 4 * 4 * 256;
-    r->pair = r->fft && d == 200 && (pe ? atoi(pe) != 0 : fits);
+    r->pair = r->fft && d == 200 && fits;
     // the relation row's loads and update on wave 1 (3 rows each; same box,
     // two rounds: 103.8 -> 104.6 M triples/s)
     a.pair_r1 = 1;
@@ -1282,8 +1334,11 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     }
     // A role: every relation row, then the previous batch's entity slots
     // (owner marks: 64-slot groups)
+    a.bm_items = (a.E.bm[0] && cprev > 0) ? (int)(((long long)N + (1 << a.E.bm_shift) - 1) >> a.E.bm_shift) : 0;
     const int a_items = rel->rows + a.E.nhot +
-                        (hole ? 4 * cprev : grouped ? (4 * cprev + 63) / 64 : 4 * cprev);
+                        (hole ? 4 * cprev
+                         : grouped ? (4 * cprev + 63) / 64
+                         : a.E.bm[0] ? a.bm_items : 4 * cprev);
     // HolE: the apply waves loop over their items within the residency the
     // scoring waves leave (direct form: 2 waves per SIMD at ~180 VGPRs; FFT: 4
     // -- caps 150 / 250 / 400 / 600 / 800 / 1100 on WN18 d = 200: 74.7 / 77.6 /
@@ -1356,12 +1411,36 @@ extern "C" skge_pipe_runner_t* skge_pipe_runner_create(void* stream, const skge_
                                     seed, epoch_key, margin, ntries, nviol_total, 0);
 }
 
+// A runner whose error word was found set (skge_pipe_runner_error), or whose
+// epoch launch failed, is invalid: the caller's tables hold whatever the
+// failing epoch left (a wrapped sum applied, a row scored stale), and every
+// later run() / profile() is refused.  (Epochs already queued behind the
+// failing one draw no negatives, so they change nothing: k_epoch_sample.)
+static int refuse_invalid(const skge_pipe_runner* r) {
+  set_error("pipelined runner: an earlier epoch failed (error word set or launch failed); the "
+            "tables hold that epoch's partial updates and the runner refuses further runs -- "
+            "restore the parameters and build a new runner");
+  (void)r;
+  return SKGE_EINVAL;
+}
+
 extern "C" int skge_pipe_runner_run(skge_pipe_runner_t* r, void* stream, int nepochs) {
   SKGE_CHECK_ARG(r && r->exec, "bad runner");
-  hot_io(r, as_stream(stream), false);
-  for (int i = 0; i < nepochs; ++i) SKGE_CHECK_HIP(hipGraphLaunch(r->exec, as_stream(stream)));
-  hot_io(r, as_stream(stream), true);
-  fused_finalize(r, as_stream(stream));
+  if (r->invalid) return refuse_invalid(r);
+  hipStream_t st = as_stream(stream);
+  hot_io(r, st, false);
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < nepochs && e == hipSuccess; ++i) e = hipGraphLaunch(r->exec, st);
+  // the epilogue runs even after a failed launch: hub rows and the fused
+  // kernel's second-buffer rows go back to the caller's tables either way
+  hot_io(r, st, true);
+  fused_finalize(r, st);
+  if (e != hipSuccess) {
+    r->invalid = true;
+    set_error("pipelined runner: hipGraphLaunch failed: %s (runner now invalid)",
+              hipGetErrorString(e));
+    return SKGE_EHIP;
+  }
   SKGE_CHECK_LAUNCH("pipelined runner finalize");
   return SKGE_OK;
 }
@@ -1370,6 +1449,7 @@ extern "C" int skge_pipe_runner_profile(skge_pipe_runner_t* r, void* stream, flo
                                         int* stats_out, int n, int trace_launch,
                                         uint64_t* trace_out, int64_t trace_len) {
   SKGE_CHECK_ARG(r && us_out && stats_out, "NULL argument");
+  if (r->invalid) return refuse_invalid(r);
   const int nl = r->nlaunch();
   SKGE_CHECK_ARG(n >= nl, "output arrays need nlaunches entries");
   hipStream_t st = as_stream(stream);
@@ -1437,6 +1517,7 @@ extern "C" int skge_pipe_runner_error(skge_pipe_runner_t* r, void* stream) {
   int v = 0;
   SKGE_CHECK_HIP(hipStreamSynchronize(as_stream(stream)));
   SKGE_CHECK_HIP(hipMemcpy(&v, r->err, 4, hipMemcpyDeviceToHost));
+  if (v) r->invalid = true;   // sticky: later run()s are refused
   return v;
 }
 

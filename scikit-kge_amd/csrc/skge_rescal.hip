@@ -26,6 +26,8 @@
 // Scores, WE, EW and dW have fixed summation orders (stable buckets, fixed
 // MFMA k order, fixed cross-wave reduction order), so the relation gradient
 // is bitwise reproducible; the entity sums use float atomics, as elsewhere.
+#include <string>
+
 #include "skge_host.h"
 
 namespace skge {
@@ -114,10 +116,46 @@ __device__ __forceinline__ float spart_sum(const RescalWs& ws, int i, int ncb) {
   return r;
 }
 
-// K slices of the GEMMs (SKGE_RS_GKS: 1 or 2; d needs at least 2 k-steps)
+// Test forms of the RESCAL path (SKGE_RESCAL_FORM, comma-separated tokens;
+// unset = the default, measured-best form).  Each token selects the simpler
+// form a GPU test compares the default against on the same draws
+// (tests/test_gpu_pairloop.py): "unfused" (no fused front), "nosplit" (one dW
+// kernel, no split-K partial tiles), "nodedup" (three GEMM rows per positive),
+// "dw3" (three dW items per positive), "wapply" (the W step in the entity
+// apply's launch), "fsplit=N" (dW splits of the fused front), "order=N" (the
+// front's role order: 0 dW first, 1 GEMM first, >= 2 interleaved).  The
+// round-5 A/B-only switches (GEMM K split, the W step in its own launch) are
+// compile-time only now (SKGE_RS_GKS_DEFAULT).
+struct RsForm {
+  bool unfused = false, nosplit = false, nodedup = false, dw3 = false, wapply = false;
+  int fsplit = 1, order = 1;
+};
+static RsForm rs_form() {
+  RsForm f;
+  const char* e = getenv("SKGE_RESCAL_FORM");
+  if (!e) return f;
+  std::string v(e);
+  size_t i = 0;
+  while (i <= v.size()) {
+    size_t j = v.find(',', i);
+    if (j == std::string::npos) j = v.size();
+    const std::string t = v.substr(i, j - i);
+    if (t == "unfused") f.unfused = true;
+    else if (t == "nosplit") f.nosplit = true;
+    else if (t == "nodedup") f.nodedup = true;
+    else if (t == "dw3") f.dw3 = true;
+    else if (t == "wapply") f.wapply = true;
+    else if (t.rfind("fsplit=", 0) == 0) f.fsplit = std::max(1, atoi(t.c_str() + 7));
+    else if (t.rfind("order=", 0) == 0) f.order = std::max(0, atoi(t.c_str() + 6));
+    i = j + 1;
+  }
+  return f;
+}
+
+// K slices of the GEMMs (SKGE_RS_GKS_DEFAULT: 1 or 2; d needs at least 2
+// k-steps; the split measured 34 -> 26 M triples/s, so 1)
 static int rs_gks(int d) {
-  const char* e = getenv("SKGE_RS_GKS");
-  const int g = e ? atoi(e) : SKGE_RS_GKS_DEFAULT;
+  const int g = SKGE_RS_GKS_DEFAULT;
   return g >= 2 && (d + SKGE_RS_KS - 1) / SKGE_RS_KS >= 2 ? 2 : 1;
 }
 
@@ -137,11 +175,8 @@ static int rs_tmax(int n, int M) { return n / RT_ITEMS + M + 1; }
 // deduplicated GEMM rows (RescalWs::npos): 2M segments of 2P rows in all
 static int rs_tmax_dedup(int P, int M) { return 4 * P / RT_ITEMS + 2 * M + 1; }
 // the device pair loop's epoch buckets deduplicate the GEMM rows
-// (SKGE_RS_DEDUP=0: three rows per positive, A/B)
-static bool rs_dedup_on() {
-  const char* e = getenv("SKGE_RS_DEDUP");
-  return !(e && atoi(e) == 0);
-}
+// (SKGE_RESCAL_FORM=nodedup: three rows per positive)
+static bool rs_dedup_on() { return !rs_form().nodedup; }
 
 // dW split over K (a relation's items): at the reference's batch size a
 // relation holds ~235 items, which one workgroup per 64 x 64 dW tile walks in
@@ -160,8 +195,7 @@ static int rs_wsplit(int n, int M, int d) {
   // nb = 2, ~92 groups: 52.5 M vs 42.0 M)
   const long long groups = ((long long)n / M + WS_GROUP - 1) / WS_GROUP;
   int sp = groups < 4 ? 1 : (int)std::min<long long>(SKGE_RS_WG_SPLIT, groups);
-  const char* ns = getenv("SKGE_RS_NOSPLIT");   // A/B and test switch: the fused kernel only
-  if (ns && atoi(ns)) sp = 1;
+  if (rs_form().nosplit) sp = 1;   // test form: the fused kernel only
   while (sp > 1 && (long long)M * nt * nt * sp * WS_TILE * WS_TILE * 4 > (64ll << 20)) --sp;
   return std::max(sp, 1);
 }
@@ -171,17 +205,16 @@ static size_t rs_wpart_bytes(int n, int M, int d) {
   return sp > 1 ? (size_t)M * nt * nt * sp * WS_TILE * WS_TILE * 4 : 0;
 }
 // the fused front (k_rescal_front_fused): splits of its dW grid -- the split-K
-// count where that applies, else SKGE_RS_FSPLIT (default 1; each split adds a
-// workgroup per tile beside the GEMM's); 0 = no fused front (SKGE_RESCAL_FUSED=0,
+// count where that applies, else the form's fsplit (default 1; each split adds
+// a workgroup per tile beside the GEMM's); 0 = no fused front (form "unfused",
 // or the partial tiles would pass 64 MB)
 static int rs_front_splits(int n, int M, int d) {
-  const char* fe = getenv("SKGE_RESCAL_FUSED");
-  if (fe && atoi(fe) == 0) return 0;
+  const RsForm f = rs_form();
+  if (f.unfused) return 0;
   const long long nt = (d + WS_TILE - 1) / WS_TILE;
   int sp = rs_wsplit(n, M, d);
   if (sp == 1) {
-    const char* fs = getenv("SKGE_RS_FSPLIT");
-    sp = fs ? std::max(1, atoi(fs)) : 1;
+    sp = f.fsplit;
     const long long groups = ((long long)n / M + WS_GROUP - 1) / WS_GROUP;
     sp = (int)std::max(1ll, std::min<long long>(sp, groups));
   }
@@ -1885,23 +1918,21 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
     // workgroup order of the two roles (k_rescal_front_fused): the GEMM grid
     // first (A/B on WN18 d = 200: 29.25 M vs 29.0 M triples/s with the dW
     // grid first, 29.2 M interleaving one dW workgroup in three)
-    const char* fo = getenv("SKGE_RS_FRONT_ORDER");
-    int order = fo ? std::max(0, atoi(fo)) : 1;
+    const RsForm form = rs_form();
+    int order = form.order;
     if (order >= 2) {   // every dW workgroup needs a slot: order * nwg <= grid
       order = std::min<long long>(order, (long long)grid.x / nwg);
       if (order < 2) order = 0;
     }
-    // combined dW: a positive's two outer products over E_s as one (SKGE_RS_DW2=0: three items)
-    // (the separate finishing kernel counts a relation's items by its bucket)
-    const char* c2 = getenv("SKGE_RS_DW2");
-    const char* sep = getenv("SKGE_RS_WSTEP_SEP");   // A/B: the W step in its own launch
-    const bool wstep_in_apply = wstep && !(sep && atoi(sep));
-    const bool comb = w.npos > 0 && wstep_in_apply && !(c2 && atoi(c2) == 0);
+    // combined dW: a positive's two outer products over E_s as one (form
+    // "dw3": three items; the separate finishing kernel counts a relation's
+    // items by its bucket)
+    const bool wstep_in_apply = wstep != nullptr;
+    const bool comb = w.npos > 0 && wstep_in_apply && !form.dw3;
     // the W step inside the front when every batch of the epoch has one dW
-    // split (SKGE_RS_WFRONT=0: in the apply, from partial tiles)
-    const char* wfe = getenv("SKGE_RS_WFRONT");
+    // split (form "wapply": in the apply, from partial tiles)
     const long long last = T - (long long)(nb - 1) * bs;
-    const bool infront = comb && w.wcur && !(wfe && atoi(wfe) == 0) &&
+    const bool infront = comb && w.wcur && !form.wapply &&
                          rs_front_splits(3 * bs, M, d) == 1 &&
                          rs_front_splits((int)(3 * last), M, d) == 1;
     WFront wf = {};

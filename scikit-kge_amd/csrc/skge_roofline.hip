@@ -80,9 +80,75 @@ __global__ __launch_bounds__(256) void k_roofline(RoofArgs a) {
   if (l == 0) a.out[g] = acc;
 }
 
+// Hand-off latency probe: the pipelined runner's publish / wait form between
+// two workgroups (blocks 0 and 1: different XCDs under round-robin placement),
+// ping-ponged `rounds` times.  One hop = a 16-B write-through (sc1) payload
+// store, a vmcnt(0) drain, an sc1 flag store (publish_row); the other side
+// polls the flag with sc1 loads + s_sleep(2) and re-reads the payload with an
+// sc1 load (ensure_applied).  Block 0 times the rounds with s_memrealtime
+// (10 ns ticks): out[0] = ticks, out[1] = payload mismatches, out[2] = 1 when
+// a bounded wait gave up.  Lines: flag 0, flag 1, payload 0, payload 1 at
+// 128-B strides.  Measurement only: not part of the training path.
+__global__ __launch_bounds__(64) void k_handoff_probe(unsigned* buf, int rounds,
+                                                      unsigned long long* out) {
+  const int me = blockIdx.x, l = lane_id();
+  unsigned* const my_flag = buf + 32 * me;
+  unsigned* const peer_flag = buf + 32 * (me ^ 1);
+  unsigned* const my_pay = buf + 64 + 32 * me;
+  unsigned* const peer_pay = buf + 64 + 32 * (me ^ 1);
+  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned bad = 0, gave_up = 0;
+  for (int i = 0; i < rounds && !gave_up; ++i) {
+    const unsigned v = 2u * (unsigned)i + 1u;
+    auto wait_for = [&](unsigned want) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(peer_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 20)) {
+          gave_up = 1;
+          return;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const unsigned got = __hip_atomic_load(peer_pay + (l & 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bad += (l < 4 && got != want + (unsigned)l) ? 1u : 0u;
+    };
+    auto publish = [&]() {
+      if (l < 4) __hip_atomic_store(my_pay + l, v + (unsigned)l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (l == 0) __hip_atomic_store(my_flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (me == 0) {
+      publish();
+      wait_for(v);
+    } else {
+      wait_for(v);
+      publish();
+    }
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  bad = (unsigned)wave_sum_int((int)bad);
+  if (l == 0) {
+    if (me == 0) out[0] = t1 - t0;
+    atomicAdd(out + 1, (unsigned long long)bad);
+    if (gave_up) atomicOr(out + 2, 1ull);
+  }
+}
+
 }  // namespace skge
 
 using namespace skge;
+
+extern "C" int skge_handoff_probe(void* stream, void* buf, int rounds, uint64_t* out) {
+  SKGE_CHECK_ARG(buf && out && rounds > 0 && rounds <= (1 << 20), "bad argument");
+  hipStream_t st = as_stream(stream);
+  SKGE_CHECK_HIP(hipMemsetAsync(buf, 0, 1024, st));
+  SKGE_CHECK_HIP(hipMemsetAsync(out, 0, 3 * sizeof(uint64_t), st));
+  hipLaunchKernelGGL(k_handoff_probe, dim3(2), dim3(64), 0, st, (unsigned*)buf, rounds,
+                     (unsigned long long*)out);
+  SKGE_CHECK_LAUNCH("handoff probe");
+  return SKGE_OK;
+}
 
 extern "C" int skge_roofline_gather(void* stream, float* P, float* A, void* S, int rows, int d,
                                     int n_gather, int rows_per_wave, int atom_rows_per_wave,

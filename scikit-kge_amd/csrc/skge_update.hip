@@ -1102,11 +1102,8 @@ int skge_rescal_pair_grad_mfma(hipStream_t st, int af, const skge_table_t* ent,
                                int P, float margin, void* workspace, size_t ws_bytes,
                                float* pscore, float* nscore, int* nviol, bool apply_w);
 
-// SKGE_RESCAL_VALU=1 forces the per-pair GEMV path (A/B comparisons)
-static bool rescal_use_mfma(int d, int M) {
-  static const bool valu = getenv("SKGE_RESCAL_VALU") && atoi(getenv("SKGE_RESCAL_VALU")) != 0;
-  return !valu && skge_rescal_mfma_ok(d, M);
-}
+// the MFMA path wherever it applies (d <= 1024, M within the scan's LDS)
+static bool rescal_use_mfma(int d, int M) { return skge_rescal_mfma_ok(d, M); }
 bool rescal_pair_mfma_selected(int d, int M) { return rescal_use_mfma(d, M); }
 
 extern "C" int skge_device_error(void* stream, int reset) {

@@ -105,6 +105,7 @@ SIGNATURES = {
     "skge_dp_scatter": (c_i, [c_p, T_P, T_P, c_i, c_i64, c_i, c_p]),
     "skge_roofline_gather": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i,
                                    ctypes.c_uint32, c_p]),
+    "skge_handoff_probe": (c_i, [c_p, c_p, c_i, c_p]),
 }
 
 _lib = None

@@ -375,11 +375,17 @@ class EpochRunner(object):
             rc = L.lib().skge_pipe_runner_error(self.handle, L.stream_ptr(self.stream))
             if rc < 0:
                 raise L.SkgeError("pipelined runner: %s" % L.lib().skge_last_error().decode())
+            # (the runner is now invalid: later epochs of this run changed
+            # nothing and every later run() is refused)
             if rc & 1:
-                raise L.SkgeError("pipelined runner: a cross-workgroup wait timed out")
+                raise L.SkgeError("pipelined runner: a cross-workgroup wait timed out; the "
+                                  "tables hold that epoch's partial updates and the runner "
+                                  "refuses further runs")
             if rc & 2:
                 raise L.SkgeError("pipelined runner: a row's per-batch count exceeded 32767 "
-                                  "(packed sums may have wrapped); use force_f32=True")
+                                  "(packed sums may have wrapped); the tables hold that "
+                                  "epoch's partial updates and the runner refuses further "
+                                  "runs; use force_f32=True")
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -461,7 +467,8 @@ class HolePipeRunner(object):
         if rc < 0:
             raise L.SkgeError("pipelined HolE runner: %s" % L.lib().skge_last_error().decode())
         if rc & 1:
-            raise L.SkgeError("pipelined HolE runner: a cross-workgroup wait timed out")
+            raise L.SkgeError("pipelined HolE runner: a cross-workgroup wait timed out; the "
+                              "runner refuses further runs")
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -241,6 +241,125 @@ def test_pipelined_runner_bitwise_equals_two_launch(n_ent, n_rel, T, d, nb, monk
             assert np.array_equal(a[k], b[k]), (k, mode)
 
 
+def race_scenario(d=200, nb=10, sleep_cycles=int(2e8), unordered=False):
+    """(fresh, racy) one-epoch results of the same TransE run: `fresh` from
+    freshly zeroed accumulators; `racy` with the runner's accumulators placed
+    (through the caching allocator) in blocks a previous user left holding
+    nonzero counts, sums and slot records, their zero fill queued on the
+    caller's stream behind a long torch.cuda._sleep, and run(1) called at
+    once.  The runner must order its first launch after that fill (round 5's
+    fix: EpochRunner syncs the caller's stream after building its tables, and
+    run() waits on it).  unordered=True neutralises exactly that ordering
+    (tools/race_check.py: shows the scenario catches the race)."""
+    from unittest import mock
+    import skge_amd as S
+    from skge_amd import param as P
+    from skge_amd.device import DeviceKG, EpochRunner
+    n_ent, n_rel, T = 3000, 11, 12000
+    trip, _ = make_kg(n_ent, n_rel, T, seed=4)
+
+    def one(racy):
+        np.random.seed(21)
+        m = S.TransE((n_ent, n_ent, n_rel), d)
+        m.add_hyperparam("margin", 2.0)
+        upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
+        kg = DeviceKG(trip, m.device)
+        torch.cuda.synchronize()
+        orig = P.Accumulator.__init__
+
+        def dirty_init(self, rows, width, device, slots=1024, mode=0, dense=False, replicas=1):
+            reps = replicas if dense else 1
+            dw = width // 2 if mode == 1 else (2 * width if mode == 3 else
+                                               (width // 4 if mode == 4 else width))
+            # blocks of exactly the sizes about to be allocated, left dirty
+            # (counts 3, packed sums 0x00010001 per word, slot records = row 1)
+            junk = [torch.full((reps * rows * dw,), 65537, dtype=torch.int32, device=device),
+                    torch.full((reps * rows,), 3, dtype=torch.int32, device=device)]
+            if not dense:
+                junk.append(torch.full((max(slots, 1),), 1, dtype=torch.int32, device=device))
+            del junk
+            torch.cuda._sleep(sleep_cycles)   # the zero fill below waits behind this
+            orig(self, rows, width, device, slots=slots, mode=mode, dense=dense,
+                 replicas=replicas)
+
+        patches = [mock.patch.object(P.Accumulator, "__init__", dirty_init)] if racy else []
+        if racy and unordered:
+            patches += [mock.patch.object(torch.cuda.Stream, "synchronize", lambda self: None),
+                        mock.patch.object(torch.cuda.Stream, "wait_stream", lambda self, o: None)]
+        for p_ in patches:
+            p_.start()
+        try:
+            r = EpochRunner(m, upd, kg, nbatches=nb, seed=9)
+            assert r.pipelined
+            r.run(1)
+        finally:
+            for p_ in reversed(patches):
+                p_.stop()
+        torch.cuda.synchronize()
+        err = L_error(r)
+        out = {"E": m.E.data.cpu().numpy().copy(), "R": m.R.data.cpu().numpy().copy(),
+               "pE": upd["E"].p2.cpu().numpy().copy(), "nviol": int(r.nviol_total.item()),
+               "err": err}
+        del r
+        torch.cuda.synchronize()
+        return out
+    return one(False), one(True)
+
+
+def L_error(r):
+    from skge_amd import _lib as L
+    return int(L.lib().skge_pipe_runner_error(r.handle, L.stream_ptr(r.stream)))
+
+
+@pytest.mark.parametrize("d", [200, 64])   # the hand-off kernel; the fused kernel (d <= 64)
+def test_runner_first_launch_ordered_after_zero_fill(d):
+    """Regression test for round 5's stream-ordering race (a reused
+    allocation reached the runner's first launch before its zero fill; seen
+    once as a spurious 'count exceeded 32767'): dirty reused blocks, the fill
+    delayed behind a long kernel on the caller's stream, run(1) at once --
+    the result must equal the run from fresh tables bit for bit."""
+    fresh, racy = race_scenario(d=d)
+    assert fresh["err"] == 0 and racy["err"] == 0
+    assert fresh["nviol"] == racy["nviol"] > 0
+    for k in ("E", "R", "pE"):
+        assert np.array_equal(fresh[k], racy[k]), k
+
+
+def test_pipelined_error_stops_updates_and_refuses_runs():
+    """A packed sum that wraps (ERR_PACKED: a row's per-batch count past
+    32767, forced here with packed=True on a star KG whose hub is the subject
+    of every triple) must not go on corrupting the tables: epochs queued after
+    the failing one change nothing (run(3) leaves the tables as run(1) does),
+    synchronize() raises, and the runner refuses every later run()."""
+    import skge_amd as S
+    from skge_amd import _lib as L
+    from skge_amd.device import DeviceKG, EpochRunner
+    n_ent, n_rel, T = 3000, 11, 24000
+    rs = np.random.RandomState(2)
+    pairs = set()
+    while len(pairs) < T:
+        pairs.add((int(rs.randint(1, n_ent)), int(rs.randint(n_rel))))
+    trip = np.array([(0, o, p) for o, p in sorted(pairs)], dtype=np.int32)
+    res = []
+    for epochs in (1, 3):
+        np.random.seed(8)
+        m = S.TransE((n_ent, n_ent, n_rel), 64)
+        m.add_hyperparam("margin", 2.0)
+        upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
+        kg = DeviceKG(trip, m.device)
+        r = EpochRunner(m, upd, kg, nbatches=2, seed=1, pipelined=True, packed=True)
+        r.run(epochs)
+        with pytest.raises(L.SkgeError, match="32767"):
+            r.synchronize()
+        with pytest.raises(L.SkgeError, match="refuses"):
+            r.run(1)
+        res.append((m.E.data.cpu().numpy().copy(), m.R.data.cpu().numpy().copy(),
+                    upd["E"].p2.cpu().numpy().copy()))
+        del r
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
+
+
 def test_trainer_device_loop_fit():
     import skge_amd as S
     np.random.seed(42)

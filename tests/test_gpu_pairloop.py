@@ -358,15 +358,15 @@ def test_hole_pipelined_runner_profile_trains_like_run():
 def test_rescal_split_k_dw_matches_fused(monkeypatch):
     """RESCAL dW split over K (batches with >= 4 groups of 128 items per
     relation: partial tiles summed in split order by a finishing kernel)
-    against the single fused dW kernel (SKGE_RS_NOSPLIT=1) on the same draws:
+    against the single fused dW kernel (SKGE_RESCAL_FORM=nosplit) on the same draws:
     equal violation totals, parameters within the fp32 tolerance (SGD)."""
     import skge_amd as S
     from skge_amd.device import DeviceKG, PairLoopRunner
     n_ent, n_rel, T, nb, d = 3000, 3, 6000, 2, 40   # 3000 positives / batch: ~3000 items / relation
     xs = make_kg(n_ent, n_rel, T, seed=4)
     out = []
-    for nosplit in ("1", "0"):
-        monkeypatch.setenv("SKGE_RS_NOSPLIT", nosplit)
+    for form in ("nosplit", ""):
+        monkeypatch.setenv("SKGE_RESCAL_FORM", form)
         m = make_model("rescal", (n_ent, n_ent, n_rel), d)
         m.add_hyperparam("margin", 0.5)
         upd = {pid: S.SGD(p, 0.05) for pid, p in m.params.items()}
@@ -512,17 +512,15 @@ def test_rescal_epoch_buckets_match_per_batch_buckets(n_ent, n_rel, T, d, nb, mo
 def test_rescal_fused_front_matches_unfused(n_ent, n_rel, T, d, nb, fsplit, order, monkeypatch):
     """The RESCAL pair loop's fused front (Linear: dW contraction and GEMMs in
     one launch, dW coefficients written with the epoch's buckets, the W step
-    after the scatter) against the unfused kernels (SKGE_RESCAL_FUSED=0) on the
+    after the scatter) against the unfused kernels (SKGE_RESCAL_FORM=unfused) on the
     same draws: equal violation totals, parameters within the fp32 tolerance
     (the entity sums are float atomics in both)."""
     import skge_amd as S
     from skge_amd.device import DeviceKG, PairLoopRunner
     xs = make_kg(n_ent, n_rel, T, seed=3)
-    monkeypatch.setenv("SKGE_RS_FSPLIT", fsplit)
-    monkeypatch.setenv("SKGE_RS_FRONT_ORDER", order)
     out = []
-    for fused in ("0", "1"):
-        monkeypatch.setenv("SKGE_RESCAL_FUSED", fused)
+    for fused in ("unfused,", ""):
+        monkeypatch.setenv("SKGE_RESCAL_FORM", "%sfsplit=%s,order=%s" % (fused, fsplit, order))
         m = make_model("rescal", (n_ent, n_ent, n_rel), d)
         m.add_hyperparam("margin", 0.2)
         upd = {pid: S.SGD(p, 0.1) for pid, p in m.params.items()}
@@ -549,15 +547,15 @@ def test_rescal_dedup_gemm_rows_match_three_rows(n_ent, n_rel, T, d, nb, af, mon
     """The RESCAL pair loop's deduplicated GEMM rows (W E_o once per (o, p) of a
     positive and its s-corrupted negative, E_s W once per (s, p) of a positive
     and its o-corrupted negative: 2 rows per positive and product instead of
-    3) against three rows per positive (SKGE_RS_DEDUP=0) on the same draws:
+    3) against three rows per positive (SKGE_RESCAL_FORM=nodedup) on the same draws:
     the scores are the same values, so violation totals are equal; dW sums
     its items in another bucket order, so parameters agree to fp32 rounding."""
     import skge_amd as S
     from skge_amd.device import DeviceKG, PairLoopRunner
     xs = make_kg(n_ent, n_rel, T, seed=5)
     out = []
-    for dedup in ("0", "1"):
-        monkeypatch.setenv("SKGE_RS_DEDUP", dedup)
+    for form in ("nodedup", ""):
+        monkeypatch.setenv("SKGE_RESCAL_FORM", form)
         np.random.seed(42)
         m = S.RESCAL((n_ent, n_ent, n_rel), d, rparam=0.05, af=af)
         m.add_hyperparam("margin", 0.2)
@@ -584,14 +582,14 @@ def test_rescal_combined_dw_matches_three_items(n_ent, n_rel, T, d, nb, monkeypa
     """The fused front's combined dW (a positive and its o-corrupted negative
     as ONE outer product E_s (x) (-(k0 + k1) E_o + E_o'), its s-corrupted
     negative as E_s' (x) E_o: two outer products per positive instead of
-    three) against three items per positive (SKGE_RS_DW2=0) on the same
+    three) against three items per positive (SKGE_RESCAL_FORM=dw3) on the same
     draws: equal violation totals, parameters within the fp32 tolerance."""
     import skge_amd as S
     from skge_amd.device import DeviceKG, PairLoopRunner
     xs = make_kg(n_ent, n_rel, T, seed=9)
     out = []
-    for dw2 in ("0", "1"):
-        monkeypatch.setenv("SKGE_RS_DW2", dw2)
+    for form in ("dw3", ""):
+        monkeypatch.setenv("SKGE_RESCAL_FORM", form)
         m = make_model("rescal", (n_ent, n_ent, n_rel), d)
         m.add_hyperparam("margin", 0.2)
         upd = {pid: S.SGD(p, 0.1) for pid, p in m.params.items()}
@@ -619,7 +617,7 @@ def test_rescal_in_front_w_step_matches_apply_side(n_ent, n_rel, T, d, nb, opt, 
     """The W step inside the fused front (written speculatively into a second
     W / state buffer, made current by the apply when the batch has violations,
     copied back into the model's W at the epoch's end) against the W step in
-    the entity apply's launch (SKGE_RS_WFRONT=0) on the same draws: equal
+    the entity apply's launch (SKGE_RESCAL_FORM=wapply) on the same draws: equal
     violation totals, parameters and W's AdaGrad state within the fp32
     tolerance after 2 epochs.  (AdaGrad only at small sizes: at WN18's, the
     entity sums' float-atomic order turns rounding-level differences of a
@@ -628,8 +626,8 @@ def test_rescal_in_front_w_step_matches_apply_side(n_ent, n_rel, T, d, nb, opt, 
     from skge_amd.device import DeviceKG, PairLoopRunner
     xs = make_kg(n_ent, n_rel, T, seed=10)
     out = []
-    for wf in ("0", "1"):
-        monkeypatch.setenv("SKGE_RS_WFRONT", wf)
+    for form in ("wapply", ""):
+        monkeypatch.setenv("SKGE_RESCAL_FORM", form)
         m = make_model("rescal", (n_ent, n_ent, n_rel), d)
         m.add_hyperparam("margin", 0.2)
         cls = S.SGD if opt == "sgd" else S.AdaGrad

@@ -28,7 +28,8 @@ pytestmark = pytest.mark.gpu
 ])
 def test_pipelined_transe_bitwise_equals_two_launch_on_zipf(n_ent, n_rel, T, d, nb, fused,
                                                             monkeypatch):
-    """k_pipe_batch gives the hub rows 16 replicas of their sums and counts,
+    """k_pipe_batch gives the hub rows HOT_REPS = 4 replicas of their sums and
+    counts (csrc/skge_pipe.h),
     and every scoring wave that reads a hub computes its value itself
     (hot_value, the applier's code): still the two-launch loop bit for bit."""
     from bench import make_zipf_kg
@@ -47,23 +48,28 @@ def test_pipelined_transe_bitwise_equals_two_launch_on_zipf(n_ent, n_rel, T, d, 
         assert np.array_equal(a[k], b[k]), k
 
 
-def test_pipelined_hot_rows_across_runs():
-    """Hot rows live in the runner's own buffers during a run (copied in
-    before the first launch, back after the flush): two run(1) calls must
-    equal one run(2) bit for bit, and the tables between runs must hold the
-    trained values."""
+@pytest.mark.parametrize("d,fused", [(200, "0"), (64, "1")])
+def test_pipelined_hot_rows_across_runs(d, fused, monkeypatch):
+    """State that lives in the runner between launches must be back in the
+    caller's tables after every run(): the hand-off kernel's hot rows (in the
+    runner's own buffers during a run, copied in before the first launch and
+    back after the flush) and the fused kernel's rows in its second buffer
+    (k_fused_fin copies them back, incl. the AdaGrad state, and the meta
+    words are cleared).  Two run(1) calls must equal one run(2) bit for bit,
+    and the tables between runs must hold the trained values."""
     import skge_amd as S
     from bench import make_zipf_kg
     from skge_amd.device import DeviceKG, EpochRunner
+    monkeypatch.setenv("SKGE_PIPE_FUSED", fused)
 
     def train(calls):
         np.random.seed(5)
-        m = S.TransE((2000, 2000, 11), 200)
+        m = S.TransE((2000, 2000, 11), d)
         m.add_hyperparam("margin", 2.0)
         upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
         kg = DeviceKG(make_zipf_kg(2000, 11, 12000, seed=3), m.device)
         r = EpochRunner(m, upd, kg, nbatches=10, seed=7, pipelined=True)
-        assert r.hot_rows > 0
+        assert (r.hot_rows > 0) == (fused == "0")
         mid = None
         for k, n in enumerate(calls):
             r.run(n)

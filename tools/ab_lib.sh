@@ -14,7 +14,8 @@ one() {  # name libpath benchargs
   python3 - "$n" "$ba" <<'PY'
 import json,sys; n=sys.argv[1]
 l=[x for x in open("gpurun_out/ablib_%s.log" % n) if x.startswith("{")][0]; j=json.loads(l)
-print(n, "[%s]" % sys.argv[2], round(j["value"]/1e6,2), j["ms_per_step"], j["roofline"].get("avg_launch_us"), j["roofline"].get("frac"))
+hp = (j.get("detail") or {}).get("handoff_probe") or {}
+print(n, "[%s]" % sys.argv[2], round(j["value"]/1e6,2), j["ms_per_step"], j["roofline"].get("avg_launch_us"), j["roofline"].get("frac"), "hop_us", hp.get("us_per_hop"))
 PY
 }
 sets=("${BENCHARGS:-}")
