@@ -28,7 +28,7 @@ contributions).  Any multi-rank measurement that raises or does not finish
 within SKGE_BENCH_DP_TIMEOUT seconds ends the job with a non-zero status
 (after rank 0 has printed its line, the failure marked in it).
 `--dry-run`: the launcher, rendezvous, the data-parallel protocol
-(skge_amd.dp.dp_step with a NumPy rank compute, gloo) and the
+(skge_amd.dp.dp_epoch with a NumPy rank compute, gloo) and the
 max-over-ranks bookkeeping on CPU, no GPU (tests/test_bench_dist.py).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--nb 100]
@@ -188,8 +188,8 @@ def acc_label(acc):
 
 def run_dry(args):
     """--dry-run: the multi-rank bookkeeping without a GPU -- rendezvous over
-    gloo, the data-parallel protocol of the N > 1 line (skge_amd.dp.dp_step:
-    slice scoring, all-gather, scatter, apply) with the float64 NumPy rank
+    gloo, the data-parallel protocol of the N > 1 line (skge_amd.dp.dp_epoch:
+    apply + slice scoring, all-gather, remote scatter) with the float64 NumPy rank
     compute of tests/dp_numpy.py on a small KG, barrier-bracketed timing, max
     over ranks and ONE line from rank 0 with the DP line's shape (not a
     measurement: "dry_run": true)."""
@@ -197,7 +197,7 @@ def run_dry(args):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from dp_numpy import NumpyDPOps
     from shard_numpy import random_records
-    from skge_amd.dp import DPExchange, dp_step
+    from skge_amd.dp import DPExchange, dp_epoch
     world, rank, _ = dist_env()
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
@@ -212,14 +212,12 @@ def run_dry(args):
     bs = T // nb
     batches = [(s0, min(bs, T - s0)) for s0 in range(0, T, bs)]
     for _ in range(args.warmup):
-        for s0, c in batches:
-            dp_step(ops, ex, s0, c)
+        dp_epoch(ops, ex, batches)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        for s0, c in batches:
-            dp_step(ops, ex, s0, c)
+        dp_epoch(ops, ex, batches)
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
@@ -792,19 +790,19 @@ def failed(x):
 def measure_dp(args, dev, nb, warmup, steps, profile=True):
     """ONE TransE-L1 model trained data parallel over the ranks
     (skge_amd.dp.DataParallelRunner; reference semantics
-    skge/base.py:1394-1427, 1306-1316): every rank holds the whole WN18 model,
-    scores its slice of each union batch (nb batches per epoch), the slices'
-    records are all-gathered over RCCL and every rank scatters + applies the
-    whole batch, so all replicas equal one GPU's run on the union batches bit
-    for bit.  Timed epochs start from the initial tables; max over ranks.
-    profile: one more eager epoch with HIP events between the phases of every
-    union batch (score / all-gather / scatter / apply on the runner stream) and
-    the rows each batch applied, for the per-rank roofline."""
+    skge/base.py:1394-1427, 1306-1316): every rank holds the whole WN18 model;
+    per union batch ONE pipelined launch applies the previous batch and scores
+    the rank's slice, the slices' records are all-gathered over RCCL and the
+    other ranks' positives added, so all replicas equal one GPU's run on the
+    union batches bit for bit.  Timed epochs start from the initial tables;
+    max over ranks.  profile: one more eager epoch with HIP events between
+    the phases of every union batch (launch / all-gather / scatter on the
+    runner stream), for the per-rank roofline."""
     import torch
     import torch.distributed as dist
     import skge_amd as S
     from skge_amd.device import DeviceKG
-    from skge_amd.dp import DataParallelRunner, dp_step, slice_of
+    from skge_amd.dp import DataParallelRunner
     world = dist.get_world_size()
     d = args.d
     trip = bench_kg(args, 0)              # ONE model: the same KG on every rank
@@ -867,53 +865,61 @@ def measure_dp(args, dev, nb, warmup, steps, profile=True):
 def dp_profile(runner, args, world):
     """Per-rank phases of one eager data-parallel epoch (HIP events on the
     runner stream; the all-gather's time is the RCCL collective's, incl. its
-    wait for the slowest rank) and their algorithmic bytes (SURVEY 8(d),
-    per rank): score 4d x 5 rows + 20 B per positive of the rank's slice + its
-    records written; all-gather G x share records received; scatter the union
-    batch's records read (its packed atomics are implementation bytes, not
-    8(d)'s); apply k d U."""
+    wait for the slowest rank) and their algorithmic bytes (per
+    rank): launch = ONE k_pipe_batch in its data-parallel form (union batch
+    b-1's rows applied, k d U, while the rank's slice of batch b is scored,
+    4d x 5 rows + 20 B per positive, and its records written); all_gather =
+    G x share records received; scatter = the other ranks' records read (none
+    at G = 1; their packed atomics are implementation bytes, not 8(d)'s).  U
+    is counted on the even batches (their accumulator copy is the caller's
+    table) and averaged."""
     import torch
     d, k = runner.d, (4 if args.opt == "sgd" else 12)
     rb = runner.rec_bytes
     ops, ex, st = runner.ops, runner.ex, runner.stream
     from skge_amd.dp import slice_of
-    names = ("score", "all_gather", "scatter", "apply")
+    names = ("launch", "all_gather", "scatter")
     ms = dict.fromkeys(names, 0.0)
     by = dict.fromkeys(names, 0.0)
+    Us = []
     runner._pad_in()
-    nbat = 0
+    nbat = len(runner.batches)
+    grouped = ex.backend is not None
     with torch.cuda.stream(st):
-        for start, count in runner.batches:
+        ops.begin()
+        for b, (start, count) in enumerate(runner.batches):
             share, lo, hi = slice_of(count, ex.G, ex.rank)
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+            remote = grouped and ex.G > 1
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             ev[0].record(st)
-            send = ops.score(start, count, lo, hi, share)
+            send = ops.batch(b, start, count, lo, hi, share, fold=not remote)
             ev[1].record(st)
-            recs = ops.gathered(ex, send, share)
+            recs = ops.gathered(ex, send, share) if grouped else send
             ev[2].record(st)
-            ops.scatter(start, count, recs)
+            if remote:
+                ops.scatter(b, start, count, recs, lo, hi)
             ev[3].record(st)
             st.synchronize()
-            U = int((runner.accE.cnt != 0).sum().item()) + int((runner.accR.cnt != 0).sum().item())
-            ea = torch.cuda.Event(enable_timing=True)
-            ea.record(st)
-            ops.apply(count)
-            ev[4].record(st)
-            st.synchronize()
+            if b % 2 == 0:   # batch b's rows, pending for launch b + 1
+                Us.append(int((runner.accE.cnt != 0).sum().item()))
             for i, n in enumerate(names):
-                ms[n] += (ea if n == "apply" else ev[i]).elapsed_time(ev[i + 1])
-            by["score"] += (hi - lo) * (4.0 * d * 5 + 20 + rb)
-            by["all_gather"] += ex.G * share * rb
-            by["scatter"] += count * rb
-            by["apply"] += k * d * U
-            nbat += 1
+                ms[n] += ev[i].elapsed_time(ev[i + 1])
+            by["launch"] += (hi - lo) * (4.0 * d * 5 + 20 + rb)
+            by["all_gather"] += ex.G * share * rb if grouped else 0.0
+            by["scatter"] += (count - (hi - lo)) * rb if remote else 0.0
+        ops.flush(nbat)
+        ops.end()
+    st.synchronize()
     runner._pad_out()
+    U = float(np.mean(Us)) if Us else 0.0
+    by["launch"] += k * d * (U + N_REL) * nbat      # each launch applies the previous batch
     ph = {}
     for n in names:
         us = 1000.0 * ms[n] / nbat
         b = by[n] / nbat
         ph[n] = {"us_per_batch": round(us, 3), "bytes_per_batch": round(b),
                  "GB_s": round(b / (us * 1e-6) / 1e9, 1) if us > 0 else None}
+    ph["launch"]["applied_rows_per_batch"] = round(U, 1)
     return ph
 
 
@@ -939,8 +945,9 @@ def dp_line(args, world, m, ph, d=None, nb=None, workload_kg=None, info=None):
         "config": {"workload": "ONE TransE-L1 d=%d model, PairwiseStochasticTrainer+%s, union "
                                "batch %d positives (nb=%d; ~%d per GPU), margin 2.0, lr 0.1, "
                                "device RandomModeSampler(1,[0,1]); data parallel over %d GPUs: "
-                               "slice scoring, all-gather of the records, replicated scatter + "
-                               "apply; step = 1 epoch" % (d, opt, bs, nb, m["per_gpu_batch"], world),
+                               "one pipelined launch per union batch (apply + slice scoring), "
+                               "all-gather of the records, the other ranks' positives added; "
+                               "step = 1 epoch" % (d, opt, bs, nb, m["per_gpu_batch"], world),
                    "global_batch": bs,
                    "parallelism": parallelism_label("dp%d" % world, info or {})},
         "roofline": None,
@@ -949,7 +956,7 @@ def dp_line(args, world, m, ph, d=None, nb=None, workload_kg=None, info=None):
                    "rank_setup": info},
     }
     if ph:
-        dom = max(("score", "scatter", "apply"), key=lambda n: ph[n]["us_per_batch"])
+        dom = max(("launch", "scatter"), key=lambda n: ph[n]["us_per_batch"])
         line["roofline"] = {
             "bound": "hbm", "kernel": "dp_" + dom, "achieved": ph[dom]["GB_s"],
             "peak": HBM_PEAK_GBS, "unit": "GB/s",

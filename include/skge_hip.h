@@ -272,36 +272,8 @@ int skge_transe_sample_grad(void *stream, int l1, const skge_table_t *ent,
                             uint64_t seed, const uint64_t *epoch_key, float margin, int ntries,
                             int *nviol, int *nviol_total, int *neg_out);
 
-/*
- * Data-parallel TransE-L1 (one model over G ranks; SURVEY.md 8(e) for WN18,
- * replacing one process's PairwiseStochasticTrainer._process_batch +
- * _batch_step, skge/base.py:1394-1427 and 1306-1316).  Every rank holds the
- * whole model and draws the same epoch order and negatives (seed, epoch_key);
- * the union batch [start, start + count) is split in slices [lo, hi).
- *   skge_dp_score   scores the slice (sampler, L1 scores, strict margin test,
- *                   sign sub-gradients, skge/transe.py:48-122) and writes one
- *                   record per positive into rec_out[(w - lo)]: header
- *                   {s, o, p, v0 | v1 << 1, s', o', 0, 0} int32 + for a
- *                   violating positive its sign vectors gp, g0, g1 as 2-bit
- *                   ternary codes, one uint32 per quad; violations into the
- *                   64 sharded counters vshards (skge_shard_fold_violations);
- *   (the caller all-gathers the G slices' records: RCCL)
- *   skge_dp_scatter adds the whole batch's records into ent / rel's packed
- *                   (SKGE_ACC_I16X4) accumulators with the slot map of
- *                   skge_transe_sample_grad (ent 4w+{s,o,s',o'}, rel w): the
- *                   counts and exact sums one GPU computes for the union
- *                   batch, so skge_accum_apply then updates every replica
- *                   bitwise like the one-GPU step.
- * Record stride: skge_dp_record_bytes(d) (0 if d % 4 != 0).
- */
-size_t skge_dp_record_bytes(int d);
-int skge_dp_score(void *stream, const skge_table_t *ent, const skge_table_t *rel, int d,
-                  const int *trip, int64_t T, const void *set, int64_t set_capacity,
-                  int64_t start, int count, int lo, int hi, uint64_t seed,
-                  const uint64_t *epoch_key, float margin, int ntries, int *vshards,
-                  void *rec_out);
-int skge_dp_scatter(void *stream, const skge_table_t *ent, const skge_table_t *rel, int d,
-                    int64_t start, int count, const void *records);
+/* Data-parallel TransE-L1 (one model over G ranks): the pipelined runner's
+ * data-parallel form, skge_pipe_runner_dp_* below. */
 
 /* perm_out[j] = perm_epoch(j) for j < n (tests / host-side replay). */
 int skge_epoch_permutation(void *stream, int64_t T, uint64_t seed, const uint64_t *epoch_key,
@@ -389,8 +361,10 @@ skge_pipe_runner_t *skge_pipe_runner_create(void *stream, const skge_table_t *en
                                             int64_t T, const void *set, int64_t set_capacity,
                                             int nbatches, uint64_t seed, uint64_t *epoch_key,
                                             float margin, int ntries, int *nviol_total);
-/* skge_pipe_runner_create with a flags word; no flags are defined (round 5
- * removed the lazy-apply variant, measured slower): flags must be 0. */
+/* skge_pipe_runner_create with a flags word: 0, or SKGE_PIPE_DP (the
+ * data-parallel form below: TransE-L1, no hot rows, driven launch by launch;
+ * run() / profile() refuse it). */
+#define SKGE_PIPE_DP 1
 skge_pipe_runner_t *skge_pipe_runner_create_ex(void *stream, const skge_table_t *ent,
                                                const skge_table_t *rel, int d, const int *trip,
                                                int64_t T, const void *set, int64_t set_capacity,
@@ -441,6 +415,35 @@ int skge_pipe_runner_hot_rows(const skge_pipe_runner_t *r);
 int skge_pipe_runner_profile(skge_pipe_runner_t *r, void *stream, float *us_out, int *stats_out,
                              int n, int trace_launch, uint64_t *trace_out, int64_t trace_len);
 void skge_pipe_runner_destroy(skge_pipe_runner_t *r);
+/* Batches per epoch (nb1; launch nb1 is the flush), or -1. */
+int skge_pipe_runner_nbatches(const skge_pipe_runner_t *r);
+
+/* ---- data-parallel form of the pipelined runner (SKGE_PIPE_DP) ----
+ * ONE model replicated over G ranks (skge_amd/dp.py; skge/base.py:1268-1284,
+ * 1394-1427 over the union batch).  Every rank creates the runner with the
+ * same tables, KG, nbatches and seed (so every rank draws the same epoch
+ * records) and runs, per epoch:
+ *   dp_begin;
+ *   for b in 0..nb1-1:
+ *     dp_batch(b, lo, hi, rec_out, fold = G == 1)  -- ONE launch: applies batch
+ *         b-1's rows (all ranks' contributions) and scores the rank's slice
+ *         [lo, hi) of batch b, adding its contributions locally and writing
+ *         one record per scored positive (skge_pipe_dp_record_bytes(d) each);
+ *     all-gather of the slices' records (the caller's collective, rank-major:
+ *         union position w's record at w);
+ *     dp_scatter(b, gathered, lo, hi)  -- adds the other ranks' positives
+ *         (skipped work when there are none);
+ *   dp_batch(nb1, 0, 0, NULL, 0) (the flush); dp_end.
+ * Sums are exact integers, so every replica equals one GPU's run over the
+ * union batches bit for bit.  Each rank's violations (its slices) go to its
+ * nviol_total at the flush. */
+size_t skge_pipe_dp_record_bytes(int d);
+int skge_pipe_runner_dp_begin(skge_pipe_runner_t *r, void *stream);
+int skge_pipe_runner_dp_batch(skge_pipe_runner_t *r, void *stream, int b, int lo, int hi,
+                              void *rec_out, int fold);
+int skge_pipe_runner_dp_scatter(skge_pipe_runner_t *r, void *stream, int b, const void *recs,
+                                int lo, int hi);
+int skge_pipe_runner_dp_end(skge_pipe_runner_t *r, void *stream);
 
 /* ---------------- row-sharded TransE-L1 step ----------------
  *

@@ -333,87 +333,6 @@ __global__ __launch_bounds__(256) void k_transe_l1_sample_grad_i16(SampleArgs a)
   count_violations(a, nv);
 }
 
-// ---- data-parallel TransE-L1 (one model over G ranks) ----
-// Every rank holds the whole model and draws the same epoch order and
-// negatives; rank g scores positives [lo, hi) of each (union) batch and writes
-// one record per positive: header {s, o, p, flags = v0 | v1 << 1} {neg0, neg1}
-// and, for a violating positive, its three sign vectors gp, g0, g1 as 2-bit
-// ternary codes (0: 0, 1: +1, 2: -1), one 32-bit word per quad q holding
-// (gp, g0, g1) bytes of its four elements.  The records of all ranks are
-// all-gathered (RCCL) and every rank scatters the whole batch with
-// transe_l1_commit -- the same counts, slots and exact packed sums as one GPU
-// scoring the union batch -- then applies it: the replicas stay bitwise equal
-// to the one-GPU run.
-__host__ __device__ inline int dp_record_words(int d) { return 8 + (((d >> 2) + 3) & ~3); }
-
-__device__ __forceinline__ uint32_t tern4(const float4& v) {
-  auto t = [](float x) -> uint32_t { return x > 0.0f ? 1u : (x < 0.0f ? 2u : 0u); };
-  return t(v.x) | (t(v.y) << 2) | (t(v.z) << 4) | (t(v.w) << 6);
-}
-__device__ __forceinline__ float4 untern4(uint32_t b) {
-  auto u = [](uint32_t c) -> float { return (float)(int)(c & 1u) - (float)(int)((c >> 1) & 1u); };
-  return make_float4(u(b), u(b >> 2), u(b >> 4), u(b >> 6));
-}
-
-template <int KQ>
-__global__ __launch_bounds__(256) void k_dp_score(SampleArgs a, int lo, int hi, uint32_t* rec) {
-  const int wpb = blockDim.x >> 6;
-  const int l = lane_id();
-  const int nq = a.d >> 2, rw = dp_record_words(a.d);
-  const uint64_t ek = *a.epoch_key;
-  const Perm pm = {(uint64_t)a.T, a.half, epoch_perm_key(a.seed, ek)};
-  const uint64_t skey = epoch_sample_key(a.seed, ek);
-  int nv = 0;
-  for (int w = lo + blockIdx.x * wpb + (threadIdx.x >> 6); w < hi; w += gridDim.x * wpb) {
-    const long long j = a.start + w;
-    float4 gp[KQ], g0[KQ], g1[KQ];
-    const PosL1 r = transe_l1_front<KQ>(a, pm, skey, j, gp, g0, g1);
-    nv += r.v0 + r.v1;
-    uint32_t* out = rec + (size_t)(w - lo) * rw;
-    if (l < 8) {
-      const int h = sel4(l & 3, r.s, r.o, r.p, r.v0 | (r.v1 << 1));
-      out[l] = (uint32_t)(l < 4 ? h : (l == 4 ? r.neg0 : (l == 5 ? r.neg1 : 0)));
-    }
-    if (r.v0 + r.v1) {
-#pragma unroll
-      for (int m = 0; m < KQ; ++m) {
-        const int q = 64 * m + l;
-        if (q < nq) out[8 + q] = tern4(gp[m]) | (tern4(g0[m]) << 8) | (tern4(g1[m]) << 16);
-      }
-    }
-  }
-  if (lane_id() == 0 && nv) atomicAdd(shard_of(a.vshards), nv);
-}
-
-template <int KQ>
-__global__ __launch_bounds__(256) void k_dp_scatter(SampleArgs a, const uint32_t* __restrict__ rec) {
-  const int wpb = blockDim.x >> 6;
-  const int l = lane_id();
-  const int nq = a.d >> 2, rw = dp_record_words(a.d);
-  for (int w = blockIdx.x * wpb + (threadIdx.x >> 6); w < a.count; w += gridDim.x * wpb) {
-    const uint32_t* in = rec + (size_t)w * rw;
-    PosL1 r;
-    r.s = (int)__builtin_amdgcn_readfirstlane(in[0]);
-    r.o = (int)__builtin_amdgcn_readfirstlane(in[1]);
-    r.p = (int)__builtin_amdgcn_readfirstlane(in[2]);
-    const int fl = (int)__builtin_amdgcn_readfirstlane(in[3]);
-    r.neg0 = (int)__builtin_amdgcn_readfirstlane(in[4]);
-    r.neg1 = (int)__builtin_amdgcn_readfirstlane(in[5]);
-    r.v0 = fl & 1;
-    r.v1 = (fl >> 1) & 1;
-    float4 gp[KQ], g0[KQ], g1[KQ];
-#pragma unroll
-    for (int m = 0; m < KQ; ++m) {
-      const int q = 64 * m + l;
-      const uint32_t x = (fl && q < nq) ? in[8 + q] : 0u;
-      gp[m] = untern4(x & 0xFFu);
-      g0[m] = untern4((x >> 8) & 0xFFu);
-      g1[m] = untern4((x >> 16) & 0xFFu);
-    }
-    transe_l1_commit<KQ>(a, a.start + w, w, r, gp, g0, g1);
-  }
-}
-
 __global__ void k_perm(long long T, int half, uint64_t seed, const uint64_t* ekp, long long* out,
                        long long n) {
   const Perm pm = {(uint64_t)T, half, epoch_perm_key(seed, *ekp)};
@@ -569,77 +488,6 @@ extern "C" int skge_transe_sample_grad(void* stream, int l1, const skge_table_t*
   a.count = count;
   a.neg_out = neg_out;
   return launch_sample(a, l1 != 0, as_stream(stream));
-}
-
-extern "C" size_t skge_dp_record_bytes(int d) {
-  return d > 0 && (d & 3) == 0 ? 4 * (size_t)dp_record_words(d) : 0;
-}
-
-static int dp_kq(int d) { return (d / 4 + 63) / 64; }
-
-extern "C" int skge_dp_score(void* stream, const skge_table_t* ent, const skge_table_t* rel, int d,
-                             const int* trip, int64_t T, const void* set_slots,
-                             int64_t set_capacity, int64_t start, int count, int lo, int hi,
-                             uint64_t seed, const uint64_t* epoch_key, float margin, int ntries,
-                             int* vshards, void* rec_out) {
-  SampleArgs a;
-  int rc = fill_sample_args(a, 1, ent, rel, d, trip, T, set_slots, set_capacity, seed, epoch_key,
-                            margin, ntries, nullptr, nullptr);
-  if (rc) return rc;
-  SKGE_CHECK_ARG((d & 3) == 0 && d <= 1024, "data-parallel TransE-L1 needs d %% 4 == 0, d <= 1024");
-  SKGE_CHECK_ARG(start >= 0 && count >= 0 && start + count <= T, "batch out of range");
-  SKGE_CHECK_ARG(0 <= lo && lo <= hi && hi <= count, "slice [lo, hi) out of the batch");
-  SKGE_CHECK_ARG(vshards && (rec_out || lo == hi), "NULL argument");
-  if (lo == hi) return SKGE_OK;
-  a.start = start;
-  a.count = count;
-  a.vshards = vshards;
-  const int n = hi - lo;
-  const int blocks = std::max(1, std::min((n + 3) / 4, 16384));
-  hipStream_t st = as_stream(stream);
-  const int kq = dp_kq(d);
-#define SKGE_DS(K) \
-  hipLaunchKernelGGL((k_dp_score<K>), dim3(blocks), dim3(256), 0, st, a, lo, hi, (uint32_t*)rec_out)
-  if (kq <= 1) SKGE_DS(1);
-  else if (kq <= 2) SKGE_DS(2);
-  else SKGE_DS(4);
-#undef SKGE_DS
-  SKGE_CHECK_LAUNCH("data-parallel score");
-  return SKGE_OK;
-}
-
-extern "C" int skge_dp_scatter(void* stream, const skge_table_t* ent, const skge_table_t* rel,
-                               int d, int64_t start, int count, const void* records) {
-  int rc;
-  if ((rc = check_table(ent, "ent", true)) || (rc = check_table(rel, "rel", true)) ||
-      (rc = check_single(ent, "ent")))
-    return rc;
-  SKGE_CHECK_ARG(ent->acc_mode == SKGE_ACC_I16X4 && rel->acc_mode == SKGE_ACC_I16X4,
-                 "data-parallel scatter needs packed (int16x4) accumulators");
-  SKGE_CHECK_ARG(ent->width == d && rel->width == d && (d & 3) == 0 && d <= 1024, "bad width");
-  SKGE_CHECK_ARG(start >= 0 && count >= 0, "bad batch");
-  if (count == 0) return SKGE_OK;
-  SKGE_CHECK_ARG(records, "NULL records");
-  if ((rc = check_slots(ent, 4ll * count, "ent")) || (rc = check_slots(rel, count, "rel"))) return rc;
-  SampleArgs a = SampleArgs{};
-  a.E = ent->param;
-  a.R = rel->param;
-  a.accE = accum_of(ent);
-  a.accR = accum_of(rel);
-  a.d = d;
-  a.start = start;
-  a.count = count;
-  const int blocks = std::max(1, std::min((count + 3) / 4, 16384));
-  hipStream_t st = as_stream(stream);
-  const int kq = dp_kq(d);
-#define SKGE_DC(K) \
-  hipLaunchKernelGGL((k_dp_scatter<K>), dim3(blocks), dim3(256), 0, st, a, (const uint32_t*)records)
-  if (kq <= 1) SKGE_DC(1);
-  else if (kq <= 2) SKGE_DC(2);
-  else SKGE_DC(4);
-#undef SKGE_DC
-  SKGE_CHECK_LAUNCH("data-parallel scatter");
-  return SKGE_OK;
 }
 
 extern "C" int skge_epoch_permutation(void* stream, int64_t T, uint64_t seed,

@@ -110,6 +110,9 @@ struct PipeArgs {
   const int* rec_n1;           // [T]: o'
   long long start;             // B role: this batch's positives [start, start + count)
   int count;
+  int lo, hi;                  // B role: the positives [lo, hi) of the batch this launch scores
+                               // (data-parallel ranks: their slice; else 0, count)
+  uint32_t* dprec;             // data-parallel: one record per scored positive (pipe_dp_record_words)
   int prev_slots;              // A role: entity slots of the previous batch
   int bm_items;                // A role, bitmap mode: items over the previous batch's bitmap
   int b, nb1;                  // batch index in the epoch (nb1: the flush), batches per epoch
@@ -125,6 +128,22 @@ struct PipeArgs {
   int* err;                    // set when a bounded wait gives up
   int pair_r1;                 // HolE pair form: the wave (0 / 1) that loads and updates R[p]
 };
+
+// Data-parallel record of one scored positive (k_pipe_batch with dprec): word
+// 0 = v0 | v1 << 1, then for a violating positive one word per quad q holding
+// the ternary codes (0: 0, 1: +1, 2: -1) of its sign vectors gp, g0, g1 in
+// bytes 0-2 (the header s, o, p, s', o' every rank has from the epoch's
+// records).  Words rounded up to 16 B.
+__host__ __device__ inline int pipe_dp_record_words(int d) { return (1 + (d >> 2) + 3) & ~3; }
+
+__device__ __forceinline__ uint32_t tern4q(const float4& v) {
+  auto t = [](float x) -> uint32_t { return x > 0.0f ? 1u : (x < 0.0f ? 2u : 0u); };
+  return t(v.x) | (t(v.y) << 2) | (t(v.z) << 4) | (t(v.w) << 6);
+}
+__device__ __forceinline__ float4 untern4q(uint32_t b) {
+  auto u = [](uint32_t c) -> float { return (float)(int)(c & 1u) - (float)(int)((c >> 1) & 1u); };
+  return make_float4(u(b), u(b >> 2), u(b >> 4), u(b >> 6));
+}
 
 // Launch id: consecutive within an epoch (batches 0..nb1-1, then the flush)
 // and across epochs (epoch e+1's batch 0 follows epoch e's flush); >= 2, so

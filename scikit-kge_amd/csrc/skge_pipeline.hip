@@ -181,7 +181,7 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
   const __amdgpu_buffer_rsrc_t rec1_rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<int*>(a.rec_n1 + a.start), 0, a.count * 4, 0x00020000);
   int nv = 0;
-  for (int w = blk_b * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
+  for (int w = a.lo + blk_b * wpb + (threadIdx.x >> 6); w < a.hi; w += nB * wpb) {
     // large batches: positive w adds its relation sums into replica w % reps
     // (k_rel_fold folds them after the launch), spreading the hot rows' atomics
     unsigned long long* const racc = racc0 + (size_t)(w & rmask) * rrep;
@@ -281,6 +281,17 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
     const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // strict >, transe.py:73
     const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
     if (a.trace) tt[3] = now_10ns();
+    if (a.dprec) {   // data-parallel: the positive's record for the other ranks
+      uint32_t* out = a.dprec + (size_t)(w - a.lo) * pipe_dp_record_words(d);
+      if (l == 0) out[0] = (uint32_t)(v0 | (v1 << 1));
+      if (v0 + v1 > 0) {
+#pragma unroll
+        for (int m = 0; m < KQ; ++m) {
+          const int q = 64 * m + l;
+          if (q < nq) out[1 + q] = tern4q(gp4[m]) | (tern4q(g0[m]) << 8) | (tern4q(g1[m]) << 16);
+        }
+      }
+    }
     {
       // counts, touched slots and pending marks of this batch
       const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
@@ -776,6 +787,108 @@ __global__ __launch_bounds__(256) void k_rel_fold(PipeArgs a) {
   }
 }
 
+// Data-parallel runners (skge_amd/dp.py): after the records of union batch b
+// are all-gathered, each rank adds the OTHER ranks' positives -- union
+// positions [0, count) outside its own slice [lo, hi), which its launch
+// scored and added itself -- into batch b's accumulator copies exactly as a
+// scoring wave of k_pipe_batch does (counts, slot records 4w+k, pending marks
+// with batch b's launch id, exact packed entity sums, relation sums into
+// replica w % reps): the next launch's A role then applies the union batch,
+// bitwise as one GPU scoring all of it.  The header (s, o, p, s', o') comes
+// from the epoch's records, which every rank draws alike; the record gives
+// the violation flags and sign vectors.
+template <int KQ, bool W32, bool E8>
+__global__ __launch_bounds__(256) void k_pipe_dp_scatter(PipeArgs a, const uint32_t* __restrict__ recs) {
+  const int wpb = blockDim.x >> 6;
+  const int l = lane_id();
+  const int d = a.d, nq = d >> 2;
+  const int rcw = W32 ? 2 * nq : nq;
+  const int g = launch_id(a);
+  const int cp = a.b & 1;
+  const int rw = pipe_dp_record_words(d);
+  int* const cnt_cp = a.E.cnt[cp];
+  int* const tch_cp = a.E.touched[cp];
+  int* const pend_cp = a.E.pend[cp];
+  int* const own_cp = a.E.own[cp];
+  unsigned long long* const esum = a.E.sum[cp];
+  unsigned long long* const racc0 = a.R.acc[g % 3];
+  const size_t rrep = (size_t)a.R.rows * a.R.rw;
+  const int rmask = a.R.reps - 1;
+  const int nown = a.hi - a.lo, nrem = a.count - nown;
+  for (int i = blockIdx.x * wpb + (threadIdx.x >> 6); i < nrem; i += gridDim.x * wpb) {
+    const int w = i < a.lo ? i : i + nown;   // union position, outside [lo, hi)
+    const int4 r4 = a.rec[a.start + w];
+    const int s = __builtin_amdgcn_readfirstlane(r4.x);
+    const int o = __builtin_amdgcn_readfirstlane(r4.y);
+    const int p = __builtin_amdgcn_readfirstlane(r4.z);
+    const int neg0 = __builtin_amdgcn_readfirstlane(r4.w);
+    const int neg1 = __builtin_amdgcn_readfirstlane(a.rec_n1[a.start + w]);
+    const uint32_t* in = recs + (size_t)w * rw;
+    const int fl = (int)__builtin_amdgcn_readfirstlane(in[0]);
+    const int v0 = fl & 1, v1 = (fl >> 1) & 1;
+    unsigned long long* const racc = racc0 + (size_t)(w & rmask) * rrep;
+    {   // (k_pipe_batch's commit, lanes 0-4)
+      const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
+      const int rE = sel4(l, s, o, neg0, neg1);
+      if (l < 4) {
+        commit_slot(cnt_cp, tch_cp, rE, cE, 4 * w + l);
+        if (cE > 0) {
+          pend_cp[rE] = g;
+          if (own_cp) own_cp[rE] = 4 * w + l;
+        }
+      } else if (l == 4 && v0 + v1 > 0) {
+        atomicAdd(racc + (size_t)p * a.R.rw + rcw, (unsigned long long)(2 * (v0 + v1)));
+      }
+    }
+    if (v0 + v1 == 0) continue;
+    const float fv0 = (float)v0, fv1 = (float)v1;
+    float4 cs[KQ], co[KQ], c0[KQ], c1[KQ], cr[KQ];
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+      const int q = 64 * m + l;
+      const uint32_t x = q < nq ? in[1 + q] : 0u;
+      const float4 gp4 = untern4q(x & 0xFFu), g0 = untern4q((x >> 8) & 0xFFu),
+                   g1 = untern4q((x >> 16) & 0xFFu);
+#define SKGE_CO(X)                                             \
+  cs[m].X = fv0 * gp4.X + fv1 * (gp4.X + g1.X);                \
+  co[m].X = -(fv0 * (gp4.X + g0.X) + fv1 * gp4.X);             \
+  c0[m].X = g0.X;                                              \
+  c1[m].X = -g1.X;                                             \
+  cr[m].X = fv0 * (gp4.X + g0.X) + fv1 * (gp4.X + g1.X);
+      SKGE_CO(x)
+      SKGE_CO(y)
+      SKGE_CO(z)
+      SKGE_CO(w)
+#undef SKGE_CO
+    }
+    if (E8) {
+      unsigned int* es8 = reinterpret_cast<unsigned int*>(esum);
+      acc_row4_i8<KQ>(es8, s, cs, d);
+      acc_row4_i8<KQ>(es8, o, co, d);
+      if (v0) acc_row4_i8<KQ>(es8, neg0, c0, d);
+      if (v1) acc_row4_i8<KQ>(es8, neg1, c1, d);
+    } else {
+      add_row4_i16<KQ>(esum + (size_t)s * nq, cs, d);
+      add_row4_i16<KQ>(esum + (size_t)o * nq, co, d);
+      if (v0) add_row4_i16<KQ>(esum + (size_t)neg0 * nq, c0, d);
+      if (v1) add_row4_i16<KQ>(esum + (size_t)neg1 * nq, c1, d);
+    }
+    unsigned long long* rrow = racc + (size_t)p * a.R.rw;
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+      const int q = 64 * m + l;
+      if (q < nq) {
+        if (W32) {
+          atomicAdd(rrow + 2 * q, pack_i32x2(cr[m].x, cr[m].y));
+          atomicAdd(rrow + 2 * q + 1, pack_i32x2(cr[m].z, cr[m].w));
+        } else {
+          atomicAdd(rrow + q, pack_i16x4(cr[m]));
+        }
+      }
+    }
+  }
+}
+
 // draw every negative of the epoch: one thread per positive, the same draws and
 // first-accepted-try rule as k_transe_sample_grad (skge/sample.py:41-46).
 // err (pipelined runners; nullptr elsewhere): once a launch has set an error
@@ -856,6 +969,7 @@ struct skge_pipe_runner {
   bool pair = false;               // HolE FFT, d = 200: two waves per positive (while 2 x B waves fit the chip)
   bool fused = false;              // TransE: k_pipe_fused (nothing waits; d <= 64 by default)
   bool invalid = false;            // an error bit was read or a launch failed: run() refuses
+  bool dp = false;                 // data-parallel form (SKGE_PIPE_DP): driven launch by launch
   int n_rows = 0, d = 0;           // fused: the entity table's geometry (k_fused_fin)
   int nlaunch() const { return (int)batch.size() + 2; }
 };
@@ -888,6 +1002,44 @@ static void launch_fused(const skge_pipe_runner* r, dim3 gr, hipStream_t st, con
   }
 }
 
+// k_pipe_batch: the instance for this runner's row width, sums and batch size
+static void launch_pipe_batch(const skge_pipe_runner* r, dim3 gr, hipStream_t st,
+                              const PipeArgs& a) {
+#define SKGE_PB(K)                                                                        \
+  do {                                                                                    \
+    /* own marks: large batches (grouped owner-row apply); nhot: hot-row replicas */     \
+    const bool gp_ = a.E.own[0] != nullptr, hot_ = a.E.nhot > 0;                          \
+    const dim3 bl(gp_ ? PIPE_WG_GRP : SKGE_PIPE_WG);                      \
+    if (r->e8) {                                                                          \
+      if (gp_) {                                                                          \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, true, true>), gr, bl, 0, st, a);  \
+      } else {                                                                            \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true>), gr, bl, 0, st, a);  \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, true>), gr, bl, 0, st, a);        \
+      }                                                                                   \
+    } else if (hot_) {                                                                    \
+      if (gp_) {                                                                          \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true, true>), gr, bl, 0, st, a); \
+      } else {                                                                            \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, false, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, false, true>), gr, bl, 0, st, a); \
+      }                                                                                   \
+    } else if (gp_) {                                                                     \
+      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true>), gr, bl, 0, st, a); \
+      else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true>), gr, bl, 0, st, a);   \
+    } else {                                                                              \
+      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false>), gr, bl, 0, st, a);   \
+      else hipLaunchKernelGGL((k_pipe_batch<K, false, false>), gr, bl, 0, st, a);         \
+    }                                                                                     \
+  } while (0)
+  if (r->kq <= 1) SKGE_PB(1);
+  else if (r->kq <= 2) SKGE_PB(2);
+  else SKGE_PB(4);
+#undef SKGE_PB
+}
+
 // Enqueue one epoch: draw the negatives, nb1 batch launches, the flush, the
 // key advance.  ev (optional, nlaunch + 1 events) brackets every launch;
 // stats (optional) collects per-launch claim / violation counts.
@@ -913,44 +1065,14 @@ static void enqueue_epoch(const skge_pipe_runner* r, hipStream_t st, hipEvent_t*
       a.stats_viol = stats + (3 * i + 2) * sh;
     }
     if (trace && i == trace_launch) a.trace = trace;
-#define SKGE_PB(K)                                                                        \
-  do {                                                                                    \
-    /* own marks: large batches (grouped owner-row apply); nhot: hot-row replicas */     \
-    const bool gp_ = a.E.own[0] != nullptr, hot_ = a.E.nhot > 0;                          \
-    const dim3 gr(r->grid[k]), bl(gp_ ? PIPE_WG_GRP : SKGE_PIPE_WG);                      \
-    if (r->e8) {                                                                          \
-      if (gp_) {                                                                          \
-        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, true>), gr, bl, 0, st, a); \
-        else hipLaunchKernelGGL((k_pipe_batch<K, false, true, true>), gr, bl, 0, st, a);  \
-      } else {                                                                            \
-        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true>), gr, bl, 0, st, a);  \
-        else hipLaunchKernelGGL((k_pipe_batch<K, false, true>), gr, bl, 0, st, a);        \
-      }                                                                                   \
-    } else if (hot_) {                                                                    \
-      if (gp_) {                                                                          \
-        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true, true>), gr, bl, 0, st, a); \
-        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true, true>), gr, bl, 0, st, a); \
-      } else {                                                                            \
-        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, false, true>), gr, bl, 0, st, a); \
-        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, false, true>), gr, bl, 0, st, a); \
-      }                                                                                   \
-    } else if (gp_) {                                                                     \
-      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true>), gr, bl, 0, st, a); \
-      else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true>), gr, bl, 0, st, a);   \
-    } else {                                                                              \
-      if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false>), gr, bl, 0, st, a);   \
-      else hipLaunchKernelGGL((k_pipe_batch<K, false, false>), gr, bl, 0, st, a);         \
-    }                                                                                     \
-  } while (0)
     if (r->hole) {
       launch_hole_pipe(km_for(a.d), r->pair, r->fft, dim3(r->grid[k]),
                        dim3(r->pair ? 128 : SKGE_PIPE_WG), r->lds, st, a);
     } else if (r->fused) {
       launch_fused(r, dim3(r->grid[k]), st, a);
-    } else if (r->kq <= 1) SKGE_PB(1);
-    else if (r->kq <= 2) SKGE_PB(2);
-    else SKGE_PB(4);
-#undef SKGE_PB
+    } else {
+      launch_pipe_batch(r, dim3(r->grid[k]), st, a);
+    }
     if (r->rfold && a.count > 0) {
       const size_t words = (size_t)a.R.rows * a.R.rw;
       if (r->hole)   // fp32 sums + an int count per row
@@ -1088,8 +1210,13 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
                                        const void* set, int64_t set_capacity, int nbatches,
                                        uint64_t seed, uint64_t* epoch_key, float margin,
                                        int ntries, int* nviol_total, int flags, bool hole, int af) {
-  if (flags) {
+  if (flags & ~SKGE_PIPE_DP) {
     set_error("pipelined runner: unknown flags %d", flags);
+    return nullptr;
+  }
+  const bool dp = (flags & SKGE_PIPE_DP) != 0;
+  if (dp && hole) {
+    set_error("pipelined runner: the data-parallel form is TransE-L1 only");
     return nullptr;
   }
   if (!ent || !rel) {
@@ -1137,6 +1264,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   const int nb1 = (int)batches.size();
   skge_pipe_runner* r = new skge_pipe_runner();
   r->hole = hole;
+  r->dp = dp;
   r->e8 = !hole && ent->acc_mode == SKGE_ACC_I8X4;
   const int nq = d / 4;
   const int N = ent->rows;
@@ -1151,7 +1279,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   {
     const char* fe = getenv("SKGE_PIPE_FUSED");
     const bool ok = !hole && !grouped && nq <= 64 && (long long)N < SLOT_BUF;
-    r->fused = ok && (fe ? atoi(fe) != 0 : nq <= 16);
+    r->fused = ok && !dp && (fe ? atoi(fe) != 0 : nq <= 16);
   }
   PipeArgs a = {};
   auto upd = [](const skge_table_t* s) {
@@ -1209,7 +1337,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
         t.own[0] = (int*)dalloc(r, (size_t)N * 4);
         t.own[1] = (int*)dalloc(r, (size_t)N * 4);
         ok = ok && t.own[0] && t.own[1];
-      } else if (!hole && SKGE_PIPE_BITMAP && ((long long)N >> SKGE_PIPE_BM_SHIFT) < 4 * bs) {
+      } else if (!hole && !dp && SKGE_PIPE_BITMAP && ((long long)N >> SKGE_PIPE_BM_SHIFT) < 4 * bs) {
         // touched-row bitmaps: fewer apply items than slot records
         t.bm_shift = SKGE_PIPE_BM_SHIFT;
         for (int k = 0; k < 2; ++k) {
@@ -1217,7 +1345,9 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
           ok = ok && t.bm[k];
         }
       }
-      if (ok && !hole && !r->e8) ok = find_hot_rows(r, as_stream(stream), t, trip, T, nb1, N, d);
+      // (the data-parallel form keeps every row in the tables: no hot rows)
+      if (ok && !hole && !r->e8 && !dp)
+        ok = find_hot_rows(r, as_stream(stream), t, trip, T, nb1, N, d);
     }
     RelTab& q = a.R;
     const int M = rel->rows;
@@ -1317,6 +1447,9 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     a.b = b;
     a.start = b < nb1 ? batches[b].first : 0;
     a.count = b < nb1 ? (int)batches[b].second : 0;
+    a.lo = 0;
+    a.hi = a.count;
+    a.dprec = nullptr;
     const int cprev = b >= 1 ? (int)batches[b - 1].second : 0;
     a.prev_slots = 4 * cprev;
     if (r->fused) {
@@ -1360,6 +1493,14 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     r->grid.push_back(a.nA + (a.count > 0 ? nBb : 0));
   }
   hipStream_t st = as_stream(stream);
+  if (dp) {   // driven launch by launch by the caller (skge_pipe_runner_dp_*), no graph
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      set_error("hipStreamSynchronize failed");
+      pipe_free(r);
+      return nullptr;
+    }
+    return r;
+  }
   if (hipStreamSynchronize(st) != hipSuccess ||
       hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
     set_error("hipStreamBeginCapture failed");
@@ -1425,7 +1566,8 @@ static int refuse_invalid(const skge_pipe_runner* r) {
 }
 
 extern "C" int skge_pipe_runner_run(skge_pipe_runner_t* r, void* stream, int nepochs) {
-  SKGE_CHECK_ARG(r && r->exec, "bad runner");
+  SKGE_CHECK_ARG(r && (r->exec || r->dp), "bad runner");
+  SKGE_CHECK_ARG(!r->dp, "data-parallel runner: drive it with skge_pipe_runner_dp_*");
   if (r->invalid) return refuse_invalid(r);
   hipStream_t st = as_stream(stream);
   hot_io(r, st, false);
@@ -1449,6 +1591,7 @@ extern "C" int skge_pipe_runner_profile(skge_pipe_runner_t* r, void* stream, flo
                                         int* stats_out, int n, int trace_launch,
                                         uint64_t* trace_out, int64_t trace_len) {
   SKGE_CHECK_ARG(r && us_out && stats_out, "NULL argument");
+  SKGE_CHECK_ARG(!r->dp, "profile(): not for the data-parallel form");
   if (r->invalid) return refuse_invalid(r);
   const int nl = r->nlaunch();
   SKGE_CHECK_ARG(n >= nl, "output arrays need nlaunches entries");
@@ -1510,6 +1653,101 @@ extern "C" int skge_pipe_runner_profile(skge_pipe_runner_t* r, void* stream, flo
     if (e) (void)hipEventDestroy(e);
   if (rc != SKGE_OK) set_error("pipelined runner profile failed");
   return rc;
+}
+
+// ---- data-parallel form (SKGE_PIPE_DP): the caller's per-epoch sequence is
+// dp_begin, then for every batch b: dp_batch(b, own slice) -> all-gather of
+// the slice records -> dp_scatter(b, gathered records), then dp_batch(nb1)
+// (the flush) and dp_end.  Every call is stream-ordered and capturable. ----
+static void rel_fold_launch(const skge_pipe_runner* r, hipStream_t st, const PipeArgs& a) {
+  if (!r->rfold || a.count <= 0) return;
+  const size_t words = (size_t)a.R.rows * a.R.rw;
+  hipLaunchKernelGGL(k_rel_fold, dim3((unsigned)std::min<size_t>((words + 255) / 256, 4096)),
+                     dim3(256), 0, st, a);
+}
+
+extern "C" size_t skge_pipe_dp_record_bytes(int d) {
+  return d > 0 && d % 4 == 0 ? 4 * (size_t)pipe_dp_record_words(d) : 0;
+}
+
+extern "C" int skge_pipe_runner_nbatches(const skge_pipe_runner_t* r) {
+  return r ? (int)r->batch.size() - 1 : -1;
+}
+
+extern "C" int skge_pipe_runner_dp_begin(skge_pipe_runner_t* r, void* stream) {
+  SKGE_CHECK_ARG(r && r->dp, "not a data-parallel pipelined runner");
+  if (r->invalid) return refuse_invalid(r);
+  long long blocks = (r->T + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_epoch_sample, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
+                     r->trip, r->T, r->half, r->seed, (const uint64_t*)r->epoch_key, r->set,
+                     r->n_ent, r->ntries, r->rec, r->rec_n1, (const int*)r->err);
+  SKGE_CHECK_LAUNCH("dp epoch sample");
+  return SKGE_OK;
+}
+
+extern "C" int skge_pipe_runner_dp_batch(skge_pipe_runner_t* r, void* stream, int b, int lo,
+                                         int hi, void* rec_out, int fold) {
+  SKGE_CHECK_ARG(r && r->dp, "not a data-parallel pipelined runner");
+  if (r->invalid) return refuse_invalid(r);
+  const int nb1 = (int)r->batch.size() - 1;
+  SKGE_CHECK_ARG(b >= 0 && b <= nb1, "batch %d out of [0, %d]", b, nb1);
+  PipeArgs a = r->batch[b];
+  SKGE_CHECK_ARG(0 <= lo && lo <= hi && hi <= a.count, "slice [%d, %d) out of the batch", lo, hi);
+  SKGE_CHECK_ARG(rec_out || lo == hi, "NULL record buffer");
+  a.lo = lo;
+  a.hi = hi;
+  a.dprec = (uint32_t*)rec_out;
+  const int wpb = (a.E.own[0] ? PIPE_WG_GRP : SKGE_PIPE_WG) / 64;
+  const int nBb = hi > lo ? std::min((hi - lo + wpb - 1) / wpb, 16384) : 0;
+  hipStream_t st = as_stream(stream);
+  launch_pipe_batch(r, dim3((unsigned)(a.nA + nBb)), st, a);
+  if (fold) rel_fold_launch(r, st, a);
+  SKGE_CHECK_LAUNCH("dp batch");
+  return SKGE_OK;
+}
+
+extern "C" int skge_pipe_runner_dp_scatter(skge_pipe_runner_t* r, void* stream, int b,
+                                           const void* recs, int lo, int hi) {
+  SKGE_CHECK_ARG(r && r->dp, "not a data-parallel pipelined runner");
+  if (r->invalid) return refuse_invalid(r);
+  const int nb1 = (int)r->batch.size() - 1;
+  SKGE_CHECK_ARG(b >= 0 && b < nb1, "batch %d out of [0, %d)", b, nb1);
+  PipeArgs a = r->batch[b];
+  SKGE_CHECK_ARG(0 <= lo && lo <= hi && hi <= a.count, "slice [%d, %d) out of the batch", lo, hi);
+  const int nrem = a.count - (hi - lo);
+  SKGE_CHECK_ARG(recs || nrem == 0, "NULL records");
+  a.lo = lo;
+  a.hi = hi;
+  hipStream_t st = as_stream(stream);
+  if (nrem > 0) {
+    const dim3 gr((unsigned)std::max(1, std::min((nrem + 3) / 4, 16384))), bl(256);
+    const uint32_t* rc = (const uint32_t*)recs;
+#define SKGE_DS(K)                                                                              \
+  do {                                                                                          \
+    if (r->e8) {                                                                                \
+      if (r->w32) hipLaunchKernelGGL((k_pipe_dp_scatter<K, true, true>), gr, bl, 0, st, a, rc);  \
+      else hipLaunchKernelGGL((k_pipe_dp_scatter<K, false, true>), gr, bl, 0, st, a, rc);        \
+    } else {                                                                                    \
+      if (r->w32) hipLaunchKernelGGL((k_pipe_dp_scatter<K, true, false>), gr, bl, 0, st, a, rc); \
+      else hipLaunchKernelGGL((k_pipe_dp_scatter<K, false, false>), gr, bl, 0, st, a, rc);       \
+    }                                                                                           \
+  } while (0)
+    if (r->kq <= 1) SKGE_DS(1);
+    else if (r->kq <= 2) SKGE_DS(2);
+    else SKGE_DS(4);
+#undef SKGE_DS
+  }
+  rel_fold_launch(r, st, a);
+  SKGE_CHECK_LAUNCH("dp scatter");
+  return SKGE_OK;
+}
+
+extern "C" int skge_pipe_runner_dp_end(skge_pipe_runner_t* r, void* stream) {
+  SKGE_CHECK_ARG(r && r->dp, "not a data-parallel pipelined runner");
+  hipLaunchKernelGGL(k_pipe_advance, dim3(1), dim3(1), 0, as_stream(stream), r->epoch_key);
+  SKGE_CHECK_LAUNCH("dp end");
+  return SKGE_OK;
 }
 
 extern "C" int skge_pipe_runner_error(skge_pipe_runner_t* r, void* stream) {

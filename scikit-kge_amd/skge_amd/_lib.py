@@ -99,10 +99,12 @@ SIGNATURES = {
     "skge_shard_score": (c_i, [c_p, T_P, c_i, c_p, c_p, c_i64, c_i, c_p, c_p, c_f, c_p, c_p]),
     "skge_shard_accum": (c_i, [c_p, T_P, c_i, c_p, c_p, c_i64]),
     "skge_shard_fold_violations": (c_i, [c_p, c_p, c_p]),
-    "skge_dp_record_bytes": (c_sz, [c_i]),
-    "skge_dp_score": (c_i, [c_p, T_P, T_P, c_i, c_p, c_i64, c_p, c_i64, c_i64, c_i, c_i, c_i,
-                            c_u64, c_p, c_f, c_i, c_p, c_p]),
-    "skge_dp_scatter": (c_i, [c_p, T_P, T_P, c_i, c_i64, c_i, c_p]),
+    "skge_pipe_runner_nbatches": (c_i, [c_p]),
+    "skge_pipe_dp_record_bytes": (c_sz, [c_i]),
+    "skge_pipe_runner_dp_begin": (c_i, [c_p, c_p]),
+    "skge_pipe_runner_dp_batch": (c_i, [c_p, c_p, c_i, c_i, c_i, c_p, c_i]),
+    "skge_pipe_runner_dp_scatter": (c_i, [c_p, c_p, c_i, c_p, c_i, c_i]),
+    "skge_pipe_runner_dp_end": (c_i, [c_p, c_p]),
     "skge_roofline_gather": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i,
                                    ctypes.c_uint32, c_p]),
     "skge_handoff_probe": (c_i, [c_p, c_p, c_i, c_p]),

@@ -7,22 +7,27 @@ its gradients segment-meaned and applied before the next batch starts
 (PairwiseStochasticTrainer._process_batch + _batch_step, skge/base.py:1394-1427
 and 1306-1316).  Here every rank draws the SAME epoch order and negatives
 (the keyed device sampler, one seed), and each union batch [start, start +
-count) is split into G slices:
+count) is split into G slices.  Per union batch b, on every rank:
 
-    score     rank g scores its slice: sampler, L1 scores, strict margin
-              test, sign sub-gradients -> one record per positive        [HIP]
+    launch    ONE launch of the one-GPU pipelined runner (k_pipe_batch in
+              its data-parallel form): apply union batch b-1's rows while
+              scoring the rank's slice of batch b -- its contributions added
+              locally, one record per positive written for the others  [HIP]
     gather    the G slices' records, all-gathered                        [RCCL]
-    scatter   every rank adds the whole batch's records into its exact
-              packed row sums, counts and touched slots                  [HIP]
-    apply     segment mean + AdaGrad + normalize of every touched row    [HIP]
+    scatter   the OTHER ranks' positives added into the same exact packed
+              sums, counts, slot records and pending marks (none at G = 1) [HIP]
 
-A record is the positive's (s, o, p, s', o'), its violation flags and, if it
-violates, its three sign vectors as 2-bit codes (240 B at d = 200).  The
-scatter runs the one-GPU kernel's own commit code over the union batch, and
-TransE-L1's sums are exact integers, so every replica ends each batch with
-the parameters ONE GPU computes for that union batch -- bit for bit (tests).
+and the epoch ends with the flush (applies the last batch).  A record is the
+positive's violation flags and, if it violates, its three sign vectors as
+2-bit codes (208 B at d = 200); the header (s, o, p, s', o') every rank has
+from the common epoch draws.  The scatter runs the scoring wave's own commit
+code, and TransE-L1's sums are exact integers, so every replica ends each
+batch with the parameters ONE GPU computes for that union batch -- bit for
+bit (tests).  Round 5's form (score, all-gather, scatter, apply: four serial
+phases, three launches) took ~60 us of kernels per union batch against 8.6
+us for the one-GPU launch; this one is that launch plus the exchange.
 
-The protocol (`dp_step`) is written against two small interfaces -- the
+The protocol (`dp_epoch`) is written against two small interfaces -- the
 rank's compute (`DPOps`) and the collective (`DPExchange`) -- so a CPU test
 drives the same protocol over gloo with a NumPy compute stand-in
 (tests/dp_numpy.py).  Under the "nccl" backend (RCCL) the whole epoch --
@@ -33,6 +38,8 @@ import torch
 import torch.distributed as dist
 
 from . import _lib as L
+
+SKGE_PIPE_DP = 1   # skge_pipe_runner_create_ex flag (include/skge_hip.h)
 
 
 def slice_of(count, G, rank):
@@ -84,57 +91,64 @@ class DPExchange(object):
         return int(t.item())
 
 
-def dp_step(ops, ex, start, count):
-    """One union batch of the data-parallel job (positions start .. start +
-    count of the common epoch order); see the module docstring."""
-    share, lo, hi = slice_of(count, ex.G, ex.rank)
-    send = ops.score(start, count, lo, hi, share)     # [share] records of this rank
-    recs = ops.gathered(ex, send, share)              # [G * share] records, rank-major
-    ops.scatter(start, count, recs)
-    ops.apply(count)
+def dp_epoch(ops, ex, batches):
+    """One epoch of the data-parallel job over the union batches (start,
+    count) of the common epoch order; see the module docstring.  Launch b
+    applies union batch b-1 and scores this rank's slice of batch b (its own
+    contributions added locally); the slices' records are all-gathered (a
+    real collective whenever a process group exists, also at G == 1) and the
+    other ranks' positives added; the flush applies the last batch."""
+    ops.begin()
+    grouped = ex.backend is not None
+    for b, (start, count) in enumerate(batches):
+        share, lo, hi = slice_of(count, ex.G, ex.rank)
+        remote = grouped and ex.G > 1
+        send = ops.batch(b, start, count, lo, hi, share, fold=not remote)
+        if grouped:
+            recs = ops.gathered(ex, send, share)
+            if remote:
+                ops.scatter(b, start, count, recs, lo, hi)
+    ops.flush(len(batches))
+    ops.end()
 
 
 class DPOps(object):
-    """The HIP compute of one rank (skge_dp_score / skge_dp_scatter /
-    skge_accum_apply, csrc/skge_epoch.hip, skge_update.hip)."""
+    """The HIP compute of one rank: the pipelined runner's data-parallel form
+    (skge_pipe_runner_dp_*, csrc/skge_pipeline.hip: k_pipe_batch over the
+    rank's slice with record output, k_pipe_dp_scatter for the other ranks'
+    records)."""
 
     def __init__(self, runner):
         self.r = runner
 
-    def score(self, start, count, lo, hi, share):
+    def begin(self):
         r = self.r
-        rb = r.rec_bytes
-        send = r.send[:share * rb]
-        L.check(L.lib().skge_dp_score(r.sp, r.te, r.tr, r.d, L.ptr(r.kg.trip), r.kg.T,
-                                      L.ptr(r.kg.slots), r.kg.capacity, start, count, lo, hi,
-                                      r.seed, L.ptr(r.epoch_key), r.margin, r.ntries,
-                                      L.ptr(r.vshards), L.ptr(send)), "dp score")
-        return send
+        L.check(L.lib().skge_pipe_runner_dp_begin(r.handle, r.sp), "dp begin")
+
+    def batch(self, b, start, count, lo, hi, share, fold):
+        r = self.r
+        send = r.send[:max(share, 1) * r.rec_bytes]
+        L.check(L.lib().skge_pipe_runner_dp_batch(r.handle, r.sp, b, lo, hi, L.ptr(send),
+                                                  int(bool(fold))), "dp batch")
+        return send[:share * r.rec_bytes]
 
     def gathered(self, ex, send, share):
         r = self.r
-        if ex.backend is None:       # one process: the slice is the batch
-            return send
         out = r.recv[:ex.G * share * r.rec_bytes]
         return ex.all_gather(out, send)
 
-    def scatter(self, start, count, recs):
+    def scatter(self, b, start, count, recs, lo, hi):
         r = self.r
-        L.check(L.lib().skge_dp_scatter(r.sp, r.te, r.tr, r.d, start, count, L.ptr(recs)),
+        L.check(L.lib().skge_pipe_runner_dp_scatter(r.handle, r.sp, b, L.ptr(recs), lo, hi),
                 "dp scatter")
 
-    def apply(self, count):
+    def flush(self, nb):
         r = self.r
-        L.check(L.lib().skge_accum_apply(r.sp, (L.SkgeTable * 2)(r.te, r.tr), 2,
-                                         L.int_array(4 * count, count)), "dp apply")
+        L.check(L.lib().skge_pipe_runner_dp_batch(r.handle, r.sp, nb, 0, 0, None, 0), "dp flush")
 
-
-class _PaddedParam(object):
-    """What table_struct reads of a Parameter: a zero-padded fp32 copy."""
-
-    def __init__(self, rows, width, dev):
-        self.rows, self.width = rows, width
-        self.data = torch.zeros((rows, width), dtype=torch.float32, device=dev)
+    def end(self):
+        r = self.r
+        L.check(L.lib().skge_pipe_runner_dp_end(r.handle, r.sp), "dp end")
 
 
 class DataParallelRunner(object):
@@ -144,16 +158,21 @@ class DataParallelRunner(object):
 
     Every rank passes the same initial model, updaters' learning rate, KG,
     nbatches and seed; the union batches follow np.split's geometry over the
-    KG (skge/base.py:1246-1268).  capture: None (auto) captures each rank's
-    epoch -- kernels and RCCL all-gathers -- into one CUDA graph under the
-    "nccl" backend (or with no process group), and runs eagerly under gloo.
+    KG (skge/base.py:1246-1268).  The rank's compute is the one-GPU pipelined
+    runner in its data-parallel form (one launch per union batch: apply of
+    the previous batch + scoring of the rank's slice; then the all-gather of
+    the slices' records and the other ranks' positives added).  capture:
+    None (auto) captures each rank's epoch -- kernels and RCCL all-gathers --
+    into one CUDA graph under the "nccl" backend (or with no process group),
+    and runs eagerly under gloo.
     """
 
     def __init__(self, model, updaters, kg, nbatches, seed=0, ntries=100, group=None, stream=None,
                  capture=None):
         from .transe import TransE
-        from .param import Accumulator, table_struct, post_code
-        from .device import packed_count_bound, relation_replicas, PACKED_MAX
+        from .device import (EpochRunner, packed_count_bound, relation_replicas, padded_width,
+                             _tail8, PACKED_MAX)
+        import os
         if not isinstance(model, TransE) or not model.l1 or model.d > 1024:
             raise ValueError("data-parallel runner: TransE-L1 with d <= 1024")
         self.ex = DPExchange(group)
@@ -168,89 +187,67 @@ class DataParallelRunner(object):
         # device.EpochRunner does), copied in and out around every run().  A
         # zero column stays zero (sign(0) = 0 contributions, AdaGrad and the
         # projection keep 0 at 0) and adds nothing to a score or a norm.
-        from .device import padded_width
-        self.d = int(model.d) if model.d % 4 == 0 else padded_width(int(model.d))
-        self._pad = self.d != int(model.d)
+        self.d_pad = padded_width(int(model.d))
+        self._pad = model.d % 4 != 0
+        self.d = self.d_pad if self._pad else int(model.d)
         self.margin = float(model.margin)
         self.seed = int(seed) & (2 ** 64 - 1)
         self.ntries = int(ntries)
         T = kg.T
         if not 1 <= nbatches <= T:
             raise ValueError("nbatches must be in [1, T]")
+        self.nbatches = nbatches
         bs = T // nbatches
         self.batches = [(s0, min(bs, T - s0)) for s0 in range(0, T, bs)]
         if packed_count_bound(kg, model.E.rows, bs) > PACKED_MAX:
             raise ValueError("data-parallel runner: an entity's per-batch count could pass 32767 "
                              "(exact packed sums); use more batches")
-        reps = relation_replicas(kg, model.R.rows, bs)
-        if reps == 0:
+        rel_reps = relation_replicas(kg, model.R.rows, bs)
+        if rel_reps == 0:
             raise ValueError("data-parallel runner: a relation's per-batch count exceeds what 32 "
                              "packed accumulator copies hold; use more batches")
-        E, R = model.params["E"], model.params["R"]
-        self.accE = Accumulator(E.rows, self.d, dev, slots=4 * bs, mode=L.SKGE_ACC_I16X4)
-        self.accR = Accumulator(R.rows, self.d, dev, mode=L.SKGE_ACC_I16X4, dense=True,
-                                replicas=reps)
-        if self._pad:
-            self._padded = []
-            tabs = []
-            for pid, acc in (("E", self.accE), ("R", self.accR)):
-                u, P = updaters[pid], model.params[pid]
-                pp = _PaddedParam(P.rows, self.d, dev)
-                st = u.state()
-                sp = None if st is None else torch.zeros_like(pp.data)
-                self._padded.append((P, pp.data, st, sp))
-                tabs.append(table_struct(pp, sp, acc, opt=u.opt, post=post_code(u.param.post),
-                                         lr=float(u.learning_rate)))
-            self.te, self.tr = tabs
-        else:
-            self.te = updaters["E"].table(self.accE, counters=False)
-            self.tr = updaters["R"].table(self.accR, counters=False)
-        self.rec_bytes = int(L.lib().skge_dp_record_bytes(self.d))
+        e8 = (packed_count_bound(kg, model.E.rows, bs, _tail8) <= 127 and
+              os.environ.get("SKGE_PIPE_E8", "1") != "0")
+        # the one-GPU pipelined runner's tables (same encodings: the same sums)
+        EpochRunner._tables(self, model, updaters, True, 1, rel_w32=rel_reps != 1, ent_i8=e8,
+                            pad=self._pad)
+        self.rec_bytes = int(L.lib().skge_pipe_dp_record_bytes(self.d))
         share_max = -(-bs // self.G)
         self.send = torch.zeros(max(share_max, 1) * self.rec_bytes, dtype=torch.uint8, device=dev)
         self.recv = torch.zeros(self.G * max(share_max, 1) * self.rec_bytes, dtype=torch.uint8,
                                 device=dev)
-        self.vshards = torch.zeros(64 * 32, dtype=torch.int32, device=dev)
         self.nviol_total = torch.zeros(1, dtype=torch.int32, device=dev)   # this rank's slices
         self.epoch_key = torch.zeros(1, dtype=torch.int64, device=dev)
+        torch.cuda.current_stream(dev).synchronize()   # the zero fills, before the runner's stream
+        h = L.lib().skge_pipe_runner_create_ex(
+            self.sp, self.te, self.tr, self.d, L.ptr(kg.trip), kg.T, L.ptr(kg.slots), kg.capacity,
+            int(nbatches), self.seed, L.ptr(self.epoch_key), self.margin, self.ntries,
+            L.ptr(self.nviol_total), SKGE_PIPE_DP)
+        if not h:
+            raise L.SkgeError("data-parallel runner: %s" % L.lib().skge_last_error().decode())
+        self.handle = h
         self.ops = DPOps(self)
         if capture is None:
             capture = self.ex.backend in (None, "nccl")
         self.capture = bool(capture)
         self.graph = None
-        self.nlaunches = 3 * len(self.batches) + 2
-        self.ncollectives = len(self.batches) if self.ex.backend is not None else 0
-        torch.cuda.current_stream(dev).synchronize()
+        # launches per epoch: the draw, nb1 batch launches (+ nb1 remote
+        # scatters when G > 1), the flush, the key advance
+        nb1 = len(self.batches)
+        self.nlaunches = nb1 * (2 if self.G > 1 else 1) + 3
+        self.ncollectives = nb1 if self.ex.backend is not None else 0
 
     # ---- one epoch ----
     def _epoch(self):
-        for start, count in self.batches:
-            dp_step(self.ops, self.ex, start, count)
-        L.check(L.lib().skge_shard_fold_violations(self.sp, L.ptr(self.vshards),
-                                                   L.ptr(self.nviol_total)), "dp fold")
-        L.check(L.lib().skge_epoch_advance(self.sp, L.ptr(self.epoch_key)), "dp advance")
+        dp_epoch(self.ops, self.ex, self.batches)
 
     def _pad_in(self):
-        if not self._pad:
-            return
-        d = self.model.d
-        self.stream.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.stream):
-            for P, Pp, st, sp in self._padded:
-                Pp[:, :d].copy_(P.data)
-                if st is not None:
-                    sp[:, :d].copy_(st)
+        from .device import EpochRunner
+        EpochRunner._pad_in(self)
 
     def _pad_out(self):
-        if not self._pad:
-            return
-        d = self.model.d
-        with torch.cuda.stream(self.stream):
-            for P, Pp, st, sp in self._padded:
-                P.data.copy_(Pp[:, :d])
-                if st is not None:
-                    st.copy_(sp[:, :d])
-        torch.cuda.current_stream().wait_stream(self.stream)
+        from .device import EpochRunner
+        EpochRunner._pad_out(self)
 
     def run(self, nepochs=1):
         # ordered after the caller's stream (parameters it wrote), and its later
@@ -281,11 +278,27 @@ class DataParallelRunner(object):
 
     def synchronize(self):
         self.stream.synchronize()
-        rc = L.lib().skge_device_error(self.sp, 1)
+        rc = L.lib().skge_pipe_runner_error(self.handle, self.sp)
+        if rc < 0:
+            raise L.SkgeError("data-parallel runner: %s" % L.lib().skge_last_error().decode())
+        if rc & 1:
+            raise L.SkgeError("data-parallel runner: a cross-workgroup wait timed out; the "
+                              "runner refuses further runs")
         if rc & 2:
             raise L.SkgeError("data-parallel runner: a row's per-batch count exceeded 32767 "
-                              "(packed sums may have wrapped)")
+                              "(packed sums may have wrapped); the runner refuses further runs")
 
     def total_violations(self):
         """Violating pairs of all ranks (every pair is scored by one rank)."""
         return self.ex.sum_int(int(self.nviol_total.item()))
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                self.graph = None
+                self.stream.synchronize()
+                L.lib().skge_pipe_runner_destroy(h)
+            except Exception:
+                pass
+            self.handle = None

@@ -1,7 +1,7 @@
 """bench.py's multi-GPU bookkeeping on CPU: a world-size-2 gloo job checks the
 rank environment, the max-over-ranks timing and the whole-job value; the
 `--gpus N --dry-run` launcher runs the N > 1 line's data-parallel protocol
-(skge_amd.dp.dp_step with the NumPy rank compute over gloo) and must print ONE
+(skge_amd.dp.dp_epoch with the NumPy rank compute over gloo) and must print ONE
 line shaped like the one-model DP line (parallelism dpN, strong scaling,
 identical replicas).  The protocol's numerics: tests/test_dp_protocol.py."""
 import json

@@ -1,6 +1,8 @@
-"""The data-parallel step's protocol (skge_amd.dp.dp_step: every rank scores
-its slice of the union batch, the slices' records are all-gathered, every
-rank scatters and applies the whole batch) over world-size 2 and 3 gloo jobs
+"""The data-parallel epoch's protocol (skge_amd.dp.dp_epoch: per union batch
+one launch applies the previous batch and scores this rank's slice, adding
+its contributions locally; the slices' records are all-gathered and the
+other ranks' positives added; the flush applies the last batch) over
+world-size 2 and 3 gloo jobs
 on CPU, with the NumPy rank compute of tests/dp_numpy.py.  After every batch
 each rank's replica must equal ONE process's reference step
 (oracle.pairwise_step: skge/transe.py:48-165 + AdaGrad + normalize) over the
@@ -45,16 +47,14 @@ def _worker(rank, world, port, batches, out):
     for p in (ROOT, os.path.join(ROOT, "scikit-kge_amd"), os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
     import torch.distributed as dist
-    from skge_amd.dp import DPExchange, dp_step
+    from skge_amd.dp import DPExchange, dp_epoch
     from dp_numpy import NumpyDPOps
     dist.init_process_group("gloo", init_method="env://")
     E, R, rec, rec_n1 = _problem()
     ops = NumpyDPOps(rec, rec_n1, E, R, MARGIN, LR)
     ex = DPExchange()
-    snaps = []
-    for start, count in batches:
-        dp_step(ops, ex, start, count)
-        snaps.append((ops.E.copy(), ops.R.copy(), ops.AE.copy()))
+    dp_epoch(ops, ex, batches)
+    snaps = ops.snaps               # the tables after every union batch's apply
     dist.barrier()
     dist.destroy_process_group()
     out.put((rank, snaps, ops.nviol))
@@ -80,6 +80,7 @@ def test_dp_protocol_matches_union_batch(world, batches):
     from oracle import skge_oracle as O
     from shard_numpy import union_pairs
     res = _run(world, batches)
+    assert all(len(r[1]) == len(batches) for r in res)
     E, R, rec, rec_n1 = _problem()
     params = {"E": E.copy(), "R": R.copy()}
     state = {k: np.zeros_like(v) for k, v in params.items()}

@@ -250,3 +250,90 @@ def test_two_ranks_on_one_gpu_match_union_oracle(D2):
     assert np.array_equal(res[0][4], res[1][4])          # relation replicas identical
     parity_util.check(res[0][3], params["E"], "shard 2 ranks d%d E" % D2, lr=0.1, p2=state["E"])
     parity_util.check(res[0][4], params["R"], "shard 2 ranks d%d R" % D2, lr=0.1, p2=state["R"])
+
+
+def test_config5_rows_past_2_31_elements_match_oracle():
+    """Config 5's row range (|E| = 50M at d = 512 puts row r at element offset
+    r * 512, past 2^31 from row 4,194,304 on): a d = 512 table of 4.3M rows
+    (8.8 GB, and as much again for its AdaGrad state) whose positives use only
+    rows >= 4,194,304 as s and o (the corruptions are uniform over all rows).
+    Two batches of 4096 positives through the sharded step at G = 1, compared
+    on every touched row and its AdaGrad state with oracle.pairwise_step on
+    the gathered sub-table; the single-GPU device runners (pipelined and
+    two-launch) must reproduce the sharded step bit for bit on the whole
+    table (the G = 1 identity test_single_rank_bitwise_equals_device_runner
+    checks at small sizes)."""
+    import skge_amd as S
+    from skge_amd.shard import ShardedRunner
+    from skge_amd.device import DeviceKG, EpochRunner
+    from shard_numpy import union_pairs
+    N, M, d, B = 4_300_000, 16, 512, 4096
+    LO = 1 << 22                     # first row whose element offset r * 512 reaches 2^31
+    assert LO * d == 1 << 31 and N > LO
+    dev = torch.device("cuda", 0)
+    rs = np.random.RandomState(17)
+    keys = set()
+    while len(keys) < 2 * B:
+        s, o, p = (int(x) for x in (rs.randint(LO, N), rs.randint(LO, N), rs.randint(M)))
+        keys.add((s, o, p))
+    trip = np.array(sorted(keys), dtype=np.int32)
+    rs.shuffle(trip)
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    E0 = torch.empty((N, d), dtype=torch.float32, device=dev)
+    E0.uniform_(-0.08, 0.08, generator=g)
+    for r0 in range(0, N, 1 << 20):
+        blk = E0[r0:r0 + (1 << 20)]
+        blk.div_(blk.norm(dim=1, keepdim=True))
+    R0 = torch.empty((M, d), dtype=torch.float32, device=dev)
+    R0.uniform_(-0.1, 0.1, generator=g)
+    seed = 23
+    # ---- the sharded step at G = 1, two batches, replayed by the oracle ----
+    r = ShardedRunner(N, E0.clone(), R0.clone(), torch.as_tensor(trip, device=dev), 2, seed=seed)
+    r.sample_epoch()
+    torch.cuda.synchronize()
+    rec, rec_n1 = r.rec.cpu().numpy(), r.rec_n1.cpu().numpy()
+    ids = np.concatenate([rec[:, 0], rec[:, 1], rec[:, 3], rec_n1])
+    rows = np.unique(ids[ids >= 0])
+    assert rows[-1] >= LO and (rec[:, :2] >= LO).all()
+    for b in range(2):
+        r.step(b * B, B)
+    r.fold_violations()
+    r.synchronize()
+    sub = torch.as_tensor(rows, device=dev, dtype=torch.int64)
+    E_sh, p2_sh = r.E.data[sub].cpu().numpy(), r.updE.p2[sub].cpu().numpy()
+    R_sh, pR_sh = r.R.data.cpu().numpy(), r.updR.p2.cpu().numpy()
+    nv_sh = int(r.nviol_total.item())
+    full_sh = (r.E.data.clone(), r.updE.p2.clone())
+    del r
+    remap = lambda x: np.where(x[:, :2] >= 0, np.searchsorted(rows, x[:, :2]), x[:, :2])
+    params = {"E": E0[sub].cpu().numpy().astype(np.float64), "R": R0.cpu().numpy().astype(np.float64)}
+    state = {k: np.zeros_like(v) for k, v in params.items()}
+    nv = 0
+    for b in range(2):
+        pos, neg = union_pairs([(rec, rec_n1, b * B, B)])
+        pos[:, :2], neg[:, :2] = remap(pos), remap(neg)
+        nv += O.pairwise_step("transe", params, state, pos, neg, 0.1, 2.0, "adagrad", l1=True)[2]
+    assert nv_sh == nv > 0
+    parity_util.check(E_sh, params["E"], "c5 rows>2^31 E", lr=0.1, p2=state["E"])
+    parity_util.check(p2_sh, state["E"], "c5 rows>2^31 p2 E")
+    parity_util.check(R_sh, params["R"], "c5 rows>2^31 R", lr=0.1, p2=state["R"])
+    parity_util.check(pR_sh, state["R"], "c5 rows>2^31 p2 R")
+    # ---- the single-GPU device runners: one epoch = the same two batches ----
+    kg = DeviceKG(trip, dev)
+    for pipelined in (None, False):
+        m = S.TransE((N, N, M), d, init="device_nunif")
+        m.add_hyperparam("margin", 2.0)
+        m.E.data.copy_(E0)
+        m.R.data.copy_(R0)
+        upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
+        er = EpochRunner(m, upd, kg, nbatches=2, seed=seed, pipelined=pipelined)
+        er.run(1)
+        er.synchronize()
+        torch.cuda.synchronize()
+        assert int(er.nviol_total.item()) == nv, (pipelined, er.pipelined)
+        assert torch.equal(m.E.data, full_sh[0]), (pipelined, er.pipelined)
+        assert torch.equal(upd["E"].p2, full_sh[1]), (pipelined, er.pipelined)
+        assert np.array_equal(m.R.data.cpu().numpy(), R_sh)
+        del er, m, upd
+        torch.cuda.empty_cache()
