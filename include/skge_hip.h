@@ -340,9 +340,9 @@ void skge_pair_runner_destroy(skge_pair_runner_t *r);
  * applier writes the row's other buffer (the runner's second copy of E and
  * its AdaGrad state; run() and profile() end by copying every row back into
  * the caller's tables).  Otherwise k_pipe_batch: apply waves beside scoring
- * waves that wait for a pending row's publisher (below 16k slot records the
- * apply items walk a touched-row bitmap, 32 rows each; above, owner marks over
- * the slot records).  Needs ent
+ * waves that wait for a pending row's publisher (one apply wave per slot
+ * record below 16k slot records; above, owner marks over the slot records).
+ * Needs ent
  * in SKGE_ACC_I16X4 mode (SKGE_ACC_I8X4: int8x4 sums, counts <= 127), rel in
  * SKGE_ACC_I16X4 or SKGE_ACC_I32X2 mode (the encoding of the relation sums
  * the runner keeps), d % 4 == 0, an entity table with slot records (capacity

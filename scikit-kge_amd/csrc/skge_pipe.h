@@ -44,13 +44,6 @@ struct PipeTab {               // entity table
                                // (plain stores, one survives): the A role applies a row from
                                // that slot only, so duplicate slots cost no claim
   int* done;                   // [rows]: id of the launch whose update of the row was last applied
-  // touched-row bitmaps (k_pipe_batch below 16k slot records): bit r of
-  // bm[parity] set by every scoring lane that records row r; the next launch's
-  // A role gives one item to each 2^bm_shift rows and applies only the set
-  // bits' rows (cleared as it reads them), so the apply waves number
-  // rows / 2^bm_shift instead of one per slot record (nullptr: slot records)
-  unsigned* bm[2];
-  int bm_shift;
   // hot rows (skewed KGs): rows expected in >= HOT_MIN slots per batch add
   // their sums and counts into HOT_REPS replicas (positive w into replica
   // w % HOT_REPS) instead of one row and record no slot or mark; their values
@@ -114,7 +107,6 @@ struct PipeArgs {
                                // (data-parallel ranks: their slice; else 0, count)
   uint32_t* dprec;             // data-parallel: one record per scored positive (pipe_dp_record_words)
   int prev_slots;              // A role: entity slots of the previous batch
-  int bm_items;                // A role, bitmap mode: items over the previous batch's bitmap
   int b, nb1;                  // batch index in the epoch (nb1: the flush), batches per epoch
   const uint64_t* epoch_key;
   int d, nA;                   // nA: workgroups of the A role

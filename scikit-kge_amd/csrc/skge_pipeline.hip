@@ -46,14 +46,6 @@
 
 namespace skge {
 
-// touched-row bitmaps below 16k slot records (PipeTab::bm), rows per apply item
-#ifndef SKGE_PIPE_BITMAP
-#define SKGE_PIPE_BITMAP 0
-#endif
-#ifndef SKGE_PIPE_BM_SHIFT
-#define SKGE_PIPE_BM_SHIFT 5
-#endif
-
 // k_pipe_batch (large batches: more than 16k slot records per batch; smaller
 // batches run k_pipe_fused below): nA apply workgroups (dispatched first: they
 // start the hand-offs the scoring waves may wait on), then the scoring ones.
@@ -80,9 +72,8 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
     // owner marks (large batches): items are groups of 64 slots, scanned
     // lane-parallel; else one slot per item
     const int* const ownp = a.E.own[pp];
-    unsigned* const bmp = a.E.bm[pp];
     const int nH = a.E.nhot, nRH = nR + nH;   // then one item per hot row
-    const int total = nRH + (bmp ? a.bm_items : ownp ? (a.prev_slots + 63) / 64 : a.prev_slots);
+    const int total = nRH + (ownp ? (a.prev_slots + 63) / 64 : a.prev_slots);
     const int wa = blk_a * wpb + (threadIdx.x >> 6);
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
     // the flush scores nothing: plain stores (WN18 nb = 2, same box: 496 -> 539 M)
@@ -94,28 +85,6 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
         rel_publish<KQ, W32>(a, w, rd, rw, ra_prev, ra_old);
       } else if (w < nRH) {
         if (HOT) apply_hot<KQ>(a.E, w - nR, g, d);
-      } else if (bmp) {
-        // rows [i << sh, (i + 1) << sh) of the bitmap: the set bits' rows,
-        // GRP_ROWS per claim / load / drain round trip; the bits cleared
-        // (launch g + 1's scoring waves set them again)
-        const int sh = a.E.bm_shift, i = w - nRH;
-        const int r0 = i << sh, wi = r0 >> 5, b0 = r0 & 31;
-        const unsigned msk = sh >= 5 ? 0xffffffffu : ((1u << (1 << sh)) - 1u) << b0;
-        unsigned m = (unsigned)__builtin_amdgcn_readfirstlane((int)bmp[wi]) & msk;
-        if (m && l == 0) atomicAnd(bmp + wi, ~msk);
-        while (m) {
-          // lanes j < n: the rows of m's next n set bits
-          int rl = 0, n = 0;
-#pragma unroll
-          for (int j = 0; j < GRP_ROWS; ++j) {
-            if (!m) break;
-            const int k = __ffs(m) - 1;
-            m &= m - 1u;
-            if (l == j) rl = 32 * wi + k;
-            ++n;
-          }
-          claim_and_apply_rows<KQ, E8>(a.E, pp, rl, n, d, gp, wt);
-        }
       } else if (ownp) {
         // 64 slots: their rows and owner marks in two vector loads; only the
         // slot each row's owner mark names applies it (no claim on duplicates)
@@ -169,7 +138,6 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
   int* const tch_cp = opaque_ptr(a.E.touched[cp]);
   int* const pend_cp = opaque_ptr(a.E.pend[cp]);
   int* const own_cp = a.E.own[cp];
-  unsigned* const bm_cp = a.E.bm[cp];
   unsigned long long* const racc0 = opaque_ptr(a.R.acc[ra_cur]);
   const size_t rrep = (size_t)a.R.rows * a.R.rw;   // words per relation replica
   const int rmask = a.R.reps - 1;                  // reps: a power of two (k_rel_fold)
@@ -300,14 +268,7 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
         if (cE > 0) atomicAdd(a.E.hcnt[g % 3] + hx * HOT_REPS + (w & (HOT_REPS - 1)), cE);
         tch_cp[4 * w + l] = -1;
       } else if (l < 4) {
-        if (bm_cp) {   // touched-row bitmap instead of slot records
-          if (cE > 0) {
-            atomicAdd(cnt_cp + rE, cE);
-            atomicOr(bm_cp + (rE >> 5), 1u << (rE & 31));
-          }
-        } else {
-          commit_slot(cnt_cp, tch_cp, rE, cE, 4 * w + l);
-        }
+        commit_slot(cnt_cp, tch_cp, rE, cE, 4 * w + l);
         if (cE > 0) {
           pend_cp[rE] = g;
           if (own_cp) own_cp[rE] = 4 * w + l;   // large batches: this slot may own the row
@@ -1337,13 +1298,6 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
         t.own[0] = (int*)dalloc(r, (size_t)N * 4);
         t.own[1] = (int*)dalloc(r, (size_t)N * 4);
         ok = ok && t.own[0] && t.own[1];
-      } else if (!hole && !dp && SKGE_PIPE_BITMAP && ((long long)N >> SKGE_PIPE_BM_SHIFT) < 4 * bs) {
-        // touched-row bitmaps: fewer apply items than slot records
-        t.bm_shift = SKGE_PIPE_BM_SHIFT;
-        for (int k = 0; k < 2; ++k) {
-          t.bm[k] = (unsigned*)dalloc(r, (size_t)((N + 31) / 32) * 4);
-          ok = ok && t.bm[k];
-        }
       }
       // (the data-parallel form keeps every row in the tables: no hot rows)
       if (ok && !hole && !r->e8 && !dp)
@@ -1467,11 +1421,9 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
     }
     // A role: every relation row, then the previous batch's entity slots
     // (owner marks: 64-slot groups)
-    a.bm_items = (a.E.bm[0] && cprev > 0) ? (int)(((long long)N + (1 << a.E.bm_shift) - 1) >> a.E.bm_shift) : 0;
     const int a_items = rel->rows + a.E.nhot +
                         (hole ? 4 * cprev
-                         : grouped ? (4 * cprev + 63) / 64
-                         : a.E.bm[0] ? a.bm_items : 4 * cprev);
+                         : grouped ? (4 * cprev + 63) / 64 : 4 * cprev);
     // HolE: the apply waves loop over their items within the residency the
     // scoring waves leave (direct form: 2 waves per SIMD at ~180 VGPRs; FFT: 4
     // -- caps 150 / 250 / 400 / 600 / 800 / 1100 on WN18 d = 200: 74.7 / 77.6 /
