@@ -68,7 +68,8 @@ class DPExchange(object):
 
     def all_gather(self, out, inp):
         """out [G * n] <- every rank's inp [n], rank-major (a real collective
-        whenever a process group exists, also at G == 1)."""
+        whenever a process group exists, also at G == 1).  inp may be this
+        rank's slice of out (in place)."""
         if self.backend is None:
             if out.data_ptr() != inp.data_ptr():
                 out[:inp.numel()].copy_(inp)
@@ -126,11 +127,15 @@ class DPOps(object):
         L.check(L.lib().skge_pipe_runner_dp_begin(r.handle, r.sp), "dp begin")
 
     def batch(self, b, start, count, lo, hi, share, fold):
+        # the records go straight into this rank's slot of the gather buffer
+        # (an in-place all-gather: no copy of the own slice; at G = 1 none)
         r = self.r
-        send = r.send[:max(share, 1) * r.rec_bytes]
-        L.check(L.lib().skge_pipe_runner_dp_batch(r.handle, r.sp, b, lo, hi, L.ptr(send),
+        rb = r.rec_bytes
+        off = r.rank * share * rb
+        L.check(L.lib().skge_pipe_runner_dp_batch(r.handle, r.sp, b, lo, hi,
+                                                  L.ptr(r.recv[off:off + max(share, 1) * rb]),
                                                   int(bool(fold))), "dp batch")
-        return send[:share * r.rec_bytes]
+        return r.recv[off:off + share * rb]
 
     def gathered(self, ex, send, share):
         r = self.r
@@ -213,9 +218,8 @@ class DataParallelRunner(object):
                             pad=self._pad)
         self.rec_bytes = int(L.lib().skge_pipe_dp_record_bytes(self.d))
         share_max = -(-bs // self.G)
-        self.send = torch.zeros(max(share_max, 1) * self.rec_bytes, dtype=torch.uint8, device=dev)
-        self.recv = torch.zeros(self.G * max(share_max, 1) * self.rec_bytes, dtype=torch.uint8,
-                                device=dev)
+        self.recv = torch.zeros((self.G * max(share_max, 1) + 1) * self.rec_bytes,
+                                dtype=torch.uint8, device=dev)
         self.nviol_total = torch.zeros(1, dtype=torch.int32, device=dev)   # this rank's slices
         self.epoch_key = torch.zeros(1, dtype=torch.int64, device=dev)
         torch.cuda.current_stream(dev).synchronize()   # the zero fills, before the runner's stream
