@@ -190,6 +190,87 @@ __device__ __forceinline__ void ensure_applied_f(const PipeTab& t, int pp, int r
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the re-read below the poll
 }
 
+// Hot entity rows (PipeTab::hot; the pair form on skewed KGs), fp32 sums: the
+// scheme of TransE's hot_value / apply_hot (skge_pipe.h).  A hub's sums and
+// count go to replica w % HOT_REPS of three rotating copies (launch g adds
+// into copy g % 3); its value after launch g lives in hP[g & 1].  A scoring
+// wave of launch g that reads a hub computes the value batch b scores with --
+// the previous value hP[(g-1) & 1] updated with copy (g-1) % 3, inputs nobody
+// writes during launch g -- itself, with the replicas added in index order
+// and the applier's arithmetic (row_update_f): every reader and the A-role
+// item get the same bits, and nobody waits on a hub.  Float atomics make the
+// replica sums themselves order-dependent (as every HolE sum is), so the
+// runner equals the two-launch loop to fp32 rounding.  Replica rows hold
+// 2 * hw floats.
+template <int KQ>
+__device__ __forceinline__ int hot_value_f(const PipeTab& t, int h, int g, int d, float4 (&p)[KQ],
+                                           float4 (&a)[KQ]) {
+  const int l = lane_id(), nq = d >> 2, hwf = 2 * t.hw;
+  const int src = (g - 1) & 1, cp = (g - 1) % 3;
+  const float4* prow = reinterpret_cast<const float4*>(t.hP[src] + (size_t)h * d);
+  const float4* arow = reinterpret_cast<const float4*>((t.hA[src] ? t.hA[src] : t.hP[src]) +
+                                                       (size_t)h * d);
+  const float* hrow = reinterpret_cast<const float*>(t.hsum[cp]) + (size_t)h * HOT_REPS * hwf;
+  const int cl = l < HOT_REPS ? t.hcnt[cp][h * HOT_REPS + l] : 0;
+  const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  float4 x[HOT_REPS][KQ], sm[KQ];
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    const int q = 64 * m + l, qc = q < nq ? q : nq - 1;
+    p[m] = prow[qc];
+    a[m] = t.hA[src] ? arow[qc] : z;
+#pragma unroll
+    for (int k = 0; k < HOT_REPS; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(hrow + (size_t)k * hwf)[qc];
+      x[k][m] = q < nq ? v : z;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < KQ; ++m) {
+    sm[m] = x[0][m];
+#pragma unroll
+    for (int k = 1; k < HOT_REPS; ++k) {
+      sm[m].x += x[k][m].x;
+      sm[m].y += x[k][m].y;
+      sm[m].z += x[k][m].z;
+      sm[m].w += x[k][m].w;
+    }
+  }
+  const int c = wave_sum_int(cl);
+  if (c) {
+    row_update_f<KQ>(t.u, c, d, sm, p, a);
+  } else {
+#pragma unroll
+    for (int m = 0; m < KQ; ++m)
+      if (64 * m + l >= nq) p[m] = z;
+  }
+  return c;
+}
+
+// launch g's item for hot row h: its value after the launch into hP[g & 1]
+// (plain stores: read by later launches only), the replica copy launch g + 1
+// adds into ((g - 2) % 3) zeroed
+template <int KQ>
+__device__ __forceinline__ void apply_hot_f(const PipeTab& t, int h, int g, int d) {
+  const int l = lane_id(), nq = d >> 2, hwf = 2 * t.hw;
+  float4 p[KQ], a[KQ];
+  const int c = hot_value_f<KQ>(t, h, g, d, p, a);
+  store_row4<KQ>(t.hP[g & 1], h, d, p);
+  if (t.hA[0]) store_row4<KQ>(t.hA[g & 1], h, d, a);
+  const int old = (g - 2) % 3;
+  float* hrow = reinterpret_cast<float*>(t.hsum[old]) + (size_t)h * HOT_REPS * hwf;
+#pragma unroll
+  for (int k = 0; k < HOT_REPS; ++k)
+#pragma unroll
+    for (int m = 0; m < KQ; ++m) {
+      const int q = 64 * m + l;
+      if (q < nq)
+        reinterpret_cast<float4*>(hrow + (size_t)k * hwf)[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+  if (l < HOT_REPS) t.hcnt[old][h * HOT_REPS + l] = 0;
+  if (c && t.claims && l == 0) atomicAdd(shard_of(t.claims), 1);
+}
+
 // relation row R_b[row] from R_{b-1} (buffer rd) and batch b-1's fp32 sums
 // (copy ra: floats [0, d), count at float d); zero past the row
 template <int KQ>
@@ -265,7 +346,7 @@ __device__ __forceinline__ void rel_publish_f(const PipeArgs& a, int w, int rd, 
 // split between them (fft_run_c2: the same butterflies, the same bits), both
 // compute the spectra and scores (identical values), and each issues half of
 // the contribution rows' atomics -- so a positive's serial chain is shorter.
-template <int KM>
+template <int KM, bool HOT>
 __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* smem, int blk_b,
                                                      int nB) {
   const int hw = (int)(threadIdx.x >> 6);   // the wave's half of the pair
@@ -305,8 +386,9 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
     float4 xa[1], xb[1], xr[1] = {};
     load_row4<1>(a.E.P, ra_row, d, xa);
     load_row4<1>(a.E.P, rb_row, d, xb);
-    int mark = 0;
+    int mark = 0, hxl = -1;
     if (l < 2) mark = a.E.pend[pp][l ? rb_row : ra_row];
+    if (HOT && l < 4) hxl = a.E.hot[sel4(l, s, o, n0r, n1r)];   // hub rows: no marks, no waits
     if (hw == a.pair_r1) {
       float4 rav[1];
       int c;
@@ -319,6 +401,19 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
       if (pend & 2ull) ensure_applied_f<1>(a.E, pp, rb_row, d, gp, a.err);
       if (pend & 1ull) load_row4_sc1<1>(a.E.P, ra_row, d, xa);
       if (pend & 2ull) load_row4_sc1<1>(a.E.P, rb_row, d, xb);
+    }
+    if (HOT) {   // this wave's hub rows: the value after batch b-1, computed here
+      const int ha = __builtin_amdgcn_readlane(hxl, hw ? 1 : 0);
+      const int hb = __builtin_amdgcn_readlane(hxl, hw ? 3 : 2);
+      float4 hv[1], hav[1];
+      if (ha >= 0) {
+        hot_value_f<1>(a.E, ha, g, d, hv, hav);
+        xa[0] = hv[0];
+      }
+      if (hb >= 0) {
+        hot_value_f<1>(a.E, hb, g, d, hv, hav);
+        xb[0] = hv[0];
+      }
     }
     if (a.trace) tt[2] = now_10ns();
     __syncthreads();   // the previous positive's buffers are free, the twiddles in place
@@ -351,7 +446,10 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
     if (hw == 0) {
       const int cE = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
       const int rE = sel4(l, s, o, neg0, neg1);
-      if (l < 4) {
+      if (HOT && l < 4 && hxl >= 0) {   // hub: count into its replica, no slot record
+        if (cE > 0) atomicAdd(a.E.hcnt[g % 3] + hxl * HOT_REPS + (w & (HOT_REPS - 1)), cE);
+        a.E.touched[cp][4 * w + l] = -1;
+      } else if (l < 4) {
         commit_slot(a.E.cnt[cp], a.E.touched[cp], rE, cE, 4 * w + l);
         if (cE > 0) a.E.pend[cp][rE] = g;
       } else if (l == 4 && v0 + v1 > 0) {
@@ -367,16 +465,29 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
     const float g0 = af_g_given_f(a.af, f0), g1 = af_g_given_f(a.af, f1);   // hole.py:67
     const float* z = hole_fft_rows_pair(wb, tw, hs, v0, v1, gpf, g0, g1, hw);
     const unsigned long long inv_dt = a.trace ? now_10ns() - tt[3] : 0ull;
+    // an entity row's target: its sums, or a hub's replica w % HOT_REPS
+    auto ent_row = [&](int k, int row, int t) {
+      const int h = HOT ? __builtin_amdgcn_readlane(hxl, k) : -1;
+      if (h >= 0) {
+        Accum aH = {};
+        aH.sum = reinterpret_cast<float*>(a.E.hsum[g % 3]) +
+                 ((size_t)h * HOT_REPS + (w & (HOT_REPS - 1))) * (2 * a.E.hw);
+        aH.width = d;
+        acc_fft_row<KM>(aH, 0, z, t, d);
+      } else {
+        acc_fft_row<KM>(aE, row, z, t, d);
+      }
+    };
     if (hw == 0) {
       Accum aR = {};
       aR.sum = racc + (size_t)p * rstride;
       aR.width = d;
       acc_fft_row<KM>(aR, 0, z, 2, d);
-      acc_fft_row<KM>(aE, s, z, 0, d);
+      ent_row(0, s, 0);
     } else {
-      acc_fft_row<KM>(aE, o, z, 1, d);
-      if (v0) acc_fft_row<KM>(aE, neg0, z, 3, d);
-      if (v1) acc_fft_row<KM>(aE, neg1, z, 3 + v0, d);
+      ent_row(1, o, 1);
+      if (v0) ent_row(2, neg0, 3);
+      if (v1) ent_row(3, neg1, 3 + v0);
     }
     __builtin_amdgcn_wave_barrier();
     stamp(pend | (1ull << 8) | ((unsigned long long)v0 << 9) | ((unsigned long long)v1 << 10) |
@@ -388,9 +499,10 @@ __device__ __forceinline__ void hole_pipe_score_pair(const PipeArgs& a, float* s
   }
 }
 
-template <int KM, bool FFT, bool PAIR = false>
+template <int KM, bool FFT, bool PAIR = false, bool HOT = false>
 __global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
   static_assert(!PAIR || FFT, "the pair form is the FFT form's");
+  static_assert(!HOT || PAIR, "hot rows: the pair form only");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6;
   const int l = lane_id();
@@ -409,10 +521,15 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
     const int wa = blk_a * wpb + wave;
     const unsigned long long ta0 = a.trace ? now_10ns() : 0ull;
     if (a.b == a.nb1 && wa == 0) fold_shards(a.nviol_shards, a.nviol_total);
-    // items w = wa, wa + S, ...: relation rows w < nR, then entity slots w - nR
+    // items w = wa, wa + S, ...: relation rows w < nR, hot rows, then entity
+    // slots w - nR - nH
     const int S = a.nA * wpb;
-    for (int w = wa; w < nR; w += S) rel_publish_f<1>(a, w, rd, rw, ra_prev, ra_old);
-    const int k0 = wa >= nR ? wa - nR : wa - nR + ((nR - wa + S - 1) / S) * S;
+    const int nRH = nR + a.E.nhot;
+    for (int w = wa; w < nRH; w += S) {
+      if (w < nR) rel_publish_f<1>(a, w, rd, rw, ra_prev, ra_old);
+      else if (HOT) apply_hot_f<1>(a.E, w - nR, g, d);
+    }
+    const int k0 = wa >= nRH ? wa - nRH : wa - nRH + ((nRH - wa + S - 1) / S) * S;
     apply_slots_f<1>(a.E, pp, k0, S, a.prev_slots, d, gp);
     if (a.trace && l == 0) {   // diagnostics (skge_pipe_runner_profile, tools/hole_trace.py)
       unsigned long long* tr = a.trace + 2 + 6 * (size_t)a.count + 2 * (size_t)wa;
@@ -424,7 +541,7 @@ __global__ __launch_bounds__(SKGE_PIPE_WG) void k_hole_pipe(PipeArgs a) {
   // ---- B role: score batch b (k_hole_pos's arithmetic), scatter into cp / ra_cur ----
   const int blk_b = blk - a.nA;
   if constexpr (PAIR) {
-    hole_pipe_score_pair<KM>(a, smem, blk_b, nB);
+    hole_pipe_score_pair<KM, HOT>(a, smem, blk_b, nB);
     return;
   }
   // FFT: the workgroup's twiddle table, then per wave two transform buffers
@@ -594,7 +711,9 @@ __global__ __launch_bounds__(256) void k_rel_fold_f(PipeArgs a) {
 void launch_hole_pipe(int km, bool pair, bool fft, dim3 gr, dim3 bl, size_t lds, hipStream_t st,
                       const PipeArgs& a) {
 #define SKGE_HPIPE(K)                                                          \
-  if (pair)                                                                    \
+  if (pair && a.E.nhot > 0)                                                    \
+    hipLaunchKernelGGL((k_hole_pipe<K, true, true, true>), gr, bl, lds, st, a); \
+  else if (pair)                                                               \
     hipLaunchKernelGGL((k_hole_pipe<K, true, true>), gr, bl, lds, st, a);      \
   else if (fft)                                                                \
     hipLaunchKernelGGL((k_hole_pipe<K, true>), gr, bl, lds, st, a);            \

@@ -46,6 +46,12 @@
 
 namespace skge {
 
+// HolE pair form: hub rows as TransE's (skge_hole_pipe.hip hot_value_f); 0
+// builds the round-5 form for same-box A/Bs (tools/ab_lib.sh)
+#ifndef SKGE_HPIPE_HOT
+#define SKGE_HPIPE_HOT 1
+#endif
+
 // k_pipe_batch (large batches: more than 16k slot records per batch; smaller
 // batches run k_pipe_fused below): nA apply workgroups (dispatched first: they
 // start the hand-offs the scoring waves may wait on), then the scoring ones.
@@ -1111,8 +1117,7 @@ __global__ void k_ent_occ(const int* __restrict__ trip, long long T, int* occ) {
 }
 
 static bool find_hot_rows(skge_pipe_runner* r, hipStream_t st, PipeTab& t, const int* trip,
-                          long long T, int nb1, int N, int d) {
-  const int nq = d / 4;
+                          long long T, int nb1, int N, int d, int row_words) {
   t.hot = t.hot_rows = nullptr;
   t.nhot = 0;
   int* occ = nullptr;
@@ -1142,7 +1147,7 @@ static bool find_hot_rows(skge_pipe_runner* r, hipStream_t st, PipeTab& t, const
     rows[j] = cand[j].second;
     h[rows[j]] = j;
   }
-  t.hw = (nq + 15) / 16 * 16;
+  t.hw = (row_words + 15) / 16 * 16;   // 8-B words per replica row: whole 128-B lines
   int* dh = (int*)dalloc(r, (size_t)N * 4);
   int* dr = (int*)dalloc(r, (size_t)nh * 4);
   bool got = dh && dr;
@@ -1226,6 +1231,14 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   skge_pipe_runner* r = new skge_pipe_runner();
   r->hole = hole;
   r->dp = dp;
+  // HolE at d = 200 in the FFT form: two waves per positive (the pair form)
+  // while the batch's 2 x B scoring waves fit the chip's 4-wave-per-SIMD
+  // residency.  WN18 d = 200, same box: nb = 100 93.7 -> 106.7 M triples/s
+  // (14.6 -> 12.8 us per launch); nb = 2 (70k positives per launch) 157 ->
+  // 142 M, so off there
+  int64_t maxb = 0;
+  for (const auto& bt : batches) maxb = std::max(maxb, bt.second);
+  const bool hole_pair = hole && hole_use_fft(d) && d == 200 && 2 * maxb <= 4 * 4 * 256;
   r->e8 = !hole && ent->acc_mode == SKGE_ACC_I8X4;
   const int nq = d / 4;
   const int N = ent->rows;
@@ -1299,9 +1312,10 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
         t.own[1] = (int*)dalloc(r, (size_t)N * 4);
         ok = ok && t.own[0] && t.own[1];
       }
-      // (the data-parallel form keeps every row in the tables: no hot rows)
-      if (ok && !hole && !r->e8 && !dp)
-        ok = find_hot_rows(r, as_stream(stream), t, trip, T, nb1, N, d);
+      // (the data-parallel form keeps every row in the tables: no hot rows;
+      // HolE: the pair form only, fp32 sums of d floats per replica row)
+      if (ok && !r->e8 && !dp && (!hole || (hole_pair && SKGE_HPIPE_HOT)))
+        ok = find_hot_rows(r, as_stream(stream), t, trip, T, nb1, N, d, hole ? d / 2 : nq);
     }
     RelTab& q = a.R;
     const int M = rel->rows;
@@ -1374,14 +1388,7 @@ static skge_pipe_runner_t* pipe_create(void* stream, const skge_table_t* ent,
   a.af = af;
   r->fft = hole && hole_use_fft(d);
   {
-    // two waves per positive (while the batch's 2 x B scoring waves fit the
-    // chip's 4-wave-per-SIMD residency).  WN18
-    // d = 200, same box: nb = 100 93.7 -> 106.7 M triples/s (14.6 -> 12.8 us per
-    // launch); nb = 2 (70k positives per launch) 157 -> 142 M, so off there
-    int64_t maxb = 0;
-    for (const auto& bt : batches) maxb = std::max(maxb, bt.second);
-    const bool fits = 2 * maxb <= 4 * 4 * 256;
-    r->pair = r->fft && d == 200 && fits;
+    r->pair = hole_pair;
     // the relation row's loads and update on wave 1 (3 rows each; same box,
     // two rounds: 103.8 -> 104.6 M triples/s)
     a.pair_r1 = 1;

@@ -446,6 +446,7 @@ class HolePipeRunner(object):
             raise L.SkgeError("skge_hole_pipe_runner_create: %s" % lib.skge_last_error().decode())
         self.handle = h
         self.nlaunches = lib.skge_pipe_runner_nlaunches(h)
+        self.hot_rows = lib.skge_pipe_runner_hot_rows(h)   # hub rows (pair form, skewed KGs)
 
     @staticmethod
     def eligible(model):

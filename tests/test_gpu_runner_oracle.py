@@ -195,6 +195,33 @@ def test_config1_padded_runner_three_batches_vs_oracle():
                                 "config1 padded runner sgd 3 batches", l1=True) > 0
 
 
+@pytest.mark.parametrize("kind", ["transe", "hole"])
+def test_runner_skewed_kg_hot_rows_vs_oracle(kind):
+    """SURVEY 8(d)'s skew variant (bench.make_zipf_kg: entity ids Zipf(1.1),
+    WN18's entity and relation counts) on the shipped runners with their
+    hub rows in replicated sums whose updated values every reader computes
+    itself (TransE: k_pipe_batch's hot rows; HolE: k_hole_pipe's pair form):
+    one epoch of 3 batches of B = 1414, SGD, after a first epoch, replayed
+    DIRECTLY by the oracle -- not only against another HIP runner
+    (test_gpu_skew.py)."""
+    import skge_amd as S
+    from bench import make_zipf_kg
+    from skge_amd.device import DeviceKG
+    name, ckw, margin, okw = CASES[kind]
+    np.random.seed(42)
+    m = getattr(S, name)((N, N, M), D, **ckw)
+    m.add_hyperparam("margin", margin)
+    upd = {pid: S.SGD(p, 0.1) for pid, p in m.params.items()}
+    kg = DeviceKG(make_zipf_kg(N, M, 3 * B, seed=7), m.device)
+    r = _runner(kind, m, upd, kg, 3, 45)
+    assert r.hot_rows > 0, "the skewed KG must give the runner hub rows"
+    with torch.cuda.stream(r.stream):
+        r.run(1)
+        r.synchronize()
+        assert _epoch_vs_oracle(kind, m, upd, r, kg, 45, 1, 3, "sgd",
+                                "%s runner zipf hot rows sgd 3 batches" % kind, **okw) > 0
+
+
 GRAD_CASES = [("transe", 200), ("transe", 50), ("hole", 200), ("rescal", 200)]
 
 
