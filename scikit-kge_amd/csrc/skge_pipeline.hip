@@ -155,7 +155,11 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
   const __amdgpu_buffer_rsrc_t rec1_rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<int*>(a.rec_n1 + a.start), 0, a.count * 4, 0x00020000);
   int nv = 0;
+#ifdef SKGE_ABL_NODP   // timing-only A/B: the round-5 loop bounds, no record branch
+  for (int w = blk_b * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
+#else
   for (int w = a.lo + blk_b * wpb + (threadIdx.x >> 6); w < a.hi; w += nB * wpb) {
+#endif
     // large batches: positive w adds its relation sums into replica w % reps
     // (k_rel_fold folds them after the launch), spreading the hot rows' atomics
     unsigned long long* const racc = racc0 + (size_t)(w & rmask) * rrep;
@@ -255,7 +259,11 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
     const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // strict >, transe.py:73
     const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
     if (a.trace) tt[3] = now_10ns();
+#ifdef SKGE_ABL_NODP
+    if (false) {
+#else
     if (a.dprec) {   // data-parallel: the positive's record for the other ranks
+#endif
       uint32_t* out = a.dprec + (size_t)(w - a.lo) * pipe_dp_record_words(d);
       if (l == 0) out[0] = (uint32_t)(v0 | (v1 << 1));
       if (v0 + v1 > 0) {
