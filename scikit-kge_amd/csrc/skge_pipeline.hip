@@ -56,7 +56,11 @@ namespace skge {
 // batches run k_pipe_fused below): nA apply workgroups (dispatched first: they
 // start the hand-offs the scoring waves may wait on), then the scoring ones.
 // GRP: owner marks, GRP_ROWS owner rows per apply round trip.
-template <int KQ, bool W32, bool E8, bool GRP = false, bool HOT = false>
+// DP: the data-parallel form (a slice [lo, hi) of the batch scored, records
+// written); its own instance, so the one-GPU kernel keeps round 5's code (the
+// slice bounds and the record branch in the shared instance cost 10.45 ->
+// 11.15 us per launch, same box: VERDICT r05 item 4's A/B)
+template <int KQ, bool W32, bool E8, bool GRP = false, bool HOT = false, bool DP = false>
 __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch(PipeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int l = lane_id();
@@ -155,11 +159,8 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
   const __amdgpu_buffer_rsrc_t rec1_rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<int*>(a.rec_n1 + a.start), 0, a.count * 4, 0x00020000);
   int nv = 0;
-#ifdef SKGE_ABL_NODP   // timing-only A/B: the round-5 loop bounds, no record branch
-  for (int w = blk_b * wpb + (threadIdx.x >> 6); w < a.count; w += nB * wpb) {
-#else
-  for (int w = a.lo + blk_b * wpb + (threadIdx.x >> 6); w < a.hi; w += nB * wpb) {
-#endif
+  const int lo = DP ? a.lo : 0, hi = DP ? a.hi : a.count;
+  for (int w = lo + blk_b * wpb + (threadIdx.x >> 6); w < hi; w += nB * wpb) {
     // large batches: positive w adds its relation sums into replica w % reps
     // (k_rel_fold folds them after the launch), spreading the hot rows' atomics
     unsigned long long* const racc = racc0 + (size_t)(w & rmask) * rrep;
@@ -259,12 +260,8 @@ __global__ __launch_bounds__(GRP ? PIPE_WG_GRP : SKGE_PIPE_WG) void k_pipe_batch
     const int v0 = (neg0 >= 0 && ns0 + a.margin > pscore) ? 1 : 0;   // strict >, transe.py:73
     const int v1 = (neg1 >= 0 && ns1 + a.margin > pscore) ? 1 : 0;
     if (a.trace) tt[3] = now_10ns();
-#ifdef SKGE_ABL_NODP
-    if (false) {
-#else
-    if (a.dprec) {   // data-parallel: the positive's record for the other ranks
-#endif
-      uint32_t* out = a.dprec + (size_t)(w - a.lo) * pipe_dp_record_words(d);
+    if (DP && a.dprec) {   // data-parallel: the positive's record for the other ranks
+      uint32_t* out = a.dprec + (size_t)(w - lo) * pipe_dp_record_words(d);
       if (l == 0) out[0] = (uint32_t)(v0 | (v1 << 1));
       if (v0 + v1 > 0) {
 #pragma unroll
@@ -1009,9 +1006,39 @@ static void launch_pipe_batch(const skge_pipe_runner* r, dim3 gr, hipStream_t st
       else hipLaunchKernelGGL((k_pipe_batch<K, false, false>), gr, bl, 0, st, a);         \
     }                                                                                     \
   } while (0)
-  if (r->kq <= 1) SKGE_PB(1);
-  else if (r->kq <= 2) SKGE_PB(2);
-  else SKGE_PB(4);
+// the data-parallel instances (no hot rows in that form)
+#define SKGE_PBD(K)                                                                       \
+  do {                                                                                    \
+    const bool gp_ = a.E.own[0] != nullptr;                                               \
+    const dim3 bl(gp_ ? PIPE_WG_GRP : SKGE_PIPE_WG);                                      \
+    if (gp_) {                                                                            \
+      if (r->e8) {                                                                        \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, true, false, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, true, true, false, true>), gr, bl, 0, st, a); \
+      } else {                                                                            \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, true, false, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, true, false, true>), gr, bl, 0, st, a); \
+      }                                                                                   \
+    } else {                                                                              \
+      if (r->e8) {                                                                        \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, true, false, false, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, true, false, false, true>), gr, bl, 0, st, a); \
+      } else {                                                                            \
+        if (r->w32) hipLaunchKernelGGL((k_pipe_batch<K, true, false, false, false, true>), gr, bl, 0, st, a); \
+        else hipLaunchKernelGGL((k_pipe_batch<K, false, false, false, false, true>), gr, bl, 0, st, a); \
+      }                                                                                   \
+    }                                                                                     \
+  } while (0)
+  if (r->dp) {
+    if (r->kq <= 1) SKGE_PBD(1);
+    else if (r->kq <= 2) SKGE_PBD(2);
+    else SKGE_PBD(4);
+  } else {
+    if (r->kq <= 1) SKGE_PB(1);
+    else if (r->kq <= 2) SKGE_PB(2);
+    else SKGE_PB(4);
+  }
+#undef SKGE_PBD
 #undef SKGE_PB
 }
 
