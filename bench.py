@@ -649,8 +649,8 @@ def main():
                                                                    opt=args.opt)
         k = prof["dominant"]
         kname = {"transe_sample_grad": "sample_grad", "accum_apply": "k_apply",
-                 "pipe_batch": "k_pipe_batch"}[k["name"]]
-        # config 1's own PMC pass (pmc_c1.json: d=50 padded to 52, SGD), not config 2's
+                 "pipe_batch": "k_pipe_batch", "pipe_fused": "k_pipe_fused"}[k["name"]]
+        # config 1's own PMC pass (pmc_c1.json: d=50 padded to 64, SGD), not config 2's
         traffic, traffic_src = pmc_traffic(kname, "pmc.json" if args.config == 2 else
                                            "pmc_c%d.json" % args.config)
         line = {
@@ -1121,8 +1121,10 @@ def pipe_profile(runner, kg, nb, d, epochs=1, gpu_ms_per_epoch=None, hole=False,
         avg_us = (1000.0 * gpu_ms_per_epoch - t_other / epochs) / n
     bpl = b_pipe / (n * epochs)       # implementation bytes (packed sums, atomics)
     apl = total / (n * epochs)        # SURVEY 8(d) algorithmic bytes
-    kern = {("hole_pipe" if hole else "pipe_batch"): {
-                           "name": "hole_pipe" if hole else "pipe_batch", "avg_us": avg_us,
+    # the batch kernel the runner launches (k_pipe_batch / k_pipe_fused / k_hole_pipe)
+    kn = "hole_pipe" if hole else getattr(runner, "kernel", "k_pipe_batch")[2:]
+    kern = {kn: {
+                           "name": kn, "avg_us": avg_us,
                            "launches": n,
                            "eager_avg_us": eager_us, "bytes_per_launch": apl,
                            "achieved_gbs": apl / (avg_us * 1e-6) / 1e9,
@@ -1133,7 +1135,7 @@ def pipe_profile(runner, kg, nb, d, epochs=1, gpu_ms_per_epoch=None, hole=False,
                              "bytes_per_launch": 40.0 * T,
                              "achieved_gbs": 40.0 * T / (us0 / epochs * 1e-6) / 1e9}}
     g = geo / geo[3]
-    return {"kernels": kern, "dominant": kern["hole_pipe" if hole else "pipe_batch"],
+    return {"kernels": kern, "dominant": kern[kn],
             "epoch_bytes": total / epochs,
             "geometry": {"positives": g[0], "atomic_rows": g[1], "applied_rows": g[2]},
             # the 8(d) formula's inputs per launch (averaged over the profiled
@@ -1251,7 +1253,7 @@ def make_config5_kg(n_ent, n_rel, n_triples, dev, seed):
 
 # kernel_profile's names -> the HIP kernel names rocprofv3 reports
 PMC_KERNEL = {"transe_sample_grad": "k_transe_l1_sample_grad", "accum_apply": "k_apply",
-              "pipe_batch": "k_pipe_batch"}
+              "pipe_batch": "k_pipe_batch", "pipe_fused": "k_pipe_fused"}
 
 
 def run_config5(args):

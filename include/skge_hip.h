@@ -402,6 +402,9 @@ int skge_pipe_runner_nlaunches(const skge_pipe_runner_t *r);
  * bitwise the same result), so nothing waits on a hub and its atomics do not
  * serialise on one row.  Returns their number (0: none). */
 int skge_pipe_runner_hot_rows(const skge_pipe_runner_t *r);
+/* The batch kernel the runner launches: 0 k_pipe_batch, 1 k_pipe_fused,
+ * 2 k_hole_pipe (-1: NULL runner) -- what a profile of its launches is named. */
+int skge_pipe_runner_kernel(const skge_pipe_runner_t *r);
 /* One epoch launched eagerly (trains like run(1)) with HIP events around every
  * launch: us_out[i] = launch i's duration (i = 0: negative draws, 1..nb1:
  * batches, nb1+1: flush, nb1+2: key advance); stats_out[3i..3i+2] = entity

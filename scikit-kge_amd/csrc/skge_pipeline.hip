@@ -1757,6 +1757,10 @@ extern "C" int skge_pipe_runner_nlaunches(const skge_pipe_runner_t* r) {
   return r ? r->nlaunch() : -1;
 }
 
+extern "C" int skge_pipe_runner_kernel(const skge_pipe_runner_t* r) {
+  return r ? (r->hole ? 2 : (r->fused ? 1 : 0)) : -1;
+}
+
 extern "C" int skge_pipe_runner_hot_rows(const skge_pipe_runner_t* r) {
   return r ? (r->batch.empty() ? 0 : r->batch[0].E.nhot) : -1;
 }

@@ -1954,8 +1954,10 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
 #undef SKGE_FRONT
     RescalWs wsc = w;
     wsc.coef = nullptr;   // dW was formed from the bucketing's coefficients
+#ifndef SKGE_ABL_RS_NO_SCATTER   // timing-only ablation (NOT a correct build): no scatter launch
     SKGE_KM_SWITCH(k_rescal_pos_scatter, dim3(blocks), dim3(256), 0, st, rec, rec_n1, start,
                    count, d, af, margin, wsc, accum_of(ent), nviol)
+#endif
     if (wstep_in_apply) {   // the caller's entity apply runs the W step
       *wstep = WStep{w.wpart, w.rel_off, comb ? w.n01 : nullptr, rel->param, rel->state,
                      rel->upd_count, nviol, M, d, fsplits, rel->opt, rel->lr, rel->rin, rel->rout,

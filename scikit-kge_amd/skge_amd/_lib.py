@@ -89,6 +89,7 @@ SIGNATURES = {
     "skge_pipe_runner_profile": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_p, c_i64]),
     "skge_pipe_runner_nlaunches": (c_i, [c_p]),
     "skge_pipe_runner_hot_rows": (c_i, [c_p]),
+    "skge_pipe_runner_kernel": (c_i, [c_p]),
     "skge_pipe_runner_destroy": (None, [c_p]),
     "skge_shard_route_workspace_bytes": (c_sz, [c_i, c_i]),
     "skge_shard_route": (c_i, [c_p, c_p, c_p, c_i64, c_i, c_i, c_p, c_p, c_p, c_p, c_sz]),

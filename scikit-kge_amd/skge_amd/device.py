@@ -230,6 +230,7 @@ class EpochRunner(object):
                 self.handle = h
                 self.nlaunches = lib.skge_pipe_runner_nlaunches(h)
                 self.hot_rows = lib.skge_pipe_runner_hot_rows(h)
+                self.kernel = ("k_pipe_batch", "k_pipe_fused")[lib.skge_pipe_runner_kernel(h)]
                 return
             err = lib.skge_last_error().decode()
             if not (self._auto and "allocation" in err):
@@ -238,6 +239,7 @@ class EpochRunner(object):
             self.accE = self.accR = self.te = self.tr = None
             torch.cuda.empty_cache()
         self.pipelined = False
+        self.kernel = "k_transe_sample_grad"
         if self._pad:   # the two-launch runner takes any d: no padded copies
             self._pad = False
             packed = packed and model.d % 4 == 0
