@@ -223,11 +223,9 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
                : skge_rescal_pos_grad_mfma(st, af, ent, rel, d, pos + 3 * start, neg + 6 * start,
                                            r->rec, r->rec_n1, start, count, margin, r->ws,
                                            r->ws_bytes, gate);
-#ifdef SKGE_ABL_RS_NO_APPLY   // timing-only ablation (NOT a correct build): no apply launch
-      if (false) {
-#else
-      if (!rc) {   // the entity table's apply (and W's, unless the dW kernel updated it)
-#endif
+      if (!rc && wst.applied) {   // the one-launch batch applied the entity rows and W
+        if (wst.cur) wsync = wst;
+      } else if (!rc) {   // the entity table's apply (and W's, unless the dW kernel updated it)
         skge_table_t te = *ent;
         te.gate = gate;
         const int ns = 4 * count;
