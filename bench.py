@@ -1721,11 +1721,8 @@ def run_config34(args):
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline(   # N = 1 only
             trip, d, nb, args.cpu_seconds, kind, margin)
         name = {"hole": "HolE", "rescal": "RESCAL"}[kind]
-        # RESCAL: one k_rescal_batch launch per batch (SKGE_RESCAL_FORM=split: the
-        # fused front, the scatter and the apply as three launches)
-        rs_split = "split" in os.environ.get("SKGE_RESCAL_FORM", "")
         tkern = "k_hole_pipe" if prof is not None else (
-            ("k_rescal_front" if rs_split else "k_rescal_batch") if kind == "rescal" else "k_hole")
+            "k_rescal_front" if kind == "rescal" else "k_hole")
         traffic, traffic_src = pmc_traffic(tkern, "pmc_c%d.json" % args.config)
         line = {
             "metric": "triples/sec (score+grad+update), WN18 %s d=%d pairwise, 1 MI355X "

@@ -160,15 +160,8 @@ struct WStep {
   int* cur;               // 0: W_b in W / A (the caller's), 1: in W1 / A1
   float* W1;
   float* A1;
-  // set by the one-launch RESCAL batch (k_rescal_batch): the entity apply and
-  // this step already ran in the batch's launch; only the epoch end's W sync
-  // (cur) is left to the caller
-  int applied;
 };
 int apply_with_wstep(hipStream_t st, const skge_table_t* ent, int nslots, const WStep& w);
-// the device address of the apply kernels' error word (skge_device_error;
-// skge_update.hip), or nullptr
-int* device_error_word();
 // end of an epoch with the in-front W step: the current buffer back into the
 // caller's W / state, cur = 0 (skge_rescal.hip)
 int rescal_w_sync(hipStream_t st, const WStep& w);

@@ -223,9 +223,7 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
                : skge_rescal_pos_grad_mfma(st, af, ent, rel, d, pos + 3 * start, neg + 6 * start,
                                            r->rec, r->rec_n1, start, count, margin, r->ws,
                                            r->ws_bytes, gate);
-      if (!rc && wst.applied) {   // the one-launch batch applied the entity rows and W
-        if (wst.cur) wsync = wst;
-      } else if (!rc) {   // the entity table's apply (and W's, unless the dW kernel updated it)
+      if (!rc) {   // the entity table's apply (and W's, unless the dW kernel updated it)
         skge_table_t te = *ent;
         te.gate = gate;
         const int ns = 4 * count;

@@ -28,7 +28,7 @@
 // is bitwise reproducible; the entity sums use float atomics, as elsewhere.
 #include <string>
 
-#include "skge_apply.h"
+#include "skge_host.h"
 
 namespace skge {
 
@@ -86,9 +86,6 @@ struct RescalWs {
   float* W1;
   float* A1;
   int* wcur;
-  // the one-launch batch's role counters (k_rescal_batch; epoch buckets: [nb][4]
-  // ints zeroed with the buckets, or null)
-  int* rsync;
   // GEMM K split (SKGE_RS_GKS, 1 = off): the WE / EW rows and partial scores
   // come in gks slices over k, slice k at WE + k * part_stride (spart + k *
   // spart_stride); consumers add the slices in index order (deterministic)
@@ -126,14 +123,11 @@ __device__ __forceinline__ float spart_sum(const RescalWs& ws, int i, int ncb) {
 // kernel, no split-K partial tiles), "nodedup" (three GEMM rows per positive),
 // "dw3" (three dW items per positive), "wapply" (the W step in the entity
 // apply's launch), "fsplit=N" (dW splits of the fused front), "order=N" (the
-// front's role order: 0 dW first, 1 GEMM first, >= 2 interleaved; the
-// one-launch batch keeps 1), "split" (front, scatter and apply as three
-// launches instead of one k_rescal_batch).  The
+// front's role order: 0 dW first, 1 GEMM first, >= 2 interleaved).  The
 // round-5 A/B-only switches (GEMM K split, the W step in its own launch) are
 // compile-time only now (SKGE_RS_GKS_DEFAULT).
 struct RsForm {
-  bool unfused = false, nosplit = false, nodedup = false, dw3 = false, wapply = false,
-       split = false;
+  bool unfused = false, nosplit = false, nodedup = false, dw3 = false, wapply = false;
   int fsplit = 1, order = 1;
 };
 static RsForm rs_form() {
@@ -151,7 +145,6 @@ static RsForm rs_form() {
     else if (t == "nodedup") f.nodedup = true;
     else if (t == "dw3") f.dw3 = true;
     else if (t == "wapply") f.wapply = true;
-    else if (t == "split") f.split = true;
     else if (t.rfind("fsplit=", 0) == 0) f.fsplit = std::max(1, atoi(t.c_str() + 7));
     else if (t.rfind("order=", 0) == 0) f.order = std::max(0, atoi(t.c_str() + 6));
     i = j + 1;
@@ -273,21 +266,8 @@ static size_t rescal_ws_layout(int n, int M, int d, void* base, RescalWs* ws) {
   w.n01 = nullptr;
   w.W1 = w.A1 = nullptr;
   w.wcur = nullptr;
-  w.rsync = nullptr;
   if (ws) *ws = w;
   return off;
-}
-
-// a 4-B store of a value another workgroup reads in the same launch (WT):
-// write-through (sc1, an agent-scope relaxed atomic store), so the producer
-// needs no release fence before its counter add (MI355X_MICROARCH.md,
-// inter-workgroup visibility, R1); otherwise a plain store
-template <bool WT, typename T>
-__device__ __forceinline__ void st_pub(T* p, T v) {
-  if (WT)
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    *p = v;
 }
 
 // triple k of the batch: list a (na triples: the positives), then list b
@@ -720,7 +700,7 @@ constexpr int SBN = SB0 > SB1 ? SB0 : SB1;
 constexpr int GEMM_LDS_FLOATS = 2 * RT_ITEMS * (KS + 4) + 2 * SBN + 4 * RT_ITEMS;
 
 // workgroup `bid` of the GEMM grid (k_rescal_gemm, k_rescal_front_fused)
-template <bool VEC, bool WT = false>
+template <bool VEC>
 __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
                                                  const float* __restrict__ W, int d,
                                                  const RescalWs& ws, int bid,
@@ -901,7 +881,7 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
       const int it = wave * 16 + 4 * g + reg;
-      if (it < cnt && col < d) st_pub<WT>(out + (size_t)s_gid[it] * d + col, acc[q][reg]);
+      if (it < cnt && col < d) out[(size_t)s_gid[it] * d + col] = acc[q][reg];
       if (prod == 0) ps[reg] += (col < d) ? acc[q][reg] * ev[q][reg] : 0.0f;
       if (prod == 0 && two) ps2[reg] += (col < d) ? acc[q][reg] * ev2[q][reg] : 0.0f;
     }
@@ -915,7 +895,7 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
       v += __shfl_xor(v, 2, 64);
       v += __shfl_xor(v, 1, 64);
       const int it = wave * 16 + 4 * g + reg;
-      if (c == 0 && it < cnt) st_pub<WT>(spart + (size_t)s_gid[it] * ncb + cb, v);
+      if (c == 0 && it < cnt) spart[(size_t)s_gid[it] * ncb + cb] = v;
       if (two) {   // the s-corrupted negative (item npos + 2j) of positive j = s_gid
         float v2 = ps2[reg];
         v2 += __shfl_xor(v2, 8, 64);
@@ -923,7 +903,7 @@ __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
         v2 += __shfl_xor(v2, 2, 64);
         v2 += __shfl_xor(v2, 1, 64);
         if (c == 0 && it < cnt && s_es2[it] >= 0)
-          st_pub<WT>(spart + (size_t)(ws.npos + 2 * s_gid[it]) * ncb + cb, v2);
+          spart[(size_t)(ws.npos + 2 * s_gid[it]) * ncb + cb] = v2;
       }
     }
   }
@@ -1012,18 +992,15 @@ __global__ __launch_bounds__(256) void k_rescal_scatter(const int* __restrict__ 
 // (rescal.py:296-301) summed per row, with the occurrence counts of the
 // lists (s: v0 + 2 v1, o: 2 v0 + v1, s': v0, o': v1; slots 4j..4j+3).
 // ---------------------------------------------------------------------------
-// (positives j = w0, w0 + nw, ... of the batch for this wave; the
-// workgroup's violations added to *nviol: every wave of the workgroup calls it)
-template <int KM, bool WT = false>
-__device__ __forceinline__ void rescal_pos_scatter_body(const int4* __restrict__ rec,
-                                                        const int* __restrict__ rec_n1,
-                                                        long long start, int count, int d, int af,
-                                                        float margin, const RescalWs& ws,
-                                                        const Accum& accE, int* nviol, int w0,
-                                                        int nw, int* lds_nv) {
-  const int l = lane_id(), ncb = (d + GC - 1) / GC;
+template <int KM>
+__global__ __launch_bounds__(256) void k_rescal_pos_scatter(const int4* __restrict__ rec,
+                                                            const int* __restrict__ rec_n1,
+                                                            long long start, int count, int d,
+                                                            int af, float margin, RescalWs ws,
+                                                            Accum accE, int* nviol) {
+  const int wpb = blockDim.x >> 6, l = lane_id(), ncb = (d + GC - 1) / GC;
   int nv = 0;
-  for (int j = w0; j < count; j += nw) {
+  for (int j = blockIdx.x * wpb + (threadIdx.x >> 6); j < count; j += gridDim.x * wpb) {
     const int4 r4 = rec[start + j];
     const int s = __builtin_amdgcn_readfirstlane(r4.x), o = __builtin_amdgcn_readfirstlane(r4.y);
     const int neg0 = __builtin_amdgcn_readfirstlane(r4.w);
@@ -1051,11 +1028,9 @@ __device__ __forceinline__ void rescal_pos_scatter_body(const int4* __restrict__
     }
     const int v0 = (k0 && f0 + margin > pf) ? 1 : 0;   // rescal.py:269
     const int v1 = (k1 && f1 + margin > pf) ? 1 : 0;
-    if (l < 4) {
-      const int row = sel4(l, s, o, neg0, neg1), c = sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1);
-      if (c > 0) atomicAdd(accE.cnt + row, c);   // commit_slot, the slot record published
-      if (accE.touched) st_pub<WT>(accE.touched + 4 * j + l, c > 0 ? row : -1);
-    }
+    if (l < 4)
+      commit_slot(accE, sel4(l, s, o, neg0, neg1), sel4(l, v0 + 2 * v1, 2 * v0 + v1, v0, v1),
+                  4 * j + l);
     if (v0 + v1 == 0) continue;
     nv += v0 + v1;
     // (stale rows of absent negatives are not used; deduplicated GEMM rows: W
@@ -1090,19 +1065,8 @@ __device__ __forceinline__ void rescal_pos_scatter_body(const int4* __restrict__
       acc_row<KM>(accE, neg1, x, d);
     }
   }
-  if (nviol) block_count_add(nviol, nv, lds_nv);
-}
-
-template <int KM>
-__global__ __launch_bounds__(256) void k_rescal_pos_scatter(const int4* __restrict__ rec,
-                                                            const int* __restrict__ rec_n1,
-                                                            long long start, int count, int d,
-                                                            int af, float margin, RescalWs ws,
-                                                            Accum accE, int* nviol) {
-  const int wpb = blockDim.x >> 6;
   __shared__ int lds_nv;
-  rescal_pos_scatter_body<KM>(rec, rec_n1, start, count, d, af, margin, ws, accE, nviol,
-                              blockIdx.x * wpb + (threadIdx.x >> 6), gridDim.x * wpb, &lds_nv);
+  if (nviol) block_count_add(nviol, nv, &lds_nv);
 }
 
 // ---------------------------------------------------------------------------
@@ -1339,7 +1303,7 @@ constexpr int WPART_LDS_FLOATS = 2 * WG_CH * (WG_T + 4);
 // product 1's rows, A = E_s unscaled, B = coef E_o + E_o2
 // IF: one split, and the tile's W step written into the other buffer (WFront)
 // instead of the partial tile; a relation without items copies its tile over
-template <bool VEC, bool COMB = false, bool IF = false, bool WT = false>
+template <bool VEC, bool COMB = false, bool IF = false>
 __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__ E, int d,
                                                        const RescalWs& ws,
                                                        const float* __restrict__ coef, int splits,
@@ -1510,7 +1474,7 @@ __device__ __forceinline__ void rescal_wgrad_part_body(const float* __restrict__
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg)
-      st_pub<WT>(out + (16 * wave + 4 * (l >> 4) + reg) * WG_T + 16 * j + (l & 15), acc[j][reg]);
+      out[(16 * wave + 4 * (l >> 4) + reg) * WG_T + 16 * j + (l & 15)] = acc[j][reg];
 }
 
 template <bool VEC>
@@ -1567,182 +1531,6 @@ __global__ __launch_bounds__(256) void k_rescal_front_fused(const float* __restr
                           reinterpret_cast<float(*)[RT_ITEMS][KS + 4]>(lds),
                           reinterpret_cast<float(*)[SBN]>(sb), si, si + RT_ITEMS,
                           si + 2 * RT_ITEMS, si + 3 * RT_ITEMS);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// One launch per batch (the device pair loop, Linear, epoch buckets): the
-// fused front's GEMM and dW roles, the positive scatter and the entity apply
-// (+ the W step) as four roles of ONE grid, each later role waiting in-launch
-// on counters of the roles whose results it reads:
-//   GEMM    ng  workgroups: WE / EW rows, partial scores       -> sync[0]
-//   dW      nwg workgroups: W_{b+1} (in-front step) or partials -> sync[1]
-//   scatter nsc workgroups: wait sync[0] == ng; margin tests, entity sums,
-//                           counts, violations                  -> sync[2]
-//   apply   nap workgroups: wait sync[2] == nsc and sync[1] == nwg (the apply
-//                           rewrites E rows the dW role reads; the W flip /
-//                           quads need dW done); then the entity slots, the W
-//                           quads (split dW) or the flip (in-front step)
-// Grid order is role order, so a workgroup only waits on roles dispatched
-// before it.  Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility; the
-// R1 recipe of cdna_hip_programming.md Guideline 16): the payload stored
-// write-through (sc1) or by atomics, every wave's vmcnt(0), a workgroup
-// barrier, one lane's agent counter add; the waiter polls relaxed from one
-// lane with s_sleep, then ONE agent acquire, vmcnt(0) and a barrier before
-// any load of the handed-off bytes.  Waits are bounded (error
-// word bit 8: the batch's tables are not trustworthy).  Each role's
-// arithmetic is its standalone kernel's: the same values as the split form
-// (three launches, SKGE_RESCAL_FORM=split) up to the entity sums' float-atomic
-// order.
-// ---------------------------------------------------------------------------
-#ifndef SKGE_RS_BATCH_SCATTER_WG
-#define SKGE_RS_BATCH_SCATTER_WG 256   // most scatter-role workgroups (4 positives each per pass)
-#endif
-#ifndef SKGE_RS_BATCH_APPLY_WG
-#define SKGE_RS_BATCH_APPLY_WG 1024    // most apply-role workgroups (4 slots each per pass)
-#endif
-#ifndef SKGE_RS_BATCH_APPLY_ROLE
-#define SKGE_RS_BATCH_APPLY_ROLE 1     // 0: the entity apply (+ W step) as its own launch
-#endif
-#ifndef SKGE_RS_BATCH_SLEEP
-#define SKGE_RS_BATCH_SLEEP 8          // s_sleep between polls (x 64 cycles)
-#endif
-constexpr int RS_BATCH_SCATTER_WG = SKGE_RS_BATCH_SCATTER_WG;
-constexpr int RS_BATCH_APPLY_WG = SKGE_RS_BATCH_APPLY_WG;
-// role counters: per role 8 shards (workgroup bid adds to shard bid & 7, one
-// 128-B line each), so the fan-in atomics and the polls spread over 8 lines
-constexpr int RS_SHARDS = 8, RS_SHARD_INTS = 32, RS_ROLE_INTS = RS_SHARDS * RS_SHARD_INTS;
-constexpr int RS_SYNC_INTS = 3 * RS_ROLE_INTS;   // per batch: GEMM, dW, scatter
-struct RsBatch {
-  int ng, nwg, nsc, nap;   // workgroups per role, in grid order
-  int* sync;               // [RS_SYNC_INTS] this batch's role counters (zeroed per epoch)
-  int* err;                // the device error word (skge_device_error)
-  const int4* rec;         // scatter: the epoch's records, this batch's positives
-  const int* rec_n1;
-  long long start;
-  int count, af;
-  float margin;
-  int* nviol;              // the batch's violation count (the apply's gate)
-  TableDev te;             // apply: the entity table (slot records)
-  WStep w;                 // apply: the W step (cur: flip; else quads from partials)
-};
-
-// every handed-off byte was stored write-through (st_pub<true>) or by an
-// atomic: each wave drains its stores, the barrier joins the waves, one lane
-// adds to the counter (R1: no release fence -- a per-workgroup L2 write-back
-// would serialise ~60 of them per XCD per batch)
-__device__ __forceinline__ void role_signal(int* role, int bid) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_fetch_add(role + (bid & (RS_SHARDS - 1)) * RS_SHARD_INTS, 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// workgroups b of [b0, b0 + n) with b & 7 == s: shard s's count when the role is done
-__device__ __forceinline__ int rs_shard_target(int b0, int n, int s) {
-  auto f = [s](int m) { return m > s ? (m - s + RS_SHARDS - 1) / RS_SHARDS : 0; };
-  return f(b0 + n) - f(b0);
-}
-
-// wave 0 polls (lanes 0-7: role c0's shards; 8-15: role c1's, when c1) until
-// every shard has its role's count, then ONE agent acquire; the barrier holds
-// the workgroup until the invalidate has completed
-__device__ __forceinline__ void role_wait(int* c0, int b0, int n0, int* c1, int b1, int n1,
-                                          int* err) {
-  if (threadIdx.x < 64) {
-    const int l = threadIdx.x;
-    int* c = nullptr;
-    int tgt = 0;
-    if (l < RS_SHARDS) {
-      c = c0 + l * RS_SHARD_INTS;
-      tgt = rs_shard_target(b0, n0, l);
-    } else if (c1 && l < 2 * RS_SHARDS) {
-      c = c1 + (l - RS_SHARDS) * RS_SHARD_INTS;
-      tgt = rs_shard_target(b1, n1, l - RS_SHARDS);
-    }
-    unsigned spins = 0;
-#ifdef SKGE_ABL_RSB_NOWAIT   // timing-only ablation (NOT a correct build): no polls
-    tgt = 0;
-#endif
-    while (true) {
-      const bool ok = tgt == 0 ||
-                      __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= tgt;
-      if (__all(ok)) break;
-      __builtin_amdgcn_s_sleep(SKGE_RS_BATCH_SLEEP);
-      if (++spins > (1u << 19)) {   // never hang the GPU: report instead
-        if (l == 0) atomicOr(err, 8);
-        break;
-      }
-      if ((spins & 127u) == 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT) & 8))
-        break;   // once one wait has given up, the rest stop too
-    }
-#ifndef SKGE_ABL_RSB_NOACQ   // timing-only ablation (NOT a correct build): no acquire
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-}
-
-template <bool VEC, bool IF, int KM>
-__global__ __launch_bounds__(256) void k_rescal_batch(const float* __restrict__ E,
-                                                      const float* __restrict__ W, int d,
-                                                      RescalWs ws, int splits, WFront wf,
-                                                      RsBatch rb) {
-  __shared__ __attribute__((aligned(16))) float lds[FRONT_LDS_FLOATS];
-  __shared__ int lds_nv;
-  const int bid = (int)blockIdx.x;
-  if (bid < rb.ng) {   // GEMM role (k_rescal_front_fused, order 1)
-    float* sb = lds + 2 * RT_ITEMS * (KS + 4);
-    int* si = reinterpret_cast<int*>(sb + 2 * SBN);
-    const float* Wb = IF && *wf.cur ? wf.W1 : W;   // W_b's buffer
-    rescal_gemm_body<VEC, true>(E, Wb, d, ws, bid,
-                          reinterpret_cast<float(*)[RT_ITEMS][KS + 4]>(lds),
-                          reinterpret_cast<float(*)[SBN]>(sb), si, si + RT_ITEMS,
-                          si + 2 * RT_ITEMS, si + 3 * RT_ITEMS);
-    role_signal(rb.sync, bid);
-    return;
-  }
-  if (bid < rb.ng + rb.nwg) {   // dW role (combined dW of the deduplicated buckets)
-    rescal_wgrad_part_body<VEC, true, IF, true>(E, d, ws, ws.ecoef, splits, bid - rb.ng,
-                                          reinterpret_cast<float(*)[WG_T + 4]>(lds),
-                                          reinterpret_cast<float(*)[WG_T + 4]>(
-                                              lds + WG_CH * (WG_T + 4)),
-                                          wf);
-    role_signal(rb.sync + RS_ROLE_INTS, bid);
-    return;
-  }
-  const int wpb = blockDim.x >> 6, wv = threadIdx.x >> 6;
-  if (bid < rb.ng + rb.nwg + rb.nsc) {   // scatter role (k_rescal_pos_scatter)
-    role_wait(rb.sync, 0, rb.ng, nullptr, 0, 0, rb.err);
-    RescalWs wsc = ws;
-    wsc.coef = nullptr;   // dW was formed from the bucketing's coefficients
-    const int k = bid - rb.ng - rb.nwg;
-    rescal_pos_scatter_body<KM, true>(rb.rec, rb.rec_n1, rb.start, rb.count, d, rb.af, rb.margin, wsc,
-                                rb.te.acc, rb.nviol, k * wpb + wv, rb.nsc * wpb, &lds_nv);
-    role_signal(rb.sync + 2 * RS_ROLE_INTS, bid);
-    return;
-  }
-  // apply role (k_apply_wstep)
-  role_wait(rb.sync + 2 * RS_ROLE_INTS, rb.ng + rb.nwg, rb.nsc, rb.sync + RS_ROLE_INTS, rb.ng,
-            rb.nwg, rb.err);
-  const int k = bid - rb.ng - rb.nwg - rb.nsc;
-  const bool upd = __hip_atomic_load(rb.nviol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-  if (IF) {
-    if (k == 0 && threadIdx.x == 0) wstep_flip(rb.w);
-  } else {
-    const int nt = (d + WS_T - 1) / WS_T;
-    const long long nq = (long long)rb.w.M * nt * nt * (WS_T * WS_T / 4);
-    for (long long q = (long long)k * blockDim.x + threadIdx.x; q < nq;
-         q += (long long)rb.nap * blockDim.x)
-      wstep_quad(rb.w, q);
-  }
-  const int ns = 4 * rb.count;
-  for (int sl = k * wpb + wv; sl < ns; sl += rb.nap * wpb) {
-    const int row = __builtin_amdgcn_readfirstlane(rb.te.acc.touched[sl]);
-    if (row >= 0) apply_row_f<KM>(rb.te, row, upd, rb.err);
   }
 }
 
@@ -2042,12 +1830,9 @@ static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, Resc
   w.n01 = (int*)take((size_t)M * 4);
   w.npos = 0;   // (set per batch: rs_batch_view)
   const size_t slice = off - s0;
-  // the one-launch batch's role counters, [nb][RS_SYNC_INTS] after the slices
-  const size_t sync_off = s0 + (size_t)nb * slice;
-  w.rsync = p ? (int*)(p + sync_off) : nullptr;
   if (ws0) *ws0 = w;
   if (stride) *stride = (long long)slice;
-  return sync_off + al256((size_t)nb * RS_SYNC_INTS * 4);
+  return s0 + (size_t)nb * slice;
 }
 
 bool rescal_epoch_ok(int M) { return M <= 64; }
@@ -2074,8 +1859,6 @@ int rescal_epoch_bucket(hipStream_t st, const int* pos, const int* neg, long lon
                         int M, int d, void* ws) {
   SKGE_CHECK_ARG(rescal_epoch_ok(M), "epoch bucketing needs M <= 64");
   const RescalEpoch e = rescal_epoch_view(ws, T, bs, nb, M, d);
-  // the one-launch batches' role counters, zeroed every epoch (a memset node)
-  SKGE_CHECK_HIP(hipMemsetAsync(e.ws0.rsync, 0, (size_t)nb * RS_SYNC_INTS * 4, st));
   const long long waves = (long long)nb * e.cpb;
   const unsigned blocks = (unsigned)((waves + 3) / 4);
   hipLaunchKernelGGL(k_rs_count_ep, dim3(blocks), dim3(256), 0, st, pos, neg, e);
@@ -2156,60 +1939,6 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
     if (infront)
       wf = WFront{w.wcur, rel->param, rel->state, w.W1, w.A1, rel->opt, rel->lr, rel->rin,
                   rel->rout, rel->fixed_div};
-    const WStep wstp{w.wpart, w.rel_off, comb ? w.n01 : nullptr, rel->param, rel->state,
-                     rel->upd_count, nviol, M, d, fsplits, rel->opt, rel->lr, rel->rin, rel->rout,
-                     rel->fixed_div, infront ? w.wcur : nullptr, w.W1, w.A1};
-    // one launch for the whole batch (k_rescal_batch) where the caller's entity
-    // apply would run the W step and the entity sums are one fp32 (or
-    // fixed-point) copy; form "split": three launches
-    int* const derr = device_error_word();
-    const bool one = comb && !form.split && w.rsync && derr && km_for(d) > 0 &&
-                     (ent->acc_mode == SKGE_ACC_F32 || ent->acc_mode == SKGE_ACC_FX64) &&
-                     ent->acc_replicas <= 1 && ent->acc_touched &&
-                     (ent->opt == SKGE_SGD || ent->state);
-    if (one) {
-      RsBatch rb;
-      rb.ng = (int)grid.x - nwg;
-      rb.nwg = nwg;
-      rb.nsc = std::max(1, std::min((count + 3) / 4, RS_BATCH_SCATTER_WG));
-      rb.nap = SKGE_RS_BATCH_APPLY_ROLE ? std::max(1, std::min(count, RS_BATCH_APPLY_WG)) : 0;
-      rb.sync = w.rsync + (size_t)RS_SYNC_INTS * b;
-      rb.err = derr;
-      rb.rec = rec;
-      rb.rec_n1 = rec_n1;
-      rb.start = start;
-      rb.count = count;
-      rb.af = af;
-      rb.margin = margin;
-      rb.nviol = nviol;
-      rb.te = table_dev(ent);
-      rb.te.gate = nviol;
-      rb.w = wstp;
-      const dim3 bgrid((unsigned)(rb.ng + rb.nwg + rb.nsc + rb.nap));
-#define SKGE_RB(V, I, K)                                                                     \
-  hipLaunchKernelGGL((k_rescal_batch<V, I, K>), bgrid, dim3(256), 0, st, ent->param, rel->param, \
-                     d, w, fsplits, wf, rb)
-#define SKGE_RB_KM(V, I)                          \
-  switch (km_for(d)) {                            \
-    case 1: SKGE_RB(V, I, 1); break;              \
-    case 2: SKGE_RB(V, I, 2); break;              \
-    case 3: SKGE_RB(V, I, 3); break;              \
-    case 4: SKGE_RB(V, I, 4); break;              \
-    case 8: SKGE_RB(V, I, 8); break;              \
-    default: SKGE_RB(V, I, 16); break;            \
-  }
-      if ((d & 3) == 0) {
-        if (infront) SKGE_RB_KM(true, true) else SKGE_RB_KM(true, false)
-      } else {
-        if (infront) SKGE_RB_KM(false, true) else SKGE_RB_KM(false, false)
-      }
-#undef SKGE_RB_KM
-#undef SKGE_RB
-      *wstep = wstp;
-      wstep->applied = rb.nap > 0 ? 1 : 0;   // else the caller's apply launch runs it
-      SKGE_CHECK_LAUNCH("rescal one-launch batch");
-      return SKGE_OK;
-    }
 #define SKGE_FRONT(V, C, I)                                                                 \
   hipLaunchKernelGGL((k_rescal_front_fused<V, C, I>), grid, dim3(256), 0, st, ent->param,    \
                      rel->param, d, w, fsplits, nwg, order, wf)
@@ -2228,7 +1957,9 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
     SKGE_KM_SWITCH(k_rescal_pos_scatter, dim3(blocks), dim3(256), 0, st, rec, rec_n1, start,
                    count, d, af, margin, wsc, accum_of(ent), nviol)
     if (wstep_in_apply) {   // the caller's entity apply runs the W step
-      *wstep = wstp;
+      *wstep = WStep{w.wpart, w.rel_off, comb ? w.n01 : nullptr, rel->param, rel->state,
+                     rel->upd_count, nviol, M, d, fsplits, rel->opt, rel->lr, rel->rin, rel->rout,
+                     rel->fixed_div, infront ? w.wcur : nullptr, w.W1, w.A1};
     } else {
       WApply wa = {rel->param, rel->state, rel->opt, rel->lr, rel->rin, rel->rout,
                    rel->fixed_div, nviol, rel->upd_count};

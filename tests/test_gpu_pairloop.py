@@ -643,44 +643,3 @@ def test_rescal_in_front_w_step_matches_apply_side(n_ent, n_rel, T, d, nb, opt, 
     assert out[0][0] == out[1][0] > 0
     for k in out[0][1]:
         np.testing.assert_allclose(out[1][1][k], out[0][1][k], rtol=RTOL, atol=ATOL, err_msg=k)
-
-
-@pytest.mark.parametrize("n_ent,n_rel,T,d,nb,opt,form", [
-    (300, 7, 2000, 16, 7, "sgd", ""),                  # ragged remainder batch
-    (300, 40, 2000, 24, 50, "adagrad", ""),            # ~40 positives / batch: most relations absent
-    (300, 5, 2000, 30, 3, "adagrad", ""),              # d % 4 != 0
-    (300, 7, 2000, 36, 3, "sgd", "wapply"),            # the W quads in the apply role
-    (3000, 3, 6000, 40, 2, "sgd", ""),                 # split-K partial tiles: W quads in the apply role
-    (40943, 18, 14140, 200, 10, "sgd", ""),            # WN18 entity / relation counts, d, batch size
-    (40943, 18, 14140, 200, 9, "sgd", ""),             # odd number of batches: W ends in the 2nd buffer
-])
-def test_rescal_one_launch_batch_matches_split(n_ent, n_rel, T, d, nb, opt, form, monkeypatch):
-    """The one-launch RESCAL batch (k_rescal_batch: GEMM, dW, scatter and
-    entity apply + W step as four roles of one grid, later roles waiting
-    in-launch on counters of the earlier ones) against the same work as three
-    launches (SKGE_RESCAL_FORM=split) on the same draws: equal violation
-    totals, parameters (and W's AdaGrad state) within the fp32 tolerance after
-    2 epochs (the entity sums are float atomics in both).  A hand-off wait
-    that gave up would raise from the runner's device-error check."""
-    import skge_amd as S
-    from skge_amd.device import DeviceKG, PairLoopRunner
-    xs = make_kg(n_ent, n_rel, T, seed=12)
-    out = []
-    for f in ("split," + form, form):
-        monkeypatch.setenv("SKGE_RESCAL_FORM", f)
-        m = make_model("rescal", (n_ent, n_ent, n_rel), d)
-        m.add_hyperparam("margin", 0.2)
-        cls = S.SGD if opt == "sgd" else S.AdaGrad
-        upd = {pid: cls(p, 0.1) for pid, p in m.params.items()}
-        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), nb, seed=13)
-        with torch.cuda.stream(r.stream):
-            r.run(2)
-        r.synchronize()
-        state = {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}
-        if opt == "adagrad":
-            state["W_p2"] = upd["W"].p2.cpu().numpy().copy()
-            state["E_p2"] = upd["E"].p2.cpu().numpy().copy()
-        out.append((int(r.nviol_total.item()), state))
-    assert out[0][0] == out[1][0] > 0
-    for k in out[0][1]:
-        np.testing.assert_allclose(out[1][1][k], out[0][1][k], rtol=RTOL, atol=ATOL, err_msg=k)
