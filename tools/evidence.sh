@@ -23,7 +23,7 @@ for c in ${CONFIGS:-2 1 3 4 5}; do
   cp $D/pmc.json profiles/$R/pmc$suf.json
   python3 tools/trace_by_grid.py $D/stats > $D/kernel_trace_by_grid.json || true
   if [ "$c" = 5 ]; then   # the two-launch runner: nb launches of each batch kernel per epoch
-    nb=$(python3 -c "print(max(1, int(100_000_000 // 131072)))")   # full-batch launches per epoch
+    nb=$(python3 -c "print(-(-100_000_000 // 131072))")   # batch launches per epoch (the last one ragged)
     python3 tools/pmc_epochs.py $D $nb > profiles/$R/pmc_c5_epochs.json || true
     python3 tools/trace_epochs.py $D/stats $nb > $D/kernel_trace_epochs.json || true
   fi
