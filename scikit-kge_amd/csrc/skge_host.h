@@ -160,6 +160,10 @@ struct WStep {
   int* cur;               // 0: W_b in W / A (the caller's), 1: in W1 / A1
   float* W1;
   float* A1;
+  // set by the row-grouped RESCAL apply (skge_rescal.hip k_rescal_fold): the
+  // entity rows and the W step's flip are done; only the epoch end's W sync
+  // (cur) is left to the caller
+  int applied;
 };
 int apply_with_wstep(hipStream_t st, const skge_table_t* ent, int nslots, const WStep& w);
 // end of an epoch with the in-front W step: the current buffer back into the
@@ -174,7 +178,10 @@ bool rescal_pair_mfma_selected(int d, int M);
 bool rescal_epoch_ok(int M);
 size_t rescal_epoch_ws_bytes(int bs, int nb, int M, int d);
 int rescal_epoch_bucket(hipStream_t st, const int* pos, const int* neg, long long T, int bs, int nb,
-                        int M, int d, void* ws);
+                        int M, int d, void* ws, const int4* rec = nullptr,
+                        const int* rec_n1 = nullptr);
+// the epoch's row grouping fits (k_rs_rows_ep: 4 bs slots per batch in LDS)
+bool rs_rows_ok(int bs);
 int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent,
                                  const skge_table_t* rel, int d, const int4* rec,
                                  const int* rec_n1, long long T, int bs, int nb, int b,

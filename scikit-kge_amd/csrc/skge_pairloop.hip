@@ -199,7 +199,7 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
       rc = SKGE_EHIP;
     }
     if (!rc && rep) rc = rescal_epoch_bucket(st, pos, neg, (long long)T, (int)bs, nb, rel->rows, d,
-                                             r->ws);
+                                             r->ws, r->rec, r->rec_n1);
   }
   WStep wsync{};   // RESCAL with the in-front W step: synced back at the epoch's end
   for (int k = 0; k < nb && !rc; ++k) {
@@ -223,7 +223,9 @@ extern "C" skge_pair_runner_t* skge_pair_runner_create(
                : skge_rescal_pos_grad_mfma(st, af, ent, rel, d, pos + 3 * start, neg + 6 * start,
                                            r->rec, r->rec_n1, start, count, margin, r->ws,
                                            r->ws_bytes, gate);
-      if (!rc) {   // the entity table's apply (and W's, unless the dW kernel updated it)
+      if (!rc && wst.applied) {   // the row-grouped apply updated the entity rows and W
+        if (wst.cur) wsync = wst;
+      } else if (!rc) {   // the entity table's apply (and W's, unless the dW kernel updated it)
         skge_table_t te = *ent;
         te.gate = gate;
         const int ns = 4 * count;

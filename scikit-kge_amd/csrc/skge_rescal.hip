@@ -86,6 +86,17 @@ struct RescalWs {
   float* W1;
   float* A1;
   int* wcur;
+  // the batch's entity rows grouped (epoch buckets: k_rs_rows_ep; else null):
+  // nuniq distinct rows, row u's record urec[u] = (row, n slots, slot 0, slot 1
+  // or -1), its slots uslot[uoff[u] .. uoff[u] + n) in slot order, a slot
+  // packed as j << 4 | k1 << 3 | k0 << 2 | role (positive j, role 0-3 = s, o,
+  // s', o'; k0 / k1: its negatives exist); vword: k_rescal_fold's violation
+  // count (low half) and arrivals (high half), zeroed with the grouping
+  int4* urec;
+  int* uoff;
+  int* uslot;
+  int* nuniq;
+  unsigned long long* vword;
   // GEMM K split (SKGE_RS_GKS, 1 = off): the WE / EW rows and partial scores
   // come in gks slices over k, slice k at WE + k * part_stride (spart + k *
   // spart_stride); consumers add the slices in index order (deterministic)
@@ -123,11 +134,14 @@ __device__ __forceinline__ float spart_sum(const RescalWs& ws, int i, int ncb) {
 // kernel, no split-K partial tiles), "nodedup" (three GEMM rows per positive),
 // "dw3" (three dW items per positive), "wapply" (the W step in the entity
 // apply's launch), "fsplit=N" (dW splits of the fused front), "order=N" (the
-// front's role order: 0 dW first, 1 GEMM first, >= 2 interleaved).  The
+// front's role order: 0 dW first, 1 GEMM first, >= 2 interleaved),
+// "scatter" (the entity sums by the scatter kernel's atomics and the apply
+// launch, instead of the row-grouped apply k_rescal_fold).  The
 // round-5 A/B-only switches (GEMM K split, the W step in its own launch) are
 // compile-time only now (SKGE_RS_GKS_DEFAULT).
 struct RsForm {
-  bool unfused = false, nosplit = false, nodedup = false, dw3 = false, wapply = false;
+  bool unfused = false, nosplit = false, nodedup = false, dw3 = false, wapply = false,
+       scatter = false;
   int fsplit = 1, order = 1;
 };
 static RsForm rs_form() {
@@ -145,6 +159,7 @@ static RsForm rs_form() {
     else if (t == "nodedup") f.nodedup = true;
     else if (t == "dw3") f.dw3 = true;
     else if (t == "wapply") f.wapply = true;
+    else if (t == "scatter") f.scatter = true;
     else if (t.rfind("fsplit=", 0) == 0) f.fsplit = std::max(1, atoi(t.c_str() + 7));
     else if (t.rfind("order=", 0) == 0) f.order = std::max(0, atoi(t.c_str() + 6));
     i = j + 1;
@@ -266,6 +281,9 @@ static size_t rescal_ws_layout(int n, int M, int d, void* base, RescalWs* ws) {
   w.n01 = nullptr;
   w.W1 = w.A1 = nullptr;
   w.wcur = nullptr;
+  w.urec = nullptr;
+  w.uoff = w.uslot = w.nuniq = nullptr;
+  w.vword = nullptr;
   if (ws) *ws = w;
   return off;
 }
@@ -537,6 +555,11 @@ __device__ __forceinline__ RescalWs rs_batch_view(const RescalEpoch& e, int b) {
   w.s2 = sh(w.s2);
   w.o2 = sh(w.o2);
   w.n01 = sh(w.n01);
+  w.urec = sh(w.urec);
+  w.uoff = sh(w.uoff);
+  w.uslot = sh(w.uslot);
+  w.nuniq = sh(w.nuniq);
+  w.vword = sh(w.vword);
   w.npos = e.dedup ? rs_batch_count(e, b) : 0;
   return w;
 }
@@ -570,6 +593,85 @@ __global__ __launch_bounds__(256) void k_rs_scatter_ep(const int* __restrict__ p
   if (c >= rs_nchunks(cnt, n, e.dedup != 0)) return;
   const long long s0 = (long long)b * e.bs;
   rs_scatter_chunk(pos + 3 * s0, neg + 6 * s0, cnt, n, e.M, rs_batch_view(e, b), c);
+}
+
+// The row grouping of every batch's entity slots, once per epoch (the
+// records are drawn at the epoch's start): one workgroup per batch sorts the
+// batch's 4 count slot keys (row << 20 | packed slot, RescalWs::uslot) in LDS
+// (bitonic), then writes the distinct rows, their slot ranges and the slots
+// in slot order -- what k_rescal_fold reads instead of the scatter's atomics.
+constexpr int RS_ROWS_MAX = 8192;   // slots per batch the LDS sort holds (bs <= 2048)
+__global__ __launch_bounds__(1024) void k_rs_rows_ep(const int4* __restrict__ rec,
+                                                     const int* __restrict__ rec_n1,
+                                                     RescalEpoch e, int npad) {
+  __shared__ unsigned long long sk[RS_ROWS_MAX];
+  __shared__ int wtot[16];
+  const int b = blockIdx.x, tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
+  const int cnt = rs_batch_count(e, b), ns = 4 * cnt;
+  const long long s0 = (long long)b * e.bs;
+  const RescalWs w = rs_batch_view(e, b);
+  for (int i = tid; i < npad; i += blockDim.x) {
+    unsigned long long key = ~0ull;
+    if (i < ns) {
+      const int j = i >> 2, role = i & 3;
+      const int4 r4 = rec[s0 + j];
+      const int n1 = rec_n1[s0 + j];
+      const int row = role == 0 ? r4.x : (role == 1 ? r4.y : (role == 2 ? r4.w : n1));
+      if (row >= 0)
+        key = ((unsigned long long)row << 20) |
+              (unsigned)((j << 4) | ((n1 >= 0 ? 1 : 0) << 3) | ((r4.w >= 0 ? 1 : 0) << 2) | role);
+    }
+    sk[i] = key;
+  }
+  __syncthreads();
+  for (int k = 2; k <= npad; k <<= 1) {   // bitonic sort, ascending
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      for (int i = tid; i < npad; i += blockDim.x) {
+        const int ixj = i ^ jj;
+        if (ixj > i) {
+          const unsigned long long x = sk[i], y = sk[ixj];
+          if ((x > y) == ((i & k) == 0)) {
+            sk[i] = y;
+            sk[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // distinct rows: thread t owns keys [t ch, (t + 1) ch); a key heads a row
+  // when its row differs from the previous key's
+  const int ch = npad / (int)blockDim.x;   // npad >= blockDim.x (a power of two)
+  auto head = [&](int i) {
+    const unsigned long long x = sk[i];
+    return x != ~0ull && (i == 0 || (sk[i - 1] >> 20) != (x >> 20));
+  };
+  int heads = 0;
+  for (int q = 0; q < ch; ++q) heads += head(tid * ch + q) ? 1 : 0;
+  const int inc = wave_incl_scan(heads);
+  if (l == 63) wtot[wave] = inc;
+  __syncthreads();
+  int u = inc - heads;   // this thread's first head index
+  for (int v = 0; v < wave; ++v) u += wtot[v];
+  for (int q = 0; q < ch; ++q) {
+    const int i = tid * ch + q;
+    const unsigned long long x = sk[i];
+    if (x == ~0ull) continue;
+    w.uslot[i] = (int)(x & 0xFFFFFu);
+    if (!head(i)) continue;
+    int n = 1;   // the row's slots: the keys up to the next row
+    while (i + n < npad && sk[i + n] != ~0ull && (sk[i + n] >> 20) == (x >> 20)) ++n;
+    w.urec[u] = make_int4((int)(x >> 20), n, (int)(x & 0xFFFFFu),
+                          n > 1 ? (int)(sk[i + 1] & 0xFFFFFu) : -1);
+    w.uoff[u] = i;
+    ++u;
+  }
+  if (tid == 0) {
+    int tot = 0;
+    for (int v = 0; v < (int)(blockDim.x >> 6); ++v) tot += wtot[v];
+    *w.nuniq = tot;
+    *w.vword = 0ull;
+  }
 }
 
 // Small batches (n <= SB_MAXN triples, M <= SB_MAXM relations): the same
@@ -1067,6 +1169,191 @@ __global__ __launch_bounds__(256) void k_rescal_pos_scatter(const int4* __restri
   }
   __shared__ int lds_nv;
   if (nviol) block_count_add(nviol, nv, &lds_nv);
+}
+
+// ---------------------------------------------------------------------------
+// The device pair loop's entity update without the scatter (k_rescal_fold):
+// one wave per DISTINCT entity row of the batch (k_rs_rows_ep's grouping)
+// walks the row's slots in slot order, recomputes each slot's pair tests
+// from the partial scores and forms its contribution from the WE / EW rows
+// exactly as k_rescal_pos_scatter does (rescal.py:264-302), sums them in
+// registers (a fixed order: no float atomics, bitwise reproducible), then
+// applies the segment mean and the updater's step (skge/param.py:115-174, as
+// apply_row).  Workgroup 0 counts the batch's violations (the scatter's test
+// for every positive: the gate) and makes the in-front W step current when
+// there are any (WStep::cur; updateCounts of the relations present).
+// ---------------------------------------------------------------------------
+struct FoldTab {
+  float* P;
+  float* A;
+  int* ucnt;
+  int opt, post;
+  float lr, rin, rout, fdiv;
+};
+
+// slot `sl` of the batch: its contribution to the row (x) and its count
+template <int KM>
+__device__ __forceinline__ int fold_slot(const RescalWs& ws, int count, int d, int af, float margin,
+                                         int sl, float (&x)[KM]) {
+  const int ncb = (d + GC - 1) / GC;
+  const int j = sl >> 4, k1 = (sl >> 3) & 1, k0 = (sl >> 2) & 1, role = sl & 3;
+  const int i0 = count + 2 * j, i1 = i0 + 1;
+  // the slot's rows: s: W E_o of the positive and of (s, o', p); o: E_s W of
+  // the positive and of (s', o, p); s' / o': the negative's own row
+  // (deduplicated: the positive's)
+  const bool dd = ws.npos > 0;
+  const float* ta = (role & 1) ? ws.EW : ws.WE;
+  const int ia = role < 2 ? j : (dd ? j : (role == 2 ? i0 : i1));
+  float ra[KM], rb[KM];
+  load_row_gk<KM>(ta, ws, ia, d, ra);
+  if (role < 2) load_row_gk<KM>(ta, ws, role == 0 ? i1 : i0, d, rb);
+  const float praw = spart_sum(ws, j, ncb), raw0 = spart_sum(ws, i0, ncb),
+              raw1 = spart_sum(ws, i1, ncb);
+  const float pf = af_f(af, praw), f0 = af_f(af, raw0), f1 = af_f(af, raw1);
+  const float gp = -af_g_given_f(af, pf);   // rescal.py:275 (all pairs)
+  const float g0 = af_g_given_f(af, f0), g1 = af_g_given_f(af, f1);
+  const int v0 = (k0 && f0 + margin > pf) ? 1 : 0;   // rescal.py:269
+  const int v1 = (k1 && f1 + margin > pf) ? 1 : 0;
+  const float fv0 = (float)v0, fv1 = (float)v1;
+  if (role == 0) {
+#pragma unroll
+    for (int k = 0; k < KM; ++k) x[k] = fv0 * (gp * ra[k]) + fv1 * (gp * ra[k] + g1 * rb[k]);
+    return v0 + 2 * v1;
+  }
+  if (role == 1) {
+#pragma unroll
+    for (int k = 0; k < KM; ++k) x[k] = fv0 * (gp * ra[k] + g0 * rb[k]) + fv1 * (gp * ra[k]);
+    return 2 * v0 + v1;
+  }
+  const int v = role == 2 ? v0 : v1;
+  const float gg = role == 2 ? g0 : g1;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) x[k] = v ? gg * ra[k] : 0.0f;
+  return v;
+}
+
+template <int KM>
+__global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ rec,
+                                                     const int* __restrict__ rec_n1,
+                                                     long long start, int count, int d, int af,
+                                                     float margin, RescalWs ws, FoldTab t,
+                                                     WStep w, int* nviol, int nvw) {
+  const int l = lane_id(), ncb = (d + GC - 1) / GC;
+  if ((int)blockIdx.x < nvw) {
+    // the first nvw workgroups: the batch's violations (the scatter's test,
+    // one positive per thread); their counts and arrivals go into ONE 64-bit
+    // word (one returned atomic per workgroup), so the last to arrive holds
+    // the exact total -- the gate -- and makes the in-front W step current
+    __shared__ int lds_nv;
+    const int j = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
+    int nv = 0;
+    if (j < count) {
+      const int4 r4 = rec[start + j];
+      const int n1 = rec_n1[start + j];
+      const float pf = af_f(af, spart_sum(ws, j, ncb));
+      const float f0 = af_f(af, spart_sum(ws, count + 2 * j, ncb));
+      const float f1 = af_f(af, spart_sum(ws, count + 2 * j + 1, ncb));
+      nv = ((r4.w >= 0 && f0 + margin > pf) ? 1 : 0) + ((n1 >= 0 && f1 + margin > pf) ? 1 : 0);
+    }
+    if (threadIdx.x == 0) lds_nv = 0;
+    __syncthreads();
+    nv = wave_sum_int(nv);
+    if (l == 0 && nv) atomicAdd(&lds_nv, nv);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long add = (1ull << 32) | (unsigned)lds_nv;
+      const unsigned long long old = atomicAdd(ws.vword, add);
+      if ((int)(old >> 32) == nvw - 1) {   // the last: every count is in
+        const int tot = (int)(unsigned)(old + add);
+        *nviol = tot;
+        if (w.cur && tot != 0) {   // the in-front W step becomes current (k_apply_wstep)
+          *w.cur ^= 1;
+          if (w.opt == OPT_ADAGRAD && w.ucnt)   // updateCounts, skge/param.py:149-150
+            for (int p = 0; p < w.M; ++p)
+              if (w.rel_off[p + 1] > w.rel_off[p]) atomicAdd(w.ucnt + (p), 1);
+        }
+      }
+    }
+    return;
+  }
+  // one wave per distinct row: its record (row, slots, first two slots) and
+  // the row count in one round trip, then the slots' rows and partial scores
+  // with the row's parameters and state
+  const int u = ((int)blockIdx.x - nvw) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
+  const int nu = *ws.nuniq;
+  const int4 ur = ws.urec[u];   // (in bounds: u < 4 count)
+  if (u >= nu) return;
+  const int row = __builtin_amdgcn_readfirstlane(ur.x);
+  const int n = __builtin_amdgcn_readfirstlane(ur.y);
+  const int sa0 = __builtin_amdgcn_readfirstlane(ur.z), sb0 = __builtin_amdgcn_readfirstlane(ur.w);
+  const bool ada = t.opt == OPT_ADAGRAD;
+  float* __restrict__ prow = t.P + (size_t)row * d;
+  float* __restrict__ arow = ada ? t.A + (size_t)row * d : nullptr;
+  float p[KM], a[KM], s[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k, ec = e < d ? e : d - 1;
+    p[k] = prow[ec];
+    a[k] = ada ? arow[ec] : 0.0f;
+  }
+  int c;
+  {   // slots 0 and 1 (most rows have one or two)
+    float xa[KM], xb[KM];
+    c = fold_slot<KM>(ws, count, d, af, margin, sa0, xa);
+    if (sb0 >= 0) c += fold_slot<KM>(ws, count, d, af, margin, sb0, xb);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) s[k] = sb0 >= 0 ? xa[k] + xb[k] : xa[k];
+  }
+  if (n > 2) {
+    const int o0 = __builtin_amdgcn_readfirstlane(ws.uoff[u]);
+    for (int q = 2; q < n; q += 2) {   // the rest, two slots' loads in flight together
+      const int sa = __builtin_amdgcn_readfirstlane(ws.uslot[o0 + q]);
+      const int sb = q + 1 < n ? __builtin_amdgcn_readfirstlane(ws.uslot[o0 + q + 1]) : -1;
+      float xa[KM], xb[KM];
+      c += fold_slot<KM>(ws, count, d, af, margin, sa, xa);
+#pragma unroll
+      for (int k = 0; k < KM; ++k) s[k] += xa[k];
+      if (sb >= 0) {
+        c += fold_slot<KM>(ws, count, d, af, margin, sb, xb);
+#pragma unroll
+        for (int k = 0; k < KM; ++k) s[k] += xb[k];
+      }
+    }
+  }
+  if (c == 0) return;   // no violating occurrence: the row is not updated
+  if (ada && t.ucnt && l == 0) atomicAdd(t.ucnt + (row), 1);   // param.py:149-150
+  const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
+  float ss = 0.0f;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const bool in = l + 64 * k < d;
+    const float pv0 = in ? p[k] : 0.0f;
+    const float g = ((in ? s[k] : 0.0f) + t.rin * pv0) / div + t.rout * pv0;   // segment mean (+ rparam)
+    float pv = pv0;
+    if (ada) {
+      const float av = (in ? a[k] : 0.0f) + g * g;      // p2[idx] += g*g           param.py:147
+      a[k] = av;
+      pv = pv - (t.lr * g) / fmaxf(sqrtf(av), 1e-7f);   // P -= lr*g/max(sqrt,1e-7) param.py:152-155
+    } else {
+      pv = pv - t.lr * g;                               // P -= lr*g                param.py:130
+    }
+    p[k] = pv;
+    ss += pv * pv;
+  }
+  if (t.post != POST_NONE) {
+    ss = wave_sum(ss);
+    const float nrm = t.post == POST_NORMALIZE ? sqrtf(ss) : (ss < 1.0f ? 1.0f : ss);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) p[k] = p[k] / nrm;   // param.py:165-166 / 171-173
+  }
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int e = l + 64 * k;
+    if (e < d) {
+      prow[e] = p[k];
+      if (ada) arow[e] = a[k];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1828,6 +2115,12 @@ static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, Resc
   w.s2 = (int*)take((size_t)n * 4);
   w.o2 = (int*)take((size_t)n * 4);
   w.n01 = (int*)take((size_t)M * 4);
+  // the row grouping of the batch's 4 bs entity slots (k_rs_rows_ep)
+  w.urec = (int4*)take((size_t)4 * bs * 16);
+  w.uoff = (int*)take((size_t)4 * bs * 4);
+  w.uslot = (int*)take((size_t)4 * bs * 4);
+  w.nuniq = (int*)take(4);
+  w.vword = (unsigned long long*)take(8);
   w.npos = 0;   // (set per batch: rs_batch_view)
   const size_t slice = off - s0;
   if (ws0) *ws0 = w;
@@ -1855,8 +2148,15 @@ static RescalEpoch rescal_epoch_view(void* ws, long long T, int bs, int nb, int 
 
 // every batch's buckets of the epoch, three launches (dedup lists: pos [T][3],
 // neg [T][2][3], k_pairs_of_epoch's RESCAL form)
+static int rs_rows_npad(int bs) {
+  int n = 1024;
+  while (n < 4 * bs) n <<= 1;
+  return n;
+}
+bool rs_rows_ok(int bs) { return rs_rows_npad(bs) <= RS_ROWS_MAX; }
+
 int rescal_epoch_bucket(hipStream_t st, const int* pos, const int* neg, long long T, int bs, int nb,
-                        int M, int d, void* ws) {
+                        int M, int d, void* ws, const int4* rec, const int* rec_n1) {
   SKGE_CHECK_ARG(rescal_epoch_ok(M), "epoch bucketing needs M <= 64");
   const RescalEpoch e = rescal_epoch_view(ws, T, bs, nb, M, d);
   const long long waves = (long long)nb * e.cpb;
@@ -1865,6 +2165,9 @@ int rescal_epoch_bucket(hipStream_t st, const int* pos, const int* neg, long lon
   hipLaunchKernelGGL(k_rs_scan_ep, dim3((unsigned)nb), dim3(1024),
                      (size_t)(e.dedup ? 8 * M + 2 : 2 * M + 1) * sizeof(int), st, e);
   hipLaunchKernelGGL(k_rs_scatter_ep, dim3(blocks), dim3(256), 0, st, pos, neg, e);
+  if (rec && rec_n1 && rs_rows_ok(bs))   // the batches' entity rows grouped (k_rescal_fold)
+    hipLaunchKernelGGL(k_rs_rows_ep, dim3((unsigned)nb), dim3(1024), 0, st, rec, rec_n1, e,
+                       rs_rows_npad(bs));
   SKGE_CHECK_LAUNCH("rescal epoch bucketing");
   return SKGE_OK;
 }
@@ -1906,6 +2209,11 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
   w.s2 = sh(w.s2);
   w.o2 = sh(w.o2);
   w.n01 = sh(w.n01);
+  w.urec = sh(w.urec);
+  w.uoff = sh(w.uoff);
+  w.uslot = sh(w.uslot);
+  w.nuniq = sh(w.nuniq);
+  w.vword = sh(w.vword);
   w.npos = e.dedup ? count : 0;
   const int n = 3 * count, M = rel->rows;
   const int fsplits = af == AF_LINEAR ? rs_front_splits(n, M, d) : 0;
@@ -1954,12 +2262,27 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
 #undef SKGE_FRONT
     RescalWs wsc = w;
     wsc.coef = nullptr;   // dW was formed from the bucketing's coefficients
+    const WStep wstp{w.wpart, w.rel_off, comb ? w.n01 : nullptr, rel->param, rel->state,
+                     rel->upd_count, nviol, M, d, fsplits, rel->opt, rel->lr, rel->rin, rel->rout,
+                     rel->fixed_div, infront ? w.wcur : nullptr, w.W1, w.A1};
+    // the entity rows updated by the row-grouped apply (k_rescal_fold: no
+    // scatter launch, no entity atomics) where the W step is in the front and
+    // the epoch's row grouping exists (form "scatter": the scatter + apply)
+    if (infront && !form.scatter && w.nuniq && rs_rows_ok(bs)) {
+      const FoldTab ft{ent->param, ent->state, ent->upd_count, ent->opt, ent->post, ent->lr,
+                       ent->rin, ent->rout, ent->fixed_div};
+      const int nvw = (count + 255) / 256;   // violation-count workgroups, then one wave per row
+      SKGE_KM_SWITCH(k_rescal_fold, dim3((unsigned)(nvw + count)), dim3(256), 0, st, rec, rec_n1,
+                     start, count, d, af, margin, wsc, ft, wstp, nviol, nvw)
+      *wstep = wstp;
+      wstep->applied = 1;   // the caller's apply launch is not needed
+      SKGE_CHECK_LAUNCH("rescal positive grad (fused front, row-grouped apply)");
+      return SKGE_OK;
+    }
     SKGE_KM_SWITCH(k_rescal_pos_scatter, dim3(blocks), dim3(256), 0, st, rec, rec_n1, start,
                    count, d, af, margin, wsc, accum_of(ent), nviol)
     if (wstep_in_apply) {   // the caller's entity apply runs the W step
-      *wstep = WStep{w.wpart, w.rel_off, comb ? w.n01 : nullptr, rel->param, rel->state,
-                     rel->upd_count, nviol, M, d, fsplits, rel->opt, rel->lr, rel->rin, rel->rout,
-                     rel->fixed_div, infront ? w.wcur : nullptr, w.W1, w.A1};
+      *wstep = wstp;
     } else {
       WApply wa = {rel->param, rel->state, rel->opt, rel->lr, rel->rin, rel->rout,
                    rel->fixed_div, nviol, rel->upd_count};

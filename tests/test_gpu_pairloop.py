@@ -643,3 +643,67 @@ def test_rescal_in_front_w_step_matches_apply_side(n_ent, n_rel, T, d, nb, opt, 
     assert out[0][0] == out[1][0] > 0
     for k in out[0][1]:
         np.testing.assert_allclose(out[1][1][k], out[0][1][k], rtol=RTOL, atol=ATOL, err_msg=k)
+
+
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb,opt", [
+    (300, 7, 2000, 16, 7, "sgd"),            # ragged remainder batch
+    (300, 40, 2000, 24, 50, "adagrad"),      # ~40 positives / batch: most relations absent
+    (300, 5, 2000, 30, 3, "adagrad"),        # d % 4 != 0
+    (60, 3, 3000, 20, 8, "adagrad"),         # 375 positives over 60 rows: ~25 slots per row
+    (40943, 18, 14140, 200, 10, "sgd"),      # WN18 entity / relation counts, d, batch size
+    (40943, 18, 14140, 200, 9, "sgd"),       # odd number of batches: W ends in the 2nd buffer
+])
+def test_rescal_row_grouped_apply_matches_scatter(n_ent, n_rel, T, d, nb, opt, monkeypatch):
+    """The row-grouped entity update (k_rescal_fold: one wave per distinct
+    entity row of the batch sums its slots' contributions in registers, in
+    slot order, from the WE / EW rows and partial scores; no scatter launch,
+    no entity atomics; the epoch's row grouping by k_rs_rows_ep) against the
+    scatter's float atomics + the apply launch (SKGE_RESCAL_FORM=scatter) on the
+    same draws: equal violation totals, parameters and AdaGrad states within
+    the fp32 tolerance after 2 epochs.  (AdaGrad at small sizes only: at
+    WN18's the atomics' summation order turns rounding-level differences of a
+    near-zero first gradient into +-lr steps, as in the tests above; the
+    runner oracle tests hold the WN18 AdaGrad case to the oracle.)"""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    xs = make_kg(n_ent, n_rel, T, seed=14)
+    out = []
+    for form in ("scatter", ""):
+        monkeypatch.setenv("SKGE_RESCAL_FORM", form)
+        m = make_model("rescal", (n_ent, n_ent, n_rel), d)
+        m.add_hyperparam("margin", 0.2)
+        cls = S.SGD if opt == "sgd" else S.AdaGrad
+        upd = {pid: cls(p, 0.1) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), nb, seed=15)
+        with torch.cuda.stream(r.stream):
+            r.run(2)
+        r.synchronize()
+        state = {pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()}
+        if opt == "adagrad":
+            state["W_p2"] = upd["W"].p2.cpu().numpy().copy()
+            state["E_p2"] = upd["E"].p2.cpu().numpy().copy()
+        out.append((int(r.nviol_total.item()), state))
+    assert out[0][0] == out[1][0] > 0
+    for k in out[0][1]:
+        np.testing.assert_allclose(out[1][1][k], out[0][1][k], rtol=RTOL, atol=ATOL, err_msg=k)
+
+
+def test_rescal_row_grouped_apply_is_deterministic(monkeypatch):
+    """The row-grouped apply sums each row's contributions in slot order (no
+    float atomics), so two runs from the same state give the same bits."""
+    import skge_amd as S
+    from skge_amd.device import DeviceKG, PairLoopRunner
+    monkeypatch.delenv("SKGE_RESCAL_FORM", raising=False)
+    xs = make_kg(40943, 18, 14140, seed=16)
+    out = []
+    for _ in range(2):
+        m = make_model("rescal", (40943, 40943, 18), 200)
+        m.add_hyperparam("margin", 0.2)
+        upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), 10, seed=17)
+        with torch.cuda.stream(r.stream):
+            r.run(2)
+        r.synchronize()
+        out.append({pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()})
+    for pid in out[0]:
+        assert np.array_equal(out[0][pid], out[1][pid]), pid
