@@ -1191,25 +1191,55 @@ struct FoldTab {
   float lr, rin, rout, fdiv;
 };
 
-// slot `sl` of the batch: its contribution to the row (x) and its count
+// slot `sl` of the batch in two halves, so a wave keeps several slots' loads
+// in flight: fold_load issues the slot's WE / EW rows -- s: W E_o of the
+// positive and of (s, o', p); o: E_s W of the positive and of (s', o, p);
+// s' / o': the negative's own row (deduplicated: the positive's) -- and its
+// three items' partial scores (lane q < 3 ncb: item q / ncb, column block
+// q % ncb; K slices in sp2); fold_combine sums the scores in spart_sum's
+// order, runs the pair tests and forms the contribution (x) exactly as
+// k_rescal_pos_scatter does, returning the slot's count
 template <int KM>
-__device__ __forceinline__ int fold_slot(const RescalWs& ws, int count, int d, int af, float margin,
-                                         int sl, float (&x)[KM]) {
-  const int ncb = (d + GC - 1) / GC;
-  const int j = sl >> 4, k1 = (sl >> 3) & 1, k0 = (sl >> 2) & 1, role = sl & 3;
-  const int i0 = count + 2 * j, i1 = i0 + 1;
-  // the slot's rows: s: W E_o of the positive and of (s, o', p); o: E_s W of
-  // the positive and of (s', o, p); s' / o': the negative's own row
-  // (deduplicated: the positive's)
+struct FoldLd {
+  float ra[KM], rb[KM];
+  float sp, sp2;
+};
+
+template <int KM>
+__device__ __forceinline__ void fold_load(const RescalWs& ws, int count, int d, int sl,
+                                          FoldLd<KM>& f) {
+  const int l = lane_id(), ncb = (d + GC - 1) / GC;
+  const int j = sl >> 4, role = sl & 3, i0 = count + 2 * j, i1 = i0 + 1;
   const bool dd = ws.npos > 0;
   const float* ta = (role & 1) ? ws.EW : ws.WE;
-  const int ia = role < 2 ? j : (dd ? j : (role == 2 ? i0 : i1));
-  float ra[KM], rb[KM];
-  load_row_gk<KM>(ta, ws, ia, d, ra);
-  if (role < 2) load_row_gk<KM>(ta, ws, role == 0 ? i1 : i0, d, rb);
-  const float praw = spart_sum(ws, j, ncb), raw0 = spart_sum(ws, i0, ncb),
-              raw1 = spart_sum(ws, i1, ncb);
-  const float pf = af_f(af, praw), f0 = af_f(af, raw0), f1 = af_f(af, raw1);
+#ifdef SKGE_ABL_FOLD_NOROWS   // timing-only ablation (NOT a correct build)
+  for (int k = 0; k < KM; ++k) f.ra[k] = f.rb[k] = (float)(ta == ws.EW);
+#else
+  load_row_gk<KM>(ta, ws, role < 2 ? j : (dd ? j : (role == 2 ? i0 : i1)), d, f.ra);
+  if (role < 2) load_row_gk<KM>(ta, ws, role == 0 ? i1 : i0, d, f.rb);
+#endif
+  const int it = l / ncb, cb = l - it * ncb;
+  const size_t at = (size_t)(it == 0 ? j : (it == 1 ? i0 : i1)) * ncb + cb;
+  f.sp = l < 3 * ncb ? ws.spart[at] : 0.0f;
+  f.sp2 = (ws.gks > 1 && l < 3 * ncb) ? ws.spart[ws.spart_stride + at] : 0.0f;
+}
+
+template <int KM>
+__device__ __forceinline__ int fold_combine(const RescalWs& ws, int d, int af, float margin,
+                                            int sl, const FoldLd<KM>& f, float (&x)[KM]) {
+  const int ncb = (d + GC - 1) / GC;
+  const int k1 = (sl >> 3) & 1, k0 = (sl >> 2) & 1, role = sl & 3;
+  float raw[3];
+#pragma unroll
+  for (int it = 0; it < 3; ++it) {   // spart_sum's order
+    float r = 0.0f;
+    for (int q = 0; q < ncb; ++q) {
+      r += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(f.sp), it * ncb + q));
+      if (ws.gks > 1) r += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(f.sp2), it * ncb + q));
+    }
+    raw[it] = r;
+  }
+  const float pf = af_f(af, raw[0]), f0 = af_f(af, raw[1]), f1 = af_f(af, raw[2]);
   const float gp = -af_g_given_f(af, pf);   // rescal.py:275 (all pairs)
   const float g0 = af_g_given_f(af, f0), g1 = af_g_given_f(af, f1);
   const int v0 = (k0 && f0 + margin > pf) ? 1 : 0;   // rescal.py:269
@@ -1217,18 +1247,18 @@ __device__ __forceinline__ int fold_slot(const RescalWs& ws, int count, int d, i
   const float fv0 = (float)v0, fv1 = (float)v1;
   if (role == 0) {
 #pragma unroll
-    for (int k = 0; k < KM; ++k) x[k] = fv0 * (gp * ra[k]) + fv1 * (gp * ra[k] + g1 * rb[k]);
+    for (int k = 0; k < KM; ++k) x[k] = fv0 * (gp * f.ra[k]) + fv1 * (gp * f.ra[k] + g1 * f.rb[k]);
     return v0 + 2 * v1;
   }
   if (role == 1) {
 #pragma unroll
-    for (int k = 0; k < KM; ++k) x[k] = fv0 * (gp * ra[k] + g0 * rb[k]) + fv1 * (gp * ra[k]);
+    for (int k = 0; k < KM; ++k) x[k] = fv0 * (gp * f.ra[k] + g0 * f.rb[k]) + fv1 * (gp * f.ra[k]);
     return 2 * v0 + v1;
   }
   const int v = role == 2 ? v0 : v1;
   const float gg = role == 2 ? g0 : g1;
 #pragma unroll
-  for (int k = 0; k < KM; ++k) x[k] = v ? gg * ra[k] : 0.0f;
+  for (int k = 0; k < KM; ++k) x[k] = v ? gg * f.ra[k] : 0.0f;
   return v;
 }
 
@@ -1240,11 +1270,14 @@ __global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ re
                                                      WStep w, int* nviol, int nvw) {
   const int l = lane_id(), ncb = (d + GC - 1) / GC;
   if ((int)blockIdx.x < nvw) {
+#ifdef SKGE_ABL_FOLD_NOVC   // timing-only ablation (NOT a correct build)
+    return;
+#endif
     // the first nvw workgroups: the batch's violations (the scatter's test,
     // one positive per thread); their counts and arrivals go into ONE 64-bit
     // word (one returned atomic per workgroup), so the last to arrive holds
     // the exact total -- the gate -- and makes the in-front W step current
-    __shared__ int lds_nv;
+    __shared__ int lds_nv, lds_tot;
     const int j = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x;
     int nv = 0;
     if (j < count) {
@@ -1263,15 +1296,18 @@ __global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ re
     if (threadIdx.x == 0) {
       const unsigned long long add = (1ull << 32) | (unsigned)lds_nv;
       const unsigned long long old = atomicAdd(ws.vword, add);
-      if ((int)(old >> 32) == nvw - 1) {   // the last: every count is in
-        const int tot = (int)(unsigned)(old + add);
-        *nviol = tot;
-        if (w.cur && tot != 0) {   // the in-front W step becomes current (k_apply_wstep)
-          *w.cur ^= 1;
-          if (w.opt == OPT_ADAGRAD && w.ucnt)   // updateCounts, skge/param.py:149-150
-            for (int p = 0; p < w.M; ++p)
-              if (w.rel_off[p + 1] > w.rel_off[p]) atomicAdd(w.ucnt + (p), 1);
-        }
+      // the last to arrive has every count: the batch's total
+      lds_tot = (int)(old >> 32) == nvw - 1 ? (int)(unsigned)(old + add) : -1;
+    }
+    __syncthreads();
+    const int tot = lds_tot;
+    if (tot >= 0 && threadIdx.x < 64) {
+      if (l == 0) *nviol = tot;
+      if (w.cur && tot != 0) {   // the in-front W step becomes current (k_apply_wstep)
+        if (l == 0) *w.cur ^= 1;
+        if (w.opt == OPT_ADAGRAD && w.ucnt)   // updateCounts, skge/param.py:149-150 (lane p)
+          for (int p = l; p < w.M; p += 64)
+            if (w.rel_off[p + 1] > w.rel_off[p]) atomicAdd(w.ucnt + (p), 1);
       }
     }
     return;
@@ -1280,9 +1316,15 @@ __global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ re
   // the row count in one round trip, then the slots' rows and partial scores
   // with the row's parameters and state
   const int u = ((int)blockIdx.x - nvw) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
+#ifdef SKGE_ABL_FOLD_NOROWWAVE   // timing-only ablation (NOT a correct build)
+  return;
+#endif
   const int nu = *ws.nuniq;
   const int4 ur = ws.urec[u];   // (in bounds: u < 4 count)
   if (u >= nu) return;
+#ifdef SKGE_ABL_FOLD_URECONLY   // timing-only ablation (NOT a correct build)
+  if (ur.x != -7) return;
+#endif
   const int row = __builtin_amdgcn_readfirstlane(ur.x);
   const int n = __builtin_amdgcn_readfirstlane(ur.y);
   const int sa0 = __builtin_amdgcn_readfirstlane(ur.z), sb0 = __builtin_amdgcn_readfirstlane(ur.w);
@@ -1297,30 +1339,43 @@ __global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ re
     a[k] = ada ? arow[ec] : 0.0f;
   }
   int c;
-  {   // slots 0 and 1 (most rows have one or two)
+  {   // slots 0 and 1 (most rows have one or two): every load issued, then the sums
+    FoldLd<KM> fa, fb;
+    fold_load<KM>(ws, count, d, sa0, fa);
+    if (sb0 >= 0) fold_load<KM>(ws, count, d, sb0, fb);
     float xa[KM], xb[KM];
-    c = fold_slot<KM>(ws, count, d, af, margin, sa0, xa);
-    if (sb0 >= 0) c += fold_slot<KM>(ws, count, d, af, margin, sb0, xb);
+    c = fold_combine<KM>(ws, d, af, margin, sa0, fa, xa);
+    if (sb0 >= 0) c += fold_combine<KM>(ws, d, af, margin, sb0, fb, xb);
 #pragma unroll
     for (int k = 0; k < KM; ++k) s[k] = sb0 >= 0 ? xa[k] + xb[k] : xa[k];
   }
+#ifdef SKGE_ABL_FOLD_MAX2   // timing-only ablation (NOT a correct build)
+  if (false) {
+#else
   if (n > 2) {
+#endif
     const int o0 = __builtin_amdgcn_readfirstlane(ws.uoff[u]);
-    for (int q = 2; q < n; q += 2) {   // the rest, two slots' loads in flight together
+    for (int q = 2; q < n; q += 2) {   // the rest, two slots at a time
       const int sa = __builtin_amdgcn_readfirstlane(ws.uslot[o0 + q]);
       const int sb = q + 1 < n ? __builtin_amdgcn_readfirstlane(ws.uslot[o0 + q + 1]) : -1;
+      FoldLd<KM> fa, fb;
+      fold_load<KM>(ws, count, d, sa, fa);
+      if (sb >= 0) fold_load<KM>(ws, count, d, sb, fb);
       float xa[KM], xb[KM];
-      c += fold_slot<KM>(ws, count, d, af, margin, sa, xa);
+      c += fold_combine<KM>(ws, d, af, margin, sa, fa, xa);
 #pragma unroll
       for (int k = 0; k < KM; ++k) s[k] += xa[k];
       if (sb >= 0) {
-        c += fold_slot<KM>(ws, count, d, af, margin, sb, xb);
+        c += fold_combine<KM>(ws, d, af, margin, sb, fb, xb);
 #pragma unroll
         for (int k = 0; k < KM; ++k) s[k] += xb[k];
       }
     }
   }
   if (c == 0) return;   // no violating occurrence: the row is not updated
+#ifdef SKGE_ABL_FOLD_NOSTORE   // timing-only ablation (NOT a correct build)
+  if (s[0] != 12345.0f) return;
+#endif
   if (ada && t.ucnt && l == 0) atomicAdd(t.ucnt + (row), 1);   // param.py:149-150
   const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
   float ss = 0.0f;

@@ -834,10 +834,10 @@ template <int K>
 __global__ __launch_bounds__(256) void k_apply_wstep(TableDev t0, int n0, WStep w, int nwb) {
   if (w.cur) {   // the W step was done in the front: make it current if the batch updates
     if ((int)blockIdx.x < nwb) {
-      if (blockIdx.x == 0 && threadIdx.x == 0 && *w.gate != 0) {
-        *w.cur ^= 1;
-        if (w.opt == OPT_ADAGRAD && w.ucnt)   // updateCounts, skge/param.py:149-150
-          for (int p = 0; p < w.M; ++p)
+      if (blockIdx.x == 0 && threadIdx.x < 64 && *w.gate != 0) {   // wave 0
+        if (threadIdx.x == 0) *w.cur ^= 1;
+        if (w.opt == OPT_ADAGRAD && w.ucnt)   // updateCounts, skge/param.py:149-150: lane p
+          for (int p = threadIdx.x; p < w.M; p += 64)
             if (w.rel_off[p + 1] > w.rel_off[p]) atomicAdd(w.ucnt + (p), 1);
       }
       return;
