@@ -666,9 +666,11 @@ __global__ __launch_bounds__(1024) void k_rs_rows_ep(const int4* __restrict__ re
     w.uoff[u] = i;
     ++u;
   }
+  int tot = 0;
+  for (int v = 0; v < (int)(blockDim.x >> 6); ++v) tot += wtot[v];
+  for (int i = tot + tid; i < ns; i += blockDim.x)   // past the rows: row -1 (k_rescal_fold exits)
+    w.urec[i] = make_int4(-1, 0, -1, -1);
   if (tid == 0) {
-    int tot = 0;
-    for (int v = 0; v < (int)(blockDim.x >> 6); ++v) tot += wtot[v];
     *w.nuniq = tot;
     *w.vword = 0ull;
   }
@@ -1212,12 +1214,8 @@ __device__ __forceinline__ void fold_load(const RescalWs& ws, int count, int d, 
   const int j = sl >> 4, role = sl & 3, i0 = count + 2 * j, i1 = i0 + 1;
   const bool dd = ws.npos > 0;
   const float* ta = (role & 1) ? ws.EW : ws.WE;
-#ifdef SKGE_ABL_FOLD_NOROWS   // timing-only ablation (NOT a correct build)
-  for (int k = 0; k < KM; ++k) f.ra[k] = f.rb[k] = (float)(ta == ws.EW);
-#else
   load_row_gk<KM>(ta, ws, role < 2 ? j : (dd ? j : (role == 2 ? i0 : i1)), d, f.ra);
   if (role < 2) load_row_gk<KM>(ta, ws, role == 0 ? i1 : i0, d, f.rb);
-#endif
   const int it = l / ncb, cb = l - it * ncb;
   const size_t at = (size_t)(it == 0 ? j : (it == 1 ? i0 : i1)) * ncb + cb;
   f.sp = l < 3 * ncb ? ws.spart[at] : 0.0f;
@@ -1270,9 +1268,6 @@ __global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ re
                                                      WStep w, int* nviol, int nvw) {
   const int l = lane_id(), ncb = (d + GC - 1) / GC;
   if ((int)blockIdx.x < nvw) {
-#ifdef SKGE_ABL_FOLD_NOVC   // timing-only ablation (NOT a correct build)
-    return;
-#endif
     // the first nvw workgroups: the batch's violations (the scatter's test,
     // one positive per thread); their counts and arrivals go into ONE 64-bit
     // word (one returned atomic per workgroup), so the last to arrive holds
@@ -1316,15 +1311,8 @@ __global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ re
   // the row count in one round trip, then the slots' rows and partial scores
   // with the row's parameters and state
   const int u = ((int)blockIdx.x - nvw) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
-#ifdef SKGE_ABL_FOLD_NOROWWAVE   // timing-only ablation (NOT a correct build)
-  return;
-#endif
-  const int nu = *ws.nuniq;
-  const int4 ur = ws.urec[u];   // (in bounds: u < 4 count)
-  if (u >= nu) return;
-#ifdef SKGE_ABL_FOLD_URECONLY   // timing-only ablation (NOT a correct build)
-  if (ur.x != -7) return;
-#endif
+  const int4 ur = ws.urec[u];   // (u < 4 count; row -1 past the batch's distinct rows)
+  if (ur.x < 0) return;
   const int row = __builtin_amdgcn_readfirstlane(ur.x);
   const int n = __builtin_amdgcn_readfirstlane(ur.y);
   const int sa0 = __builtin_amdgcn_readfirstlane(ur.z), sb0 = __builtin_amdgcn_readfirstlane(ur.w);
@@ -1349,11 +1337,7 @@ __global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ re
 #pragma unroll
     for (int k = 0; k < KM; ++k) s[k] = sb0 >= 0 ? xa[k] + xb[k] : xa[k];
   }
-#ifdef SKGE_ABL_FOLD_MAX2   // timing-only ablation (NOT a correct build)
-  if (false) {
-#else
   if (n > 2) {
-#endif
     const int o0 = __builtin_amdgcn_readfirstlane(ws.uoff[u]);
     for (int q = 2; q < n; q += 2) {   // the rest, two slots at a time
       const int sa = __builtin_amdgcn_readfirstlane(ws.uslot[o0 + q]);
@@ -1373,9 +1357,6 @@ __global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ re
     }
   }
   if (c == 0) return;   // no violating occurrence: the row is not updated
-#ifdef SKGE_ABL_FOLD_NOSTORE   // timing-only ablation (NOT a correct build)
-  if (s[0] != 12345.0f) return;
-#endif
   if (ada && t.ucnt && l == 0) atomicAdd(t.ucnt + (row), 1);   // param.py:149-150
   const float div = t.fdiv > 0.0f ? t.fdiv : (float)c;
   float ss = 0.0f;
