@@ -596,79 +596,107 @@ __global__ __launch_bounds__(256) void k_rs_scatter_ep(const int* __restrict__ p
 }
 
 // The row grouping of every batch's entity slots, once per epoch (the
-// records are drawn at the epoch's start): one workgroup per batch sorts the
-// batch's 4 count slot keys (row << 20 | packed slot, RescalWs::uslot) in LDS
-// (bitonic), then writes the distinct rows, their slot ranges and the slots
-// in slot order -- what k_rescal_fold reads instead of the scatter's atomics.
-constexpr int RS_ROWS_MAX = 8192;   // slots per batch the LDS sort holds (bs <= 2048)
+// records are drawn at the epoch's start): one workgroup per batch inserts
+// the batch's 4 count slots' rows into an LDS hash table (linear probing),
+// ranks each slot within its row (LDS atomics), compacts the table into the
+// distinct rows' slot ranges, sorts each range by slot (a row has one or two
+// slots at WN18's batch: the order, hence every sum, is fixed), and writes
+// the records k_rescal_fold reads instead of the scatter's atomics.
+constexpr int RS_ROWS_MAX = 8192;   // hash entries = slots per batch at most (bs <= 2048)
 __global__ __launch_bounds__(1024) void k_rs_rows_ep(const int4* __restrict__ rec,
                                                      const int* __restrict__ rec_n1,
-                                                     RescalEpoch e, int npad) {
-  __shared__ unsigned long long sk[RS_ROWS_MAX];
-  __shared__ int wtot[16];
+                                                     RescalEpoch e) {
+  __shared__ int hkey[RS_ROWS_MAX];   // row of the entry, or -1
+  __shared__ int hcnt[RS_ROWS_MAX];   // its slots; after the compaction: its first position
+  __shared__ int sl[RS_ROWS_MAX];     // the slots, grouped by row
+  __shared__ int wt_u[16], wt_n[16];
+  constexpr int PER = RS_ROWS_MAX / 1024;   // entries and slots per thread
   const int b = blockIdx.x, tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
   const int cnt = rs_batch_count(e, b), ns = 4 * cnt;
   const long long s0 = (long long)b * e.bs;
   const RescalWs w = rs_batch_view(e, b);
-  for (int i = tid; i < npad; i += blockDim.x) {
-    unsigned long long key = ~0ull;
-    if (i < ns) {
-      const int j = i >> 2, role = i & 3;
-      const int4 r4 = rec[s0 + j];
-      const int n1 = rec_n1[s0 + j];
-      const int row = role == 0 ? r4.x : (role == 1 ? r4.y : (role == 2 ? r4.w : n1));
-      if (row >= 0)
-        key = ((unsigned long long)row << 20) |
-              (unsigned)((j << 4) | ((n1 >= 0 ? 1 : 0) << 3) | ((r4.w >= 0 ? 1 : 0) << 2) | role);
-    }
-    sk[i] = key;
+  for (int i = tid; i < RS_ROWS_MAX; i += 1024) {
+    hkey[i] = -1;
+    hcnt[i] = 0;
   }
   __syncthreads();
-  for (int k = 2; k <= npad; k <<= 1) {   // bitonic sort, ascending
-    for (int jj = k >> 1; jj > 0; jj >>= 1) {
-      for (int i = tid; i < npad; i += blockDim.x) {
-        const int ixj = i ^ jj;
-        if (ixj > i) {
-          const unsigned long long x = sk[i], y = sk[ixj];
-          if ((x > y) == ((i & k) == 0)) {
-            sk[i] = y;
-            sk[ixj] = x;
-          }
-        }
+  int he[PER], rk[PER], sv[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {   // slot i = tid + 1024 q
+    const int i = tid + 1024 * q;
+    he[q] = -1;
+    if (i >= ns) continue;
+    const int j = i >> 2, role = i & 3;
+    const int4 r4 = rec[s0 + j];
+    const int n1 = rec_n1[s0 + j];
+    const int row = role == 0 ? r4.x : (role == 1 ? r4.y : (role == 2 ? r4.w : n1));
+    if (row < 0) continue;
+    sv[q] = (j << 4) | ((n1 >= 0 ? 1 : 0) << 3) | ((r4.w >= 0 ? 1 : 0) << 2) | role;
+    int h = (int)(fmix32((uint32_t)row) & (RS_ROWS_MAX - 1));
+    while (true) {   // distinct rows <= slots <= entries: a free entry always exists
+      const int old = atomicCAS(&hkey[h], -1, row);
+      if (old == -1 || old == row) break;
+      h = (h + 1) & (RS_ROWS_MAX - 1);
+    }
+    he[q] = h;
+    rk[q] = atomicAdd(&hcnt[h], 1);
+  }
+  __syncthreads();
+  // compaction: thread t owns entries [PER t, PER t + PER)
+  int nu = 0, nsl = 0, c[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    c[q] = hcnt[PER * tid + q];
+    nu += hkey[PER * tid + q] >= 0 ? 1 : 0;
+    nsl += c[q];
+  }
+  const int iu = wave_incl_scan(nu), in = wave_incl_scan(nsl);
+  if (l == 63) {
+    wt_u[wave] = iu;
+    wt_n[wave] = in;
+  }
+  __syncthreads();
+  int u = iu - nu, off = in - nsl;
+  for (int v = 0; v < wave; ++v) {
+    u += wt_u[v];
+    off += wt_n[v];
+  }
+  int eu[PER], eo[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    eu[q] = -1;
+    eo[q] = off;
+    if (hkey[PER * tid + q] >= 0) {
+      eu[q] = u++;
+      hcnt[PER * tid + q] = off;
+    }
+    off += c[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < PER; ++q)
+    if (he[q] >= 0) sl[hcnt[he[q]] + rk[q]] = sv[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {   // each row's slots in slot order, then its record
+    if (eu[q] < 0) continue;
+    const int o = eo[q], n = c[q];
+    for (int a = o + 1; a < o + n; ++a) {   // insertion sort (n is small)
+      const int x = sl[a];
+      int z = a - 1;
+      while (z >= o && sl[z] > x) {
+        sl[z + 1] = sl[z];
+        --z;
       }
-      __syncthreads();
+      sl[z + 1] = x;
     }
-  }
-  // distinct rows: thread t owns keys [t ch, (t + 1) ch); a key heads a row
-  // when its row differs from the previous key's
-  const int ch = npad / (int)blockDim.x;   // npad >= blockDim.x (a power of two)
-  auto head = [&](int i) {
-    const unsigned long long x = sk[i];
-    return x != ~0ull && (i == 0 || (sk[i - 1] >> 20) != (x >> 20));
-  };
-  int heads = 0;
-  for (int q = 0; q < ch; ++q) heads += head(tid * ch + q) ? 1 : 0;
-  const int inc = wave_incl_scan(heads);
-  if (l == 63) wtot[wave] = inc;
-  __syncthreads();
-  int u = inc - heads;   // this thread's first head index
-  for (int v = 0; v < wave; ++v) u += wtot[v];
-  for (int q = 0; q < ch; ++q) {
-    const int i = tid * ch + q;
-    const unsigned long long x = sk[i];
-    if (x == ~0ull) continue;
-    w.uslot[i] = (int)(x & 0xFFFFFu);
-    if (!head(i)) continue;
-    int n = 1;   // the row's slots: the keys up to the next row
-    while (i + n < npad && sk[i + n] != ~0ull && (sk[i + n] >> 20) == (x >> 20)) ++n;
-    w.urec[u] = make_int4((int)(x >> 20), n, (int)(x & 0xFFFFFu),
-                          n > 1 ? (int)(sk[i + 1] & 0xFFFFFu) : -1);
-    w.uoff[u] = i;
-    ++u;
+    for (int a = o; a < o + n; ++a) w.uslot[a] = sl[a];
+    w.urec[eu[q]] = make_int4(hkey[PER * tid + q], n, sl[o], n > 1 ? sl[o + 1] : -1);
+    w.uoff[eu[q]] = o;
   }
   int tot = 0;
-  for (int v = 0; v < (int)(blockDim.x >> 6); ++v) tot += wtot[v];
-  for (int i = tot + tid; i < ns; i += blockDim.x)   // past the rows: row -1 (k_rescal_fold exits)
+  for (int v = 0; v < 16; ++v) tot += wt_u[v];
+  for (int i = tot + tid; i < ns; i += 1024)   // past the rows: row -1 (k_rescal_fold exits)
     w.urec[i] = make_int4(-1, 0, -1, -1);
   if (tid == 0) {
     *w.nuniq = tot;
@@ -2184,12 +2212,7 @@ static RescalEpoch rescal_epoch_view(void* ws, long long T, int bs, int nb, int 
 
 // every batch's buckets of the epoch, three launches (dedup lists: pos [T][3],
 // neg [T][2][3], k_pairs_of_epoch's RESCAL form)
-static int rs_rows_npad(int bs) {
-  int n = 1024;
-  while (n < 4 * bs) n <<= 1;
-  return n;
-}
-bool rs_rows_ok(int bs) { return rs_rows_npad(bs) <= RS_ROWS_MAX; }
+bool rs_rows_ok(int bs) { return 4ll * bs <= RS_ROWS_MAX; }
 
 int rescal_epoch_bucket(hipStream_t st, const int* pos, const int* neg, long long T, int bs, int nb,
                         int M, int d, void* ws, const int4* rec, const int* rec_n1) {
@@ -2202,8 +2225,7 @@ int rescal_epoch_bucket(hipStream_t st, const int* pos, const int* neg, long lon
                      (size_t)(e.dedup ? 8 * M + 2 : 2 * M + 1) * sizeof(int), st, e);
   hipLaunchKernelGGL(k_rs_scatter_ep, dim3(blocks), dim3(256), 0, st, pos, neg, e);
   if (rec && rec_n1 && rs_rows_ok(bs))   // the batches' entity rows grouped (k_rescal_fold)
-    hipLaunchKernelGGL(k_rs_rows_ep, dim3((unsigned)nb), dim3(1024), 0, st, rec, rec_n1, e,
-                       rs_rows_npad(bs));
+    hipLaunchKernelGGL(k_rs_rows_ep, dim3((unsigned)nb), dim3(1024), 0, st, rec, rec_n1, e);
   SKGE_CHECK_LAUNCH("rescal epoch bucketing");
   return SKGE_OK;
 }
