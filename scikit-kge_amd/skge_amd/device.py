@@ -196,13 +196,24 @@ class EpochRunner(object):
             raise ValueError("pipelined runner needs TransE-L1, d % 4 == 0, packed sums "
                              "and replicas == 1")
         if can_pipe and pipelined is None:
-            # the pipelined runner's scratch: the epoch's records, two more
-            # entity accumulator copies, per-row words and (k_pipe_fused) a
-            # second copy of E and its AdaGrad state (auto mode: only if it fits)
+            # the pipelined runner's scratch (auto mode: only if it fits): the
+            # epoch's records and, per entity row, k_pipe_fused (rows of <= 64
+            # floats, batches of <= 16k slot records; skge_pipeline.hip) three
+            # accumulator copies, a second copy of E and its AdaGrad state and a
+            # meta word -- k_pipe_batch two accumulator copies (the table's and
+            # one more, packed 16- or 8-bit fields) and five words (done word,
+            # pending marks and owner marks of both copies)
             torch.cuda.synchronize(dev)
             torch.cuda.empty_cache()
-            acc = E.rows * (E.width * 2 + 4) + 4 * 4 * bs   # the entity accumulator itself
-            extra = 3 * acc + kg.T * 20 + (64 << 20) + E.rows * (16 + 8 * E.width)
+            wd = self.d_pad if self._pad else model.d
+            if wd <= 64 and 4 * bs <= 4 * 4096:
+                acc = E.rows * (E.width * 2 + 4) + 4 * 4 * bs
+                extra = 3 * acc + kg.T * 20 + (64 << 20) + E.rows * (16 + 8 * E.width)
+            else:
+                e8_est = (packed_count_bound(kg, model.E.rows, bs, _tail8) <= 127 and
+                          _os.environ.get("SKGE_PIPE_E8", "1") != "0")
+                acc = E.rows * ((wd // 4) * (4 if e8_est else 8) + 4) + 2 * 4 * 4 * bs
+                extra = 2 * acc + E.rows * 5 * 4 + kg.T * 20 + (256 << 20)
             can_pipe = extra < torch.cuda.mem_get_info(dev)[0] * 0.9
         torch.cuda.current_stream().synchronize()
         lib = L.lib()

@@ -23,7 +23,9 @@ for c in ${CONFIGS:-2 1 3 4 5}; do
   cp $D/pmc.json profiles/$R/pmc$suf.json
   python3 tools/trace_by_grid.py $D/stats > $D/kernel_trace_by_grid.json || true
   if [ "$c" = 5 ]; then   # the two-launch runner: nb launches of each batch kernel per epoch
-    nb=$(python3 -c "print(-(-100_000_000 // 131072))")   # batch launches per epoch (the last one ragged)
+    # full-batch launches per epoch: nb = T // B batches of T // nb positives,
+    # the remainder a ragged batch (and, pipelined, the flush) at other grids
+    nb=$(python3 -c "T = 100_000_000; bs = T // (T // 131072); print(T // bs)")
     python3 tools/pmc_epochs.py $D $nb > profiles/$R/pmc_c5_epochs.json || true
     python3 tools/trace_epochs.py $D/stats $nb > $D/kernel_trace_epochs.json || true
   fi

@@ -23,7 +23,8 @@ def per_dispatch(path, counter):
 
 def main():
     root, per = sys.argv[1], int(sys.argv[2])
-    names = sys.argv[3:] or ["k_transe_l1_sample_grad", "k_apply"]
+    # the two-launch runner's kernels, or the pipelined runner's batch kernel
+    names = sys.argv[3:] or ["k_transe_l1_sample_grad", "k_apply", "k_pipe_batch"]
     fetch = per_dispatch(os.path.join(root, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_dispatch(os.path.join(root, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     res = {}
@@ -36,6 +37,8 @@ def main():
             return max(grids.values(), key=len) if grids else []
         f, w = rows(fetch), rows(write)
         n = min(len(f), len(w))
+        if n == 0:   # (this runner does not launch it)
+            continue
         eps = []
         for e in range(0, n, per):
             fe, we = f[e:e + per], w[e:e + per]

@@ -15,12 +15,14 @@ import sys
 
 def main():
     root, per = sys.argv[1], int(sys.argv[2])
-    names = sys.argv[3:] or ["k_transe_l1_sample_grad", "k_apply"]
+    names = sys.argv[3:] or ["k_transe_l1_sample_grad", "k_apply", "k_pipe_batch"]
     f = glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = list(csv.DictReader(open(f)))
     out = {}
     for name in names:
         sel = [r for r in rows if r["Kernel_Name"].startswith(name)]
+        if not sel:   # (this runner does not launch it)
+            continue
         grids = {}
         for r in sel:
             g = r.get("Grid_Size_X") or r.get("Grid_Size")
