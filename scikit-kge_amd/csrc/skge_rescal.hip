@@ -87,16 +87,21 @@ struct RescalWs {
   float* A1;
   int* wcur;
   // the batch's entity rows grouped (epoch buckets: k_rs_rows_ep; else null):
-  // nuniq distinct rows, row u's record urec[u] = (row, n slots, slot 0, slot 1
-  // or -1), its slots uslot[uoff[u] .. uoff[u] + n) in slot order, a slot
-  // packed as j << 4 | k1 << 3 | k0 << 2 | role (positive j, role 0-3 = s, o,
-  // s', o'; k0 / k1: its negatives exist); vword: k_rescal_fold's violation
-  // count (low half) and arrivals (high half), zeroed with the grouping
+  // a distinct row's slots in slot order, two per work item -- urec[w] = (row,
+  // slot a, slot b or -1, chunk << 16 | chunks of the row), a row's chunks
+  // consecutive, row -1 past the last item; a slot packed as j << 4 | k1 << 3
+  // | k0 << 2 | role (positive j, role 0-3 = s, o, s', o'; k0 / k1: its
+  // negatives exist); rowctr[w0]: arrivals of a multi-chunk row's items (w0
+  // its first); nuniq: distinct rows; vword: k_rescal_fold's violation count
+  // (low half) and arrivals (high half); all zeroed with the grouping.
+  // part / pcnt (shared by the batches): a multi-chunk item's partial sum and
+  // count
   int4* urec;
-  int* uoff;
-  int* uslot;
+  int* rowctr;
   int* nuniq;
   unsigned long long* vword;
+  float* part;
+  int* pcnt;
   // GEMM K split (SKGE_RS_GKS, 1 = off): the WE / EW rows and partial scores
   // come in gks slices over k, slice k at WE + k * part_stride (spart + k *
   // spart_stride); consumers add the slices in index order (deterministic)
@@ -282,8 +287,10 @@ static size_t rescal_ws_layout(int n, int M, int d, void* base, RescalWs* ws) {
   w.W1 = w.A1 = nullptr;
   w.wcur = nullptr;
   w.urec = nullptr;
-  w.uoff = w.uslot = w.nuniq = nullptr;
+  w.rowctr = w.nuniq = nullptr;
   w.vword = nullptr;
+  w.part = nullptr;
+  w.pcnt = nullptr;
   if (ws) *ws = w;
   return off;
 }
@@ -556,8 +563,7 @@ __device__ __forceinline__ RescalWs rs_batch_view(const RescalEpoch& e, int b) {
   w.o2 = sh(w.o2);
   w.n01 = sh(w.n01);
   w.urec = sh(w.urec);
-  w.uoff = sh(w.uoff);
-  w.uslot = sh(w.uslot);
+  w.rowctr = sh(w.rowctr);
   w.nuniq = sh(w.nuniq);
   w.vword = sh(w.vword);
   w.npos = e.dedup ? rs_batch_count(e, b) : 0;
@@ -599,9 +605,11 @@ __global__ __launch_bounds__(256) void k_rs_scatter_ep(const int* __restrict__ p
 // records are drawn at the epoch's start): one workgroup per batch inserts
 // the batch's 4 count slots' rows into an LDS hash table (linear probing),
 // ranks each slot within its row (LDS atomics), compacts the table into the
-// distinct rows' slot ranges, sorts each range by slot (a row has one or two
-// slots at WN18's batch: the order, hence every sum, is fixed), and writes
-// the records k_rescal_fold reads instead of the scatter's atomics.
+// distinct rows' slot ranges, sorts each range by slot (the order, hence
+// every sum, is fixed) and writes the work items k_rescal_fold reads instead
+// of the scatter's atomics: two slots per item, a row of n slots as
+// ceil(n / 2) consecutive items (one or two slots per row at WN18's batch;
+// hub rows of skewed KGs get many, merged by their last item).
 constexpr int RS_ROWS_MAX = 8192;   // hash entries = slots per batch at most (bs <= 2048)
 __global__ __launch_bounds__(1024) void k_rs_rows_ep(const int4* __restrict__ rec,
                                                      const int* __restrict__ rec_n1,
@@ -609,7 +617,7 @@ __global__ __launch_bounds__(1024) void k_rs_rows_ep(const int4* __restrict__ re
   __shared__ int hkey[RS_ROWS_MAX];   // row of the entry, or -1
   __shared__ int hcnt[RS_ROWS_MAX];   // its slots; after the compaction: its first position
   __shared__ int sl[RS_ROWS_MAX];     // the slots, grouped by row
-  __shared__ int wt_u[16], wt_n[16];
+  __shared__ int wt_u[16], wt_n[16], wt_r[16];
   constexpr int PER = RS_ROWS_MAX / 1024;   // entries and slots per thread
   const int b = blockIdx.x, tid = threadIdx.x, l = lane_id(), wave = tid >> 6;
   const int cnt = rs_batch_count(e, b), ns = 4 * cnt;
@@ -642,32 +650,36 @@ __global__ __launch_bounds__(1024) void k_rs_rows_ep(const int4* __restrict__ re
     rk[q] = atomicAdd(&hcnt[h], 1);
   }
   __syncthreads();
-  // compaction: thread t owns entries [PER t, PER t + PER)
-  int nu = 0, nsl = 0, c[PER];
+  // compaction: thread t owns entries [PER t, PER t + PER); a row of n slots
+  // becomes ceil(n / 2) work items
+  int nw = 0, nsl = 0, nu = 0, c[PER];
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     c[q] = hcnt[PER * tid + q];
-    nu += hkey[PER * tid + q] >= 0 ? 1 : 0;
+    nw += (c[q] + 1) >> 1;
     nsl += c[q];
+    nu += hkey[PER * tid + q] >= 0 ? 1 : 0;
   }
-  const int iu = wave_incl_scan(nu), in = wave_incl_scan(nsl);
+  const int iw = wave_incl_scan(nw), in = wave_incl_scan(nsl), iu = wave_incl_scan(nu);
   if (l == 63) {
-    wt_u[wave] = iu;
+    wt_u[wave] = iw;
     wt_n[wave] = in;
+    wt_r[wave] = iu;
   }
   __syncthreads();
-  int u = iu - nu, off = in - nsl;
+  int w0 = iw - nw, off = in - nsl;
   for (int v = 0; v < wave; ++v) {
-    u += wt_u[v];
+    w0 += wt_u[v];
     off += wt_n[v];
   }
-  int eu[PER], eo[PER];
+  int ew[PER], eo[PER];
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    eu[q] = -1;
+    ew[q] = -1;
     eo[q] = off;
     if (hkey[PER * tid + q] >= 0) {
-      eu[q] = u++;
+      ew[q] = w0;
+      w0 += (c[q] + 1) >> 1;
       hcnt[PER * tid + q] = off;
     }
     off += c[q];
@@ -678,10 +690,10 @@ __global__ __launch_bounds__(1024) void k_rs_rows_ep(const int4* __restrict__ re
     if (he[q] >= 0) sl[hcnt[he[q]] + rk[q]] = sv[q];
   __syncthreads();
 #pragma unroll
-  for (int q = 0; q < PER; ++q) {   // each row's slots in slot order, then its record
-    if (eu[q] < 0) continue;
-    const int o = eo[q], n = c[q];
-    for (int a = o + 1; a < o + n; ++a) {   // insertion sort (n is small)
+  for (int q = 0; q < PER; ++q) {   // each row's slots in slot order, then its work items
+    if (ew[q] < 0) continue;
+    const int o = eo[q], n = c[q], nch = (n + 1) >> 1, row = hkey[PER * tid + q];
+    for (int a = o + 1; a < o + n; ++a) {   // insertion sort (n is small but for hub rows)
       const int x = sl[a];
       int z = a - 1;
       while (z >= o && sl[z] > x) {
@@ -690,16 +702,20 @@ __global__ __launch_bounds__(1024) void k_rs_rows_ep(const int4* __restrict__ re
       }
       sl[z + 1] = x;
     }
-    for (int a = o; a < o + n; ++a) w.uslot[a] = sl[a];
-    w.urec[eu[q]] = make_int4(hkey[PER * tid + q], n, sl[o], n > 1 ? sl[o + 1] : -1);
-    w.uoff[eu[q]] = o;
+    for (int k = 0; k < nch; ++k)
+      w.urec[ew[q] + k] = make_int4(row, sl[o + 2 * k], 2 * k + 1 < n ? sl[o + 2 * k + 1] : -1,
+                                   (k << 16) | nch);
+    if (nch > 1) w.rowctr[ew[q]] = 0;
   }
-  int tot = 0;
-  for (int v = 0; v < 16; ++v) tot += wt_u[v];
-  for (int i = tot + tid; i < ns; i += 1024)   // past the rows: row -1 (k_rescal_fold exits)
-    w.urec[i] = make_int4(-1, 0, -1, -1);
+  int tot = 0, rows = 0;
+  for (int v = 0; v < 16; ++v) {
+    tot += wt_u[v];
+    rows += wt_r[v];
+  }
+  for (int i = tot + tid; i < ns; i += 1024)   // past the items: row -1 (k_rescal_fold exits)
+    w.urec[i] = make_int4(-1, -1, -1, 0);
   if (tid == 0) {
-    *w.nuniq = tot;
+    *w.nuniq = rows;
     *w.vword = 0ull;
   }
 }
@@ -1203,8 +1219,9 @@ __global__ __launch_bounds__(256) void k_rescal_pos_scatter(const int4* __restri
 
 // ---------------------------------------------------------------------------
 // The device pair loop's entity update without the scatter (k_rescal_fold):
-// one wave per DISTINCT entity row of the batch (k_rs_rows_ep's grouping)
-// walks the row's slots in slot order, recomputes each slot's pair tests
+// one wave per work item of k_rs_rows_ep's grouping (two slots of a
+// distinct entity row; a hub row's items merged by the last to arrive)
+// takes the row's slots in slot order, recomputes each slot's pair tests
 // from the partial scores and forms its contribution from the WE / EW rows
 // exactly as k_rescal_pos_scatter does (rescal.py:264-302), sums them in
 // registers (a fixed order: no float atomics, bitwise reproducible), then
@@ -1335,27 +1352,30 @@ __global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ re
     }
     return;
   }
-  // one wave per distinct row: its record (row, slots, first two slots) and
-  // the row count in one round trip, then the slots' rows and partial scores
-  // with the row's parameters and state
-  const int u = ((int)blockIdx.x - nvw) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
-  const int4 ur = ws.urec[u];   // (u < 4 count; row -1 past the batch's distinct rows)
+  // one wave per work item (two slots of a distinct row): its record in one
+  // round trip, then the slots' rows and partial scores (and, for a row of one
+  // item, the row's parameters and state)
+  const int wi = ((int)blockIdx.x - nvw) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
+  const int4 ur = ws.urec[wi];   // (wi < 4 count; row -1 past the batch's items)
   if (ur.x < 0) return;
   const int row = __builtin_amdgcn_readfirstlane(ur.x);
-  const int n = __builtin_amdgcn_readfirstlane(ur.y);
-  const int sa0 = __builtin_amdgcn_readfirstlane(ur.z), sb0 = __builtin_amdgcn_readfirstlane(ur.w);
+  const int sa0 = __builtin_amdgcn_readfirstlane(ur.y), sb0 = __builtin_amdgcn_readfirstlane(ur.z);
+  const int info = __builtin_amdgcn_readfirstlane(ur.w);
+  const int chunk = info >> 16, nch = info & 0xFFFF;
   const bool ada = t.opt == OPT_ADAGRAD;
   float* __restrict__ prow = t.P + (size_t)row * d;
   float* __restrict__ arow = ada ? t.A + (size_t)row * d : nullptr;
   float p[KM], a[KM], s[KM];
+  if (nch == 1) {
 #pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    const int e = l + 64 * k, ec = e < d ? e : d - 1;
-    p[k] = prow[ec];
-    a[k] = ada ? arow[ec] : 0.0f;
+    for (int k = 0; k < KM; ++k) {
+      const int e = l + 64 * k, ec = e < d ? e : d - 1;
+      p[k] = prow[ec];
+      a[k] = ada ? arow[ec] : 0.0f;
+    }
   }
   int c;
-  {   // slots 0 and 1 (most rows have one or two): every load issued, then the sums
+  {   // every load issued, then the sums (slot order)
     FoldLd<KM> fa, fb;
     fold_load<KM>(ws, count, d, sa0, fa);
     if (sb0 >= 0) fold_load<KM>(ws, count, d, sb0, fb);
@@ -1365,23 +1385,42 @@ __global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ re
 #pragma unroll
     for (int k = 0; k < KM; ++k) s[k] = sb0 >= 0 ? xa[k] + xb[k] : xa[k];
   }
-  if (n > 2) {
-    const int o0 = __builtin_amdgcn_readfirstlane(ws.uoff[u]);
-    for (int q = 2; q < n; q += 2) {   // the rest, two slots at a time
-      const int sa = __builtin_amdgcn_readfirstlane(ws.uslot[o0 + q]);
-      const int sb = q + 1 < n ? __builtin_amdgcn_readfirstlane(ws.uslot[o0 + q + 1]) : -1;
-      FoldLd<KM> fa, fb;
-      fold_load<KM>(ws, count, d, sa, fa);
-      if (sb >= 0) fold_load<KM>(ws, count, d, sb, fb);
-      float xa[KM], xb[KM];
-      c += fold_combine<KM>(ws, d, af, margin, sa, fa, xa);
+  if (nch > 1) {
+    // a row of several items (a hub row): each item publishes its partial sum
+    // write-through and drains, then adds to the row's arrival counter; the
+    // last to arrive sums the partials in item order (sc1 loads: every
+    // handed-off byte was stored sc1 and drained before the counter add) --
+    // the same bits whichever item arrives last
+    float* pw = ws.part + (size_t)wi * d;
 #pragma unroll
-      for (int k = 0; k < KM; ++k) s[k] += xa[k];
-      if (sb >= 0) {
-        c += fold_combine<KM>(ws, d, af, margin, sb, fb, xb);
+    for (int k = 0; k < KM; ++k) {
+      const int e = l + 64 * k;
+      if (e < d) __hip_atomic_store(pw + e, s[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (l == 0) __hip_atomic_store(ws.pcnt + wi, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int w0 = wi - chunk;
+    int old = 0;
+    if (l == 0) old = atomicAdd(ws.rowctr + w0, 1);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != nch - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the add
 #pragma unroll
-        for (int k = 0; k < KM; ++k) s[k] += xb[k];
+    for (int k = 0; k < KM; ++k) {
+      const int e = l + 64 * k, ec = e < d ? e : d - 1;
+      p[k] = prow[ec];
+      a[k] = ada ? arow[ec] : 0.0f;
+      s[k] = 0.0f;
+    }
+    c = 0;
+    for (int q = 0; q < nch; ++q) {   // item order
+      const float* pq = ws.part + (size_t)(w0 + q) * d;
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const int e = l + 64 * k, ec = e < d ? e : d - 1;
+        s[k] += __hip_atomic_load(pq + ec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      c += __hip_atomic_load(ws.pcnt + w0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if (c == 0) return;   // no violating occurrence: the row is not updated
@@ -2159,6 +2198,9 @@ static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, Resc
   // partial tiles even at one split
   const size_t wpb = std::max(rs_wpart_bytes(n, M, d), rs_front_wpart_bytes(n, M, d));
   w.wpart = wpb ? (float*)take(wpb) : nullptr;
+  // the row-grouped apply's partial sums of multi-chunk rows (k_rescal_fold)
+  w.part = (float*)take((size_t)4 * bs * d * 4);
+  w.pcnt = (int*)take((size_t)4 * bs * 4);
   // the in-front W step's second buffers (up to 256 MB)
   const bool wb = (size_t)M * d * d * 8 <= (256u << 20);
   w.W1 = wb ? (float*)take((size_t)M * d * d * 4) : nullptr;
@@ -2181,8 +2223,7 @@ static size_t rescal_epoch_layout(int bs, int nb, int M, int d, void* base, Resc
   w.n01 = (int*)take((size_t)M * 4);
   // the row grouping of the batch's 4 bs entity slots (k_rs_rows_ep)
   w.urec = (int4*)take((size_t)4 * bs * 16);
-  w.uoff = (int*)take((size_t)4 * bs * 4);
-  w.uslot = (int*)take((size_t)4 * bs * 4);
+  w.rowctr = (int*)take((size_t)4 * bs * 4);
   w.nuniq = (int*)take(4);
   w.vword = (unsigned long long*)take(8);
   w.npos = 0;   // (set per batch: rs_batch_view)
@@ -2268,8 +2309,7 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
   w.o2 = sh(w.o2);
   w.n01 = sh(w.n01);
   w.urec = sh(w.urec);
-  w.uoff = sh(w.uoff);
-  w.uslot = sh(w.uslot);
+  w.rowctr = sh(w.rowctr);
   w.nuniq = sh(w.nuniq);
   w.vword = sh(w.vword);
   w.npos = e.dedup ? count : 0;

@@ -688,19 +688,24 @@ def test_rescal_row_grouped_apply_matches_scatter(n_ent, n_rel, T, d, nb, opt, m
         np.testing.assert_allclose(out[1][1][k], out[0][1][k], rtol=RTOL, atol=ATOL, err_msg=k)
 
 
-def test_rescal_row_grouped_apply_is_deterministic(monkeypatch):
-    """The row-grouped apply sums each row's contributions in slot order (no
-    float atomics), so two runs from the same state give the same bits."""
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb", [
+    (40943, 18, 14140, 200, 10),   # WN18 geometry: rows of one or two slots
+    (60, 3, 3000, 20, 8),          # ~25 slots per row: multi-item rows merged by the last arrival
+])
+def test_rescal_row_grouped_apply_is_deterministic(n_ent, n_rel, T, d, nb, monkeypatch):
+    """The row-grouped apply sums each row's contributions in slot order, and a
+    hub row's per-item partial sums in item order (no float atomics), so two
+    runs from the same state give the same bits."""
     import skge_amd as S
     from skge_amd.device import DeviceKG, PairLoopRunner
     monkeypatch.delenv("SKGE_RESCAL_FORM", raising=False)
-    xs = make_kg(40943, 18, 14140, seed=16)
+    xs = make_kg(n_ent, n_rel, T, seed=16)
     out = []
     for _ in range(2):
-        m = make_model("rescal", (40943, 40943, 18), 200)
+        m = make_model("rescal", (n_ent, n_ent, n_rel), d)
         m.add_hyperparam("margin", 0.2)
         upd = {pid: S.AdaGrad(p, 0.1) for pid, p in m.params.items()}
-        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), 10, seed=17)
+        r = PairLoopRunner(m, upd, DeviceKG(xs, m.device), nb, seed=17)
         with torch.cuda.stream(r.stream):
             r.run(2)
         r.synchronize()
