@@ -1236,7 +1236,13 @@ struct FoldTab {
   int* ucnt;
   int opt, post;
   float lr, rin, rout, fdiv;
+  Accum acc;   // the entity accumulator: hub rows' sums (rows of more than RS_FOLD_MERGE items)
 };
+// a row of at most this many items (2 slots each) is merged from partial sums
+// in item order (bitwise reproducible); a larger one (a hub of a skewed KG)
+// adds its items into the entity accumulator (fp32 atomics, or exact
+// fixed-point ones in the deterministic mode)
+constexpr int RS_FOLD_MERGE = 8;
 
 // slot `sl` of the batch in two halves, so a wave keeps several slots' loads
 // in flight: fold_load issues the slot's WE / EW rows -- s: W E_o of the
@@ -1386,18 +1392,25 @@ __global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ re
     for (int k = 0; k < KM; ++k) s[k] = sb0 >= 0 ? xa[k] + xb[k] : xa[k];
   }
   if (nch > 1) {
-    // a row of several items (a hub row): each item publishes its partial sum
-    // write-through and drains, then adds to the row's arrival counter; the
-    // last to arrive sums the partials in item order (sc1 loads: every
-    // handed-off byte was stored sc1 and drained before the counter add) --
-    // the same bits whichever item arrives last
-    float* pw = ws.part + (size_t)wi * d;
+    // a row of several items: each item publishes its partial sum -- up to
+    // RS_FOLD_MERGE items write-through into its own slot, more (a hub row)
+    // into the entity accumulator with atomics -- drains, then adds to the
+    // row's arrival counter; the last to arrive reads the partials in item
+    // order (sc1 loads: every handed-off byte was stored sc1 or by an atomic
+    // and drained before the counter add) or the accumulated row, and applies
+    const bool hub = nch > RS_FOLD_MERGE;
+    if (hub) {
+      acc_row<KM>(t.acc, row, s, d);
+      if (l == 0 && c) atomicAdd(t.acc.cnt + row, c);
+    } else {
+      float* pw = ws.part + (size_t)wi * d;
 #pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      const int e = l + 64 * k;
-      if (e < d) __hip_atomic_store(pw + e, s[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < KM; ++k) {
+        const int e = l + 64 * k;
+        if (e < d) __hip_atomic_store(pw + e, s[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (l == 0) __hip_atomic_store(ws.pcnt + wi, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (l == 0) __hip_atomic_store(ws.pcnt + wi, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int w0 = wi - chunk;
     int old = 0;
@@ -1410,17 +1423,55 @@ __global__ __launch_bounds__(256) void k_rescal_fold(const int4* __restrict__ re
       const int e = l + 64 * k, ec = e < d ? e : d - 1;
       p[k] = prow[ec];
       a[k] = ada ? arow[ec] : 0.0f;
-      s[k] = 0.0f;
     }
-    c = 0;
-    for (int q = 0; q < nch; ++q) {   // item order
-      const float* pq = ws.part + (size_t)(w0 + q) * d;
+    if (hub) {   // the accumulated row and count, then zeroed for the next batch
+      const bool fx = t.acc.mode == ACC_FX64;
+      float* srow = t.acc.sum + (size_t)row * t.acc.width;
+      unsigned long long* xrow = reinterpret_cast<unsigned long long*>(t.acc.sum) +
+                                 (size_t)row * t.acc.width;
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
         const int e = l + 64 * k, ec = e < d ? e : d - 1;
-        s[k] += __hip_atomic_load(pq + ec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s[k] = fx ? fx_dec((long long)__hip_atomic_load(xrow + ec, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT))
+                  : __hip_atomic_load(srow + ec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      c += __hip_atomic_load(ws.pcnt + w0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      c = __hip_atomic_load(t.acc.cnt + row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const int e = l + 64 * k;
+        if (e < d) {
+          if (fx)
+            xrow[e] = 0ull;
+          else
+            srow[e] = 0.0f;
+        }
+      }
+      if (l == 0) t.acc.cnt[row] = 0;
+    } else {   // the items' partials, all loads in flight, summed in item order
+      float v[RS_FOLD_MERGE][KM];
+      int cv[RS_FOLD_MERGE];
+#pragma unroll
+      for (int q = 0; q < RS_FOLD_MERGE; ++q) {
+        const int qq = q < nch ? q : 0;
+        const float* pq = ws.part + (size_t)(w0 + qq) * d;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+          const int e = l + 64 * k, ec = e < d ? e : d - 1;
+          v[q][k] = __hip_atomic_load(pq + ec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        cv[q] = __hip_atomic_load(ws.pcnt + w0 + qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      c = 0;
+#pragma unroll
+      for (int k = 0; k < KM; ++k) s[k] = 0.0f;
+#pragma unroll
+      for (int q = 0; q < RS_FOLD_MERGE; ++q) {
+        if (q >= nch) break;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) s[k] += v[q][k];
+        c += cv[q];
+      }
     }
   }
   if (c == 0) return;   // no violating occurrence: the row is not updated
@@ -2368,7 +2419,7 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
     // the epoch's row grouping exists (form "scatter": the scatter + apply)
     if (infront && !form.scatter && w.nuniq && rs_rows_ok(bs)) {
       const FoldTab ft{ent->param, ent->state, ent->upd_count, ent->opt, ent->post, ent->lr,
-                       ent->rin, ent->rout, ent->fixed_div};
+                       ent->rin, ent->rout, ent->fixed_div, accum_of(ent)};
       const int nvw = (count + 255) / 256;   // violation-count workgroups, then one wave per row
       SKGE_KM_SWITCH(k_rescal_fold, dim3((unsigned)(nvw + count)), dim3(256), 0, st, rec, rec_n1,
                      start, count, d, af, margin, wsc, ft, wstp, nviol, nvw)

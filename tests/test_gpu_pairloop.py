@@ -688,18 +688,32 @@ def test_rescal_row_grouped_apply_matches_scatter(n_ent, n_rel, T, d, nb, opt, m
         np.testing.assert_allclose(out[1][1][k], out[0][1][k], rtol=RTOL, atol=ATOL, err_msg=k)
 
 
-@pytest.mark.parametrize("n_ent,n_rel,T,d,nb", [
-    (40943, 18, 14140, 200, 10),   # WN18 geometry: rows of one or two slots
-    (60, 3, 3000, 20, 8),          # ~25 slots per row: multi-item rows merged by the last arrival
+@pytest.mark.parametrize("n_ent,n_rel,T,d,nb,det", [
+    (40943, 18, 14140, 200, 10, False),   # WN18 geometry: rows of 1-4 slots, merged in order
+    (60, 3, 3000, 20, 8, True),           # ~25 slots per row: hub rows, fixed-point atomics
 ])
-def test_rescal_row_grouped_apply_is_deterministic(n_ent, n_rel, T, d, nb, monkeypatch):
-    """The row-grouped apply sums each row's contributions in slot order, and a
-    hub row's per-item partial sums in item order (no float atomics), so two
-    runs from the same state give the same bits."""
+def test_rescal_row_grouped_apply_is_deterministic(n_ent, n_rel, T, d, nb, det, monkeypatch):
+    """The row-grouped apply sums each row's contributions in slot order and a
+    row's items' partial sums in item order (no float atomics while a row has
+    at most 16 slots in a batch); hub rows past that add through the entity
+    accumulator, exact in the deterministic mode.  Two runs from the same
+    state give the same bits."""
     import skge_amd as S
     from skge_amd.device import DeviceKG, PairLoopRunner
     monkeypatch.delenv("SKGE_RESCAL_FORM", raising=False)
     xs = make_kg(n_ent, n_rel, T, seed=16)
+    out = []
+    prev = S.deterministic()
+    S.set_deterministic(det)
+    try:
+        out = _two_runs(S, DeviceKG, PairLoopRunner, xs, n_ent, n_rel, d, nb)
+    finally:
+        S.set_deterministic(prev)
+    for pid in out[0]:
+        assert np.array_equal(out[0][pid], out[1][pid]), pid
+
+
+def _two_runs(S, DeviceKG, PairLoopRunner, xs, n_ent, n_rel, d, nb):
     out = []
     for _ in range(2):
         m = make_model("rescal", (n_ent, n_ent, n_rel), d)
@@ -710,5 +724,4 @@ def test_rescal_row_grouped_apply_is_deterministic(n_ent, n_rel, T, d, nb, monke
             r.run(2)
         r.synchronize()
         out.append({pid: p.data.cpu().numpy().copy() for pid, p in m.params.items()})
-    for pid in out[0]:
-        assert np.array_equal(out[0][pid], out[1][pid]), pid
+    return out
