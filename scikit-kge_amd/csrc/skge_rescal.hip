@@ -43,6 +43,11 @@ constexpr int GC = 64;          // output columns per GEMM tile
 #define SKGE_RS_GKS_DEFAULT 1   // A/B: SKGE_RS_GKS
 #endif
 constexpr int KS = SKGE_RS_KS;  // k per staged step
+// the fused front's k-step below RS_KS_SMALL_BS positives per batch (k order
+// unchanged: the same bits); WN18 d = 200, same box: nb = 100 KS 16 / 32 / 64
+// -> 36.3 / 35.8 / 26.8 M triples/s, nb = 2 KS 16 / 32 -> 70.1 / 72.5 M
+// (profiles/r06/ab_rescal_ks.txt)
+constexpr int KS_SMALL = 16, RS_KS_SMALL_BS = 8192;
 constexpr int RS_MAX_D = 1024;  // d of the MFMA path
 constexpr int RS_MAX_M = 8192;  // relations (k_rs_scan keeps 2M+1 ints in LDS)
 
@@ -842,17 +847,20 @@ __global__ __launch_bounds__(1024) void k_rs_bucket_small(const int* __restrict_
 // ---------------------------------------------------------------------------
 // B: product 0 as [GC][KS + 4] (W rows as loaded, column-major B), product 1
 // as [KS][GC + 4]; both read conflict-free by the MFMA loop
-constexpr int SB0 = GC * (KS + 4), SB1 = KS * (GC + 4);
-constexpr int SBN = SB0 > SB1 ? SB0 : SB1;
+constexpr int rs_sbn(int ks) {
+  return GC * (ks + 4) > ks * (GC + 4) ? GC * (ks + 4) : ks * (GC + 4);
+}
+constexpr int SBN = rs_sbn(KS);
 // one GEMM workgroup's LDS: sA [2][RT_ITEMS][KS + 4], sB [2][SBN], 4 x RT_ITEMS ints
-constexpr int GEMM_LDS_FLOATS = 2 * RT_ITEMS * (KS + 4) + 2 * SBN + 4 * RT_ITEMS;
+constexpr int gemm_lds_floats(int ks) { return 2 * RT_ITEMS * (ks + 4) + 2 * rs_sbn(ks) + 4 * RT_ITEMS; }
 
 // workgroup `bid` of the GEMM grid (k_rescal_gemm, k_rescal_front_fused)
-template <bool VEC>
+template <bool VEC, int KS = skge::KS>
 __device__ __forceinline__ void rescal_gemm_body(const float* __restrict__ E,
                                                  const float* __restrict__ W, int d,
                                                  const RescalWs& ws, int bid,
-                                                 float (*sA)[RT_ITEMS][KS + 4], float (*sB)[SBN],
+                                                 float (*sA)[RT_ITEMS][KS + 4],
+                                                 float (*sB)[rs_sbn(KS)],
                                                  int* s_row, int* s_gid, int* s_es, int* s_es2) {
   const int ncb = (d + GC - 1) / GC;
   // plain: (tile, product, column block, K slice); deduplicated (ws.npos > 0):
@@ -1937,14 +1945,15 @@ __global__ __launch_bounds__(256) void k_rescal_wgrad_part(const float* __restri
 // violations) follows the scatter.  The LDS is one buffer carved per role.
 // Same arithmetic, same k order as the unfused kernels: bitwise the same W.
 // ---------------------------------------------------------------------------
-constexpr int FRONT_LDS_FLOATS =
-    GEMM_LDS_FLOATS > WPART_LDS_FLOATS ? GEMM_LDS_FLOATS : WPART_LDS_FLOATS;
-template <bool VEC, bool COMB, bool IF>
+constexpr int front_lds_floats(int ks) {
+  return gemm_lds_floats(ks) > WPART_LDS_FLOATS ? gemm_lds_floats(ks) : WPART_LDS_FLOATS;
+}
+template <bool VEC, bool COMB, bool IF, int KS>
 __global__ __launch_bounds__(256) void k_rescal_front_fused(const float* __restrict__ E,
                                                             const float* __restrict__ W, int d,
                                                             RescalWs ws, int splits, int nwg,
                                                             int order, WFront wf) {
-  __shared__ __attribute__((aligned(16))) float lds[FRONT_LDS_FLOATS];
+  __shared__ __attribute__((aligned(16))) float lds[front_lds_floats(KS)];
   const int bid = (int)blockIdx.x, ng = (int)gridDim.x - nwg;
   // role of workgroup bid: order 0 = the dW grid first, 1 = the GEMM grid
   // first, r >= 2 = one dW workgroup every r workgroups (while they last)
@@ -1966,12 +1975,12 @@ __global__ __launch_bounds__(256) void k_rescal_front_fused(const float* __restr
                                 reinterpret_cast<float(*)[WG_T + 4]>(lds + WG_CH * (WG_T + 4)), wf);
   } else {
     float* sb = lds + 2 * RT_ITEMS * (KS + 4);
-    int* si = reinterpret_cast<int*>(sb + 2 * SBN);
+    int* si = reinterpret_cast<int*>(sb + 2 * rs_sbn(KS));
     const float* Wb = IF && *wf.cur ? wf.W1 : W;   // W_b's buffer
-    rescal_gemm_body<VEC>(E, Wb, d, ws, gid,
-                          reinterpret_cast<float(*)[RT_ITEMS][KS + 4]>(lds),
-                          reinterpret_cast<float(*)[SBN]>(sb), si, si + RT_ITEMS,
-                          si + 2 * RT_ITEMS, si + 3 * RT_ITEMS);
+    rescal_gemm_body<VEC, KS>(E, Wb, d, ws, gid,
+                              reinterpret_cast<float(*)[RT_ITEMS][KS + 4]>(lds),
+                              reinterpret_cast<float(*)[rs_sbn(KS)]>(sb), si, si + RT_ITEMS,
+                              si + 2 * RT_ITEMS, si + 3 * RT_ITEMS);
   }
 }
 
@@ -2396,9 +2405,16 @@ int skge_rescal_pos_grad_mfma_ep(hipStream_t st, int af, const skge_table_t* ent
     if (infront)
       wf = WFront{w.wcur, rel->param, rel->state, w.W1, w.A1, rel->opt, rel->lr, rel->rin,
                   rel->rout, rel->fixed_div};
-#define SKGE_FRONT(V, C, I)                                                                 \
-  hipLaunchKernelGGL((k_rescal_front_fused<V, C, I>), grid, dim3(256), 0, st, ent->param,    \
-                     rel->param, d, w, fsplits, nwg, order, wf)
+    const bool ks_small = bs < RS_KS_SMALL_BS;
+#define SKGE_FRONT(V, C, I)                                                                  \
+  do {                                                                                       \
+    if (ks_small)                                                                            \
+      hipLaunchKernelGGL((k_rescal_front_fused<V, C, I, KS_SMALL>), grid, dim3(256), 0, st,  \
+                         ent->param, rel->param, d, w, fsplits, nwg, order, wf);             \
+    else                                                                                     \
+      hipLaunchKernelGGL((k_rescal_front_fused<V, C, I, KS>), grid, dim3(256), 0, st,        \
+                         ent->param, rel->param, d, w, fsplits, nwg, order, wf);             \
+  } while (0)
     if ((d & 3) == 0) {
       if (infront) SKGE_FRONT(true, true, true);
       else if (comb) SKGE_FRONT(true, true, false);
