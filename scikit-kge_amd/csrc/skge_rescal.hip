@@ -212,7 +212,13 @@ static bool rs_dedup_on() { return !rs_form().nodedup; }
 #define SKGE_RS_WG_SPLIT 8   // most splits per tile (1 disables)
 #endif
 constexpr int WS_TILE = 64;                 // == WG_T below
-constexpr int WS_GROUP = 128;               // items per group == WG_PF * WG_CH below
+#ifndef SKGE_RS_WG_PF
+// chunks of 64 items loaded together in the dW tiles; A/B on WN18 d=200: round
+// 1 1 group of 4 chunks 20.5M, 2 chunks 24.2M; round 6 (fused front, config 4,
+// profiles/r06/ab_rescal_dw_prefetch.txt) 1 / 2 / 4 -> 30.7 / 36.2 / 23.5 M
+#define SKGE_RS_WG_PF 2
+#endif
+constexpr int WS_GROUP = SKGE_RS_WG_PF * 64;   // items per group == WG_PF * WG_CH below
 static int rs_wsplit(int n, int M, int d) {
   const long long nt = (d + WS_TILE - 1) / WS_TILE;
   // (at the reference's batch, ~2 groups per relation, the extra launch costs
@@ -1585,9 +1591,6 @@ constexpr int WG_T = 64;    // rows / columns of a dW tile
 constexpr int WG_CH = 64;   // items staged per step
 constexpr int WG_TPI = 256 / WG_CH;       // threads per item
 constexpr int WG_FPT = WG_T / WG_TPI;     // row floats per thread and operand
-#ifndef SKGE_RS_WG_PF
-#define SKGE_RS_WG_PF 2   // A/B on WN18 d=200: 1 group of 4 chunks 20.5M, 2 chunks 24.2M, round 1 (1-deep pipeline) 23.3M
-#endif
 constexpr int WG_PF = SKGE_RS_WG_PF;      // chunks of items loaded together
 
 template <bool APPLY, bool VEC>
