@@ -139,11 +139,10 @@ typedef struct skge_table {
 int skge_abi_version(void);
 const char *skge_last_error(void);
 /* Synchronizes the stream and returns the error bits raised by device kernels
- * since the last reset (2 = a packed row's count exceeded 32767; 4 = a decoded
- * SKGE_ACC_FX64 sum was at or past 2^22 in gradient units, half its wrap-around
- * range -- a PARTIAL guard: it catches true sums of magnitude in [2^22, 3*2^22),
- * which decode to >= 2^22 wrapped or not; a sum past 3*2^22 can wrap back below
- * 2^22 unflagged); reset != 0 clears them. */
+ * since the last reset (2 = a packed row's count exceeded 32767; 4 = an
+ * SKGE_ACC_FX64 sum wrapped past its 2^23 range in gradient units -- every
+ * fixed-point add checks its own signed overflow -- or a decoded sum was at
+ * or past 2^22, half that range); reset != 0 clears them. */
 int skge_device_error(void *stream, int reset);
 
 /*

@@ -108,6 +108,7 @@ struct Accum {
   int mode;
   int replicas;    // >= 1; copies of sum/cnt, [replicas][rows][...]
   int rows;
+  int* err = nullptr;   // ACC_FX64: the device error word (bit 4: a sum wrapped)
 };
 
 enum AccMode : int { ACC_F32 = 0, ACC_I16X4 = 1, ACC_I32X2 = 2, ACC_FX64 = 3, ACC_I8X4 = 4 };
@@ -125,10 +126,11 @@ __device__ __host__ __forceinline__ int acc_row_dwords(int mode, int width) {
 // converts the sum back once.  Range: |sum| < 2^23 per element and batch,
 // i.e. (a row's occurrences in the batch) x max |contribution| < 8.4e6 -- WN18
 // RESCAL at nb = 2 (~5e4 pairs of one relation, |E_s E_o| <= 1) stays far
-// inside; the applies flag any decoded sum at or past 2^22 (skge_device_error
-// bit 4, raised by the runners' synchronize()) -- a partial guard: a true sum
-// in [2^22, 3*2^22) is caught wrapped or not, one past 3*2^22 can wrap back
-// below 2^22 unflagged.
+// inside.  Every add is a returned atomic and checks its own signed overflow
+// (old and addend of one sign, the result of the other), so any wrap of a
+// partial sum sets skge_device_error bit 4 (raised by the runners'
+// synchronize()) when it happens; the applies also flag a decoded sum at or
+// past 2^22 (half the range).
 constexpr float FX_SCALE = 1099511627776.0f;            // 2^40
 __device__ __forceinline__ long long fx_enc(float v) { return __float2ll_rn(v * FX_SCALE); }
 __device__ __forceinline__ float fx_dec(long long x) {
@@ -221,11 +223,18 @@ __device__ __forceinline__ void acc_row(const Accum& a, int row, const float (&v
   const int l = lane_id();
   if (a.mode == ACC_FX64) {   // deterministic: exact fixed-point integer sums
     unsigned long long* base = reinterpret_cast<unsigned long long*>(a.sum) + (size_t)row * a.width;
+    bool wrapped = false;
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
       const int e = l + 64 * k;
-      if (e < d && v[k] != 0.0f) atomicAdd(base + e, (unsigned long long)fx_enc(v[k]));
+      if (e < d && v[k] != 0.0f) {
+        const long long add = fx_enc(v[k]);
+        const unsigned long long old = atomicAdd(base + e, (unsigned long long)add);
+        const long long res = (long long)(old + (unsigned long long)add);
+        wrapped = wrapped || ((((long long)old ^ res) & (add ^ res)) < 0);
+      }
     }
+    if (wrapped && a.err) atomicOr(a.err, 4);
     return;
   }
   float* base = a.sum + (size_t)row * a.width;

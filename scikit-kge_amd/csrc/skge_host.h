@@ -50,6 +50,7 @@ inline int km_for(int d) {
   return 0;
 }
 
+int* dev_err_word();   // skge_update.hip: the device error word (Accum::err)
 inline Accum accum_of(const skge_table_t* t) {
   Accum a;
   a.sum = t->acc_sum;
@@ -59,6 +60,7 @@ inline Accum accum_of(const skge_table_t* t) {
   a.mode = t->acc_mode;
   a.replicas = t->acc_replicas > 1 ? t->acc_replicas : 1;
   a.rows = t->rows;
+  a.err = t->acc_mode == SKGE_ACC_FX64 ? dev_err_word() : nullptr;
   return a;
 }
 

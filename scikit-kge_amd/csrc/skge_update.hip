@@ -13,13 +13,19 @@ namespace skge {
 
 // error bits raised by apply kernels (read with skge_device_error):
 // 2 = a packed int16x4 row's count exceeded 32767 (its sums may have wrapped)
-// 4 = a deterministic fixed-point (ACC_FX64) sum decoded at or past half its
-//     range (|sum| >= 2^22 in gradient units; it wraps at 2^23).  A PARTIAL
-//     guard: true sums of magnitude in [2^22, 3*2^22) decode to >= 2^22
-//     (wrapped or not) and are caught; a sum past 3*2^22 can wrap back below
-//     2^22 and pass.  The range is sized so the largest case measured (WN18
-//     RESCAL at nb = 2) stays orders of magnitude inside it (skge_device.h).
+// 4 = a deterministic fixed-point (ACC_FX64) sum wrapped (its 2^23 range in
+//     gradient units; every add checks its own signed overflow, acc_row) or
+//     decoded at or past half its range.  The range is sized so the largest
+//     case measured (WN18 RESCAL at nb = 2) stays orders of magnitude inside
+//     it (skge_device.h).
 __device__ int g_skge_dev_err = 0;
+
+int* dev_err_word() {   // the error word's device address (Accum::err)
+  static int* p = nullptr;
+  if (!p && hipGetSymbolAddress(reinterpret_cast<void**>(&p), HIP_SYMBOL(g_skge_dev_err)) != hipSuccess)
+    p = nullptr;
+  return p;
+}
 
 // FX64 sums wrap silently past +-2^63 (2^23 in gradient units, FX_SCALE):
 // flag any decoded element at or past half of that range (partial: see above)

@@ -171,7 +171,7 @@ def ptr(t):
 def check_device_error(stream_handle, what="device"):
     """Read and reset the apply kernels' error word (skge_device_error) and
     raise on its bits: 2 = a packed row's count passed 32767, 4 = a
-    deterministic fixed-point sum reached half its range."""
+    deterministic fixed-point sum wrapped or reached half its range."""
     rc = lib().skge_device_error(stream_handle, 1)
     if rc < 0:
         raise SkgeError("%s: %s" % (what, lib().skge_last_error().decode()))
@@ -179,8 +179,7 @@ def check_device_error(stream_handle, what="device"):
         raise SkgeError("%s: a row's per-batch count exceeded 32767 (packed sums may have "
                         "wrapped); use force_f32=True" % what)
     if rc & 4:
-        raise SkgeError("%s: a deterministic fixed-point (FX64) sum decoded at or past 2^22 "
-                        "(half of its 2^23 wrap-around range; this guard is partial: a sum past "
-                        "3*2^22 can wrap back below 2^22 unflagged); use more batches or the "
-                        "default float sums" % what)
+        raise SkgeError("%s: a deterministic fixed-point (FX64) sum wrapped past its 2^23 "
+                        "range (caught at the add) or decoded at or past 2^22 (half of it); use "
+                        "more batches or the default float sums" % what)
     return rc

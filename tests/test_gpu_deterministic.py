@@ -87,7 +87,8 @@ def test_deterministic_step_matches_oracle(det, kind):
 @pytest.mark.parametrize("mag", [1.0, 5.0e6])
 def test_fx64_range_flag(mag):
     """FX64 sums wrap past 2^23 gradient units.  An apply that
-    decodes a sum at or past 2^22 sets skge_device_error bit 4, which
+    decodes a sum at or past 2^22 (half the range) sets skge_device_error
+    bit 4 (a wrap itself is caught at the add, below), which
     check_device_error (every runner's synchronize) raises; ordinary sums do
     not."""
     import skge_amd as S
@@ -111,3 +112,43 @@ def test_fx64_range_flag(mag):
     else:
         with pytest.raises(L.SkgeError, match="FX64"):
             L.check_device_error(L.stream_ptr(), "fx64")
+
+
+@pytest.mark.parametrize("preset", [0, 2 ** 63 - 1])
+def test_fx64_wrap_caught_when_added(det, preset):
+    """the decode-time range check alone misses a sum that wraps
+    back inside half the range.  Every fixed-point add is a returned atomic
+    that checks its own signed overflow (acc_row): a row whose sums sit at
+    the top of the range and receive positive contributions sets
+    skge_device_error bit 4 in the producer itself -- no apply or collect
+    (which would decode) runs here; from zero nothing is flagged."""
+    from skge_amd import _lib as L
+    np.random.seed(5)
+    n, nr, d, P = 50, 3, 64, 40
+    m = det.TransE((n, n, nr), d, l1=False)
+    m.add_hyperparam("margin", 1.0e9)           # every pair violates
+    rs = np.random.RandomState(1)
+    s, o, p = rs.randint(0, n, P), rs.randint(0, n, P), rs.randint(0, nr, P)
+    s[:] = 7                                    # row 7 in every positive
+    pos = torch.tensor(np.stack([s, o, p], 1), dtype=torch.int32, device="cuda")
+    neg = torch.tensor(np.stack([s, rs.randint(0, n, P), p], 1), dtype=torch.int32,
+                       device="cuda")
+    te, tr = m._tables("pairwise", slots=m._pair_slots(P))
+    acc = m.accumulator("E")
+    assert acc.mode == L.SKGE_ACC_FX64
+    x = acc.sum.view(torch.int64).view(-1, d)
+    x.zero_()
+    x[7] = preset
+    nviol = torch.zeros(1, dtype=torch.int32, device="cuda")
+    L.lib().skge_device_error(L.stream_ptr(), 1)
+    L.check(L.lib().skge_pair_grad(L.stream_ptr(), m._kernel_model(), m._af_code(), te, tr, d,
+                                   L.ptr(pos), L.ptr(neg), P, 1.0e9, None, None, None,
+                                   L.ptr(nviol)), "pair_grad")
+    torch.cuda.synchronize()
+    assert int(nviol.item()) == P
+    if preset == 0:
+        L.check_device_error(L.stream_ptr(), "fx64")
+    else:
+        with pytest.raises(L.SkgeError, match="FX64"):
+            L.check_device_error(L.stream_ptr(), "fx64")
+    L.lib().skge_device_error(L.stream_ptr(), 1)   # leave the global error word clean
